@@ -1,0 +1,54 @@
+"""Loaders for the golden fixtures in tests/golden (data only; see make_golden.py)."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import torch
+
+from oracle import simpo_ref as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def bits_to_bf16(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(a.astype(np.uint16).view(np.int16).copy()).view(torch.bfloat16)
+
+
+def load(name: str):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def dims_of(z) -> O.JanusDims:
+    return O.JanusDims(**json.loads(str(z["dims"])))
+
+
+def step_inputs(z):
+    tt, lens = z["text_tokens"], z["text_lens"]
+    text = [torch.from_numpy(tt[i, : lens[i]].copy()).view(1, -1) for i in range(len(lens))]
+    chosen = torch.from_numpy(z["chosen_ids"].astype(np.int64))
+    rejected = torch.from_numpy(z["rejected_ids"].astype(np.int64))
+    return text, chosen, rejected
+
+
+def step_weights(z, name: str, dims: O.JanusDims):
+    """Weights for a step fixture: the shared tiny weight file, or regenerated
+    from the recorded seed (checked against the recorded sha256)."""
+    if name.startswith("step_tiny"):
+        wz = load("step_tiny_weights.npz")
+        return {k: bits_to_bf16(wz[k]) for k in wz.files}
+    w = O.init_weights(dims, seed=int(z["weights_seed"]), dtype=torch.bfloat16, lora_b_std=1e-2)
+    return w
+
+
+def step_outputs(z):
+    out = {k[5:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("out::") and k != "out::logged"}
+    out["logged"] = json.loads(str(z["out::logged"]))
+    out["grads"] = {k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("grad::")}
+    return out
+
+
+def rel_err(a: torch.Tensor, b: torch.Tensor) -> float:
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
