@@ -1,0 +1,182 @@
+/*
+ * libospo_hip.so -- C ABI of the MI355X-native (gfx950 / CDNA4) SimPO training
+ * path for Janus-Pro (OSPO step 5).  Plain pointers, sizes and a hipStream_t;
+ * no framework types.  Every function validates shapes/alignment BEFORE any
+ * launch and returns an ospo_status (0 = OK).  The library allocates nothing:
+ * every buffer (workspaces included) is owned by the caller.  All work is
+ * enqueued asynchronously on `stream`; no function synchronises the host.
+ *
+ * Each entry point names the reference interface it replaces (file:line under
+ * the reference tree OSPO-NeurIPS2025/OSPO; "HF" = transformers 4.38.2 Llama,
+ * "peft" = peft 0.7.1 lora.Linear, both upstream of the reference).
+ *
+ * Conventions: bf16 = IEEE bfloat16 (2 bytes), row-major, leading dimensions in
+ * ELEMENTS.  Token rows of a batch are laid out sequence-major: row = s*T + t.
+ */
+#ifndef OSPO_HIP_H
+#define OSPO_HIP_H
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  OSPO_OK = 0,
+  OSPO_ERR_SHAPE = 1,       /* shape / leading-dimension / tile-multiple violation */
+  OSPO_ERR_ALIGN = 2,       /* pointer not 16-byte aligned where required */
+  OSPO_ERR_HIP = 3,         /* launch failed (hipGetLastError) */
+  OSPO_ERR_UNSUPPORTED = 4, /* configuration not built */
+  OSPO_ERR_ARG = 5          /* bad scalar argument (loss type, null pointer) */
+} ospo_status;
+
+const char* ospo_strerror(int status);
+int ospo_abi_version(void);
+
+/* ------------------------------------------------------------------ GEMM ---
+ * Linear layers of the Llama decoder with fused peft LoRA (peft lora.Linear
+ * .forward, reached from ospo/utils/model.py:50-60; call sites HF
+ * LlamaAttention/LlamaMLP q,k,v,o,gate,up,down) and the frozen Linear layers
+ * of gen_head (janus/models/modeling_vlm.py:47-51) / gen_aligner
+ * (janus/models/projector.py:39-45).
+ *
+ * C[M,N] (bf16) = round( alpha * (A[M,K] . B[N,K]^T + A2[M,K2] . B2[N,K2]^T) + bias[N] )
+ *                 [+ residual[M,N], added after rounding and rounded again]
+ * A, A2 row-major with K contiguous; B, B2 row-major with K contiguous (the
+ * nn.Linear weight layout [out,in]).  A2/B2 is the LoRA K-extension
+ * (A2 = scaling * lora_A(x), B2 = block-diagonal lora_B), may be NULL (K2 = 0).
+ * Requires N % 256 == 0 (or N % 64 == 0 for N <= 256), K % 64 == 0, K2 % 64 == 0;
+ * M arbitrary.  MFMA bf16 (v_mfma_f32_16x16x32_bf16), fp32 accumulation. */
+int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
+                      const void* A2, int lda2, const void* B2, int ldb2, int K2, float alpha,
+                      const void* bias, const void* residual, int ldr, void* C, int ldc,
+                      hipStream_t stream);
+
+/* C[M,N] (fp32) += alpha * op(A)[M,K] . op(B)[N,K]^T, split over K into
+ * `k_splits` workgroup slices summed with fp32 atomics (C must be initialised).
+ * a_kmajor = 0: A stored [M][K] (lda >= K); 1: A stored [K][M] (lda >= M).
+ * b_kmajor = 0: B stored [N][K];            1: B stored [K][N].
+ * Used for the LoRA down-projections u = x.A^T / g = dy.B (skinny N) and the
+ * LoRA weight gradients dA = g^T.x, dB = dy^T.u (both operands K-major).
+ * diag_nblk > 0 selects the block-diagonal scatter of a packed dB:
+ * element (n, j) is kept only when j / diag_r == n / diag_nblk and lands at
+ * C + n*diag_r + (j % diag_r)  (ldc ignored) -- peft B_q|B_k|B_v contiguous.
+ * Requires K % 64 == 0; N % 64 == 0; M arbitrary (stores predicated on m < M; a
+ * K-major A must have lda >= roundup(M, 64) readable columns). */
+int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
+                     int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
+                     int diag_nblk, int diag_r, hipStream_t stream);
+
+/* dst[i] (bf16) = round(scale * src[i]) for i < n (fp32 -> bf16 with scale). */
+int ospo_f32_to_bf16(const float* src, void* dst, long n, float scale, hipStream_t stream);
+
+/* -------------------------------------------------------------- RMSNorm ---
+ * HF LlamaRMSNorm: y = w * bf16(x * rsqrt(mean(x^2) + eps)); rstd saved (fp32).
+ * bwd: dx = dres + d/dx  (dres may be NULL); weight frozen (no dw).
+ * Requires D % 8 == 0, D <= 16384. */
+int ospo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int M, int D, float eps,
+                     hipStream_t stream);
+int ospo_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
+                     const void* dres, void* dx, int M, int D, hipStream_t stream);
+
+/* ----------------------------------------------------------------- RoPE ---
+ * HF apply_rotary_pos_emb (rotate-half; position t = row % T) in place on the
+ * q and k column blocks of a [rows, ld] buffer: x*cos + rotate_half(x)*sin with
+ * each product and the sum rounded to bf16 as eager bf16 PyTorch does.
+ * cos_tab/sin_tab: bf16 [T][head_dim/2] (HF LlamaRotaryEmbedding values, the
+ * caller computes them once).  bwd applies the transpose rotation to grads. */
+int ospo_rope_fwd(void* qkv, int ld, int q_col, int k_col, int S, int T, int n_heads,
+                  int head_dim, const void* cos_tab, const void* sin_tab, hipStream_t stream);
+int ospo_rope_bwd(void* dqkv, int ld, int q_col, int k_col, int S, int T, int n_heads,
+                  int head_dim, const void* cos_tab, const void* sin_tab, hipStream_t stream);
+
+/* --------------------------------------------------------------- SwiGLU ---
+ * HF LlamaMLP: h = bf16(bf16(silu(g)) * u) with gu = [g | u] (cols [0,F), [F,2F)). */
+int ospo_swiglu_fwd(const void* gu, int ld_gu, void* h, int ld_h, int M, int F, hipStream_t stream);
+int ospo_swiglu_bwd(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu,
+                    int M, int F, hipStream_t stream);
+
+/* ------------------------------------------------------------ attention ---
+ * Causal softmax attention per (sequence s, head h), HF eager semantics
+ * (scores * scale, causal mask, fp32 softmax), flash-style on MFMA.
+ * q/k/v/o rows s*T+t, head h at column offset h*head_dim.  lse: fp32
+ * [S, H, T] (natural-log sum-exp of the scaled scores).  head_dim == 128.
+ * bwd needs workspaces: delta fp32 [S*H*T], dq_acc fp32 [S*T, H*head_dim]
+ * (zeroed by the function).  dq/dk/dv are written (bf16) into dqkv. */
+int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
+                        int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
+                        hipStream_t stream);
+int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col,
+                        const void* o, int ld_o, const void* dout, int ld_do, const float* lse,
+                        float* delta_ws, float* dq_acc_ws, void* dqkv, int ld_dqkv, int S, int T,
+                        int n_heads, int head_dim, float scale, hipStream_t stream);
+
+/* ------------------------------------------------------- embed / gather ---
+ * preprocess_batch (ospo/wrapper/train.py:224-239, 267-277) + concatenated_inputs
+ * (:282-314): x0[s*T+t] = text_emb[text_ids[s % B][t]] for t < Lt (id < 0 -> zero
+ * row, the right zero-padding), img_emb[s*N + t - Lt] for t >= Lt; S = 2B.
+ * gen_aligner_in: out[r] = bf16(gelu(bf16(gen_embed[ids[r]] . w1^T + b1)))
+ * (modeling_vlm.py:263-264, first Linear + GELU of projector mlp_gelu). */
+int ospo_assemble_inputs(const int* text_ids, int B, int Lt, const void* text_table, const void* img_emb,
+                         int N, int D, void* x0, hipStream_t stream);
+int ospo_gen_aligner_in(const int* ids, int R, const void* gen_embed, int E, const void* w1,
+                        const void* b1, int D, void* out, hipStream_t stream);
+/* dst[s*N + i] = src[s*T + t0 + i] (rows of D); scatter: dst rows zero elsewhere. */
+int ospo_gather_rows(const void* src, int ld_src, int S, int T, int t0, int N, int D, void* dst,
+                     hipStream_t stream);
+int ospo_scatter_rows(const void* src, int S, int T, int t0, int N, int D, void* dst, int ld_dst,
+                      int total_rows, hipStream_t stream);
+
+/* y = bf16(gelu(x)); dx = bf16(dy * gelu'(x_pre)) -- gen_head GELU (modeling_vlm.py:49). */
+int ospo_gelu_fwd(const void* x, void* y, long n, hipStream_t stream);
+int ospo_gelu_bwd(const void* dy, const void* x_pre, void* dx, long n, hipStream_t stream);
+
+/* ---------------------------------------------------------- log-probs ---
+ * get_batch_logps (ospo/wrapper/train.py:375-396), average_log_prob=True, on
+ * the R = S*N gathered image-token rows: logp[r] = logit[r, lab[r]] - lse[r]
+ * (fp32 log-softmax of bf16 logits); seq_logps[s] = mean over its N rows.
+ * bwd: dlogits[r, v] = g[r / N] / N * (1[v == lab[r]] - exp(logit - lse)). */
+int ospo_logprob_fwd(const void* logits, int V, const int* labels, int R, int N, float* lse,
+                     float* token_logp, float* seq_logps, hipStream_t stream);
+int ospo_logprob_bwd(const void* logits, int V, const int* labels, const float* lse, int R, int N,
+                     const float* g_seq, void* dlogits, hipStream_t stream);
+
+/* ---------------------------------------------------------------- SimPO ---
+ * simpo_loss (ospo/wrapper/train.py:317-342) + losses.mean() (:419).
+ * logps = [chosen(B) | rejected(B)] fp32.  loss_type 0 = sigmoid, 1 = hinge.
+ * fwd writes losses[B], loss_mean[1], rewards[2B] (= beta * logps).
+ * bwd: glogps[2B] = d(g_loss * mean(losses)) / d logps. */
+int ospo_simpo_fwd(const float* logps, int B, float beta, float gamma_beta_ratio,
+                   float label_smoothing, int loss_type, float* losses, float* loss_mean,
+                   float* rewards, hipStream_t stream);
+int ospo_simpo_bwd(const float* logps, int B, float beta, float gamma_beta_ratio,
+                   float label_smoothing, int loss_type, const float* g_loss, float* glogps,
+                   hipStream_t stream);
+
+/* ------------------------------------------------------------ LoRA pack ---
+ * Build the per-layer fused LoRA operands from the flat bf16 LoRA parameter
+ * buffer (layout in ospo_amd/lora.py): for module group g of layer l with
+ * nmods modules of rank r, input dim Kin and per-module output Nmod:
+ *   Acat [Rp][Kin]   rows j < nmods*r = stacked lora_A, rest zero
+ *   AcatT[Kin][Rp]   its transpose
+ *   Bcat [nmods*Nmod][Rp] block-diagonal stacked lora_B
+ * Rp = roundup(nmods*r, 64). */
+int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int Kin, int Nmod,
+                   int Rp, void* Acat, void* AcatT, void* Bcat, hipStream_t stream);
+
+/* ------------------------------------------------------------ optimizer ---
+ * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip
+ * (ospo/utils/train.py:30, gradient_clip_val) + torch AdamW
+ * (train.py:108-115) on bf16 params with bf16 moments, fp32 grads.
+ * sumsq_out[0] += sum(g^2) (fp32 atomics; caller zeroes).  adamw reads the
+ * device-resident sumsq, so no host sync is needed; step is 1-based. */
+int ospo_sumsq(const float* g, long n, float* sumsq_out, hipStream_t stream);
+int ospo_adamw_clip(void* params, const float* grads, void* exp_avg, void* exp_avg_sq, long n,
+                    float lr, float beta1, float beta2, float eps, float weight_decay, int step,
+                    const float* sumsq, float max_norm, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OSPO_HIP_H */

@@ -1,0 +1,83 @@
+"""ctypes binding of libospo_hip.so (the C ABI declared in include/ospo_hip.h).
+
+The product path has NO fallback: if the library is missing or a call returns
+a non-zero ospo_status, this raises.  ``ValueError`` for shape/argument
+violations (mirroring ``ospo/wrapper/train.py:382-383,335-337``), ``RuntimeError``
+for HIP launch failures.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_long, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OSPO_HIP_LIB", os.path.join(_HERE, "libospo_hip.so"))
+
+P, I, L, F = c_void_p, c_int, c_long, c_float
+
+# name -> argtypes (restype is always c_int = ospo_status)
+SIGNATURES = {
+    "ospo_abi_version": [],
+    "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P],
+    "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],
+    "ospo_f32_to_bf16": [P, P, L, F, P],
+    "ospo_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
+    "ospo_rmsnorm_bwd": [P, P, P, P, P, P, I, I, P],
+    "ospo_rope_fwd": [P, I, I, I, I, I, I, I, P, P, P],
+    "ospo_rope_bwd": [P, I, I, I, I, I, I, I, P, P, P],
+    "ospo_swiglu_fwd": [P, I, P, I, I, I, P],
+    "ospo_swiglu_bwd": [P, I, P, I, P, I, I, I, P],
+    "ospo_flash_attn_fwd": [P, I, I, I, I, P, I, P, I, I, I, I, F, P],
+    "ospo_flash_attn_bwd": [P, I, I, I, I, P, I, P, I, P, P, P, P, I, I, I, I, I, F, P],
+    "ospo_assemble_inputs": [P, I, I, P, P, I, I, P, P],
+    "ospo_gen_aligner_in": [P, I, P, I, P, P, I, P, P],
+    "ospo_gather_rows": [P, I, I, I, I, I, I, P, P],
+    "ospo_scatter_rows": [P, I, I, I, I, I, P, I, I, P],
+    "ospo_gelu_fwd": [P, P, L, P],
+    "ospo_gelu_bwd": [P, P, P, L, P],
+    "ospo_logprob_fwd": [P, I, P, I, I, P, P, P, P],
+    "ospo_logprob_bwd": [P, I, P, P, I, I, P, P, P],
+    "ospo_simpo_fwd": [P, I, F, F, F, I, P, P, P, P],
+    "ospo_simpo_bwd": [P, I, F, F, F, I, P, P, P],
+    "ospo_lora_pack": [P, P, I, I, I, I, I, P, P, P, P],
+    "ospo_sumsq": [P, L, P, P],
+    "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],
+}
+
+_lib = None
+
+
+class OspoError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the library once; raise loudly when it is absent (no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OspoError(f"libospo_hip.so not found at {LIB_PATH}: build it with "
+                            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, argt in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.argtypes = argt
+            fn.restype = c_int
+        h.ospo_strerror.argtypes = [c_int]
+        h.ospo_strerror.restype = ctypes.c_char_p
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(SIGNATURES) + ["ospo_strerror"]
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().ospo_strerror(rc).decode()
+        if rc in (1, 2, 5):
+            raise ValueError(f"{name}: {msg} (status {rc})")
+        raise OspoError(f"{name}: {msg} (status {rc})")

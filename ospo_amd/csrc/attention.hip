@@ -1,0 +1,426 @@
+// Causal flash attention (forward + backward) for the Janus-Pro decoder on gfx950.
+// Replaces HF 4.38.2 LlamaAttention eager path (QK^T/sqrt(d), causal mask, fp32
+// softmax, PV) reached from ospo/wrapper/train.py:352 -- no [T,T] matrix is
+// ever materialised.
+//
+// Forward: workgroup = 4 waves = 64 query rows of one (sequence, head); each
+// wave owns 16 query rows.  S^T = K.Q^T is computed with the KEY on the MFMA
+// row and the QUERY on the lane, so the online softmax of one query row is
+// lane-local (+2 shuffles across the 4 lane groups), and the P^T accumulator
+// feeds P.V directly as the B operand (k order permuted identically on both
+// sides).  V^T fragments come from ds_read_b64_tr_b16 (hardware transpose).
+//
+// Backward: workgroup = 4 waves = 64 keys; each wave owns 16 keys, keeps dK^T
+// and dV^T of them in registers and sweeps the query tiles at/after its block.
+// dQ is summed across key blocks with fp32 atomics (dq_acc workspace).
+//
+// LDS images are [row][128 x bf16] (256-B rows) with 16-B chunk swizzle
+// chunk ^ 2*(row & 7): conflict-free for both the ds_read_b128 row reads and
+// the ds_read_b64_tr_b16 column reads (CDNA4 LDS banking, 64 x 4 B banks).
+#include "common.h"
+
+namespace {
+
+constexpr int HD = 128;     // head dim
+constexpr int QB = 64;      // query rows per workgroup (fwd) / per tile (bwd)
+constexpr int KB = 64;      // keys per tile (fwd) / per workgroup (bwd)
+constexpr int ROWB = HD * 2;
+constexpr int TILE_BYTES = 64 * ROWB;  // 16 KiB
+
+__device__ __forceinline__ int aswz(int row) { return (row & 7) << 1; }
+__device__ __forceinline__ int aoff(int row, int chunk) { return row * ROWB + ((chunk ^ aswz(row)) << 4); }
+
+__device__ __forceinline__ void glds16(const void* gsrc, char* lds_dst_uniform) {
+  __builtin_amdgcn_global_load_lds(gsrc, (LDS_AS void*)lds_dst_uniform, 16, 0, 0);
+}
+
+// Stage 64 rows x 128 bf16 (rows row0.., clamped to [0, row_lim)) of a strided
+// buffer into an LDS image.  4 waves x 4 pieces of 1 KiB (4 rows each).
+__device__ __forceinline__ void stage64(const bf16* base, int ld, int row0, int row_lim, int col0, char* lds,
+                                        int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = wave * 4 + i;
+    const int row = p * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ aswz(row);
+    int gr = row0 + row;
+    gr = gr < row_lim ? gr : row_lim - 1;
+    glds16(base + (long)gr * ld + col0 + ch * 8, lds + p * 1024);
+  }
+}
+
+// 16x32 fragment, row read: rows r0+(lane&15), k = 32*s + 8*(lane>>4) .. +7
+__device__ __forceinline__ bf16x8 frag_row(const char* lds, int r0, int s, int lane) {
+  const int r = r0 + (lane & 15);
+  return *reinterpret_cast<const bf16x8*>(lds + aoff(r, 4 * s + (lane >> 4)));
+}
+
+// 16x32 fragment, transposed read for an operand whose k runs along the image
+// ROWS in the permuted accumulator order: element j<4 <- row kbase+4g+j,
+// j>=4 <- row kbase+16+4g+(j-4); the 16 fragment rows are image columns c0..c0+15.
+__device__ __forceinline__ bf16x8 frag_tr_perm(const char* lds, int kbase, int c0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int r1 = kbase + 4 * g + q;
+  const int r2 = r1 + 16;
+  const int x = (c0 >> 3) + (p >> 1);
+  const int h = (p & 1) << 3;
+  i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(lds + r1 * ROWB + ((x ^ aswz(r1)) << 4) + h));
+  i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(lds + r2 * ROWB + ((x ^ aswz(r2)) << 4) + h));
+  i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Same, natural k order (element j <- row kbase + 8g + j): for the dQ = dS.K product.
+__device__ __forceinline__ bf16x8 frag_tr_nat(const char* lds, int kbase, int c0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int r1 = kbase + 8 * g + q;
+  const int r2 = r1 + 4;
+  const int x = (c0 >> 3) + (p >> 1);
+  const int h = (p & 1) << 3;
+  i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(lds + r1 * ROWB + ((x ^ aswz(r1)) << 4) + h));
+  i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(lds + r2 * ROWB + ((x ^ aswz(r2)) << 4) + h));
+  i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 pack_perm(const f32x4& a, const f32x4& b) {
+  bf16x8 v;
+  v[0] = f2bf(a[0]); v[1] = f2bf(a[1]); v[2] = f2bf(a[2]); v[3] = f2bf(a[3]);
+  v[4] = f2bf(b[0]); v[5] = f2bf(b[1]); v[6] = f2bf(b[2]); v[7] = f2bf(b[3]);
+  return v;
+}
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+// ============================================================== forward ====
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
+                                                       bf16* __restrict__ out, int ldo, float* __restrict__ lse,
+                                                       int T, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
+  const int g = lane >> 4, l16 = lane & 15;
+  const long rowbase = (long)s * T;
+  const int rows_lim_seq = T;  // clamp inside the sequence
+
+  // this lane's query row
+  const int qrow = qb * QB + wave * 16 + l16;
+  const int qr_c = qrow < T ? qrow : T - 1;
+  bf16x8 qf[4];
+  {
+    const bf16* qp = qkv + (rowbase + qr_c) * ldq + qc + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) qf[d] = *reinterpret_cast<const bf16x8*>(qp + 32 * d + 8 * g);
+  }
+
+  f32x4 o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f, l_run = 0.f;
+
+  const int n_kv = qb + 1;  // causal: key tiles 0..qb
+  const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
+  const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
+
+  stage64(kbase, ldq, 0, rows_lim_seq, 0, smem, wave, lane);
+  stage64(vbase, ldq, 0, rows_lim_seq, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < n_kv; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < n_kv) {
+      char* nb = smem + (buf ^ 1) * 2 * TILE_BYTES;
+      stage64(kbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nb, wave, lane);
+      stage64(vbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nb + TILE_BYTES, wave, lane);
+    }
+    const char* Ks = smem + buf * 2 * TILE_BYTES;
+    const char* Vs = Ks + TILE_BYTES;
+
+    // S^T[key][q] for 4 key sub-tiles of 16
+    f32x4 st[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) st[t] = MFMA(frag_row(Ks, 16 * t, d, lane), qf[d], st[t]);
+    }
+    // scale + mask, tile max
+    const bool diag = (kt == qb) || ((kt + 1) * KB > T);
+    float tmax = -1e30f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = st[t][j] * scale;
+        if (diag) {
+          const int key = kt * KB + 16 * t + 4 * g + j;
+          if (key > qrow || key >= T) v = -1e30f;
+        }
+        st[t][j] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = __expf(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = (st[t][j] <= -1e29f) ? 0.f : __expf(st[t][j] - m_new);
+        st[t][j] = p;
+        psum += p;
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] *= alpha;
+
+    // O^T[d][q] += V^T[d][key] . P^T[key][q]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8 pb = pack_perm(st[2 * u], st[2 * u + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[dt] = MFMA(frag_tr_perm(Vs, 32 * u, 16 * dt, lane), pb, o[dt]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (qrow < T) {
+    const float inv = 1.f / l_run;
+    bf16* op = out + (rowbase + qrow) * ldo + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      uint2 pk;
+      pk.x = pack2(o[dt][0] * inv, o[dt][1] * inv);
+      pk.y = pack2(o[dt][2] * inv, o[dt][3] * inv);
+      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = pk;
+    }
+    if (g == 0) lse[((long)s * H + h) * T + qrow] = m_run + __logf(l_run);
+  }
+}
+
+// ============================================================ backward =====
+// delta[s,h,t] = sum_d dO[t, h*HD + d] * O[t, h*HD + d]
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict__ o, int ldo,
+                                                         const bf16* __restrict__ dout, int ldd,
+                                                         float* __restrict__ delta, int S, int T, int H) {
+  const int lane = threadIdx.x & 63;
+  const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per (row, head)
+  if (item >= (long)S * T * H) return;
+  const int h = item % H;
+  const long row = item / H;
+  const int s = row / T, t = row % T;
+  const bf16* op = o + row * ldo + h * HD;
+  const bf16* dp = dout + row * ldd + h * HD;
+  const unsigned ov = reinterpret_cast<const unsigned*>(op)[lane];
+  const unsigned dv = reinterpret_cast<const unsigned*>(dp)[lane];
+  float acc = bits2f(ov & 0xffff) * bits2f(dv & 0xffff) + bits2f(ov >> 16) * bits2f(dv >> 16);
+  acc = wave_sum(acc);
+  if (lane == 0) delta[((long)s * H + h) * T + t] = acc;
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
+                                                       const bf16* __restrict__ dout, int ldd,
+                                                       const float* __restrict__ lse, const float* __restrict__ delta,
+                                                       float* __restrict__ dq_acc, bf16* __restrict__ dqkv, int ldg,
+                                                       int T, int H, float scale) {
+  // LDS: K image | Q image | dO image | dS image [64 q][64 key] | lse[64] | delta[64]
+  constexpr int DS_PITCH = 64 * 2 + 16;
+  __shared__ __attribute__((aligned(16))) char smem[3 * TILE_BYTES + 64 * DS_PITCH + 2 * 64 * 4];
+  char* Ks = smem;
+  char* Qs = smem + TILE_BYTES;
+  char* Os = smem + 2 * TILE_BYTES;
+  char* Ss = smem + 3 * TILE_BYTES;
+  float* Ls = reinterpret_cast<float*>(Ss + 64 * DS_PITCH);
+  float* Dl = Ls + 64;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
+  const int g = lane >> 4, l16 = lane & 15;
+  const long rowbase = (long)s * T;
+  const int nq = (T + QB - 1) / QB;
+
+  // this wave's 16 keys; lane l16 owns key kb*64 + wave*16 + l16 (for B fragments)
+  const int key_l = kb * KB + wave * 16 + l16;
+  const int key_c = key_l < T ? key_l : T - 1;
+  bf16x8 kf[4], vf[4];
+  {
+    const bf16* kp = qkv + (rowbase + key_c) * ldq + kc + h * HD;
+    const bf16* vp = qkv + (rowbase + key_c) * ldq + vc + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      kf[d] = *reinterpret_cast<const bf16x8*>(kp + 32 * d + 8 * g);
+      vf[d] = *reinterpret_cast<const bf16x8*>(vp + 32 * d + 8 * g);
+    }
+  }
+  stage64(qkv + rowbase * ldq + kc + h * HD, ldq, kb * KB, T, 0, Ks, wave, lane);
+
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { dk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+  const bf16* qbase = qkv + rowbase * ldq + qc + h * HD;
+  const bf16* obase = dout + rowbase * ldd + h * HD;
+  const float* lse_sh = lse + ((long)s * H + h) * T;
+  const float* del_sh = delta + ((long)s * H + h) * T;
+
+  for (int qt = kb; qt < nq; ++qt) {
+    __syncthreads();  // previous tile's LDS reads done
+    stage64(qbase, ldq, qt * QB, T, 0, Qs, wave, lane);
+    stage64(obase, ldd, qt * QB, T, 0, Os, wave, lane);
+    if (threadIdx.x < 64) {
+      const int q = qt * QB + threadIdx.x;
+      Ls[threadIdx.x] = q < T ? lse_sh[q] : 0.f;
+      Dl[threadIdx.x] = q < T ? del_sh[q] : 0.f;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // S[q][key] and dP[q][key] for 4 q sub-tiles; lane: key = l16, q = 16a + 4g + j
+    f32x4 sv[4], dp[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      sv[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        sv[a] = MFMA(frag_row(Qs, 16 * a, d, lane), kf[d], sv[a]);
+        dp[a] = MFMA(frag_row(Os, 16 * a, d, lane), vf[d], dp[a]);
+      }
+    }
+    // P and dS (fp32), masks
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ql = 16 * a + 4 * g + j;
+        const int q = qt * QB + ql;
+        float p = __expf(sv[a][j] * scale - Ls[ql]);
+        if (q >= T || key_l > q || key_l >= T) p = 0.f;
+        sv[a][j] = p;
+        dp[a][j] = p * (dp[a][j] - Dl[ql]);
+      }
+    // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8 pb = pack_perm(sv[2 * u], sv[2 * u + 1]);
+      const bf16x8 sb = pack_perm(dp[2 * u], dp[2 * u + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        dv[dt] = MFMA(frag_tr_perm(Os, 32 * u, 16 * dt, lane), pb, dv[dt]);
+        dk[dt] = MFMA(frag_tr_perm(Qs, 32 * u, 16 * dt, lane), sb, dk[dt]);
+      }
+    }
+    // dS (bf16, scaled) -> LDS image [q][key] for the dQ product
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ql = 16 * a + 4 * g + j;
+        *reinterpret_cast<bf16*>(Ss + ql * DS_PITCH + (wave * 16 + l16) * 2) = f2bf(dp[a][j] * scale);
+      }
+    __syncthreads();
+    // dQ[q][d] (this wave: 16 q rows) = dS[q][key(64)] . K[key][d]
+    {
+      const int qr0 = wave * 16;
+      f32x4 dq[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ss + (qr0 + l16) * DS_PITCH + (32 * u + 8 * g) * 2);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) dq[dt] = MFMA(af, frag_tr_nat(Ks, 32 * u, 16 * dt, lane), dq[dt]);
+      }
+      // lane: col d = 16dt + l16, rows q = qr0 + 4g + j
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = qt * QB + qr0 + 4 * g + j;
+        if (q >= T) continue;
+        float* dst = dq_acc + (rowbase + q) * (long)(H * HD) + h * HD + l16;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) atomicAdd(dst + 16 * dt, dq[dt][j]);
+      }
+    }
+  }
+
+  // write dK (= scale * dS^T Q), dV: lane holds [d = 16dt + 4g + j][key = l16]
+  if (key_l < T) {
+    bf16* kp = dqkv + (rowbase + key_l) * ldg + kc + h * HD;
+    bf16* vp = dqkv + (rowbase + key_l) * ldg + vc + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      uint2 a, b;
+      a.x = pack2(dk[dt][0] * scale, dk[dt][1] * scale); a.y = pack2(dk[dt][2] * scale, dk[dt][3] * scale);
+      b.x = pack2(dv[dt][0], dv[dt][1]); b.y = pack2(dv[dt][2], dv[dt][3]);
+      *reinterpret_cast<uint2*>(kp + 16 * dt + 4 * g) = a;
+      *reinterpret_cast<uint2*>(vp + 16 * dt + 4 * g) = b;
+    }
+  }
+}
+
+// dq (fp32 workspace) -> bf16 q columns of dqkv
+__global__ void dq_store_kernel(const float* __restrict__ dq_acc, bf16* __restrict__ dqkv, int ldg, int qc,
+                                long rows, int W) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= rows * W) return;
+  const long r = i / W;
+  const int c = i % W;
+  const f32x4 v = *reinterpret_cast<const f32x4*>(dq_acc + i);
+  uint2 pk;
+  pk.x = pack2(v[0], v[1]);
+  pk.y = pack2(v[2], v[3]);
+  *reinterpret_cast<uint2*>(dqkv + r * ldg + qc + c) = pk;
+}
+
+}  // namespace
+
+extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
+                                   int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
+                                   hipStream_t stream) {
+  if (!qkv || !o || !lse) return OSPO_ERR_ARG;
+  if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
+  if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || q_col % 8 || k_col % 8 || v_col % 8)
+    return OSPO_ERR_SHAPE;
+  if (!aligned16(qkv) || !aligned16(o)) return OSPO_ERR_ALIGN;
+  dim3 grid((T + QB - 1) / QB, n_heads, S);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+                     (bf16*)o, ld_o, lse, T, n_heads, scale);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, const void* o,
+                                   int ld_o, const void* dout, int ld_do, const float* lse, float* delta_ws,
+                                   float* dq_acc_ws, void* dqkv, int ld_dqkv, int S, int T, int n_heads,
+                                   int head_dim, float scale, hipStream_t stream) {
+  if (!qkv || !o || !dout || !lse || !delta_ws || !dq_acc_ws || !dqkv) return OSPO_ERR_ARG;
+  if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
+  if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || ld_do % 8 || ld_dqkv % 8) return OSPO_ERR_SHAPE;
+  if (!aligned16(qkv) || !aligned16(o) || !aligned16(dout) || !aligned16(dqkv) || !aligned16(dq_acc_ws))
+    return OSPO_ERR_ALIGN;
+  const long rows = (long)S * T;
+  const int W = n_heads * HD;
+  if (hipMemsetAsync(dq_acc_ws, 0, rows * W * sizeof(float), stream) != hipSuccess) return OSPO_ERR_HIP;
+  const long items = rows * n_heads;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((items + 3) / 4), dim3(256), 0, stream, (const bf16*)o, ld_o,
+                     (const bf16*)dout, ld_do, delta_ws, S, T, n_heads);
+  OSPO_CHECK_LAUNCH();
+  dim3 grid((T + KB - 1) / KB, n_heads, S);
+  hipLaunchKernelGGL(attn_bwd_kernel, grid, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+                     (const bf16*)dout, ld_do, lse, delta_ws, dq_acc_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale);
+  OSPO_CHECK_LAUNCH();
+  const long n4 = rows * W / 4;
+  hipLaunchKernelGGL(dq_store_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream, dq_acc_ws, (bf16*)dqkv,
+                     ld_dqkv, q_col, rows, W);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}

@@ -1,0 +1,334 @@
+// MFMA bf16 GEMM family for gfx950 (CDNA4): the Linear layers of the Janus-Pro
+// decoder with the peft LoRA update fused as a K-extension, and the fp32-atomic
+// skinny / transposed GEMMs that produce the LoRA activations and gradients.
+//
+// Design (MI355X-first, not a translation of any CUDA tiling):
+//  * 64-lane waves, v_mfma_f32_16x16x32_bf16, fp32 accumulators in registers.
+//  * Operand tiles stream HBM -> LDS with global_load_lds_dwordx4 (LDS-DMA, no
+//    VGPR round trip), double buffered; BK = 64.
+//  * M/N-major tiles ([rows][64 k], 128-B rows) are XOR-swizzled per 16-B chunk
+//    (chunk ^ row&7) on the global SOURCE address so the lane-linear DMA image
+//    reads back conflict-free with ds_read_b128.
+//  * K-major tiles ([64 k][cols]) are read with ds_read_b64_tr_b16 (hardware
+//    transpose) so dA = g^T x and dB = dy^T u need no transpose pass; their
+//    chunk swizzle makes the transposed reads conflict-free.
+//  * bf16 epilogue stages the tile in LDS and writes 16-B coalesced rows,
+//    fusing alpha, bias and the bf16 residual add of the decoder layer.
+//  * The LoRA update x.A^T.B^T*s is one more K segment (A2 = s*u, B2 = packed
+//    block-diagonal lora_B), so the adapter costs Rp/K extra MFMAs, no pass.
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+// ---------------------------------------------------------------- swizzles
+__device__ __forceinline__ int mmaj_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+template <int ROWB>
+__device__ __forceinline__ int kmaj_swz(int row) {
+  if constexpr (ROWB == 128)
+    return (row & 2) | ((row & 8) >> 1);
+  else
+    return ((row & 3) << 1) | (row & 8);
+}
+
+__device__ __forceinline__ void glds16(const void* gsrc, char* lds_dst_uniform) {
+  __builtin_amdgcn_global_load_lds(gsrc, (LDS_AS void*)lds_dst_uniform, 16, 0, 0);
+}
+
+// Stage one BK-deep tile of an operand (TM rows of the m/n dim) into LDS.
+// Work split: 1-KiB pieces, wave w takes pieces w, w+NW, ...
+template <int TM, bool KMAJ, int NW>
+__device__ __forceinline__ void stage_tile(const bf16* __restrict__ base, int ld, int row0, int rows_total,
+                                           int k0, char* lds, int wave, int lane) {
+  constexpr int PIECES = TM * BK * 2 / 1024;
+  if constexpr (!KMAJ) {
+#pragma unroll
+    for (int p = wave; p < PIECES; p += NW) {
+      const int row = p * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (row & 7);
+      int grow = row0 + row;
+      grow = grow < rows_total ? grow : rows_total - 1;
+      glds16(base + (long)grow * ld + k0 + c * 8, lds + p * 1024);
+    }
+  } else {
+    constexpr int LPR = TM / 8;     // lanes (16-B chunks) per k-row
+    constexpr int RPP = 64 / LPR;   // k-rows per piece
+    constexpr int ROWB = TM * 2;
+#pragma unroll
+    for (int p = wave; p < PIECES; p += NW) {
+      const int row = p * RPP + lane / LPR;
+      const int x = (lane % LPR) ^ kmaj_swz<ROWB>(row);
+      glds16(base + (long)(k0 + row) * ld + row0 + x * 8, lds + p * 1024);
+    }
+  }
+}
+
+// Read the MFMA fragment (16 rows of the m/n dim x 32 k) for k-substep s.
+template <int TM, bool KMAJ>
+__device__ __forceinline__ bf16x8 read_frag(const char* lds, int r0, int s, int lane) {
+  if constexpr (!KMAJ) {
+    const int r = r0 + (lane & 15);
+    const int c = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(lds + mmaj_off(r, c));
+  } else {
+    constexpr int ROWB = TM * 2;
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int row = 32 * s + 8 * g + q;
+    const int x = (r0 >> 3) + (p >> 1);
+    const int o1 = row * ROWB + ((x ^ kmaj_swz<ROWB>(row)) << 4) + ((p & 1) << 3);
+    const int o2 = (row + 4) * ROWB + ((x ^ kmaj_swz<ROWB>(row + 4)) << 4) + ((p & 1) << 3);
+    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(lds + o1));
+    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(lds + o2));
+    i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+enum { EPI_BF16 = 0, EPI_F32_ATOMIC = 1 };
+
+struct GemmArgs {
+  const bf16* A; const bf16* B; const bf16* A2; const bf16* B2;
+  int lda, ldb, lda2, ldb2;
+  int M, N, K, K2;
+  float alpha;
+  const bf16* bias;
+  const bf16* res; int ldr;
+  void* C; int ldc;
+  int k_splits;
+  int diag_nblk, diag_r;
+};
+
+template <int WM, int WN, int FM, int FN, bool AK, bool BKM, int EPI>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * FM * 16;
+  constexpr int BN = WN * FN * 16;
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int CPITCH = BN * 2 + 16;
+  constexpr int CBYTES = (EPI == EPI_BF16) ? BM * CPITCH : 0;
+  constexpr int LDS_BYTES = (2 * STAGE > CBYTES) ? 2 * STAGE : CBYTES;
+  constexpr bool SWAP = (EPI == EPI_BF16);
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  // tile coordinates (blockIdx.x over N tiles, y over M tiles)
+  const int n0 = blockIdx.x * BN;
+  const int m0 = blockIdx.y * BM;
+
+  const int nt1 = args.K / BK;
+  const int nt2 = args.K2 / BK;
+  const int nt = nt1 + nt2;
+  int t_begin = 0, t_end = nt;
+  if (args.k_splits > 1) {
+    t_begin = (int)((long)nt * blockIdx.z / args.k_splits);
+    t_end = (int)((long)nt * (blockIdx.z + 1) / args.k_splits);
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int t, int buf) {
+    char* la = smem + buf * STAGE;
+    char* lb = la + A_BYTES;
+    if (t < nt1) {
+      stage_tile<BM, AK, NW>(args.A, args.lda, m0, args.M, t * BK, la, wave, lane);
+      stage_tile<BN, BKM, NW>(args.B, args.ldb, n0, args.N, t * BK, lb, wave, lane);
+    } else {
+      const int k0 = (t - nt1) * BK;
+      stage_tile<BM, false, NW>(args.A2, args.lda2, m0, args.M, k0, la, wave, lane);
+      stage_tile<BN, false, NW>(args.B2, args.ldb2, n0, args.N, k0, lb, wave, lane);
+    }
+  };
+
+  if (t_begin < t_end) {
+    stage(t_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+      const int buf = (t - t_begin) & 1;
+      if (t + 1 < t_end) stage(t + 1, buf ^ 1);
+      const char* la = smem + buf * STAGE;
+      const char* lb = la + A_BYTES;
+      const bool ext = t >= nt1;  // the K-extension tiles are always M/N-major
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[FM], bfr[FN];
+        if (AK && !ext) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AK>(la, wm * FM * 16 + i * 16, s, lane);
+        } else {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, false>(la, wm * FM * 16 + i * 16, s, lane);
+        }
+        if (BKM && !ext) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BKM>(lb, wn * FN * 16 + j * 16, s, lane);
+        } else {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, false>(lb, wn * FN * 16 + j * 16, s, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            if constexpr (SWAP)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  const int g = lane >> 4, l16 = lane & 15;
+  if constexpr (EPI == EPI_BF16) {
+    // registers -> LDS tile [BM][BN] (bf16, rounded after alpha/bias)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int nl = wn * FN * 16 + j * 16 + 4 * g;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (args.bias) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b4[q] = bf2f(args.bias[n0 + nl + q]);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ml = wm * FM * 16 + i * 16 + l16;
+        const f32x4 v = acc[i][j];
+        uint2 pk;
+        pk.x = pack2(v[0] * args.alpha + b4[0], v[1] * args.alpha + b4[1]);
+        pk.y = pack2(v[2] * args.alpha + b4[2], v[3] * args.alpha + b4[3]);
+        *reinterpret_cast<uint2*>(smem + ml * CPITCH + nl * 2) = pk;
+      }
+    }
+    __syncthreads();
+    constexpr int CPR = BN / 8;  // 16-B chunks per row
+    bf16* C = reinterpret_cast<bf16*>(args.C);
+    for (int c = threadIdx.x; c < BM * CPR; c += NW * 64) {
+      const int r = c / CPR, cc = c % CPR;
+      const int m = m0 + r;
+      if (m >= args.M) continue;
+      u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * CPITCH + cc * 16);
+      if (args.res) {
+        const u32x4 rv = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + cc * 8);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = bits2f(v[q] & 0xffff) + bits2f(rv[q] & 0xffff);
+          const float hi = bits2f(v[q] >> 16) + bits2f(rv[q] >> 16);
+          v[q] = pack2(lo, hi);
+        }
+      }
+      *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8) = v;
+    }
+  } else {
+    float* C = reinterpret_cast<float*>(args.C);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * FN * 16 + j * 16 + l16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = m0 + wm * FM * 16 + i * 16 + 4 * g + q;
+          if (m >= args.M) continue;
+          const float v = acc[i][j][q] * args.alpha;
+          if (args.diag_nblk > 0) {
+            if (n / args.diag_r != m / args.diag_nblk) continue;
+            atomicAdd(C + (long)m * args.diag_r + (n % args.diag_r), v);
+          } else {
+            atomicAdd(C + (long)m * args.ldc + n, v);
+          }
+        }
+      }
+  }
+}
+
+template <int WM, int WN, int FM, int FN, bool AK, bool BKM, int EPI>
+int launch(const GemmArgs& a, hipStream_t s) {
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  if (a.N % BN) return OSPO_ERR_SHAPE;
+  // K-major A: the tile loads columns up to roundup(M, BM) (must exist), stores are predicated on M
+  if (AK && a.lda < ((a.M + BM - 1) / BM) * BM) return OSPO_ERR_SHAPE;
+  dim3 grid(a.N / BN, (a.M + BM - 1) / BM, a.k_splits > 1 ? a.k_splits : 1);
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AK, BKM, EPI>), grid, dim3(WM * WN * 64), 0, s, a);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+// Pick the bf16 NT tile: the one whose (waves of 256 CUs) x (rows per tile) is
+// smallest -- tile-count quantisation dominates at M ~ 5k (SURVEY §8d shapes).
+int pick_nt_tile(int M, int N) {
+  if (N % 256) return 64;
+  const int cus = 256;
+  long best = -1;
+  int pick = 256;
+  for (int bm : {256, 160}) {
+    const long tiles = (long)((M + bm - 1) / bm) * (N / 256);
+    const long waves = (tiles + cus - 1) / cus;
+    const long cost = waves * bm;
+    if (best < 0 || cost < best) { best = cost; pick = bm; }
+  }
+  return pick;
+}
+
+}  // namespace
+
+extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
+                                 const void* A2, int lda2, const void* B2, int ldb2, int K2, float alpha,
+                                 const void* bias, const void* residual, int ldr, void* C, int ldc,
+                                 hipStream_t stream) {
+  if (!A || !B || !C) return OSPO_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK || K2 < 0 || K2 % BK || N % 64) return OSPO_ERR_SHAPE;
+  if (K2 > 0 && (!A2 || !B2)) return OSPO_ERR_ARG;
+  if (lda < K || ldb < K || ldc < N || (lda % 8) || (ldb % 8) || (ldc % 8)) return OSPO_ERR_SHAPE;
+  if (K2 > 0 && (lda2 < K2 || ldb2 < K2 || lda2 % 8 || ldb2 % 8)) return OSPO_ERR_SHAPE;
+  if (residual && (ldr < N || ldr % 8)) return OSPO_ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(B) || !aligned16(C) || (residual && !aligned16(residual)) ||
+      (K2 > 0 && (!aligned16(A2) || !aligned16(B2))))
+    return OSPO_ERR_ALIGN;
+  GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
+             M, N, K, K2, alpha, (const bf16*)bias, (const bf16*)residual, ldr, C, ldc, 1, 0, 0};
+  switch (pick_nt_tile(M, N)) {
+    case 256: return launch<2, 4, 8, 4, false, false, EPI_BF16>(a, stream);
+    case 160: return launch<2, 4, 5, 4, false, false, EPI_BF16>(a, stream);
+    default: return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
+  }
+}
+
+extern "C" int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
+                                int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
+                                int diag_nblk, int diag_r, hipStream_t stream) {
+  if (!A || !B || !C) return OSPO_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK || N % 64) return OSPO_ERR_SHAPE;
+  if (k_splits < 1) k_splits = 1;
+  if (k_splits > K / BK) k_splits = K / BK;
+  if (a_kmajor ? (lda < ((M + 63) / 64) * 64) : (lda < K)) return OSPO_ERR_SHAPE;
+  if (b_kmajor ? (ldb < N) : (ldb < K)) return OSPO_ERR_SHAPE;
+  if ((lda % 8) || (ldb % 8)) return OSPO_ERR_SHAPE;
+  if (diag_nblk > 0 && diag_r <= 0) return OSPO_ERR_ARG;
+  if (diag_nblk <= 0 && ldc < N) return OSPO_ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(B)) return OSPO_ERR_ALIGN;
+  GemmArgs a{(const bf16*)A, (const bf16*)B, nullptr, nullptr, lda, ldb, 0, 0, M, N, K, 0, alpha,
+             nullptr, nullptr, 0, C, ldc, k_splits, diag_nblk, diag_r};
+  const bool wideN = (N % 256 == 0);
+  const bool tallM = a_kmajor ? (M % 256 == 0 && lda >= M) : (M >= 1024);
+  if (!a_kmajor && !b_kmajor) return launch<2, 2, 2, 2, false, false, EPI_F32_ATOMIC>(a, stream);
+  if (!a_kmajor && b_kmajor) return launch<2, 2, 2, 2, false, true, EPI_F32_ATOMIC>(a, stream);
+  if (a_kmajor && !b_kmajor) return OSPO_ERR_UNSUPPORTED;
+  // both K-major (LoRA weight gradients)
+  if (wideN && !tallM) return launch<2, 4, 2, 4, true, true, EPI_F32_ATOMIC>(a, stream);   // 64 x 256
+  if (tallM && !wideN) return launch<4, 2, 4, 2, true, true, EPI_F32_ATOMIC>(a, stream);   // 256 x 64
+  return launch<2, 2, 2, 2, true, true, EPI_F32_ATOMIC>(a, stream);
+}

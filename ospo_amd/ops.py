@@ -1,0 +1,219 @@
+"""Torch-tensor front end of the HIP kernels (device memory + stream plumbing only).
+
+Every function enqueues on ``torch.cuda.current_stream()`` and calls the C ABI
+in ``_lib``; there is no eager-PyTorch fallback on this path.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._lib import call
+
+BF16 = torch.bfloat16
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _s() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _chk(t: torch.Tensor, dtype, name: str):
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor")
+
+
+def _ld(t: torch.Tensor) -> int:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("expected a row-major 2-D view")
+    return t.stride(0)
+
+
+# ------------------------------------------------------------------ GEMM
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0,
+            bias=None, residual=None) -> torch.Tensor:
+    """out[M,N] = bf16(alpha*(a.b^T + a2.b2^T) + bias) [+ residual]  (nn.Linear layout b=[N,K])."""
+    for t, n in ((a, "a"), (b, "b"), (out, "out")):
+        _chk(t, BF16, n)
+    M, K = a.shape
+    N = b.shape[0]
+    if b.shape[1] != K or out.shape[0] != M or out.shape[1] != N:
+        raise ValueError(f"gemm_nt shape mismatch a{tuple(a.shape)} b{tuple(b.shape)} out{tuple(out.shape)}")
+    K2 = 0
+    if a2 is not None:
+        K2 = a2.shape[1]
+        if a2.shape[0] != M or b2.shape != (N, K2):
+            raise ValueError("gemm_nt K-extension shape mismatch")
+    call("ospo_gemm_nt_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K,
+         _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2, float(alpha),
+         _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), _s())
+    return out
+
+
+def gemm_f32acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a_kmajor: bool, b_kmajor: bool,
+                k_splits: int = 1, alpha: float = 1.0, diag: Optional[tuple] = None) -> torch.Tensor:
+    """out[M,N] (fp32) += alpha * op(a) . op(b)^T.
+    a_kmajor: a is [K, M] else [M, K];  b_kmajor: b is [K, N] else [N, K].
+    diag=(nblk, r): block-diagonal scatter (see include/ospo_hip.h)."""
+    _chk(a, BF16, "a")
+    _chk(b, BF16, "b")
+    _chk(out, torch.float32, "out")
+    K, M = a.shape if a_kmajor else a.shape[::-1]
+    Kb, N = b.shape if b_kmajor else b.shape[::-1]
+    if K != Kb:
+        raise ValueError(f"gemm_f32acc K mismatch {K} vs {Kb}")
+    nblk, r = diag if diag else (0, 0)
+    ldc = _ld(out) if not diag else 0
+    call("ospo_gemm_f32acc", _p(a), _ld(a), int(a_kmajor), _p(b), _ld(b), int(b_kmajor), M, N, K, int(k_splits),
+         float(alpha), _p(out), ldc, nblk, r, _s())
+    return out
+
+
+def f32_to_bf16(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    _chk(src, torch.float32, "src")
+    _chk(dst, BF16, "dst")
+    if src.numel() != dst.numel() or not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("f32_to_bf16: size/contiguity mismatch")
+    call("ospo_f32_to_bf16", _p(src), _p(dst), src.numel(), float(scale), _s())
+    return dst
+
+
+# ---------------------------------------------------------------- RMSNorm
+def rmsnorm_fwd(x, w, y, rstd, eps: float):
+    M, D = x.shape
+    call("ospo_rmsnorm_fwd", _p(x), _p(w), _p(y), _p(rstd), M, D, float(eps), _s())
+    return y
+
+
+def rmsnorm_bwd(dy, x, w, rstd, dx, dres=None):
+    M, D = x.shape
+    call("ospo_rmsnorm_bwd", _p(dy), _p(x), _p(w), _p(rstd), _p(dres), _p(dx), M, D, _s())
+    return dx
+
+
+# ------------------------------------------------------------------- RoPE
+def rope(qkv, q_col, k_col, S, T, n_heads, head_dim, cos_tab, sin_tab, backward=False):
+    call("ospo_rope_bwd" if backward else "ospo_rope_fwd", _p(qkv), _ld(qkv), q_col, k_col, S, T, n_heads,
+         head_dim, _p(cos_tab), _p(sin_tab), _s())
+    return qkv
+
+
+def rope_tables(T: int, head_dim: int, theta: float, device) -> tuple:
+    """HF LlamaRotaryEmbedding: fp32 inv_freq/outer product, cos/sin cast to bf16; first half only."""
+    inv_freq = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.int64).float() / head_dim))
+    freqs = torch.outer(torch.arange(T, dtype=torch.float32), inv_freq)
+    return (freqs.cos().to(BF16).contiguous().to(device), freqs.sin().to(BF16).contiguous().to(device))
+
+
+# ----------------------------------------------------------------- SwiGLU
+def swiglu_fwd(gu, h):
+    M, F2 = gu.shape
+    call("ospo_swiglu_fwd", _p(gu), _ld(gu), _p(h), _ld(h), M, F2 // 2, _s())
+    return h
+
+
+def swiglu_bwd(dh, gu, dgu):
+    M, F2 = gu.shape
+    call("ospo_swiglu_bwd", _p(dh), _ld(dh), _p(gu), _ld(gu), _p(dgu), _ld(dgu), M, F2 // 2, _s())
+    return dgu
+
+
+# -------------------------------------------------------------- attention
+def flash_attn_fwd(qkv, q_col, k_col, v_col, o, lse, S, T, n_heads, head_dim, scale):
+    call("ospo_flash_attn_fwd", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(lse), S, T, n_heads,
+         head_dim, float(scale), _s())
+    return o, lse
+
+
+def flash_attn_bwd(qkv, q_col, k_col, v_col, o, dout, lse, delta_ws, dq_ws, dqkv, S, T, n_heads, head_dim, scale):
+    call("ospo_flash_attn_bwd", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(dout), _ld(dout),
+         _p(lse), _p(delta_ws), _p(dq_ws), _p(dqkv), _ld(dqkv), S, T, n_heads, head_dim, float(scale), _s())
+    return dqkv
+
+
+# -------------------------------------------------------- embed / gather
+def assemble_inputs(text_ids, B, Lt, table, img_emb, N, D, x0):
+    call("ospo_assemble_inputs", _p(text_ids), B, Lt, _p(table), _p(img_emb), N, D, _p(x0), _s())
+    return x0
+
+
+def gen_aligner_in(ids, gen_embed, w1, b1, out):
+    R = ids.numel()
+    E = gen_embed.shape[1]
+    D = w1.shape[0]
+    call("ospo_gen_aligner_in", _p(ids), R, _p(gen_embed), E, _p(w1), _p(b1), D, _p(out), _s())
+    return out
+
+
+def gather_rows(src, S, T, t0, N, dst):
+    call("ospo_gather_rows", _p(src), _ld(src), S, T, t0, N, src.shape[1], _p(dst), _s())
+    return dst
+
+
+def scatter_rows(src, S, T, t0, N, dst):
+    call("ospo_scatter_rows", _p(src), S, T, t0, N, src.shape[1], _p(dst), _ld(dst), dst.shape[0], _s())
+    return dst
+
+
+def gelu_fwd(x, y):
+    call("ospo_gelu_fwd", _p(x), _p(y), x.numel(), _s())
+    return y
+
+
+def gelu_bwd(dy, x_pre, dx):
+    call("ospo_gelu_bwd", _p(dy), _p(x_pre), _p(dx), dy.numel(), _s())
+    return dx
+
+
+# ---------------------------------------------------------------- logprob
+def logprob_fwd(logits, labels, N, lse, tok, seq):
+    R, V = logits.shape
+    call("ospo_logprob_fwd", _p(logits), V, _p(labels), R, N, _p(lse), _p(tok), _p(seq), _s())
+    return seq
+
+
+def logprob_bwd(logits, labels, lse, N, g_seq, dlogits):
+    R, V = logits.shape
+    call("ospo_logprob_bwd", _p(logits), V, _p(labels), _p(lse), R, N, _p(g_seq), _p(dlogits), _s())
+    return dlogits
+
+
+# ------------------------------------------------------------------ SimPO
+LOSS_TYPES = {"sigmoid": 0, "hinge": 1}
+
+
+def loss_type_id(loss_type: str) -> int:
+    if loss_type not in LOSS_TYPES:
+        raise ValueError(f"Unknown loss type: {loss_type}. Should be one of ['sigmoid', 'hinge']")
+    return LOSS_TYPES[loss_type]
+
+
+def simpo_fwd(logps, B, beta, gbr, ls, loss_type, losses, mean, rewards):
+    call("ospo_simpo_fwd", _p(logps), B, float(beta), float(gbr), float(ls), loss_type_id(loss_type), _p(losses),
+         _p(mean), _p(rewards), _s())
+
+
+def simpo_bwd(logps, B, beta, gbr, ls, loss_type, g_loss, glogps):
+    call("ospo_simpo_bwd", _p(logps), B, float(beta), float(gbr), float(ls), loss_type_id(loss_type), _p(g_loss),
+         _p(glogps), _s())
+
+
+# ------------------------------------------------------------- LoRA pack
+def lora_pack(A_flat, B_flat, nmods, r, Kin, Nmod, Rp, Acat, AcatT, Bcat):
+    call("ospo_lora_pack", _p(A_flat), _p(B_flat), nmods, r, Kin, Nmod, Rp, _p(Acat), _p(AcatT), _p(Bcat), _s())
+
+
+# -------------------------------------------------------------- optimizer
+def sumsq(g, out):
+    call("ospo_sumsq", _p(g), g.numel(), _p(out), _s())
+
+
+def adamw_clip(p, g, m, v, lr, beta1, beta2, eps, wd, step, sumsq_buf, max_norm):
+    call("ospo_adamw_clip", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
+         float(eps), float(wd), int(step), _p(sumsq_buf), float(max_norm), _s())

@@ -1,0 +1,348 @@
+"""Per-kernel numerics on the MI355X: each HIP kernel (through the C ABI) against
+a plain PyTorch fp32 reference of the same op (or the oracle where it defines
+the op).  Integer-valued operands are used where the result must be exact."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import simpo_ref as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from ospo_amd import _lib
+    _lib.lib()
+    torch.manual_seed(0)
+
+
+def ops():
+    from ospo_amd import ops as _ops
+    return _ops
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rnd(*shape, s=1.0):
+    return (torch.randn(*shape, device=DEV) * s).to(torch.bfloat16)
+
+
+def ints(*shape, lo=-3, hi=4):
+    return torch.randint(lo, hi, shape, device=DEV).to(torch.bfloat16)
+
+
+def relerr(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+# ------------------------------------------------------------------ GEMM NT
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 256, 128), (4800, 512, 256), (160, 1024, 192),
+                                   (64, 64, 64), (100, 192, 128)])
+def test_gemm_nt_exact_integers(M, N, K):
+    a, b = ints(M, K), ints(N, K)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(a, b, out)
+    ref = a.float() @ b.float().T  # |ref| <= 9*K*... small ints, exactly representable
+    ref_bf = bf(ref).float()
+    assert torch.equal(out.float(), ref_bf), (out.float() - ref_bf).abs().max()
+
+
+def test_gemm_nt_asymmetric_identity():
+    """A = I-like selector with an asymmetric B catches a transposed C write."""
+    M = N = K = 256
+    a = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.arange(N * K, device=DEV).reshape(N, K).remainder(251).to(torch.bfloat16)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(a, b, out)
+    assert torch.equal(out, b.T.contiguous())
+
+
+@pytest.mark.parametrize("M,N,K,K2", [(600, 512, 256, 64), (4800, 1024, 512, 64), (777, 256, 128, 128)])
+def test_gemm_nt_lora_bias_residual(M, N, K, K2):
+    a, b = rnd(M, K), rnd(N, K, s=0.05)
+    a2, b2 = rnd(M, K2), rnd(N, K2, s=0.05)
+    bias, res = rnd(N), rnd(M, N)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(a, b, out, a2=a2, b2=b2, alpha=0.5, bias=bias, residual=res)
+    acc = 0.5 * (a.float() @ b.float().T + a2.float() @ b2.float().T) + bias.float()
+    ref = bf(bf(acc).float() + res.float()).float()
+    assert relerr(out.float(), ref) < 4e-3
+
+
+def test_gemm_nt_rejects_bad_shapes():
+    a, b = rnd(64, 96), rnd(64, 96)
+    out = torch.empty(64, 64, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        ops().gemm_nt(a, b, out)  # K % 64 != 0
+
+
+# --------------------------------------------------------------- GEMM f32acc
+@pytest.mark.parametrize("a_k,b_k,M,N,K,splits", [
+    (False, False, 4800, 64, 256, 4),    # u = x . A^T
+    (False, True, 600, 64, 512, 3),      # g = dy . B
+    (True, True, 64, 512, 640, 5),       # dA = g^T x
+    (True, True, 1024, 64, 640, 4),      # dB = dy^T u
+    (True, True, 128, 128, 256, 1),
+])
+def test_gemm_f32acc_layouts(a_k, b_k, M, N, K, splits):
+    A = ints(K, M) if a_k else ints(M, K)
+    B = ints(K, N) if b_k else ints(N, K)
+    Aop = A.float().T if a_k else A.float()
+    Bop = B.float().T if b_k else B.float()
+    out = torch.full((M, N), 0.5, device=DEV, dtype=torch.float32)
+    ops().gemm_f32acc(A, B, out, a_kmajor=a_k, b_kmajor=b_k, k_splits=splits, alpha=2.0)
+    ref = 0.5 + 2.0 * (Aop @ Bop.T)
+    assert torch.equal(out, ref), (out - ref).abs().max()
+
+
+def test_gemm_f32acc_blockdiag_scatter():
+    """dB of a packed q|k|v LoRA: keep only the diagonal blocks, peft layout."""
+    r, nblk, nm = 16, 256, 3
+    M = 320
+    dy = ints(M, nm * nblk)
+    u = ints(M, 64)
+    out = torch.zeros(nm * nblk * r, device=DEV, dtype=torch.float32)
+    ops().gemm_f32acc(dy, u, out.view(nm * nblk, r), a_kmajor=True, b_kmajor=True, k_splits=2, diag=(nblk, r))
+    full = dy.float().T @ u.float()  # [nm*nblk, 64]
+    ref = torch.cat([full[i * nblk:(i + 1) * nblk, i * r:(i + 1) * r] for i in range(nm)], 0).reshape(-1)
+    assert torch.equal(out, ref)
+
+
+# ------------------------------------------------------------------ RMSNorm
+@pytest.mark.parametrize("M,D", [(37, 256), (600, 4096), (5, 2048)])
+def test_rmsnorm(M, D):
+    x, w = rnd(M, D), bf(1 + 0.1 * torch.randn(D, device=DEV))
+    y = torch.empty_like(x)
+    rstd = torch.empty(M, device=DEV)
+    ops().rmsnorm_fwd(x, w, y, rstd, 1e-6)
+    ref = O.rmsnorm(x, w, 1e-6)
+    assert relerr(y.float(), ref.float()) < 4e-3
+    # backward vs fp32 autograd
+    dy, dres = rnd(M, D), rnd(M, D)
+    xf = x.float().requires_grad_(True)
+    yf = w.float() * (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6))
+    yf.backward(dy.float())
+    dx = torch.empty_like(x)
+    ops().rmsnorm_bwd(dy, x, w, rstd, dx, dres=dres)
+    assert relerr(dx.float(), xf.grad + dres.float()) < 4e-3
+
+
+# --------------------------------------------------------------------- RoPE
+def test_rope_fwd_bwd():
+    S, T, H, hd = 2, 72, 3, 128
+    D = H * hd
+    qkv = rnd(S * T + 5, 3 * D)
+    cos, sin = ops().rope_tables(T, hd, 1e4, DEV)
+    x = qkv.clone()
+    ops().rope(x, 0, D, S, T, H, hd, cos, sin)
+    c, s = O.rope_cos_sin(T, hd, 1e4, torch.bfloat16)
+    c, s = c.to(DEV), s.to(DEV)
+    for col in (0, D):
+        src = qkv[: S * T, col:col + D].view(S, T, H, hd).transpose(1, 2)
+        ref = O.apply_rope(src, c, s).transpose(1, 2).reshape(S * T, D)
+        assert torch.equal(x[: S * T, col:col + D], ref)
+    assert torch.equal(x[:, 2 * D:], qkv[:, 2 * D:])  # v untouched
+    assert torch.equal(x[S * T:], qkv[S * T:])        # pad rows untouched
+    # bwd: transpose rotation (fp32 autograd reference)
+    g = rnd(S * T, 3 * D)
+    src = qkv[: S * T, :D].float().view(S, T, H, hd).transpose(1, 2).requires_grad_(True)
+    out = O.apply_rope(src, c.float(), s.float())
+    out.backward(g[:, :D].float().view(S, T, H, hd).transpose(1, 2))
+    gx = g.clone()
+    ops().rope(gx, 0, D, S, T, H, hd, cos, sin, backward=True)
+    ref = src.grad.transpose(1, 2).reshape(S * T, D)
+    assert relerr(gx[:, :D].float(), ref) < 4e-3
+
+
+# ------------------------------------------------------------------- SwiGLU
+def test_swiglu():
+    M, Fd = 333, 512
+    gu = rnd(M, 2 * Fd)
+    h = torch.empty(M, Fd, device=DEV, dtype=torch.bfloat16)
+    ops().swiglu_fwd(gu, h)
+    ref = F.silu(gu[:, :Fd]) * gu[:, Fd:]
+    assert relerr(h.float(), ref.float()) < 2e-3
+    assert (h != ref).float().mean().item() < 0.01
+    dh = rnd(M, Fd)
+    g = gu.float().requires_grad_(True)
+    (F.silu(g[:, :Fd]) * g[:, Fd:]).backward(dh.float())
+    dgu = torch.empty_like(gu)
+    ops().swiglu_bwd(dh, gu, dgu)
+    assert relerr(dgu.float(), g.grad) < 5e-3
+
+
+# ---------------------------------------------------------------- attention
+def attn_ref(q, k, v, scale):
+    T = q.shape[-2]
+    s = (q @ k.transpose(-1, -2)) * scale
+    s = s.masked_fill(torch.ones(T, T, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+    return torch.softmax(s, -1) @ v
+
+
+@pytest.mark.parametrize("S,T,H", [(2, 72, 2), (1, 64, 1), (2, 600, 2), (1, 130, 3)])
+def test_flash_attention(S, T, H):
+    hd = 128
+    D = H * hd
+    rows = S * T + 7
+    qkv = rnd(rows, 3 * D)
+    o = torch.zeros(rows, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(S * H * T, device=DEV)
+    scale = 1 / math.sqrt(hd)
+    ops().flash_attn_fwd(qkv, 0, D, 2 * D, o, lse, S, T, H, hd, scale)
+    qf = qkv[: S * T].float().view(S, T, 3, H, hd).permute(2, 0, 3, 1, 4).requires_grad_(True)
+    ref = attn_ref(qf[0], qf[1], qf[2], scale)
+    ref_rows = ref.transpose(1, 2).reshape(S * T, D)
+    assert relerr(o[: S * T].float(), ref_rows) < 8e-3
+    s_ = (qf[0] @ qf[1].transpose(-1, -2)) * scale
+    s_ = s_.masked_fill(torch.ones(T, T, dtype=torch.bool, device=DEV).triu(1), float("-inf"))
+    assert relerr(lse.view(S, H, T), torch.logsumexp(s_, -1)) < 1e-4
+    # backward
+    do = rnd(rows, D)
+    ref.backward(do[: S * T].float().view(S, T, H, hd).transpose(1, 2))
+    dqkv = torch.zeros(rows, 3 * D, device=DEV, dtype=torch.bfloat16)
+    delta = torch.empty(S * H * T, device=DEV)
+    dq = torch.empty(S * T, D, device=DEV)
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, dq, dqkv, S, T, H, hd, scale)
+    g = qf.grad.permute(1, 3, 0, 2, 4).reshape(S * T, 3 * D)
+    for i, nm in enumerate("qkv"):
+        e = relerr(dqkv[: S * T, i * D:(i + 1) * D].float(), g[:, i * D:(i + 1) * D])
+        assert e < 2e-2, (nm, e)
+
+
+# ------------------------------------------------------- embed / gather / gelu
+def test_assemble_and_aligner():
+    B, Lt, N, D, V = 2, 5, 8, 256, 50
+    ids = torch.tensor([[3, 4, 5, -1, -1], [7, 8, 9, 10, 11]], device=DEV, dtype=torch.int32)
+    table = rnd(V, D)
+    img = rnd(2 * B * N, D)
+    x0 = torch.empty(2 * B * (Lt + N), D, device=DEV, dtype=torch.bfloat16)
+    ops().assemble_inputs(ids, B, Lt, table, img, N, D, x0)
+    T = Lt + N
+    for s in range(2 * B):
+        for t in range(T):
+            row = x0[s * T + t]
+            if t < Lt:
+                i = int(ids[s % B, t])
+                exp = table[i] if i >= 0 else torch.zeros_like(row)
+            else:
+                exp = img[s * N + t - Lt]
+            assert torch.equal(row, exp)
+    E = 8
+    gid = torch.randint(0, 100, (37,), device=DEV, dtype=torch.int32)
+    emb, w1, b1 = rnd(100, E), rnd(D, E, s=0.3), rnd(D, s=0.1)
+    out = torch.empty(37, D, device=DEV, dtype=torch.bfloat16)
+    ops().gen_aligner_in(gid, emb, w1, b1, out)
+    ref = F.gelu(F.linear(emb[gid.long()].float(), w1.float(), b1.float()))
+    assert relerr(out.float(), ref) < 4e-3
+
+
+def test_gather_scatter_gelu():
+    S, T, t0, N, D = 3, 20, 4, 15, 64
+    src = rnd(S * T + 3, D)
+    dst = torch.empty(S * N, D, device=DEV, dtype=torch.bfloat16)
+    ops().gather_rows(src, S, T, t0, N, dst)
+    ref = src[: S * T].view(S, T, D)[:, t0:t0 + N].reshape(S * N, D)
+    assert torch.equal(dst, ref)
+    back = torch.full((S * T + 3, D), 7.0, device=DEV, dtype=torch.bfloat16)
+    ops().scatter_rows(dst, S, T, t0, N, back)
+    exp = torch.zeros_like(back)
+    exp[: S * T].view(S, T, D)[:, t0:t0 + N] = dst.view(S, N, D)
+    assert torch.equal(back, exp)
+    x = rnd(1000 * 8)
+    y = torch.empty_like(x)
+    ops().gelu_fwd(x, y)
+    assert relerr(y.float(), F.gelu(x.float())) < 4e-3
+    dy = rnd(1000 * 8)
+    dx = torch.empty_like(x)
+    ops().gelu_bwd(dy, x, dx)
+    xf = x.float().requires_grad_(True)
+    F.gelu(xf).backward(dy.float())
+    assert relerr(dx.float(), xf.grad) < 4e-3
+
+
+# ------------------------------------------------------------ logprob / SimPO
+def test_logprob_fwd_bwd():
+    S, N, V = 4, 24, 16384
+    logits = rnd(S * N, V, s=2.0)
+    labels = torch.randint(0, V, (S * N,), device=DEV, dtype=torch.int32)
+    lse = torch.empty(S * N, device=DEV)
+    tok = torch.empty(S * N, device=DEV)
+    seq = torch.empty(S, device=DEV)
+    ops().logprob_fwd(logits, labels, N, lse, tok, seq)
+    lf = logits.float().requires_grad_(True)
+    lp = torch.gather(lf.log_softmax(-1), 1, labels.long()[:, None])[:, 0]
+    ref_seq = lp.view(S, N).mean(-1)
+    assert relerr(seq, ref_seq) < 1e-5
+    g = torch.randn(S, device=DEV)
+    ref_seq.backward(g)
+    dl = torch.empty_like(logits)
+    ops().logprob_bwd(logits, labels, lse, N, g, dl)
+    assert relerr(dl.float(), lf.grad) < 4e-3
+
+
+@pytest.mark.parametrize("beta,gbr,ls,lt", [(10.0, 0.5, 0.0, "sigmoid"), (2.0, 0.0, 0.1, "sigmoid"),
+                                            (10.0, 0.5, 0.0, "hinge")])
+def test_simpo(beta, gbr, ls, lt):
+    B = 5
+    lp = (torch.randn(2 * B, device=DEV) * 0.3 - 9.7).requires_grad_(True)
+    losses, cr, rr = O.simpo_loss(lp[:B], lp[B:], beta, gbr, ls, lt)
+    losses.mean().backward()
+    lo, mean, rew, glp = (torch.empty(B, device=DEV), torch.empty(1, device=DEV), torch.empty(2 * B, device=DEV),
+                          torch.empty(2 * B, device=DEV))
+    ops().simpo_fwd(lp.detach(), B, beta, gbr, ls, lt, lo, mean, rew)
+    ops().simpo_bwd(lp.detach(), B, beta, gbr, ls, lt, torch.ones(1, device=DEV), glp)
+    torch.testing.assert_close(lo, losses.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(mean[0], losses.mean().detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(rew, torch.cat([cr, rr]), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(glp, lp.grad, rtol=1e-5, atol=1e-6)
+    with pytest.raises(ValueError):
+        ops().simpo_fwd(lp.detach(), B, beta, gbr, ls, "ipo", lo, mean, rew)
+
+
+# ---------------------------------------------------------------- LoRA pack
+def test_lora_pack():
+    nm, r, Kin, Nmod, Rp = 3, 16, 256, 128, 64
+    A = rnd(nm * r, Kin)
+    Bf = rnd(nm, Nmod, r)
+    Acat = torch.empty(Rp, Kin, device=DEV, dtype=torch.bfloat16)
+    AcatT = torch.empty(Kin, Rp, device=DEV, dtype=torch.bfloat16)
+    Bcat = torch.empty(nm * Nmod, Rp, device=DEV, dtype=torch.bfloat16)
+    ops().lora_pack(A, Bf, nm, r, Kin, Nmod, Rp, Acat, AcatT, Bcat)
+    expA = torch.zeros(Rp, Kin, device=DEV, dtype=torch.bfloat16)
+    expA[: nm * r] = A
+    assert torch.equal(Acat, expA) and torch.equal(AcatT, expA.T)
+    expB = torch.zeros(nm * Nmod, Rp, device=DEV, dtype=torch.bfloat16)
+    for i in range(nm):
+        expB[i * Nmod:(i + 1) * Nmod, i * r:(i + 1) * r] = Bf[i]
+    assert torch.equal(Bcat, expB)
+
+
+# -------------------------------------------------------------- optimizer
+def test_clip_adamw_matches_torch():
+    n = 10000
+    p0 = rnd(n, s=0.02)
+    g = torch.randn(n, device=DEV) * 0.05
+    ps = {"w": p0.cpu().clone()}
+    state = {}
+    O.clip_and_adamw(ps, {"w": g.cpu()}, state, lr=4e-5, betas=(0.9, 0.95), eps=1e-8, max_norm=1.0)
+    O.clip_and_adamw(ps, {"w": (g * 0.5).cpu()}, state, lr=4e-5, betas=(0.9, 0.95), eps=1e-8, max_norm=1.0)
+    p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+    for step, gg in ((1, g), (2, g * 0.5)):
+        ss = torch.zeros(1, device=DEV)
+        ops().sumsq(gg, ss)
+        assert abs(ss.item() - float((gg.double() ** 2).sum())) / float((gg.double() ** 2).sum()) < 1e-5
+        ops().adamw_clip(p, gg, m, v, 4e-5, 0.9, 0.95, 1e-8, 0.0, step, ss, 1.0)
+    ref = ps["w"].to(DEV)
+    # within one bf16 ulp, or one AdamW step (the clip coefficient is computed from
+    # fp32 grads here and from bf16 grads in torch, which can flip a rounding)
+    tol = torch.maximum(ref.float().abs() * 2 ** -7 * 1.01, torch.full_like(ref.float(), 1.5 * 4e-5 * 2))
+    assert bool(((p.float() - ref.float()).abs() <= tol).all())
+    assert (p != ref).float().mean().item() < 0.02
