@@ -1,0 +1,180 @@
+"""Throughput of the Janus-Pro-7B SimPO training step on MI355X (BASELINE.json metric).
+
+python bench.py [--gpus N --steps K --warmup W]    (N>1: launched by torch.distributed.run)
+
+A step = forward of 2B sequences (chosen | rejected, T = 24 text + 576 image
+tokens) through the LoRA'd Janus-Pro-7B LLM and gen_head, SimPO loss, backward
+to the LoRA adapters, RCCL all-reduce of the LoRA grads (N>1), clip + AdamW.
+Synthetic data (random-init weights of the 7B architecture, random prompt and
+VQ ids; there is no checkpoint or dataset offline).  Prints ONE JSON line on
+rank 0.  See DESIGN.md "Measurement".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+METRIC = "preference-pairs/sec (whole node), Janus-Pro-7B SimPO @576 img tokens, 1/2/4/8 GPU"
+
+
+def algorithmic_flops_per_pair(T=600, N=576, L=30, D=4096, F=11008, r=16, Dg=4096, V=16384, A_in=8):
+    """fwd + bwd (activation grads + LoRA grads), no recompute, no text lm_head."""
+    p_lin = L * (4 * D * D + 3 * D * F)
+    p_lora = L * r * (4 * (D + D) + 2 * (D + F) + (F + D))
+    p_gh = D * Dg + Dg * V
+    p_al = A_in * D + D * D
+    attn_f = 2 * L * D * T * (T + 1)  # causal QK^T + PV
+    fwd = 2 * T * p_lin + attn_f + 2 * T * p_lora + 2 * N * p_gh + 2 * N * p_al
+    bwd = 2 * T * p_lin + 2 * attn_f + 4 * T * p_lora + 2 * N * p_gh
+    return 2 * (fwd + bwd)  # two sequences per pair
+
+
+def synthetic_batch(B, Lt, N, vocab, img_vocab, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    lens = torch.randint(Lt // 2, Lt + 1, (B,), generator=g)
+    lens[0] = Lt
+    text = torch.full((B, Lt), -1, dtype=torch.int32)
+    for i in range(B):
+        text[i, : lens[i]] = torch.randint(0, vocab, (int(lens[i]),), generator=g, dtype=torch.int32)
+    chosen = torch.randint(0, img_vocab, (B, N), generator=g, dtype=torch.int32)
+    rejected = torch.randint(0, img_vocab, (B, N), generator=g, dtype=torch.int32)
+    return text.to(device), chosen.to(device), rejected.to(device)
+
+
+def cpu_baseline(Lt=24, N=576):
+    """The CPU oracle (oracle/simpo_ref.py, bf16 CPU path) on a bounded sample:
+    one pair, full 7B shapes, fwd+bwd with 1 and with 2 decoder layers;
+    t_layer = t2 - t1, t_head = t1 - t_layer, per-pair = t_head + 30 * t_layer."""
+    from oracle import simpo_ref as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    text = [torch.randint(0, 4096, (1, Lt), generator=g, dtype=torch.int32)]
+    ch = torch.randint(0, 16384, (1, N), generator=g)
+    rj = torch.randint(0, 16384, (1, N), generator=g)
+    times = {}
+    for L in (1, 2):
+        dims = O.JanusDims(n_layers=L, vocab=4096)
+        w = O.init_weights(dims, seed=1, dtype=torch.bfloat16)
+        t0 = time.perf_counter()
+        O.simpo_step(text, ch, rj, w, dims, dtype=torch.bfloat16)
+        times[L] = time.perf_counter() - t0
+        del w
+    t_layer = max(times[2] - times[1], 1e-6)
+    t_head = max(times[1] - t_layer, 0.0)
+    t_pair = t_head + 30 * t_layer
+    return {"value": round(1.0 / t_pair, 5), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"1 pair (T={Lt + N}), oracle bf16 fwd+bwd with 1 and 2 full-size 7B decoder layers "
+                      f"({times[1]:.1f}s, {times[2]:.1f}s): t_layer {t_layer:.2f}s, head+loss {t_head:.2f}s, "
+                      f"scaled to 30 layers = {t_pair:.1f}s/pair"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs-per-gpu", type=int, default=4)
+    ap.add_argument("--text-len", type=int, default=24)
+    ap.add_argument("--img-tokens", type=int, default=576)
+    ap.add_argument("--layers", type=int, default=30)
+    ap.add_argument("--lora-r", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timer", action="store_true")
+    args = ap.parse_args()
+
+    from ospo_amd import dist as odist
+    from ospo_amd import ops
+    from ospo_amd.engine import JANUS_PRO_7B, SimPOEngine, synthetic_weights
+    from ospo_amd.simpo import SimPOConfig, SimPOLossBuffers, train_step
+
+    world, rank, local = odist.init()
+    dev = torch.device("cuda", local)
+    dims = JANUS_PRO_7B.__class__(**{**JANUS_PRO_7B.__dict__, "n_layers": args.layers, "lora_r": args.lora_r,
+                                     "lora_alpha": 2 * args.lora_r})
+    B, Lt, N = args.pairs_per_gpu, args.text_len, args.img_tokens
+    weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)  # identical on every rank (same seeds)
+    eng = SimPOEngine(dims, weights, device=dev, max_pairs=B, max_text_len=Lt, n_img_tokens=N)
+    del weights
+    torch.cuda.empty_cache()
+    cfg = SimPOConfig()
+    buf = SimPOLossBuffers(B, dev)
+    allreduce = odist.GradAllReduce(world) if world > 1 else None
+    batches = [synthetic_batch(B, Lt, N, dims.vocab, dims.img_vocab, seed=1000 * rank + i, device=dev)
+               for i in range(4)]
+
+    for i in range(args.warmup):
+        train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
+    timer = None if args.no_kernel_timer else ops.KernelTimer()
+    odist.barrier()
+    torch.cuda.synchronize()
+    ops.set_kernel_timer(timer)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
+    odist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ops.set_kernel_timer(None)
+    loss = float(out["loss"].item())
+    if not math.isfinite(loss):
+        raise RuntimeError(f"non-finite loss {loss}")
+    t = torch.tensor([dt], device=dev)
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    dt = float(t.item())
+    if rank != 0:
+        return
+    global_batch = B * world
+    value = global_batch * args.steps / dt
+    ms = dt / args.steps * 1e3
+    T = Lt + N
+    flops_pair = algorithmic_flops_per_pair(T=T, N=N, L=dims.n_layers, r=dims.lora_r)
+    roof = None
+    kern = {}
+    if timer is not None:
+        kern = timer.summary()
+        dom = max(kern, key=lambda k: kern[k]["ms"])
+        d = kern[dom]
+        achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "gemm_pmc.json")
+        if os.path.exists(pmc):
+            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "kernel": f"{dom} (gemm_kernel MFMA bf16)", "launches": d["count"],
+                "avg_launch_us": round(d["ms"] * 1e3 / d["count"], 2),
+                "step_mfma_frac": round(flops_pair * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)}
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (random-init Janus-Pro-7B-shaped weights, random prompt/VQ token ids)",
+        "config": {"workload": f"Janus-Pro-{'7B' if dims.n_layers == 30 else str(dims.n_layers) + 'L'} SimPO "
+                               f"train step, LoRA r={dims.lora_r}, {N} image tokens, {B} pairs/GPU",
+                   "global_batch": global_batch, "seq_len": T, "parallelism": f"dp{world}",
+                   "algorithmic_tflop_per_pair": round(flops_pair / 1e12, 3)},
+        "roofline": roof,
+        "loss": round(loss, 5),
+        "gemm_kernels": {k: {"count": v["count"], "ms": round(v["ms"], 2),
+                             "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)} for k, v in kern.items()},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(Lt=Lt, N=N)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -53,6 +53,9 @@ int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int
                       const void* bias, const void* residual, int ldr, void* C, int ldc,
                       hipStream_t stream);
 
+/* Row count of the tile ospo_gemm_nt_bf16 uses for an M x N output (256, 160 or 64). */
+int ospo_gemm_nt_tile(int M, int N);
+
 /* C[M,N] (fp32) += alpha * op(A)[M,K] . op(B)[N,K]^T, split over K into
  * `k_splits` workgroup slices summed with fp32 atomics (C must be initialised).
  * a_kmajor = 0: A stored [M][K] (lda >= K); 1: A stored [K][M] (lda >= M).

@@ -20,6 +20,7 @@ P, I, L, F = c_void_p, c_int, c_long, c_float
 SIGNATURES = {
     "ospo_abi_version": [],
     "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P],
+    "ospo_gemm_nt_tile": [I, I],
     "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],
     "ospo_f32_to_bf16": [P, P, L, F, P],
     "ospo_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
@@ -72,6 +73,11 @@ def lib():
 
 def exported_symbols():
     return list(SIGNATURES) + ["ospo_strerror"]
+
+
+def query(name: str, *args) -> int:
+    """Call an entry point that returns a value rather than a status."""
+    return getattr(lib(), name)(*args)
 
 
 def call(name: str, *args) -> None:

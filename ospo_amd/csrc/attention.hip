@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float v = st[t][j] * scale;
+        float v = round_bf(round_bf(st[t][j]) * scale);  // HF eager bf16: matmul out, then * scale, each rounded
         if (diag) {
           const int key = kt * KB + 16 * t + 4 * g + j;
           if (key > qrow || key >= T) v = -1e30f;
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ 
       for (int j = 0; j < 4; ++j) {
         const int ql = 16 * a + 4 * g + j;
         const int q = qt * QB + ql;
-        float p = __expf(sv[a][j] * scale - Ls[ql]);
+        float p = __expf(round_bf(round_bf(sv[a][j]) * scale) - Ls[ql]);
         if (q >= T || key_l > q || key_l >= T) p = 0.f;
         sv[a][j] = p;
         dp[a][j] = p * (dp[a][j] - Dl[ql]);

@@ -307,6 +307,8 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   }
 }
 
+extern "C" int ospo_gemm_nt_tile(int M, int N) { return pick_nt_tile(M, N); }
+
 extern "C" int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
                                 int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
                                 int diag_nblk, int diag_r, hipStream_t stream) {

@@ -1,0 +1,75 @@
+"""Data parallelism over RCCL (torch.distributed backend "nccl" == RCCL on ROCm).
+
+One process per GPU; preference pairs are sharded across ranks (the
+DistributedSampler role of PL's DDPStrategy, ospo/utils/train.py:26-28); the
+only data-path collective is the sum of the flat fp32 LoRA-gradient buffer
+(DDP's bucketed all-reduce), divided by world size.  Frozen weights are built
+locally on every rank -- nothing but the LoRA init is broadcast.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def env_world():
+    return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def init(backend: Optional[str] = None):
+    world, rank, local = env_world()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+class GradAllReduce:
+    """Sum + average the flat fp32 gradient buffer in fixed-size buckets.
+
+    Buckets are contiguous slices (whole layers of the LoRA layout), issued
+    back-to-back as async collectives and waited together."""
+
+    def __init__(self, world: int, bucket_elems: int = 16 * 1024 * 1024, group=None):
+        self.world, self.bucket, self.group = world, bucket_elems, group
+
+    def __call__(self, flat: torch.Tensor):
+        if self.world <= 1:
+            return flat
+        works = []
+        for i in range(0, flat.numel(), self.bucket):
+            works.append(dist.all_reduce(flat[i:i + self.bucket], op=dist.ReduceOp.SUM, group=self.group,
+                                         async_op=True))
+        for w in works:
+            w.wait()
+        flat.mul_(1.0 / self.world)
+        return flat
+
+
+def broadcast_(t: torch.Tensor, src: int = 0, group=None):
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.broadcast(t, src, group=group)
+    return t
+
+
+def all_reduce_mean_(t: torch.Tensor, group=None):
+    """sync_dist=True logging (train.py:91-93,435-443): one fused all-reduce of the scalars."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.mul_(1.0 / dist.get_world_size(group))
+    return t
+
+
+def barrier():
+    if dist.is_initialized():
+        dist.barrier()

@@ -1,0 +1,424 @@
+"""The SimPO policy engine: Janus-Pro LLM + LoRA + gen_head on the HIP kernels.
+
+One call of ``forward`` runs what the reference runs from ``preprocess_batch``
+(ospo/wrapper/train.py:219-279, minus VQ encode: token ids are given) through
+``concatenated_forward`` (:345-372) and ``get_batch_logps`` (:375-396) and
+returns the per-sequence mean log-prob of the 2B sequences (chosen first).
+``backward`` takes d(loss)/d(logps) and accumulates the LoRA gradients into the
+flat fp32 buffer (ospo_amd/lora.py layout) -- the autograd of train.py:448-456
++ PL's backward, written out explicitly.
+
+MI355X-first memory plan (288 GB HBM3E per GPU):
+  * frozen weights are stored twice, W [out,in] and W^T [in,out], so every
+    forward AND backward product is an "NT" MFMA GEMM with K contiguous on
+    both operands (7B: +13 GB);
+  * q|k|v and gate|up are fused into single GEMMs (N = 3D, 2F);
+  * every activation the backward needs stays resident (7B, B=4 pairs:
+    ~19 GB) -- no gradient-checkpoint recompute (the reference recomputes:
+    ospo/utils/model.py:45-46), and the [2B, T, 102400] text lm_head the
+    reference evaluates and discards is never computed;
+  * LoRA runs as a K-extension of the frozen GEMM (A2 = s*x.A^T, B2 =
+    block-diagonal packed B), and its gradients land in the flat buffer by
+    fp32-atomic transposed GEMMs.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import ops
+from .lora import LoraLayout, roundup
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+@dataclass
+class ModelDims:
+    n_layers: int
+    d_model: int
+    d_ff: int
+    n_heads: int
+    head_dim: int
+    vocab: int
+    img_vocab: int
+    img_embed: int
+    gen_head_dim: int
+    rope_theta: float = 10000.0
+    rms_eps: float = 1e-6
+    lora_r: int = 16
+    lora_alpha: int = 32
+
+    @classmethod
+    def from_any(cls, d) -> "ModelDims":
+        keys = cls.__dataclass_fields__.keys()
+        src = d if isinstance(d, dict) else d.__dict__
+        return cls(**{k: src[k] for k in keys if k in src})
+
+    @property
+    def lora_scale(self) -> float:
+        return self.lora_alpha / self.lora_r
+
+
+JANUS_PRO_7B = ModelDims(30, 4096, 11008, 32, 128, 102400, 16384, 8, 4096)
+JANUS_PRO_1B = ModelDims(24, 2048, 5632, 16, 128, 102400, 16384, 8, 2048)
+
+
+def _dev(t: torch.Tensor, device) -> torch.Tensor:
+    return t.to(device=device, dtype=BF16).contiguous()
+
+
+class SimPOEngine:
+    """Device-resident Janus-Pro SimPO policy (one per GPU / rank)."""
+
+    def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_pairs: int = 4,
+                 max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0):
+        if lora_dropout and lora_dropout > 0:
+            raise NotImplementedError(
+                "lora_dropout > 0 is not on the built path yet (peft lora.Linear dropout on the adapter input); "
+                "set lora.lora_dropout=0.0 (the parity configuration) or lora.ignore_dropout=true")
+        if dims.head_dim != 128:
+            raise ValueError("head_dim must be 128 (Janus-Pro)")
+        if dims.d_model % 256 or dims.d_ff % 256 or dims.gen_head_dim % 256 or dims.img_vocab % 256:
+            raise ValueError("d_model, d_ff, gen_head_dim and img_vocab must be multiples of 256")
+        self.dims, self.device = dims, torch.device(device)
+        D, Fd, L = dims.d_model, dims.d_ff, dims.n_layers
+        self.layout = LoraLayout(L, D, Fd, dims.lora_r)
+        self.scale = dims.lora_scale
+        dev = self.device
+        w = weights
+        # ---- frozen weights, fused and transposed copies
+        self.embed = _dev(w["embed_tokens"], dev)
+        self.layers = []
+        for i in range(L):
+            p = f"layers.{i}."
+            wqkv = torch.cat([w[p + "q_proj"], w[p + "k_proj"], w[p + "v_proj"]], 0)
+            wgu = torch.cat([w[p + "gate_proj"], w[p + "up_proj"]], 0)
+            lay = {
+                "ln_in": _dev(w[p + "input_layernorm"], dev), "ln_post": _dev(w[p + "post_attention_layernorm"], dev),
+                "qkv": _dev(wqkv, dev), "o": _dev(w[p + "o_proj"], dev), "gu": _dev(wgu, dev),
+                "down": _dev(w[p + "down_proj"], dev),
+            }
+            for k in ("qkv", "o", "gu", "down"):
+                lay[k + "T"] = lay[k].t().contiguous()
+            self.layers.append(lay)
+        self.norm = _dev(w["norm"], dev)
+        self.gh_w1, self.gh_b1 = _dev(w["gen_head.w1"], dev), _dev(w["gen_head.b1"], dev)
+        self.gh_w2, self.gh_b2 = _dev(w["gen_head.w2"], dev), _dev(w["gen_head.b2"], dev)
+        self.gh_w1T, self.gh_w2T = self.gh_w1.t().contiguous(), self.gh_w2.t().contiguous()
+        self.al_w1, self.al_b1 = _dev(w["gen_aligner.w1"], dev), _dev(w["gen_aligner.b1"], dev)
+        self.al_w2, self.al_b2 = _dev(w["gen_aligner.w2"], dev), _dev(w["gen_aligner.b2"], dev)
+        self.gen_embed = _dev(w["gen_embed"], dev)
+        # ---- LoRA flat state
+        n = self.layout.numel
+        self.lora = torch.zeros(n, dtype=BF16, device=dev)
+        lora_src = {k: v for k, v in w.items() if ".lora_" in k}
+        if lora_src:
+            staging = torch.zeros(n, dtype=BF16)
+            self.layout.to_flat({k: v.to(BF16).cpu() for k, v in lora_src.items()}, staging)
+            self.lora.copy_(staging)
+        self.grads = torch.zeros(n, dtype=F32, device=dev)
+        self.exp_avg = torch.zeros(n, dtype=BF16, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=BF16, device=dev)
+        self.opt_step = 0
+        self._sumsq = torch.zeros(1, dtype=F32, device=dev)
+        # packed LoRA operands per layer / group
+        self.packed = []
+        for i in range(L):
+            d = {}
+            for gname, g in self.layout.groups.items():
+                d[gname] = (torch.zeros(g.Rp, g.Kin, dtype=BF16, device=dev),
+                            torch.zeros(g.Kin, g.Rp, dtype=BF16, device=dev),
+                            torch.zeros(g.nmods * g.Nmod, g.Rp, dtype=BF16, device=dev))
+            self.packed.append(d)
+        self.pack_lora()
+        self._alloc(max_pairs, max_text_len, n_img_tokens)
+        self._rope_T = -1
+
+    def ensure_capacity(self, pairs: int, text_len: int):
+        """Grow the activation buffers when a batch exceeds them (ragged prompts)."""
+        if pairs > self.cap_pairs or text_len + self.N > self.cap_T:
+            self._alloc(max(pairs, self.cap_pairs), max(text_len, self.cap_T - self.N), self.N)
+
+    # ------------------------------------------------------------ setup
+    def _alloc(self, max_pairs, max_text_len, N):
+        dims, dev = self.dims, self.device
+        D, Fd, L, H = dims.d_model, dims.d_ff, dims.n_layers, dims.n_heads
+        S = 2 * max_pairs
+        Tm = max_text_len + N
+        self.cap_pairs, self.cap_T, self.N = max_pairs, Tm, N
+        Mc = roundup(S * Tm, 64)
+        self.Mcap = Mc
+        Rmax = max(g.Rp for g in self.layout.groups.values())
+        z = lambda *s, dt=BF16: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
+        self.acts = []
+        for _ in range(L):
+            self.acts.append({
+                "x": z(Mc, D), "xn1": z(Mc, D), "rstd1": z(Mc, dt=F32), "u_qkv": z(Mc, self.layout.groups["qkv"].Rp),
+                "qkv": z(Mc, 3 * D), "lse": z(S * H * Tm, dt=F32), "attn": z(Mc, D),
+                "u_o": z(Mc, self.layout.groups["o"].Rp), "xmid": z(Mc, D), "xn2": z(Mc, D), "rstd2": z(Mc, dt=F32),
+                "u_gu": z(Mc, self.layout.groups["gu"].Rp), "gu": z(Mc, 2 * Fd), "h": z(Mc, Fd),
+                "u_d": z(Mc, self.layout.groups["down"].Rp),
+            })
+        self.x_final = z(Mc, D)
+        self.hf = z(Mc, D)
+        self.rstd_f = z(Mc, dt=F32)
+        R = S * N
+        Dg, V = dims.gen_head_dim, dims.img_vocab
+        self.img_ids = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.text_ids = torch.zeros(max_pairs * max(max_text_len, 1), dtype=torch.int32, device=dev)
+        self.e1 = z(R, D)
+        self.img_emb = z(R, D)
+        self.hsel = z(R, D)
+        self.zpre = z(R, Dg)
+        self.zact = z(R, Dg)
+        self.logits = z(R, V)
+        self.lse_tok = z(R, dt=F32)
+        self.tok_logp = z(R, dt=F32)
+        self.seq_logps = z(S, dt=F32)
+        # backward scratch (shared by all layers)
+        self.u32_flat = z(Mc * Rmax, dt=F32)
+        self.gsc_flat = z(Mc * Rmax)
+        self.dx = z(Mc, D)
+        self.dxmid = z(Mc, D)
+        self.dxn = z(Mc, D)
+        self.dattn = z(Mc, D)
+        self.dqkv = z(Mc, 3 * D)
+        self.dgu = z(Mc, 2 * Fd)
+        self.dh = z(Mc, Fd)
+        self.delta_ws = z(S * H * Tm, dt=F32)
+        self.dq_ws = z(Mc, D, dt=F32)
+        self.dz = z(R, Dg)
+        self.dhsel = z(R, D)
+
+    def pack_lora(self):
+        """Rebuild the packed A / A^T / block-diagonal B operands from the flat params."""
+        r = self.layout.r
+        for i in range(self.dims.n_layers):
+            base = self.layout.layer_off(i)
+            for gname, g in self.layout.groups.items():
+                Acat, AcatT, Bcat = self.packed[i][gname]
+                A = self.lora[base + g.a_off: base + g.a_off + g.nmods * r * g.Kin]
+                B = self.lora[base + g.b_off: base + g.b_off + g.nmods * g.Nmod * r]
+                ops.lora_pack(A, B, g.nmods, r, g.Kin, g.Nmod, g.Rp, Acat, AcatT, Bcat)
+
+    def lora_tensors(self) -> Dict[str, torch.Tensor]:
+        return self.layout.from_flat(self.lora)
+
+    def grad_tensors(self) -> Dict[str, torch.Tensor]:
+        return self.layout.from_flat(self.grads)
+
+    def _rope(self, T):
+        if T != self._rope_T:
+            self.cos, self.sin = ops.rope_tables(T, self.dims.head_dim, self.dims.rope_theta, self.device)
+            self._rope_T = T
+
+    # ------------------------------------------------------------ LoRA helpers
+    def _u32(self, Rp: int) -> torch.Tensor:
+        return self.u32_flat[: self.Mcap * Rp].view(self.Mcap, Rp)
+
+    def _lora_down(self, x, Acat, out_bf16, M):
+        """out = bf16(scale * x . Acat^T)  ([Mcap, Rp]; rows >= M come out zero)."""
+        Rp, K = Acat.shape
+        u32 = self._u32(Rp)
+        u32.zero_()
+        ops.gemm_f32acc(x[:M], Acat, u32, a_kmajor=False, b_kmajor=False, k_splits=max(1, min(K // 256, 8)))
+        ops.f32_to_bf16(u32, out_bf16, self.scale)
+
+    def _lora_g(self, dy, Bcat, M):
+        """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows >= M zero)."""
+        K, Rp = Bcat.shape
+        u32 = self._u32(Rp)
+        u32.zero_()
+        ops.gemm_f32acc(dy[:M], Bcat, u32, a_kmajor=False, b_kmajor=True, k_splits=max(1, min(K // 512, 8)))
+        g = self.gsc_flat[: self.Mcap * Rp].view(self.Mcap, Rp)
+        ops.f32_to_bf16(u32, g, self.scale)
+        return g
+
+    # ------------------------------------------------------------ forward
+    def forward(self, text_ids: torch.Tensor, chosen_ids: torch.Tensor, rejected_ids: torch.Tensor) -> torch.Tensor:
+        """text_ids int32 [B, Lt] (-1 = right padding, ragged prompts), chosen/rejected
+        int [B, N] VQ token ids.  Returns seq_logps fp32 [2B] (chosen first)."""
+        dims = self.dims
+        B, Lt = text_ids.shape
+        N = chosen_ids.shape[1]
+        self.ensure_capacity(B, Lt)
+        if N != self.N:
+            raise ValueError(f"batch (B={B}, Lt={Lt}, N={N}) exceeds engine capacity "
+                             f"(pairs={self.cap_pairs}, T={self.cap_T}, N={self.N})")
+        if Lt < 1:
+            raise ValueError("need at least one text token (the <begin_of_image> tag)")
+        S, T = 2 * B, Lt + N
+        M = S * T
+        self.B, self.S, self.T, self.Lt, self.M = B, S, T, Lt, M
+        self.Mk = roundup(M, 64)
+        D, Fd, H, hd = dims.d_model, dims.d_ff, dims.n_heads, dims.head_dim
+        self._rope(T)
+        ids = self.img_ids[: S * N].view(S, N)
+        ids[:B].copy_(chosen_ids, non_blocking=True)
+        ids[B:].copy_(rejected_ids, non_blocking=True)
+        tids = self.text_ids[: B * Lt].view(B, Lt)
+        tids.copy_(text_ids, non_blocking=True)
+        R = S * N
+        # gen_aligner(gen_embed(ids)) -> image embeds; assemble [text | img] rows (train.py:267-277, 286-312)
+        ops.gen_aligner_in(self.img_ids[:R], self.gen_embed, self.al_w1, self.al_b1, self.e1[:R])
+        ops.gemm_nt(self.e1[:R], self.al_w2, self.img_emb[:R], bias=self.al_b2)
+        x = self.acts[0]["x"] if dims.n_layers else self.x_final
+        ops.assemble_inputs(tids, B, Lt, self.embed, self.img_emb[:R], N, D, x)
+        scale_attn = 1.0 / math.sqrt(hd)
+        for i in range(dims.n_layers):
+            a, lw, pk = self.acts[i], self.layers[i], self.packed[i]
+            x = a["x"]
+            ops.rmsnorm_fwd(x[:M], lw["ln_in"], a["xn1"][:M], a["rstd1"][:M], dims.rms_eps)
+            Acat, _, Bcat = pk["qkv"]
+            self._lora_down(a["xn1"], Acat, a["u_qkv"], M)
+            ops.gemm_nt(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat)
+            ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
+            ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn)
+            Acat, _, Bcat = pk["o"]
+            self._lora_down(a["attn"], Acat, a["u_o"], M)
+            ops.gemm_nt(a["attn"][:M], lw["o"], a["xmid"][:M], a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
+            ops.rmsnorm_fwd(a["xmid"][:M], lw["ln_post"], a["xn2"][:M], a["rstd2"][:M], dims.rms_eps)
+            Acat, _, Bcat = pk["gu"]
+            self._lora_down(a["xn2"], Acat, a["u_gu"], M)
+            ops.gemm_nt(a["xn2"][:M], lw["gu"], a["gu"][:M], a2=a["u_gu"][:M], b2=Bcat)
+            ops.swiglu_fwd(a["gu"][:M], a["h"][:M])
+            Acat, _, Bcat = pk["down"]
+            self._lora_down(a["h"], Acat, a["u_d"], M)
+            xn = self.acts[i + 1]["x"] if i + 1 < dims.n_layers else self.x_final
+            ops.gemm_nt(a["h"][:M], lw["down"], xn[:M], a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
+        ops.rmsnorm_fwd(self.x_final[:M], self.norm, self.hf[:M], self.rstd_f[:M], dims.rms_eps)
+        # gen_head on the N positions that predict image tokens: t = Lt-1 .. T-2 (train.py:385-391)
+        ops.gather_rows(self.hf, S, T, Lt - 1, N, self.hsel[:R])
+        ops.gemm_nt(self.hsel[:R], self.gh_w1, self.zpre[:R], bias=self.gh_b1)
+        ops.gelu_fwd(self.zpre[:R], self.zact[:R])
+        ops.gemm_nt(self.zact[:R], self.gh_w2, self.logits[:R], bias=self.gh_b2)
+        ops.logprob_fwd(self.logits[:R], self.img_ids[:R], N, self.lse_tok[:R], self.tok_logp[:R],
+                        self.seq_logps[:S])
+        return self.seq_logps[:S]
+
+    # ------------------------------------------------------------ backward
+    def zero_grad(self):
+        self.grads.zero_()
+
+    def backward(self, g_seq: torch.Tensor):
+        """g_seq fp32 [2B] = dL/d seq_logps.  Accumulates LoRA grads into self.grads."""
+        dims = self.dims
+        S, T, Lt, M, Mk, N = self.S, self.T, self.Lt, self.M, self.Mk, self.N
+        D, Fd, H, hd = dims.d_model, dims.d_ff, dims.n_heads, dims.head_dim
+        R = S * N
+        g_seq = g_seq.to(device=self.device, dtype=F32).contiguous()
+        # log-softmax/gather backward, in place over the logits buffer
+        ops.logprob_bwd(self.logits[:R], self.img_ids[:R], self.lse_tok[:R], N, g_seq, self.logits[:R])
+        ops.gemm_nt(self.logits[:R], self.gh_w2T, self.dz[:R])
+        ops.gelu_bwd(self.dz[:R], self.zpre[:R], self.dz[:R])
+        ops.gemm_nt(self.dz[:R], self.gh_w1T, self.dhsel[:R])
+        ops.scatter_rows(self.dhsel[:R], S, T, Lt - 1, N, self.dxn[:M])
+        ops.rmsnorm_bwd(self.dxn[:M], self.x_final[:M], self.norm, self.rstd_f[:M], self.dx[:M])
+        scale_attn = 1.0 / math.sqrt(hd)
+        lay = self.layout
+        for i in reversed(range(dims.n_layers)):
+            a, lw, pk = self.acts[i], self.layers[i], self.packed[i]
+            gbase = lay.layer_off(i)
+            dx = self.dx  # gradient w.r.t. this layer's output (bf16)
+            # ---- down_proj: out = xmid + h W_d^T + s (h A_d^T) B_d^T
+            g = lay.groups["down"]
+            Acat, AcatT, Bcat = pk["down"]
+            gs = self._lora_g(dx, Bcat, M)
+            ops.gemm_nt(dx[:M], lw["downT"], self.dh[:M], a2=gs[:M], b2=AcatT)
+            self._lora_grads(gs, a["h"], dx, a["u_d"], g, gbase)
+            ops.swiglu_bwd(self.dh[:M], a["gu"][:M], self.dgu[:M])
+            # ---- gate/up
+            g = lay.groups["gu"]
+            Acat, AcatT, Bcat = pk["gu"]
+            gs = self._lora_g(self.dgu, Bcat, M)
+            ops.gemm_nt(self.dgu[:M], lw["guT"], self.dxn[:M], a2=gs[:M], b2=AcatT)
+            self._lora_grads(gs, a["xn2"], self.dgu, a["u_gu"], g, gbase)
+            ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], self.dxmid[:M],
+                            dres=dx[:M])
+            # ---- o_proj
+            g = lay.groups["o"]
+            Acat, AcatT, Bcat = pk["o"]
+            gs = self._lora_g(self.dxmid, Bcat, M)
+            ops.gemm_nt(self.dxmid[:M], lw["oT"], self.dattn[:M], a2=gs[:M], b2=AcatT)
+            self._lora_grads(gs, a["attn"], self.dxmid, a["u_o"], g, gbase)
+            # ---- attention + RoPE
+            ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, self.dq_ws,
+                               self.dqkv, S, T, H, hd, scale_attn)
+            ops.rope(self.dqkv, 0, D, S, T, H, hd, self.cos, self.sin, backward=True)
+            # ---- q/k/v
+            g = lay.groups["qkv"]
+            Acat, AcatT, Bcat = pk["qkv"]
+            gs = self._lora_g(self.dqkv, Bcat, M)
+            ops.gemm_nt(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT)
+            self._lora_grads(gs, a["xn1"], self.dqkv, a["u_qkv"], g, gbase)
+            ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M])
+
+    def _lora_grads(self, gs, x_in, dy, u, g, gbase):
+        """dA = g_s^T . x_in  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal)."""
+        r = self.layout.r
+        Mk = self.Mk
+        a_off = gbase + g.a_off
+        dA = self.grads[a_off: a_off + g.nmods * r * g.Kin].view(g.nmods * r, g.Kin)
+        ks = max(1, min(Mk // 512, 16))
+        ops.gemm_f32acc(gs[:Mk], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True, k_splits=ks)
+        b_off = gbase + g.b_off
+        dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
+        ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=max(1, min(Mk // 1024, 8)),
+                        diag=(g.Nmod, r))
+
+    # ------------------------------------------------------------ optimizer
+    def grad_norm_sq(self) -> torch.Tensor:
+        self._sumsq.zero_()
+        ops.sumsq(self.grads, self._sumsq)
+        return self._sumsq
+
+    def optimizer_step(self, lr=4e-5, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0, max_norm=1.0):
+        """PL clip (gradient_clip_val) + AdamW on the flat bf16 LoRA params, then repack.
+        The pre-clip norm stays on device (``self._sumsq``); no host sync."""
+        self.opt_step += 1
+        self.grad_norm_sq()
+        ops.adamw_clip(self.lora, self.grads, self.exp_avg, self.exp_avg_sq, lr, betas[0], betas[1], eps,
+                       weight_decay, self.opt_step, self._sumsq, max_norm if max_norm else 0.0)
+        self.pack_lora()
+
+
+def synthetic_weights(dims: ModelDims, device, seed: int = 0, lora_seed: int = 1, std: float = 0.02,
+                      lora_b_std: float = 1e-3) -> Dict[str, torch.Tensor]:
+    """Random-init weights of the Janus-Pro architecture, generated ON the device
+    (no checkpoint exists offline).  Same names/statistics as oracle.init_weights:
+    N(0, 0.02) linears, norms ~1, LoRA A kaiming-uniform, LoRA B ~ N(0, 1e-3)."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    D, Fd = dims.d_model, dims.d_ff
+
+    def n(*shape, s=std):
+        return (torch.randn(*shape, generator=g, device=dev) * s).to(BF16)
+
+    def norm(*shape):
+        return (1.0 + torch.randn(*shape, generator=g, device=dev) * 0.05).to(BF16)
+
+    shapes = {"q_proj": (D, D), "k_proj": (D, D), "v_proj": (D, D), "o_proj": (D, D),
+              "gate_proj": (Fd, D), "up_proj": (Fd, D), "down_proj": (D, Fd)}
+    w = {"embed_tokens": n(dims.vocab, D), "norm": norm(D)}
+    for i in range(dims.n_layers):
+        w[f"layers.{i}.input_layernorm"] = norm(D)
+        w[f"layers.{i}.post_attention_layernorm"] = norm(D)
+        for p, s in shapes.items():
+            w[f"layers.{i}.{p}"] = n(*s)
+    w["gen_head.w1"], w["gen_head.b1"] = n(dims.gen_head_dim, D), n(dims.gen_head_dim)
+    w["gen_head.w2"], w["gen_head.b2"] = n(dims.img_vocab, dims.gen_head_dim), n(dims.img_vocab)
+    w["gen_aligner.w1"], w["gen_aligner.b1"] = n(D, dims.img_embed, s=0.3), n(D)
+    w["gen_aligner.w2"], w["gen_aligner.b2"] = n(D, D), n(D)
+    w["gen_embed"] = n(dims.img_vocab, dims.img_embed, s=1.0)
+    gl = torch.Generator(device=dev).manual_seed(lora_seed)
+    r = dims.lora_r
+    for i in range(dims.n_layers):
+        for p, (o, k) in shapes.items():
+            bound = 1.0 / math.sqrt(k)
+            w[f"layers.{i}.{p}.lora_A"] = ((torch.rand(r, k, generator=gl, device=dev) * 2 - 1) * bound).to(BF16)
+            w[f"layers.{i}.{p}.lora_B"] = (torch.randn(o, r, generator=gl, device=dev) * lora_b_std).to(BF16)
+    return w

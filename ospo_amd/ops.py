@@ -9,9 +9,47 @@ from typing import Optional
 
 import torch
 
-from ._lib import call
+from ._lib import call, query
 
 BF16 = torch.bfloat16
+
+# Optional live kernel timer (bench.py): HIP events around each gemm_nt launch on
+# the launching stream, aggregated per tile configuration.
+_TIMER = None
+
+
+class KernelTimer:
+    def __init__(self):
+        self.recs = []  # (tag, algorithmic flops, start event, end event)
+
+    def start(self, stream):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
+    def add(self, tag, flops, e0, stream):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(stream)
+        self.recs.append((tag, flops, e0, e1))
+
+    def summary(self):
+        """{tag: {count, flops, ms}} (call after synchronize)."""
+        out = {}
+        for tag, fl, e0, e1 in self.recs:
+            d = out.setdefault(tag, {"count": 0, "flops": 0.0, "ms": 0.0})
+            d["count"] += 1
+            d["flops"] += fl
+            d["ms"] += e0.elapsed_time(e1)
+        return out
+
+
+def set_kernel_timer(t: Optional[KernelTimer]):
+    global _TIMER
+    _TIMER = t
+
+
+def gemm_nt_tile(M: int, N: int) -> int:
+    return query("ospo_gemm_nt_tile", M, N)
 
 
 def _p(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -50,9 +88,14 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
         K2 = a2.shape[1]
         if a2.shape[0] != M or b2.shape != (N, K2):
             raise ValueError("gemm_nt K-extension shape mismatch")
+    st = torch.cuda.current_stream()
+    e0 = _TIMER.start(st) if _TIMER is not None else None
     call("ospo_gemm_nt_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K,
          _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2, float(alpha),
-         _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), _s())
+         _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), st.cuda_stream)
+    if e0 is not None:
+        # algorithmic flops: the frozen product only (the LoRA K-extension is not counted)
+        _TIMER.add(f"gemm_nt_{gemm_nt_tile(M, N)}x{N if N < 256 else 256}", 2.0 * M * N * K, e0, st)
     return out
 
 

@@ -180,9 +180,14 @@ def test_swiglu():
 
 
 # ---------------------------------------------------------------- attention
+def bf16_scores(q, k, scale):
+    """HF eager attention in bf16: bf16(bf16(q.k^T) * scale) (rounding is identity for autograd)."""
+    return ((q @ k.transpose(-1, -2)).to(torch.bfloat16).float() * scale).to(torch.bfloat16).float()
+
+
 def attn_ref(q, k, v, scale):
     T = q.shape[-2]
-    s = (q @ k.transpose(-1, -2)) * scale
+    s = bf16_scores(q, k, scale)
     s = s.masked_fill(torch.ones(T, T, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
     return torch.softmax(s, -1) @ v
 
@@ -201,7 +206,7 @@ def test_flash_attention(S, T, H):
     ref = attn_ref(qf[0], qf[1], qf[2], scale)
     ref_rows = ref.transpose(1, 2).reshape(S * T, D)
     assert relerr(o[: S * T].float(), ref_rows) < 8e-3
-    s_ = (qf[0] @ qf[1].transpose(-1, -2)) * scale
+    s_ = bf16_scores(qf[0], qf[1], scale)
     s_ = s_.masked_fill(torch.ones(T, T, dtype=torch.bool, device=DEV).triu(1), float("-inf"))
     assert relerr(lse.view(S, H, T), torch.logsumexp(s_, -1)) < 1e-4
     # backward
