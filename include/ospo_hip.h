@@ -119,11 +119,13 @@ int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v
  * preprocess_batch (ospo/wrapper/train.py:224-239, 267-277) + concatenated_inputs
  * (:282-314): x0[s*T+t] = text_emb[text_ids[s % B][t]] for t < Lt (id < 0 -> zero
  * row, the right zero-padding), img_emb[s*N + t - Lt] for t >= Lt; S = 2B.
+ * Indices are clamped to the table (vocab / img_vocab rows) so an invalid id
+ * cannot fault; the host layer rejects them before launch.
  * gen_aligner_in: out[r] = bf16(gelu(bf16(gen_embed[ids[r]] . w1^T + b1)))
  * (modeling_vlm.py:263-264, first Linear + GELU of projector mlp_gelu). */
-int ospo_assemble_inputs(const int* text_ids, int B, int Lt, const void* text_table, const void* img_emb,
-                         int N, int D, void* x0, hipStream_t stream);
-int ospo_gen_aligner_in(const int* ids, int R, const void* gen_embed, int E, const void* w1,
+int ospo_assemble_inputs(const int* text_ids, int B, int Lt, const void* text_table, int vocab,
+                         const void* img_emb, int N, int D, void* x0, hipStream_t stream);
+int ospo_gen_aligner_in(const int* ids, int R, const void* gen_embed, int img_vocab, int E, const void* w1,
                         const void* b1, int D, void* out, hipStream_t stream);
 /* dst[s*N + i] = src[s*T + t0 + i] (rows of D); scatter: dst rows zero elsewhere. */
 int ospo_gather_rows(const void* src, int ld_src, int S, int T, int t0, int N, int D, void* dst,

@@ -234,7 +234,7 @@ __global__ void gelu_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restr
 }
 
 // ------------------------------------------------------------ input assembly
-__global__ void assemble_kernel(const int* __restrict__ ids, int B, int Lt, const bf16* __restrict__ table,
+__global__ void assemble_kernel(const int* __restrict__ ids, int B, int Lt, const bf16* __restrict__ table, int V,
                                 const bf16* __restrict__ img, int N, int D, bf16* __restrict__ x0, long rows) {
   const int cpr = D / 8;
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -246,21 +246,22 @@ __global__ void assemble_kernel(const int* __restrict__ ids, int B, int Lt, cons
   u32x4 v = {0u, 0u, 0u, 0u};
   if (t < Lt) {
     const int id = ids[(s % B) * Lt + t];
-    if (id >= 0) v = reinterpret_cast<const u32x4*>(table + (long)id * D)[c];
+    // id < 0: right padding (zero row); ids >= V are rejected by the host, clamped here so they cannot fault
+    if (id >= 0) v = reinterpret_cast<const u32x4*>(table + (long)min(id, V - 1) * D)[c];
   } else {
     v = reinterpret_cast<const u32x4*>(img + ((long)s * N + (t - Lt)) * D)[c];
   }
   reinterpret_cast<u32x4*>(x0 + r * D)[c] = v;
 }
 
-__global__ void gen_aligner_in_kernel(const int* __restrict__ ids, int R, const bf16* __restrict__ emb, int E,
+__global__ void gen_aligner_in_kernel(const int* __restrict__ ids, int R, const bf16* __restrict__ emb, int V, int E,
                                       const bf16* __restrict__ w1, const bf16* __restrict__ b1, int D,
                                       bf16* __restrict__ out) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= (long)R * D) return;
   const long r = tid / D;
   const int d = tid % D;
-  const bf16* e = emb + (long)ids[r] * E;
+  const bf16* e = emb + (long)min(max(ids[r], 0), V - 1) * E;
   const bf16* wr = w1 + (long)d * E;
   float acc = 0.f;
   for (int j = 0; j < E; ++j) acc += bf2f(e[j]) * bf2f(wr[j]);
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(256) void logprob_fwd_kernel(const bf16* __restrict
   if (threadIdx.x == 0) {
     const float l = mx + __logf(se);
     lse[r] = l;
-    tok[r] = bf2f(logits[r * V + labels[r]]) - l;
+    tok[r] = bf2f(logits[r * V + min(max(labels[r], 0), V - 1)]) - l;
   }
 }
 
@@ -575,25 +576,26 @@ extern "C" int ospo_gelu_bwd(const void* dy, const void* x_pre, void* dx, long n
   return OSPO_OK;
 }
 
-extern "C" int ospo_assemble_inputs(const int* text_ids, int B, int Lt, const void* text_table, const void* img_emb,
-                                    int N, int D, void* x0, hipStream_t st) {
+extern "C" int ospo_assemble_inputs(const int* text_ids, int B, int Lt, const void* text_table, int vocab,
+                                    const void* img_emb, int N, int D, void* x0, hipStream_t st) {
   if (!text_table || !img_emb || !x0 || (Lt > 0 && !text_ids)) return OSPO_ERR_ARG;
-  if (B <= 0 || Lt < 0 || N <= 0 || D % 8) return OSPO_ERR_SHAPE;
+  if (B <= 0 || Lt < 0 || N <= 0 || D % 8 || vocab <= 0) return OSPO_ERR_SHAPE;
   if (!aligned16(text_table) || !aligned16(img_emb) || !aligned16(x0)) return OSPO_ERR_ALIGN;
   const long rows = 2L * B * (Lt + N);
   const long n = rows * (D / 8);
   hipLaunchKernelGGL(assemble_kernel, dim3(blocks(n)), dim3(256), 0, st, text_ids, B, Lt, (const bf16*)text_table,
-                     (const bf16*)img_emb, N, D, (bf16*)x0, rows);
+                     vocab, (const bf16*)img_emb, N, D, (bf16*)x0, rows);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
 
-extern "C" int ospo_gen_aligner_in(const int* ids, int R, const void* gen_embed, int E, const void* w1,
-                                   const void* b1, int D, void* out, hipStream_t st) {
+extern "C" int ospo_gen_aligner_in(const int* ids, int R, const void* gen_embed, int img_vocab, int E,
+                                   const void* w1, const void* b1, int D, void* out, hipStream_t st) {
   if (!ids || !gen_embed || !w1 || !b1 || !out) return OSPO_ERR_ARG;
-  if (R <= 0 || E <= 0 || D <= 0) return OSPO_ERR_SHAPE;
+  if (R <= 0 || E <= 0 || D <= 0 || img_vocab <= 0) return OSPO_ERR_SHAPE;
   const long n = (long)R * D;
-  hipLaunchKernelGGL(gen_aligner_in_kernel, dim3(blocks(n)), dim3(256), 0, st, ids, R, (const bf16*)gen_embed, E,
+  hipLaunchKernelGGL(gen_aligner_in_kernel, dim3(blocks(n)), dim3(256), 0, st, ids, R, (const bf16*)gen_embed,
+                     img_vocab, E,
                      (const bf16*)w1, (const bf16*)b1, D, (bf16*)out);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;

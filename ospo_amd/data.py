@@ -51,14 +51,14 @@ class SyntheticTokenizer:
         return ids
 
 
-def load_tokenizer(path: Optional[str]):
+def load_tokenizer(path: Optional[str], vocab: int = 102400):
     if path:
         try:
             from transformers import AutoTokenizer
             return AutoTokenizer.from_pretrained(path)
         except Exception:  # offline / absent: fall through to the synthetic stand-in
             pass
-    return SyntheticTokenizer()
+    return SyntheticTokenizer(vocab=vocab, bos_id=vocab - 2, pad_token_id=vocab - 1)
 
 
 class PreferenceDataset(Dataset):
@@ -114,12 +114,12 @@ class PreferenceDataset(Dataset):
                 self.get_image_tokens(item_id, "rejected"))
 
 
-def train_dataloader(config, tokenizer, rank: int = 0, world: int = 1) -> DataLoader:
+def train_dataloader(config, tokenizer, rank: int = 0, world: int = 1, img_vocab: int = 16384) -> DataLoader:
     """TrainDataModule.train_dataloader (datamodule.py:35-43) + the DistributedSampler PL's DDP adds."""
     tr = config["dataset"]["train"]
     ds = PreferenceDataset(seed=config["experiment"]["seed"], data_path=tr["data_path"], tokenizer=tokenizer,
                            num_samples=tr.get("num_samples"), token_cache=tr.get("token_cache"),
-                           synthetic_tokens=tr.get("synthetic_tokens", True))
+                           synthetic_tokens=tr.get("synthetic_tokens", True), img_vocab=img_vocab)
     sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True,
                                  seed=config["experiment"]["seed"]) if world > 1 else None
     return DataLoader(ds, batch_size=tr["batch_size"], shuffle=sampler is None, sampler=sampler,

@@ -251,6 +251,10 @@ class SimPOEngine:
                              f"(pairs={self.cap_pairs}, T={self.cap_T}, N={self.N})")
         if Lt < 1:
             raise ValueError("need at least one text token (the <begin_of_image> tag)")
+        for t, hi, name in ((text_ids, dims.vocab, "text id"), (chosen_ids, dims.img_vocab, "chosen VQ id"),
+                            (rejected_ids, dims.img_vocab, "rejected VQ id")):
+            if not t.is_cuda and t.numel() and (int(t.max()) >= hi or int(t.min()) < (-1 if t is text_ids else 0)):
+                raise ValueError(f"{name} out of range [0, {hi})")
         S, T = 2 * B, Lt + N
         M = S * T
         self.B, self.S, self.T, self.Lt, self.M = B, S, T, Lt, M

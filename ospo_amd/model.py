@@ -149,6 +149,6 @@ def get_model(mode: str = "train", dtype=torch.bfloat16, config=None, device=Non
     engine = SimPOEngine(dims, w, device=device, max_pairs=bs, max_text_len=max_text_len, n_img_tokens=n_img_tokens,
                          lora_dropout=dropout)
     del w
-    tokenizer = load_tokenizer(get(config, "model.tokenizer_path"))
+    tokenizer = load_tokenizer(get(config, "model.tokenizer_path"), vocab=dims.vocab)
     lora_cfg = {"lora_rank": r, "lora_alpha": alpha, "lora_dropout": dropout, "target_modules": targets}
     return JanusProPolicy(engine, lora_cfg, synthetic), None, None, tokenizer

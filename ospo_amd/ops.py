@@ -182,15 +182,15 @@ def flash_attn_bwd(qkv, q_col, k_col, v_col, o, dout, lse, delta_ws, dq_ws, dqkv
 
 # -------------------------------------------------------- embed / gather
 def assemble_inputs(text_ids, B, Lt, table, img_emb, N, D, x0):
-    call("ospo_assemble_inputs", _p(text_ids), B, Lt, _p(table), _p(img_emb), N, D, _p(x0), _s())
+    call("ospo_assemble_inputs", _p(text_ids), B, Lt, _p(table), table.shape[0], _p(img_emb), N, D, _p(x0), _s())
     return x0
 
 
 def gen_aligner_in(ids, gen_embed, w1, b1, out):
     R = ids.numel()
-    E = gen_embed.shape[1]
+    V, E = gen_embed.shape
     D = w1.shape[0]
-    call("ospo_gen_aligner_in", _p(ids), R, _p(gen_embed), E, _p(w1), _p(b1), D, _p(out), _s())
+    call("ospo_gen_aligner_in", _p(ids), R, _p(gen_embed), V, E, _p(w1), _p(b1), D, _p(out), _s())
     return out
 
 

@@ -1,0 +1,190 @@
+"""CPU-side tests (no GPU): the C ABI library loads and exports every symbol
+include/ospo_hip.h declares, its pre-launch validation returns the documented
+status codes, and the host logic (LoRA layout, config, data, checkpoint layout,
+FLOP model) behaves like the reference's."""
+import ctypes
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ospo_hip.h")
+LIB = os.path.join(ROOT, "ospo_amd", "libospo_hip.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "ospo_amd", "csrc"), "-j8"], check=True)
+    from ospo_amd import _lib
+    return _lib.lib()
+
+
+def header_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(ospo_[a-z0-9_]+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol(lib):
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/ospo_hip.h but not exported"
+    from ospo_amd import _lib
+    assert sorted(set(_lib.exported_symbols())) == syms, "ctypes signature table out of sync with the header"
+
+
+def test_abi_version_and_strerror(lib):
+    assert lib.ospo_abi_version() == 1
+    assert lib.ospo_strerror(1) == b"shape / leading-dimension violation"
+
+
+def test_validation_before_launch(lib):
+    """Shape/alignment/argument violations return a status BEFORE any HIP call (no GPU here)."""
+    from ospo_amd import _lib
+    P = ctypes.c_void_p
+    buf = (ctypes.c_char * 4096)()
+    a = ctypes.addressof(buf)
+    # K % 64 != 0
+    rc = lib.ospo_gemm_nt_bf16(P(a), 96, P(a), 96, 64, 64, 96, None, 0, None, 0, 0, ctypes.c_float(1.0),
+                               None, None, 0, P(a), 64, None)
+    assert rc == 1
+    # misaligned A
+    rc = lib.ospo_gemm_nt_bf16(P(a + 2), 64, P(a), 64, 64, 64, 64, None, 0, None, 0, 0, ctypes.c_float(1.0),
+                               None, None, 0, P(a), 64, None)
+    assert rc == 2
+    # null output
+    rc = lib.ospo_gemm_nt_bf16(P(a), 64, P(a), 64, 64, 64, 64, None, 0, None, 0, 0, ctypes.c_float(1.0),
+                               None, None, 0, None, 64, None)
+    assert rc == 5
+    # unknown SimPO loss type -> OSPO_ERR_ARG, like train.py:335-337 raising ValueError
+    rc = lib.ospo_simpo_fwd(P(a), 2, ctypes.c_float(10), ctypes.c_float(0.5), ctypes.c_float(0), 7, P(a), P(a),
+                            P(a), None)
+    assert rc == 5
+    with pytest.raises(ValueError):
+        _lib.call("ospo_simpo_fwd", P(a), 2, ctypes.c_float(10), ctypes.c_float(0.5), ctypes.c_float(0), 7,
+                  P(a), P(a), P(a), None)
+    # attention head_dim other than 128 unsupported
+    rc = lib.ospo_flash_attn_fwd(P(a), 384, 0, 128, 256, P(a), 128, P(a), 1, 8, 1, 64, ctypes.c_float(0.1), None)
+    assert rc == 4
+    # logprob rows not a multiple of N
+    rc = lib.ospo_logprob_fwd(P(a), 64, P(a), 10, 3, P(a), P(a), P(a), None)
+    assert rc == 1
+    # nt tile heuristic: 160-row tiles at M ~ 4.8k (quantisation over 256 CUs)
+    assert lib.ospo_gemm_nt_tile(4800, 4096) == 160
+    assert lib.ospo_gemm_nt_tile(4608, 16384) == 256
+    assert lib.ospo_gemm_nt_tile(100, 192) == 64
+
+
+def test_lora_layout_7b():
+    from ospo_amd.lora import LoraLayout, peft_key
+    lay = LoraLayout(30, 4096, 11008, 16)
+    assert lay.numel == 37_478_400  # 37.48 M LoRA params at r=16
+    sl = lay.slices()
+    assert len(sl) == 30 * 7 * 2
+    offs = sorted((o, s[0] * s[1]) for _, o, s in sl)
+    pos = 0
+    for o, n in offs:  # contiguous, non-overlapping
+        assert o == pos
+        pos += n
+    assert pos == lay.numel
+    g = lay.groups["qkv"]
+    assert g.Rp == 64 and g.a_off == 0
+    assert peft_key("layers.3.q_proj.lora_A") == \
+        "model.language_model.base_model.model.model.layers.3.self_attn.q_proj.lora_A.default.weight"
+    assert peft_key("layers.0.down_proj.lora_B").endswith("layers.0.mlp.down_proj.lora_B.default.weight")
+    lay32 = LoraLayout(30, 4096, 11008, 32)
+    assert lay32.groups["qkv"].Rp == 128 and lay32.numel == 2 * lay.numel
+
+
+def test_lora_flat_roundtrip_matches_oracle_names():
+    from oracle import simpo_ref as O
+    from ospo_amd.lora import LoraLayout
+    dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=64, img_vocab=256, gen_head_dim=256)
+    w = O.init_lora(dims, seed=4, dtype=torch.bfloat16)
+    lay = LoraLayout(2, 256, 512, 16)
+    flat = torch.zeros(lay.numel, dtype=torch.bfloat16)
+    lay.to_flat(w, flat)
+    back = lay.from_flat(flat)
+    assert set(back) == set(w)
+    for k in w:
+        assert torch.equal(back[k], w[k])
+    # stacked A of a group == packed Acat rows (dA lands in place)
+    g = lay.groups["qkv"]
+    blk = flat[g.a_off:g.a_off + 3 * 16 * 256].view(48, 256)
+    assert torch.equal(blk, torch.cat([w[f"layers.0.{p}.lora_A"] for p in ("q_proj", "k_proj", "v_proj")]))
+
+
+def test_build_config_dotlist_and_aliases(tmp_path):
+    from ospo_amd.config import build_config, save_config
+    cfg = build_config(os.path.join(ROOT, "configs", "step5.yaml"),
+                       argv=["experiment.max_training_steps=3", "lora.lora_rank=16", "base.exp_name=x",
+                             "optimizer.betas=[0.9,0.99]", "base.resume=null"])
+    assert cfg.experiment.max_training_steps == 3 and cfg.lora.lora_rank == 16
+    assert cfg.use_lora is True and cfg.use_peft is True  # alias (SURVEY §5 defect i)
+    assert cfg.optimizer.betas == [0.9, 0.99] and cfg.base.resume is None
+    assert cfg["algo"]["beta"] == 10
+    p = save_config(str(tmp_path), cfg)
+    assert json.load(open(p))["lora"]["lora_rank"] == 16  # JSON text in config.yaml, like common.py:102-108
+
+
+def test_preference_dataset_prompt_and_collate():
+    from ospo_amd.data import PreferenceDataset, SyntheticTokenizer, sft_prompt
+    assert sft_prompt("A black umbrella") == "User: A black umbrella\n\nAssistant:<begin_of_image>"
+    ds = PreferenceDataset(seed=42, data_path=os.path.join(ROOT, "tests", "golden", "train_step4.json"),
+                           tokenizer=SyntheticTokenizer(), num_samples=4)
+    assert len(ds) == 4
+    items = [ds[i] for i in range(4)]
+    ids, text, ch, rj = ds.collate_fn(items)
+    assert all(t.dtype == torch.int32 and t.shape[0] == 1 for t in text)
+    assert all(c.shape == (1, 576) and int(c.max()) < 16384 for c in ch)
+    again = ds[0]
+    assert torch.equal(again[2], items[0][2])  # deterministic tokens
+    with pytest.raises(ValueError):
+        ds.decode({"item_id": "x", "prompt": "p"})
+
+
+def test_algorithmic_flops_match_survey():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert abs(bench.algorithmic_flops_per_pair() / 1e12 - 30.37) < 0.01
+
+
+def test_checkpoint_roundtrip_cpu(tmp_path):
+    """Lightning .ckpt layout with peft keys; resume restores adapters and AdamW moments."""
+    from ospo_amd.ckpt import load_checkpoint, save_checkpoint, step_ckpt_name
+    from ospo_amd.lora import LoraLayout, peft_key
+    from ospo_amd.wrapper.train import ConstantLR, FusedLoraAdamW
+
+    class StubEngine:
+        def __init__(self):
+            self.layout = LoraLayout(2, 256, 512, 16)
+            self.lora = torch.randn(self.layout.numel).to(torch.bfloat16)
+            self.exp_avg = torch.randn(self.layout.numel).to(torch.bfloat16)
+            self.exp_avg_sq = torch.rand(self.layout.numel).to(torch.bfloat16)
+            self.opt_step = 7
+
+        def lora_tensors(self):
+            return self.layout.from_flat(self.lora)
+
+        def pack_lora(self):
+            pass
+
+    e = StubEngine()
+    opt = FusedLoraAdamW(e, 4e-5, (0.9, 0.95), 1e-8, 0.0, 1.0)
+    sched = ConstantLR(opt)
+    p = save_checkpoint(str(tmp_path / step_ckpt_name(5)), e, opt, sched, epoch=1, global_step=5)
+    assert os.path.basename(p) == "step=000005.ckpt"
+    ck = torch.load(p, weights_only=True)
+    for k in ("state_dict", "optimizer_states", "lr_schedulers", "epoch", "global_step", "pytorch-lightning_version"):
+        assert k in ck
+    assert peft_key("layers.1.up_proj.lora_B") in ck["state_dict"]
+    e2 = StubEngine()
+    opt2 = FusedLoraAdamW(e2, 4e-5, (0.9, 0.95), 1e-8, 0.0, 1.0)
+    load_checkpoint(p, e2, opt2, ConstantLR(opt2))
+    assert torch.equal(e2.lora, e.lora) and torch.equal(e2.exp_avg_sq, e.exp_avg_sq) and e2.opt_step == 7
