@@ -53,6 +53,12 @@ int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int
                       const void* bias, const void* residual, int ldr, void* C, int ldc,
                       hipStream_t stream);
 
+/* Tuning knob (process-global) selecting the NT GEMM schedule: 0 = register-double-
+ * buffered fragments, 3-deep LDS-DMA ring (160-row tiles), XCD-aware tile order,
+ * s_setprio (default); 1 = simple double-buffered; 2 = 0 without the XCD remap;
+ * 3 = 0 with a 2-deep ring; 4 = 0 without s_setprio. */
+int ospo_set_gemm_variant(int variant);
+
 /* Row count of the tile ospo_gemm_nt_bf16 uses for an M x N output (256, 160 or 64). */
 int ospo_gemm_nt_tile(int M, int N);
 

@@ -21,6 +21,7 @@ SIGNATURES = {
     "ospo_abi_version": [],
     "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P],
     "ospo_gemm_nt_tile": [I, I],
+    "ospo_set_gemm_variant": [I],
     "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],
     "ospo_f32_to_bf16": [P, P, L, F, P],
     "ospo_rmsnorm_fwd": [P, P, P, P, I, I, F, P],

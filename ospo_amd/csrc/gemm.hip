@@ -267,20 +267,208 @@ int launch(const GemmArgs& a, hipStream_t s) {
   return OSPO_OK;
 }
 
-// Pick the bf16 NT tile: the one whose (waves of 256 CUs) x (rows per tile) is
-// smallest -- tile-count quantisation dominates at M ~ 5k (SURVEY §8d shapes).
+// ----------------------------------------------------------------------------
+// Pipelined NT GEMM helpers (8 waves 2 x 4, tile BM x 256, BK = 64).
+//  * LDS-DMA loads of later tiles stay in flight across a raw s_barrier (counted
+//    vmcnt; __syncthreads() would drain them -- guide "Pipelining across barriers");
+//  * XCD-aware tile order: block b runs on XCD b % 8 (round-robin dispatch), so each
+//    XCD gets a contiguous range of tile ids, grouped GM tile-rows deep so its
+//    co-resident tiles share operand panels in its L2 (T1); speed only, never results;
+//  * s_setprio(1) around each MFMA cluster (T5).
+// Wait until at most n of this wave's vector-memory ops are outstanding.  n is wave-uniform;
+// rounding it DOWN to a supported constant only waits longer, so it is always safe.
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if (n == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ----------------------------------------------------------------------------
+// v3: the barrier sits BETWEEN the two k-substep MFMA clusters of a K-tile, and the
+// MFMA fragments are double-buffered in registers, so the cluster after each barrier
+// runs on fragments read before it while the next tile's first fragments load:
+//   read(t,1)->SB | MFMA(SA) | vmcnt(0) lgkmcnt(0) s_barrier | stage(t+2) | read(t+1,0)->SA | MFMA(SB)
+// Two LDS buffers; tile t+2 streams into tile t's buffer right after the barrier that
+// certifies every wave finished reading it.  Loads get one K-tile of slack.
+template <int FM, int STAGES, bool REMAP, bool PRIO>
+__global__ __launch_bounds__(512) void gemm_nt_v3_kernel(const GemmArgs args, int tiles_m, int tiles_n) {
+  constexpr int WN = 4, FN = 4, NW = 8;
+  constexpr int BM = 2 * FM * 16, BN = WN * FN * 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int PA = A_BYTES / 1024, PT = PA + B_BYTES / 1024;
+  constexpr int CPITCH = BN * 2 + 16;
+  constexpr int LDS_BYTES = (STAGES * STAGE > BM * CPITCH) ? STAGES * STAGE : BM * CPITCH;
+  static_assert(LDS_BYTES <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int ppw = (PT - wave + NW - 1) / NW;  // LDS-DMA pieces this wave issues per tile
+
+  int m0, n0;
+  if (REMAP) {
+    const int nwg = gridDim.x, wg = blockIdx.x;
+    const int xcd = wg & 7, slot = wg >> 3, q = nwg >> 3, r = nwg & 7;
+    const int tid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+    constexpr int GM = 4;
+    const int gsize = GM * tiles_n;
+    const int first_m = (tid / gsize) * GM;
+    const int gm = min(tiles_m - first_m, GM);
+    const int within = tid % gsize;
+    m0 = (first_m + within % gm) * BM;
+    n0 = (within / gm) * BN;
+  } else {
+    m0 = (blockIdx.x / tiles_n) * BM;
+    n0 = (blockIdx.x % tiles_n) * BN;
+  }
+  const int nt1 = args.K / BK, nt = nt1 + args.K2 / BK;
+
+  const bf16* const pA = args.A;
+  const bf16* const pB = args.B;
+  const bf16* const pA2 = args.A2;
+  const bf16* const pB2 = args.B2;
+  const int lda1 = args.lda, ldb1 = args.ldb, lda2 = args.lda2, ldb2 = args.ldb2;
+  const int Mlast = args.M - 1, Nlast = args.N - 1;
+  const int rr8 = lane >> 3, c8 = lane & 7;
+  auto stage = [&](int t, int buf) {
+    char* la = smem + buf * STAGE;
+    char* lb = la + A_BYTES;
+    const bool ext = t >= nt1;
+    const bf16* Ab = ext ? pA2 : pA;
+    const bf16* Bb = ext ? pB2 : pB;
+    const int lda = ext ? lda2 : lda1;
+    const int ldb = ext ? ldb2 : ldb1;
+    const int k0 = (ext ? t - nt1 : t) * BK;
+#pragma unroll
+    for (int p = wave; p < PT; p += NW) {
+      if (p < PA) {
+        const int row = p * 8 + rr8;
+        const int g = min(m0 + row, Mlast);
+        glds16(Ab + (long)g * lda + k0 + ((c8 ^ (row & 7)) << 3), la + p * 1024);
+      } else {
+        const int row = (p - PA) * 8 + rr8;
+        const int g = min(n0 + row, Nlast);
+        glds16(Bb + (long)g * ldb + k0 + ((c8 ^ (row & 7)) << 3), lb + (p - PA) * 1024);
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 aA[FM], bA[FN], aB[FM], bB[FN];
+  auto rd = [&](const char* buf, int s, bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, false>(buf, wm * FM * 16 + i * 16, s, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, false>(buf + A_BYTES, wn * FN * 16 + j * 16, s, lane);
+  };
+  auto mm = [&](const bf16x8 (&af)[FM], const bf16x8 (&bfr)[FN]) {
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: tiles 0 .. STAGES-1 in flight, wait for tile 0
+  for (int s0 = 0; s0 < STAGES && s0 < nt; ++s0) stage(s0, s0);
+  wait_vmcnt(ppw * (min(STAGES, nt) - 1));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  rd(smem, 0, aA, bA);
+  for (int t = 0; t < nt; ++t) {
+    const char* cur = smem + (t % STAGES) * STAGE;
+    rd(cur, 1, aB, bB);
+    mm(aA, bA);
+    __builtin_amdgcn_sched_barrier(0);
+    // tile t+1 must have landed; tiles t+2 .. min(t+STAGES, nt)-1 may stay in flight
+    wait_vmcnt(ppw * max(0, min(t + STAGES, nt) - t - 2));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // tile t's buffer is free (its fragments are in registers): refill it with tile t+STAGES
+    if (t + STAGES < nt) stage(t + STAGES, t % STAGES);
+    if (t + 1 < nt) rd(smem + ((t + 1) % STAGES) * STAGE, 0, aA, bA);
+    mm(aB, bB);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const int g = lane >> 4, l16 = lane & 15;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nl = wn * FN * 16 + j * 16 + 4 * g;
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (args.bias) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) b4[qq] = bf2f(args.bias[n0 + nl + qq]);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = wm * FM * 16 + i * 16 + l16;
+      const f32x4 v = acc[i][j];
+      uint2 pk;
+      pk.x = pack2(v[0] * args.alpha + b4[0], v[1] * args.alpha + b4[1]);
+      pk.y = pack2(v[2] * args.alpha + b4[2], v[3] * args.alpha + b4[3]);
+      *reinterpret_cast<uint2*>(smem + ml * CPITCH + nl * 2) = pk;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  bf16* C = reinterpret_cast<bf16*>(args.C);
+  for (int c = threadIdx.x; c < BM * CPR; c += NW * 64) {
+    const int rr = c / CPR, cc = c % CPR;
+    const int m = m0 + rr;
+    if (m >= args.M) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(smem + rr * CPITCH + cc * 16);
+    if (args.res) {
+      const u32x4 rv = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + cc * 8);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float lo = bits2f(v[qq] & 0xffff) + bits2f(rv[qq] & 0xffff);
+        const float hi = bits2f(v[qq] >> 16) + bits2f(rv[qq] >> 16);
+        v[qq] = pack2(lo, hi);
+      }
+    }
+    *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8) = v;
+  }
+}
+
+template <int FM, int STAGES, bool REMAP, bool PRIO>
+int launch_v3(const GemmArgs& a, hipStream_t s) {
+  constexpr int BM = 2 * FM * 16, BN = 256;
+  if (a.N % BN) return OSPO_ERR_SHAPE;
+  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
+  hipLaunchKernelGGL((gemm_nt_v3_kernel<FM, STAGES, REMAP, PRIO>), dim3(tm * tn), dim3(512), 0, s, a, tm, tn);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+int g_gemm_variant = 0;  // 0 = v3 (XCD remap, setprio), 1 = simple, 2 = v3 no remap, 3 = v3 no prio, 4 = 3-stage
+
+// Pick the bf16 NT tile: minimise (waves of 256 CUs) x (relative time per tile).  A
+// 160 x 256 tile costs ~1.1x a 256 x 256 tile per row (more LDS-DMA issue per MFMA,
+// measured on the step's shapes), but 256-row tiles quantise badly at M ~ 5k, N = 4096
+// (304 tiles = 1.19 waves).
 int pick_nt_tile(int M, int N) {
   if (N % 256) return 64;
   const int cus = 256;
-  long best = -1;
-  int pick = 256;
-  for (int bm : {256, 160}) {
-    const long tiles = (long)((M + bm - 1) / bm) * (N / 256);
-    const long waves = (tiles + cus - 1) / cus;
-    const long cost = waves * bm;
-    if (best < 0 || cost < best) { best = cost; pick = bm; }
-  }
-  return pick;
+  const long t256 = (long)((M + 255) / 256) * (N / 256);
+  const long t160 = (long)((M + 159) / 160) * (N / 256);
+  const double c256 = (double)((t256 + cus - 1) / cus) * 256.0;
+  const double c160 = (double)((t160 + cus - 1) / cus) * 160.0 * 1.1;
+  return c256 <= c160 ? 256 : 160;
 }
 
 }  // namespace
@@ -300,11 +488,28 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     return OSPO_ERR_ALIGN;
   GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
              M, N, K, K2, alpha, (const bf16*)bias, (const bf16*)residual, ldr, C, ldc, 1, 0, 0};
-  switch (pick_nt_tile(M, N)) {
-    case 256: return launch<2, 4, 8, 4, false, false, EPI_BF16>(a, stream);
-    case 160: return launch<2, 4, 5, 4, false, false, EPI_BF16>(a, stream);
-    default: return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
+  const int tile = pick_nt_tile(M, N);
+  // default schedule per tile (tools/gemm_bench.py A/B on the step's shapes): 160-row
+  // tiles run fastest on the simple double-buffered loop, 256-row tiles on v3
+  if (g_gemm_variant == 1 || tile == 64 || (g_gemm_variant == 0 && tile == 160)) {
+    switch (tile) {
+      case 256: return launch<2, 4, 8, 4, false, false, EPI_BF16>(a, stream);
+      case 160: return launch<2, 4, 5, 4, false, false, EPI_BF16>(a, stream);
+      default: return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
+    }
   }
+  switch (g_gemm_variant) {
+    case 2: return tile == 256 ? launch_v3<8, 2, false, true>(a, stream) : launch_v3<5, 3, false, true>(a, stream);
+    case 3: return tile == 256 ? launch_v3<8, 2, true, true>(a, stream) : launch_v3<5, 2, true, true>(a, stream);
+    case 4: return tile == 256 ? launch_v3<8, 2, true, false>(a, stream) : launch_v3<5, 3, true, false>(a, stream);
+    default: return tile == 256 ? launch_v3<8, 2, true, true>(a, stream) : launch_v3<5, 3, true, true>(a, stream);
+  }
+}
+
+extern "C" int ospo_set_gemm_variant(int v) {
+  if (v < 0 || v > 4) return OSPO_ERR_ARG;
+  g_gemm_variant = v;
+  return OSPO_OK;
 }
 
 extern "C" int ospo_gemm_nt_tile(int M, int N) { return pick_nt_tile(M, N); }

@@ -1,0 +1,63 @@
+"""A/B the NT GEMM variants on the SimPO step's exact shapes (M = 2B*T = 4800 rows at 4
+pairs, LoRA K-extension of 64) against torch.matmul (hipBLASLt), interleaved rounds in
+one process (cdna_hip_programming.md rule 24).  Prints one JSON line per shape."""
+import json
+import sys
+import os
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ospo_amd import ops
+from ospo_amd._lib import call
+
+M = int(os.environ.get("GB_M", "4800"))
+SHAPES = [  # name, M, N, K, K2
+    ("qkv_fwd", M, 12288, 4096, 64), ("o_fwd", M, 4096, 4096, 64), ("gu_fwd", M, 22016, 4096, 64),
+    ("down_fwd", M, 4096, 11008, 64), ("down_dx", M, 11008, 4096, 64), ("gu_dx", M, 4096, 22016, 64),
+    ("qkv_dx", M, 4096, 12288, 64), ("gh2_fwd", 4608, 16384, 4096, 0), ("gh2_dx", 4608, 4096, 16384, 0),
+]
+VARIANTS = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1").split(",")]
+ROUNDS, ITERS = 5, 10
+
+
+def timeit(fn):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    e0.record()
+    for _ in range(ITERS):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / ITERS
+
+
+def main():
+    torch.manual_seed(0)
+    for name, m, n, k, k2 in SHAPES:
+        a = (torch.rand(m, k, device="cuda") * 2 - 1).bfloat16()
+        b = (torch.rand(n, k, device="cuda") * 2 - 1).bfloat16()
+        a2 = (torch.rand(m, k2, device="cuda") * 2 - 1).bfloat16() if k2 else None
+        b2 = (torch.rand(n, k2, device="cuda") * 2 - 1).bfloat16() if k2 else None
+        out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        ref = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        res = {f"v{v}": [] for v in VARIANTS}
+        res["hipblaslt"] = []
+        for _ in range(ROUNDS):
+            for v in VARIANTS:
+                call("ospo_set_gemm_variant", v)
+                res[f"v{v}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
+            res["hipblaslt"].append(timeit(lambda: torch.matmul(a, b.t(), out=ref)))
+        call("ospo_set_gemm_variant", 0)
+        ops.gemm_nt(a, b, out, a2=a2, b2=b2)
+        exp = a.float() @ b.float().t() + (a2.float() @ b2.float().t() if k2 else 0)
+        err = float((out.float() - exp).norm() / exp.norm())
+        fl = 2.0 * m * n * k
+        line = {"shape": name, "M": m, "N": n, "K": k, "K2": k2, "tile": ops.gemm_nt_tile(m, n), "relerr": err}
+        for kk, ts in res.items():
+            t = sorted(ts)[len(ts) // 2]
+            line[kk] = {"ms": round(t, 4), "tflops": round(fl / t / 1e9, 1)}
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
