@@ -111,8 +111,9 @@ int ospo_swiglu_bwd(const void* dh, int ld_dh, const void* gu, int ld_gu, void* 
  * (scores * scale, causal mask, fp32 softmax), flash-style on MFMA.
  * q/k/v/o rows s*T+t, head h at column offset h*head_dim.  lse: fp32
  * [S, H, T] (natural-log sum-exp of the scaled scores).  head_dim == 128.
- * bwd needs workspaces: delta fp32 [S*H*T], dq_acc fp32 [S*T, H*head_dim]
- * (zeroed by the function).  dq/dk/dv are written (bf16) into dqkv. */
+ * bwd needs the workspace delta fp32 [S*H*T]; dq_acc_ws is reserved (ignored,
+ * may be NULL -- dQ is accumulated in registers, no atomics).  dq/dk/dv are
+ * written (bf16) into dqkv. */
 int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
                         int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
                         hipStream_t stream);
@@ -172,9 +173,22 @@ int ospo_simpo_bwd(const float* logps, int B, float beta, float gamma_beta_ratio
  *   Acat [Rp][Kin]   rows j < nmods*r = stacked lora_A, rest zero
  *   AcatT[Kin][Rp]   its transpose
  *   Bcat [nmods*Nmod][Rp] block-diagonal stacked lora_B
+ *   BT   [nmods*r][Nmod]  per-module lora_B^T (optional, may be NULL)
  * Rp = roundup(nmods*r, 64). */
 int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int Kin, int Nmod,
-                   int Rp, void* Acat, void* AcatT, void* Bcat, hipStream_t stream);
+                   int Rp, void* Acat, void* AcatT, void* Bcat, void* BT, hipStream_t stream);
+
+/* Skinny LoRA products (peft lora.Linear, y += s B(A x)) -- bf16 out, no
+ * atomics.  For n-tile j < n_tiles (columns 16j .. 16j+15):
+ *   out[m][16j+c] = scale * sum_{k<K} A[m][j*a_koff + k] * Bt[16j+c][k]
+ * Bt rows >= b_rows read as zero; rows M..M_out-1 and columns
+ * 16*n_tiles..out_cols-1 of out are written zero.  n_tiles <= 4, K % 32 == 0.
+ *   u = s x A_cat^T : A = x [M, K], Bt = A_cat [Rp, K], a_koff = 0
+ *   g = s dy B      : A = dy [M, nmods*Nmod], Bt = BT [nmods*r, Nmod],
+ *                     K = a_koff = Nmod, n_tiles = nmods (r == 16) */
+int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out,
+                     int K, int n_tiles, int a_koff, float scale, void* out, int ldo, int out_cols,
+                     hipStream_t stream);
 
 /* ------------------------------------------------------------ optimizer ---
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip

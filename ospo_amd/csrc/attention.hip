@@ -10,9 +10,12 @@
 // feeds P.V directly as the B operand (k order permuted identically on both
 // sides).  V^T fragments come from ds_read_b64_tr_b16 (hardware transpose).
 //
-// Backward: workgroup = 4 waves = 64 keys; each wave owns 16 keys, keeps dK^T
-// and dV^T of them in registers and sweeps the query tiles at/after its block.
-// dQ is summed across key blocks with fp32 atomics (dq_acc workspace).
+// Backward: two atomic-free kernels.  dK/dV: workgroup = 64 keys, each wave
+// owns 16 keys (dK^T, dV^T in registers) and sweeps the query tiles at/after
+// its block.  dQ: workgroup = 64 query rows sweeping key tiles 0..qb, the
+// forward's shape, dQ^T in registers.  (S, dP are recomputed by both: 7 MFMA
+// products instead of 5, but no fp32 atomics -- at T=600 the atomic dQ
+// traffic alone was ~460 MB/call.)
 //
 // LDS images are [row][128 x bf16] (256-B rows) with 16-B chunk swizzle
 // chunk ^ 2*(row & 7): conflict-free for both the ds_read_b128 row reads and
@@ -99,7 +102,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
+  const int qb = gridDim.x - 1 - blockIdx.x;  // longest key sweep first
+  const int h = blockIdx.y, s = blockIdx.z;
   const int g = lane >> 4, l16 = lane & 15;
   const long rowbase = (long)s * T;
   const int rows_lim_seq = T;  // clamp inside the sequence
@@ -226,29 +230,26 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict_
   if (lane == 0) delta[((long)s * H + h) * T + t] = acc;
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
-                                                       const bf16* __restrict__ dout, int ldd,
-                                                       const float* __restrict__ lse, const float* __restrict__ delta,
-                                                       float* __restrict__ dq_acc, bf16* __restrict__ dqkv, int ldg,
-                                                       int T, int H, float scale) {
-  // LDS: K image | Q image | dO image | dS image [64 q][64 key] | lse[64] | delta[64]
-  constexpr int DS_PITCH = 64 * 2 + 16;
-  __shared__ __attribute__((aligned(16))) char smem[3 * TILE_BYTES + 64 * DS_PITCH + 2 * 64 * 4];
-  char* Ks = smem;
-  char* Qs = smem + TILE_BYTES;
-  char* Os = smem + 2 * TILE_BYTES;
-  char* Ss = smem + 3 * TILE_BYTES;
-  float* Ls = reinterpret_cast<float*>(Ss + 64 * DS_PITCH);
-  float* Dl = Ls + 64;
+// dK / dV: workgroup = 4 waves = 64 keys of one (sequence, head); each wave
+// owns 16 keys (K, V fragments in registers, dK^T dV^T accumulators) and
+// sweeps the query tiles at/after its block.  Q / dO tiles (+ lse, delta) are
+// double-buffered in LDS through global_load_lds; no atomics.
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
+                                                            int vc, const bf16* __restrict__ dout, int ldd,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                            int ldg, int T, int H, float scale) {
+  // LDS: [Q | dO] x 2 buffers, then lse[2][64], delta[2][64]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES + 4 * 64 * 4];
+  float* Lsb = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int kb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
+  const int kb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;  // kb = 0 (longest sweep) dispatched first
   const int g = lane >> 4, l16 = lane & 15;
   const long rowbase = (long)s * T;
   const int nq = (T + QB - 1) / QB;
 
-  // this wave's 16 keys; lane l16 owns key kb*64 + wave*16 + l16 (for B fragments)
   const int key_l = kb * KB + wave * 16 + l16;
   const int key_c = key_l < T ? key_l : T - 1;
   bf16x8 kf[4], vf[4];
@@ -261,8 +262,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ 
       vf[d] = *reinterpret_cast<const bf16x8*>(vp + 32 * d + 8 * g);
     }
   }
-  stage64(qkv + rowbase * ldq + kc + h * HD, ldq, kb * KB, T, 0, Ks, wave, lane);
-
   f32x4 dk[8], dv[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { dk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -272,19 +271,31 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ 
   const float* lse_sh = lse + ((long)s * H + h) * T;
   const float* del_sh = delta + ((long)s * H + h) * T;
 
-  for (int qt = kb; qt < nq; ++qt) {
-    __syncthreads();  // previous tile's LDS reads done
+  auto stage = [&](int qt, int b) {
+    char* Qs = smem + b * 2 * TILE_BYTES;
     stage64(qbase, ldq, qt * QB, T, 0, Qs, wave, lane);
-    stage64(obase, ldd, qt * QB, T, 0, Os, wave, lane);
-    if (threadIdx.x < 64) {
-      const int q = qt * QB + threadIdx.x;
-      Ls[threadIdx.x] = q < T ? lse_sh[q] : 0.f;
-      Dl[threadIdx.x] = q < T ? del_sh[q] : 0.f;
+    stage64(obase, ldd, qt * QB, T, 0, Qs + TILE_BYTES, wave, lane);
+    if (wave < 2) {  // 64 lanes x 4 B: lse (wave 0) / delta (wave 1) of the tile's 64 queries
+      int q = qt * QB + lane;
+      q = q < T ? q : T - 1;
+      const float* src = (wave == 0 ? lse_sh : del_sh) + q;
+      __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(Lsb + (wave * 2 + b) * 64), 4, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  };
 
-    // S[q][key] and dP[q][key] for 4 q sub-tiles; lane: key = l16, q = 16a + 4g + j
+  stage(kb, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int qt = kb; qt < nq; ++qt) {
+    const int b = (qt - kb) & 1;
+    if (qt + 1 < nq) stage(qt + 1, b ^ 1);
+    const char* Qs = smem + b * 2 * TILE_BYTES;
+    const char* Os = Qs + TILE_BYTES;
+    const float* Ls = Lsb + b * 64;
+    const float* Dl = Lsb + (2 + b) * 64;
+
+    // S[q][key], dP[q][key] for 4 q sub-tiles; lane: key = l16, q = 16a + 4g + j
     f32x4 sv[4], dp[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -296,7 +307,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ 
         dp[a] = MFMA(frag_row(Os, 16 * a, d, lane), vf[d], dp[a]);
       }
     }
-    // P and dS (fp32), masks
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -306,9 +316,9 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ 
         float p = __expf(round_bf(round_bf(sv[a][j]) * scale) - Ls[ql]);
         if (q >= T || key_l > q || key_l >= T) p = 0.f;
         sv[a][j] = p;
-        dp[a][j] = p * (dp[a][j] - Dl[ql]);
+        dp[a][j] = p * (dp[a][j] - Dl[ql]) * scale;
       }
-    // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
+    // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . (scale dS)[q][key]
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const bf16x8 pb = pack_perm(sv[2 * u], sv[2 * u + 1]);
@@ -319,47 +329,18 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ 
         dk[dt] = MFMA(frag_tr_perm(Qs, 32 * u, 16 * dt, lane), sb, dk[dt]);
       }
     }
-    // dS (bf16, scaled) -> LDS image [q][key] for the dQ product
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ql = 16 * a + 4 * g + j;
-        *reinterpret_cast<bf16*>(Ss + ql * DS_PITCH + (wave * 16 + l16) * 2) = f2bf(dp[a][j] * scale);
-      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // dQ[q][d] (this wave: 16 q rows) = dS[q][key(64)] . K[key][d]
-    {
-      const int qr0 = wave * 16;
-      f32x4 dq[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ss + (qr0 + l16) * DS_PITCH + (32 * u + 8 * g) * 2);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) dq[dt] = MFMA(af, frag_tr_nat(Ks, 32 * u, 16 * dt, lane), dq[dt]);
-      }
-      // lane: col d = 16dt + l16, rows q = qr0 + 4g + j
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = qt * QB + qr0 + 4 * g + j;
-        if (q >= T) continue;
-        float* dst = dq_acc + (rowbase + q) * (long)(H * HD) + h * HD + l16;
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) atomicAdd(dst + 16 * dt, dq[dt][j]);
-      }
-    }
   }
 
-  // write dK (= scale * dS^T Q), dV: lane holds [d = 16dt + 4g + j][key = l16]
+  // lane holds [d = 16dt + 4g + j][key = l16]
   if (key_l < T) {
     bf16* kp = dqkv + (rowbase + key_l) * ldg + kc + h * HD;
     bf16* vp = dqkv + (rowbase + key_l) * ldg + vc + h * HD;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
       uint2 a, b;
-      a.x = pack2(dk[dt][0] * scale, dk[dt][1] * scale); a.y = pack2(dk[dt][2] * scale, dk[dt][3] * scale);
+      a.x = pack2(dk[dt][0], dk[dt][1]); a.y = pack2(dk[dt][2], dk[dt][3]);
       b.x = pack2(dv[dt][0], dv[dt][1]); b.y = pack2(dv[dt][2], dv[dt][3]);
       *reinterpret_cast<uint2*>(kp + 16 * dt + 4 * g) = a;
       *reinterpret_cast<uint2*>(vp + 16 * dt + 4 * g) = b;
@@ -367,18 +348,103 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16* __restrict__ 
   }
 }
 
-// dq (fp32 workspace) -> bf16 q columns of dqkv
-__global__ void dq_store_kernel(const float* __restrict__ dq_acc, bf16* __restrict__ dqkv, int ldg, int qc,
-                                long rows, int W) {
-  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i >= rows * W) return;
-  const long r = i / W;
-  const int c = i % W;
-  const f32x4 v = *reinterpret_cast<const f32x4*>(dq_acc + i);
-  uint2 pk;
-  pk.x = pack2(v[0], v[1]);
-  pk.y = pack2(v[2], v[3]);
-  *reinterpret_cast<uint2*>(dqkv + r * ldg + qc + c) = pk;
+// dQ: the forward's shape -- workgroup = 64 query rows, each wave 16 rows on
+// the lanes; sweeps key tiles 0..qb with K / V double-buffered in LDS.
+// dS^T[key][q] = P^T (dP^T - delta), dP^T = V . dO^T; dQ^T[d][q] += K^T[d][key] . dS^T.
+// dQ lives in registers for the whole sweep: no atomics, no workspace.
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
+                                                          int vc, const bf16* __restrict__ dout, int ldd,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                          int ldg, int T, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qb = gridDim.x - 1 - blockIdx.x;  // longest sweep first
+  const int h = blockIdx.y, s = blockIdx.z;
+  const int g = lane >> 4, l16 = lane & 15;
+  const long rowbase = (long)s * T;
+
+  const int qrow = qb * QB + wave * 16 + l16;
+  const int qr_c = qrow < T ? qrow : T - 1;
+  bf16x8 qf[4], of[4];
+  {
+    const bf16* qp = qkv + (rowbase + qr_c) * ldq + qc + h * HD;
+    const bf16* op = dout + (rowbase + qr_c) * ldd + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      qf[d] = *reinterpret_cast<const bf16x8*>(qp + 32 * d + 8 * g);
+      of[d] = *reinterpret_cast<const bf16x8*>(op + 32 * d + 8 * g);
+    }
+  }
+  const float lse_q = lse[((long)s * H + h) * T + qr_c];
+  const float del_q = delta[((long)s * H + h) * T + qr_c];
+
+  f32x4 dq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int n_kv = qb + 1;
+  const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
+  const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
+  stage64(kbase, ldq, 0, T, 0, smem, wave, lane);
+  stage64(vbase, ldq, 0, T, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < n_kv; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < n_kv) {
+      char* nb = smem + (buf ^ 1) * 2 * TILE_BYTES;
+      stage64(kbase, ldq, (kt + 1) * KB, T, 0, nb, wave, lane);
+      stage64(vbase, ldq, (kt + 1) * KB, T, 0, nb + TILE_BYTES, wave, lane);
+    }
+    const char* Ks = smem + buf * 2 * TILE_BYTES;
+    const char* Vs = Ks + TILE_BYTES;
+
+    f32x4 st[4], dpt[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dpt[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        st[t] = MFMA(frag_row(Ks, 16 * t, d, lane), qf[d], st[t]);
+        dpt[t] = MFMA(frag_row(Vs, 16 * t, d, lane), of[d], dpt[t]);
+      }
+    }
+    const bool diag = (kt == qb) || ((kt + 1) * KB > T);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float p = __expf(round_bf(round_bf(st[t][j]) * scale) - lse_q);
+        if (diag) {
+          const int key = kt * KB + 16 * t + 4 * g + j;
+          if (key > qrow || key >= T) p = 0.f;
+        }
+        st[t][j] = p * (dpt[t][j] - del_q) * scale;
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8 sb = pack_perm(st[2 * u], st[2 * u + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) dq[dt] = MFMA(frag_tr_perm(Ks, 32 * u, 16 * dt, lane), sb, dq[dt]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (qrow < T) {
+    bf16* dp = dqkv + (rowbase + qrow) * ldg + qc + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      uint2 pk;
+      pk.x = pack2(dq[dt][0], dq[dt][1]);
+      pk.y = pack2(dq[dt][2], dq[dt][3]);
+      *reinterpret_cast<uint2*>(dp + 16 * dt + 4 * g) = pk;
+    }
+  }
 }
 
 }  // namespace
@@ -402,25 +468,24 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
                                    int ld_o, const void* dout, int ld_do, const float* lse, float* delta_ws,
                                    float* dq_acc_ws, void* dqkv, int ld_dqkv, int S, int T, int n_heads,
                                    int head_dim, float scale, hipStream_t stream) {
-  if (!qkv || !o || !dout || !lse || !delta_ws || !dq_acc_ws || !dqkv) return OSPO_ERR_ARG;
+  (void)dq_acc_ws;  // reserved (ABI v1 atomic-dQ workspace); may be NULL
+  if (!qkv || !o || !dout || !lse || !delta_ws || !dqkv) return OSPO_ERR_ARG;
   if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
   if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || ld_do % 8 || ld_dqkv % 8) return OSPO_ERR_SHAPE;
-  if (!aligned16(qkv) || !aligned16(o) || !aligned16(dout) || !aligned16(dqkv) || !aligned16(dq_acc_ws))
-    return OSPO_ERR_ALIGN;
+  if (q_col % 8 || k_col % 8 || v_col % 8) return OSPO_ERR_SHAPE;
+  if (!aligned16(qkv) || !aligned16(o) || !aligned16(dout) || !aligned16(dqkv)) return OSPO_ERR_ALIGN;
   const long rows = (long)S * T;
-  const int W = n_heads * HD;
-  if (hipMemsetAsync(dq_acc_ws, 0, rows * W * sizeof(float), stream) != hipSuccess) return OSPO_ERR_HIP;
   const long items = rows * n_heads;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((items + 3) / 4), dim3(256), 0, stream, (const bf16*)o, ld_o,
                      (const bf16*)dout, ld_do, delta_ws, S, T, n_heads);
   OSPO_CHECK_LAUNCH();
   dim3 grid((T + KB - 1) / KB, n_heads, S);
-  hipLaunchKernelGGL(attn_bwd_kernel, grid, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
-                     (const bf16*)dout, ld_do, lse, delta_ws, dq_acc_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+                     v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale);
   OSPO_CHECK_LAUNCH();
-  const long n4 = rows * W / 4;
-  hipLaunchKernelGGL(dq_store_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream, dq_acc_ws, (bf16*)dqkv,
-                     ld_dqkv, q_col, rows, W);
+  dim3 gq((T + QB - 1) / QB, n_heads, S);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+                     (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

@@ -293,10 +293,10 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 //   read(t,1)->SB | MFMA(SA) | vmcnt(0) lgkmcnt(0) s_barrier | stage(t+2) | read(t+1,0)->SA | MFMA(SB)
 // Two LDS buffers; tile t+2 streams into tile t's buffer right after the barrier that
 // certifies every wave finished reading it.  Loads get one K-tile of slack.
-template <int FM, int STAGES, bool REMAP, bool PRIO>
-__global__ __launch_bounds__(512) void gemm_nt_v3_kernel(const GemmArgs args, int tiles_m, int tiles_n) {
-  constexpr int WN = 4, FN = 4, NW = 8;
-  constexpr int BM = 2 * FM * 16, BN = WN * FN * 16;
+template <int FM, int STAGES, bool REMAP, bool PRIO, int WM = 2, int WN = 4, int FN = 4>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_nt_v3_kernel(const GemmArgs args, int tiles_m, int tiles_n) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int PA = A_BYTES / 1024, PT = PA + B_BYTES / 1024;
   constexpr int CPITCH = BN * 2 + 16;
@@ -445,12 +445,186 @@ __global__ __launch_bounds__(512) void gemm_nt_v3_kernel(const GemmArgs args, in
   }
 }
 
-template <int FM, int STAGES, bool REMAP, bool PRIO>
-int launch_v3(const GemmArgs& a, hipStream_t s) {
+// ----------------------------------------------------------------------------
+// v4: BK = 32 stages in a deep ring.  The per-CU L2 -> LDS rate grows with the bytes
+// in flight (MI355X_MICROARCH.md "gather into LDS": ~70 GB/s/CU L2-resident, ~33 from
+// the Infinity Cache at 72 KiB in flight) and a 256 x 256 tile at full MFMA rate needs
+// ~77 GB/s/CU.  64-deep stages cap the ring at 2 x 64 KiB (one tile in flight); 32-deep
+// stages of 32 KiB give a 4-6 deep ring with 3-5 tiles in flight.
+// LDS image [rows][32 k] = 64-B rows; 16-B chunk c of row r lives at c ^ h(r),
+// h(r) = (-(r >> 2)) & 3, conflict-free for all four ds_read_b128 lane groups.
+constexpr int BK4 = 32;
+__device__ __forceinline__ int off32(int r, int c) { return r * 64 + ((c ^ ((-(r >> 2)) & 3)) << 4); }
+
+__device__ __forceinline__ void wait_vmcnt_exact(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;  // n >= 15: waiting for more is safe
+  }
+}
+
+template <int FM, int STAGES>
+__global__ __launch_bounds__(512) void gemm_nt_v4_kernel(const GemmArgs args, int tiles_m, int tiles_n) {
+  constexpr int WN = 4, FN = 4, NW = 8;
+  constexpr int BM = 2 * FM * 16, BN = WN * FN * 16;
+  constexpr int A_BYTES = BM * BK4 * 2, B_BYTES = BN * BK4 * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int PA = A_BYTES / 1024, PT = PA + B_BYTES / 1024;
+  constexpr int CPITCH = BN * 2 + 16;
+  constexpr int LDS_BYTES = (STAGES * STAGE > BM * CPITCH) ? STAGES * STAGE : BM * CPITCH;
+  static_assert(LDS_BYTES <= 163840, "LDS");
+  static_assert(A_BYTES % 1024 == 0 && B_BYTES % 1024 == 0, "pieces");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int ppw = (PT - wave + NW - 1) / NW;
+
+  int m0, n0;
+  {
+    const int nwg = gridDim.x, wg = blockIdx.x;
+    const int xcd = wg & 7, slot = wg >> 3, q = nwg >> 3, r = nwg & 7;
+    const int tid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+    constexpr int GM = 4;
+    const int gsize = GM * tiles_n;
+    const int first_m = (tid / gsize) * GM;
+    const int gm = min(tiles_m - first_m, GM);
+    const int within = tid % gsize;
+    m0 = (first_m + within % gm) * BM;
+    n0 = (within / gm) * BN;
+  }
+  const int nt1 = args.K / BK4, nt = nt1 + args.K2 / BK4;
+  const int Mlast = args.M - 1, Nlast = args.N - 1;
+  const int rr = lane >> 2, c4 = lane & 3;
+  auto stage = [&](int t, int buf) {
+    char* la = smem + buf * STAGE;
+    const bool ext = t >= nt1;
+    const bf16* Ab = ext ? args.A2 : args.A;
+    const bf16* Bb = ext ? args.B2 : args.B;
+    const int lda = ext ? args.lda2 : args.lda;
+    const int ldb = ext ? args.ldb2 : args.ldb;
+    const int k0 = (ext ? t - nt1 : t) * BK4;
+#pragma unroll
+    for (int p = wave; p < PT; p += NW) {
+      if (p < PA) {
+        const int row = p * 16 + rr;
+        const int g = min(m0 + row, Mlast);
+        glds16(Ab + (long)g * lda + k0 + ((c4 ^ ((-(row >> 2)) & 3)) << 3), la + p * 1024);
+      } else {
+        const int row = (p - PA) * 16 + rr;
+        const int g = min(n0 + row, Nlast);
+        glds16(Bb + (long)g * ldb + k0 + ((c4 ^ ((-(row >> 2)) & 3)) << 3), la + p * 1024);
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (s0 < nt) stage(s0, s0);
+  const int fr = lane & 15, fc = lane >> 4;
+  for (int t = 0; t < nt; ++t) {
+    // tile t landed (own pieces), tiles t+1 .. t+STAGES-2 may stay in flight
+    wait_vmcnt_exact(ppw * max(0, min(STAGES - 2, nt - 1 - t)));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of buffer (t-1) % STAGES retired
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile t landed; buffer (t-1) % STAGES is free
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nt) stage(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    const char* la = smem + (t % STAGES) * STAGE;
+    const char* lb = la + A_BYTES;
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(la + off32(wm * FM * 16 + i * 16 + fr, fc));
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(lb + off32(wn * FN * 16 + j * 16 + fr, fc));
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const int g = lane >> 4, l16 = lane & 15;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nl = wn * FN * 16 + j * 16 + 4 * g;
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (args.bias) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) b4[qq] = bf2f(args.bias[n0 + nl + qq]);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = wm * FM * 16 + i * 16 + l16;
+      const f32x4 v = acc[i][j];
+      uint2 pk;
+      pk.x = pack2(v[0] * args.alpha + b4[0], v[1] * args.alpha + b4[1]);
+      pk.y = pack2(v[2] * args.alpha + b4[2], v[3] * args.alpha + b4[3]);
+      *reinterpret_cast<uint2*>(smem + ml * CPITCH + nl * 2) = pk;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  bf16* C = reinterpret_cast<bf16*>(args.C);
+  for (int c = threadIdx.x; c < BM * CPR; c += NW * 64) {
+    const int r2 = c / CPR, cc = c % CPR;
+    const int m = m0 + r2;
+    if (m >= args.M) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + cc * 16);
+    if (args.res) {
+      const u32x4 rv = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + cc * 8);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float lo = bits2f(v[qq] & 0xffff) + bits2f(rv[qq] & 0xffff);
+        const float hi = bits2f(v[qq] >> 16) + bits2f(rv[qq] >> 16);
+        v[qq] = pack2(lo, hi);
+      }
+    }
+    *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8) = v;
+  }
+}
+
+template <int FM, int STAGES>
+int launch_v4(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = 2 * FM * 16, BN = 256;
+  if (a.N % BN || a.K % BK4 || a.K2 % BK4) return OSPO_ERR_SHAPE;
+  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
+  hipLaunchKernelGGL((gemm_nt_v4_kernel<FM, STAGES>), dim3(tm * tn), dim3(512), 0, s, a, tm, tn);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+template <int FM, int STAGES, bool REMAP, bool PRIO, int WM = 2, int WN = 4, int FN = 4>
+int launch_v3(const GemmArgs& a, hipStream_t s) {
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   if (a.N % BN) return OSPO_ERR_SHAPE;
   const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
-  hipLaunchKernelGGL((gemm_nt_v3_kernel<FM, STAGES, REMAP, PRIO>), dim3(tm * tn), dim3(512), 0, s, a, tm, tn);
+  hipLaunchKernelGGL((gemm_nt_v3_kernel<FM, STAGES, REMAP, PRIO, WM, WN, FN>), dim3(tm * tn), dim3(64 * WM * WN), 0,
+                     s, a, tm, tn);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
@@ -502,12 +676,16 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 2: return tile == 256 ? launch_v3<8, 2, false, true>(a, stream) : launch_v3<5, 3, false, true>(a, stream);
     case 3: return tile == 256 ? launch_v3<8, 2, true, true>(a, stream) : launch_v3<5, 2, true, true>(a, stream);
     case 4: return tile == 256 ? launch_v3<8, 2, true, false>(a, stream) : launch_v3<5, 3, true, false>(a, stream);
+    case 5:  // 4 waves (2 x 2), 128 x 128 / 80 x 128 per wave
+      return tile == 256 ? launch_v3<8, 2, true, true, 2, 2, 8>(a, stream) : launch_v3<5, 3, true, true, 2, 2, 8>(a, stream);
+    case 6: return tile == 256 ? launch_v4<8, 4>(a, stream) : launch_v4<5, 6>(a, stream);
+    case 7: return tile == 256 ? launch_v4<8, 3>(a, stream) : launch_v4<5, 4>(a, stream);
     default: return tile == 256 ? launch_v3<8, 2, true, true>(a, stream) : launch_v3<5, 3, true, true>(a, stream);
   }
 }
 
 extern "C" int ospo_set_gemm_variant(int v) {
-  if (v < 0 || v > 4) return OSPO_ERR_ARG;
+  if (v < 0 || v > 7) return OSPO_ERR_ARG;
   g_gemm_variant = v;
   return OSPO_OK;
 }

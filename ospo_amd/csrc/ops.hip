@@ -410,7 +410,7 @@ __global__ void simpo_bwd_kernel(const float* __restrict__ lp, int B, float beta
 // ---------------------------------------------------------------- LoRA pack
 __global__ void lora_pack_kernel(const bf16* __restrict__ Af, const bf16* __restrict__ Bf, int nmods, int r, int Kin,
                                  int Nmod, int Rp, bf16* __restrict__ Acat, bf16* __restrict__ AcatT,
-                                 bf16* __restrict__ Bcat) {
+                                 bf16* __restrict__ Bcat, bf16* __restrict__ BT) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long na = (long)Rp * Kin;
   const long nb = (long)nmods * Nmod * Rp;
@@ -427,6 +427,10 @@ __global__ void lora_pack_kernel(const bf16* __restrict__ Af, const bf16* __rest
     bf16 v = f2bf(0.f);
     if (j < used && j / r == n / Nmod) v = Bf[n * r + (j % r)];
     Bcat[tid] = v;
+  }
+  if (BT && tid < (long)used * Nmod) {  // per-module B^T, [nmods*r, Nmod]
+    const int jr = tid / Nmod, n = tid % Nmod;
+    BT[tid] = Bf[((long)(jr / r) * Nmod + n) * r + (jr % r)];
   }
 }
 
@@ -671,12 +675,12 @@ extern "C" int ospo_simpo_bwd(const float* logps, int B, float beta, float gbr, 
 }
 
 extern "C" int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int Kin, int Nmod, int Rp,
-                              void* Acat, void* AcatT, void* Bcat, hipStream_t st) {
+                              void* Acat, void* AcatT, void* Bcat, void* BT, hipStream_t st) {
   if (!A_flat || !B_flat || !Acat || !AcatT || !Bcat) return OSPO_ERR_ARG;
   if (nmods <= 0 || r <= 0 || Kin <= 0 || Nmod <= 0 || Rp < nmods * r) return OSPO_ERR_SHAPE;
   const long n = std::max((long)Rp * Kin, (long)nmods * Nmod * Rp);
   hipLaunchKernelGGL(lora_pack_kernel, dim3(blocks(n)), dim3(256), 0, st, (const bf16*)A_flat, (const bf16*)B_flat,
-                     nmods, r, Kin, Nmod, Rp, (bf16*)Acat, (bf16*)AcatT, (bf16*)Bcat);
+                     nmods, r, Kin, Nmod, Rp, (bf16*)Acat, (bf16*)AcatT, (bf16*)Bcat, (bf16*)BT);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

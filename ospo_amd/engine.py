@@ -132,7 +132,8 @@ class SimPOEngine:
             for gname, g in self.layout.groups.items():
                 d[gname] = (torch.zeros(g.Rp, g.Kin, dtype=BF16, device=dev),
                             torch.zeros(g.Kin, g.Rp, dtype=BF16, device=dev),
-                            torch.zeros(g.nmods * g.Nmod, g.Rp, dtype=BF16, device=dev))
+                            torch.zeros(g.nmods * g.Nmod, g.Rp, dtype=BF16, device=dev),
+                            torch.zeros(g.nmods * self.layout.r, g.Nmod, dtype=BF16, device=dev))
             self.packed.append(d)
         self.pack_lora()
         self._alloc(max_pairs, max_text_len, n_img_tokens)
@@ -190,7 +191,6 @@ class SimPOEngine:
         self.dgu = z(Mc, 2 * Fd)
         self.dh = z(Mc, Fd)
         self.delta_ws = z(S * H * Tm, dt=F32)
-        self.dq_ws = z(Mc, D, dt=F32)
         self.dz = z(R, Dg)
         self.dhsel = z(R, D)
 
@@ -200,10 +200,10 @@ class SimPOEngine:
         for i in range(self.dims.n_layers):
             base = self.layout.layer_off(i)
             for gname, g in self.layout.groups.items():
-                Acat, AcatT, Bcat = self.packed[i][gname]
+                Acat, AcatT, Bcat, BT = self.packed[i][gname]
                 A = self.lora[base + g.a_off: base + g.a_off + g.nmods * r * g.Kin]
                 B = self.lora[base + g.b_off: base + g.b_off + g.nmods * g.Nmod * r]
-                ops.lora_pack(A, B, g.nmods, r, g.Kin, g.Nmod, g.Rp, Acat, AcatT, Bcat)
+                ops.lora_pack(A, B, g.nmods, r, g.Kin, g.Nmod, g.Rp, Acat, AcatT, Bcat, BT)
 
     def lora_tensors(self) -> Dict[str, torch.Tensor]:
         return self.layout.from_flat(self.lora)
@@ -220,23 +220,27 @@ class SimPOEngine:
     def _u32(self, Rp: int) -> torch.Tensor:
         return self.u32_flat[: self.Mcap * Rp].view(self.Mcap, Rp)
 
-    def _lora_down(self, x, Acat, out_bf16, M):
-        """out = bf16(scale * x . Acat^T)  ([Mcap, Rp]; rows >= M come out zero)."""
+    def _lora_down(self, x, Acat, out_bf16, M, nmods):
+        """out = bf16(scale * x . Acat^T)  ([Mcap, Rp]; rows M..Mk-1 and unused columns zero)."""
         Rp, K = Acat.shape
-        u32 = self._u32(Rp)
-        u32.zero_()
-        ops.gemm_f32acc(x[:M], Acat, u32, a_kmajor=False, b_kmajor=False, k_splits=max(1, min(K // 256, 8)))
-        ops.f32_to_bf16(u32, out_bf16, self.scale)
+        used = nmods * self.layout.r
+        ops.lora_skinny(x, Acat, out_bf16, M, self.Mk, K, (used + 15) // 16, 0, self.scale, b_rows=used)
 
-    def _lora_g(self, dy, Bcat, M):
-        """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows >= M zero)."""
-        K, Rp = Bcat.shape
-        u32 = self._u32(Rp)
-        u32.zero_()
-        ops.gemm_f32acc(dy[:M], Bcat, u32, a_kmajor=False, b_kmajor=True, k_splits=max(1, min(K // 512, 8)))
-        g = self.gsc_flat[: self.Mcap * Rp].view(self.Mcap, Rp)
-        ops.f32_to_bf16(u32, g, self.scale)
-        return g
+    def _lora_g(self, dy, g, Bcat, BT, M):
+        """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows M..Mk-1 zero)."""
+        r = self.layout.r
+        out = self.gsc_flat[: self.Mcap * g.Rp].view(self.Mcap, g.Rp)
+        if g.nmods == 1:
+            ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, (r + 15) // 16, 0, self.scale, b_rows=r)
+        elif r == 16:
+            ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, g.nmods, g.Nmod, self.scale)
+        else:  # block-diagonal with r != 16: split-K fp32 path
+            K = Bcat.shape[0]
+            u32 = self._u32(g.Rp)
+            u32.zero_()
+            ops.gemm_f32acc(dy[:M], Bcat, u32, a_kmajor=False, b_kmajor=True, k_splits=max(1, min(K // 512, 8)))
+            ops.f32_to_bf16(u32, out, self.scale)
+        return out
 
     # ------------------------------------------------------------ forward
     def forward(self, text_ids: torch.Tensor, chosen_ids: torch.Tensor, rejected_ids: torch.Tensor) -> torch.Tensor:
@@ -272,26 +276,27 @@ class SimPOEngine:
         ops.gemm_nt(self.e1[:R], self.al_w2, self.img_emb[:R], bias=self.al_b2)
         x = self.acts[0]["x"] if dims.n_layers else self.x_final
         ops.assemble_inputs(tids, B, Lt, self.embed, self.img_emb[:R], N, D, x)
+        lay = self.layout
         scale_attn = 1.0 / math.sqrt(hd)
         for i in range(dims.n_layers):
             a, lw, pk = self.acts[i], self.layers[i], self.packed[i]
             x = a["x"]
             ops.rmsnorm_fwd(x[:M], lw["ln_in"], a["xn1"][:M], a["rstd1"][:M], dims.rms_eps)
-            Acat, _, Bcat = pk["qkv"]
-            self._lora_down(a["xn1"], Acat, a["u_qkv"], M)
+            Acat, _, Bcat, _ = pk["qkv"]
+            self._lora_down(a["xn1"], Acat, a["u_qkv"], M, lay.groups["qkv"].nmods)
             ops.gemm_nt(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat)
             ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
             ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn)
-            Acat, _, Bcat = pk["o"]
-            self._lora_down(a["attn"], Acat, a["u_o"], M)
+            Acat, _, Bcat, _ = pk["o"]
+            self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods)
             ops.gemm_nt(a["attn"][:M], lw["o"], a["xmid"][:M], a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
             ops.rmsnorm_fwd(a["xmid"][:M], lw["ln_post"], a["xn2"][:M], a["rstd2"][:M], dims.rms_eps)
-            Acat, _, Bcat = pk["gu"]
-            self._lora_down(a["xn2"], Acat, a["u_gu"], M)
+            Acat, _, Bcat, _ = pk["gu"]
+            self._lora_down(a["xn2"], Acat, a["u_gu"], M, lay.groups["gu"].nmods)
             ops.gemm_nt(a["xn2"][:M], lw["gu"], a["gu"][:M], a2=a["u_gu"][:M], b2=Bcat)
             ops.swiglu_fwd(a["gu"][:M], a["h"][:M])
-            Acat, _, Bcat = pk["down"]
-            self._lora_down(a["h"], Acat, a["u_d"], M)
+            Acat, _, Bcat, _ = pk["down"]
+            self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods)
             xn = self.acts[i + 1]["x"] if i + 1 < dims.n_layers else self.x_final
             ops.gemm_nt(a["h"][:M], lw["down"], xn[:M], a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
         ops.rmsnorm_fwd(self.x_final[:M], self.norm, self.hf[:M], self.rstd_f[:M], dims.rms_eps)
@@ -330,33 +335,33 @@ class SimPOEngine:
             dx = self.dx  # gradient w.r.t. this layer's output (bf16)
             # ---- down_proj: out = xmid + h W_d^T + s (h A_d^T) B_d^T
             g = lay.groups["down"]
-            Acat, AcatT, Bcat = pk["down"]
-            gs = self._lora_g(dx, Bcat, M)
+            Acat, AcatT, Bcat, BT = pk["down"]
+            gs = self._lora_g(dx, g, Bcat, BT, M)
             ops.gemm_nt(dx[:M], lw["downT"], self.dh[:M], a2=gs[:M], b2=AcatT)
             self._lora_grads(gs, a["h"], dx, a["u_d"], g, gbase)
             ops.swiglu_bwd(self.dh[:M], a["gu"][:M], self.dgu[:M])
             # ---- gate/up
             g = lay.groups["gu"]
-            Acat, AcatT, Bcat = pk["gu"]
-            gs = self._lora_g(self.dgu, Bcat, M)
+            Acat, AcatT, Bcat, BT = pk["gu"]
+            gs = self._lora_g(self.dgu, g, Bcat, BT, M)
             ops.gemm_nt(self.dgu[:M], lw["guT"], self.dxn[:M], a2=gs[:M], b2=AcatT)
             self._lora_grads(gs, a["xn2"], self.dgu, a["u_gu"], g, gbase)
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], self.dxmid[:M],
                             dres=dx[:M])
             # ---- o_proj
             g = lay.groups["o"]
-            Acat, AcatT, Bcat = pk["o"]
-            gs = self._lora_g(self.dxmid, Bcat, M)
+            Acat, AcatT, Bcat, BT = pk["o"]
+            gs = self._lora_g(self.dxmid, g, Bcat, BT, M)
             ops.gemm_nt(self.dxmid[:M], lw["oT"], self.dattn[:M], a2=gs[:M], b2=AcatT)
             self._lora_grads(gs, a["attn"], self.dxmid, a["u_o"], g, gbase)
             # ---- attention + RoPE
-            ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, self.dq_ws,
+            ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, None,
                                self.dqkv, S, T, H, hd, scale_attn)
             ops.rope(self.dqkv, 0, D, S, T, H, hd, self.cos, self.sin, backward=True)
             # ---- q/k/v
             g = lay.groups["qkv"]
-            Acat, AcatT, Bcat = pk["qkv"]
-            gs = self._lora_g(self.dqkv, Bcat, M)
+            Acat, AcatT, Bcat, BT = pk["qkv"]
+            gs = self._lora_g(self.dqkv, g, Bcat, BT, M)
             ops.gemm_nt(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT)
             self._lora_grads(gs, a["xn1"], self.dqkv, a["u_qkv"], g, gbase)
             ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M])

@@ -248,8 +248,15 @@ def simpo_bwd(logps, B, beta, gbr, ls, loss_type, g_loss, glogps):
 
 
 # ------------------------------------------------------------- LoRA pack
-def lora_pack(A_flat, B_flat, nmods, r, Kin, Nmod, Rp, Acat, AcatT, Bcat):
-    call("ospo_lora_pack", _p(A_flat), _p(B_flat), nmods, r, Kin, Nmod, Rp, _p(Acat), _p(AcatT), _p(Bcat), _s())
+def lora_pack(A_flat, B_flat, nmods, r, Kin, Nmod, Rp, Acat, AcatT, Bcat, BT=None):
+    call("ospo_lora_pack", _p(A_flat), _p(B_flat), nmods, r, Kin, Nmod, Rp, _p(Acat), _p(AcatT), _p(Bcat), _p(BT),
+         _s())
+
+
+def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=None):
+    """out[:M_out, :] (bf16) = scale * a . bt^T per 16-column n-tile (see ospo_lora_skinny)."""
+    call("ospo_lora_skinny", _p(a), _ld(a), _p(bt), _ld(bt), bt.shape[0] if b_rows is None else b_rows, M, M_out,
+         K, n_tiles, a_koff, float(scale), _p(out), _ld(out), out.shape[1], _s())
 
 
 # -------------------------------------------------------------- optimizer

@@ -214,8 +214,7 @@ def test_flash_attention(S, T, H):
     ref.backward(do[: S * T].float().view(S, T, H, hd).transpose(1, 2))
     dqkv = torch.zeros(rows, 3 * D, device=DEV, dtype=torch.bfloat16)
     delta = torch.empty(S * H * T, device=DEV)
-    dq = torch.empty(S * T, D, device=DEV)
-    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, dq, dqkv, S, T, H, hd, scale)
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, dqkv, S, T, H, hd, scale)
     g = qf.grad.permute(1, 3, 0, 2, 4).reshape(S * T, 3 * D)
     for i, nm in enumerate("qkv"):
         e = relerr(dqkv[: S * T, i * D:(i + 1) * D].float(), g[:, i * D:(i + 1) * D])
@@ -320,7 +319,8 @@ def test_lora_pack():
     Acat = torch.empty(Rp, Kin, device=DEV, dtype=torch.bfloat16)
     AcatT = torch.empty(Kin, Rp, device=DEV, dtype=torch.bfloat16)
     Bcat = torch.empty(nm * Nmod, Rp, device=DEV, dtype=torch.bfloat16)
-    ops().lora_pack(A, Bf, nm, r, Kin, Nmod, Rp, Acat, AcatT, Bcat)
+    BT = torch.empty(nm * r, Nmod, device=DEV, dtype=torch.bfloat16)
+    ops().lora_pack(A, Bf, nm, r, Kin, Nmod, Rp, Acat, AcatT, Bcat, BT)
     expA = torch.zeros(Rp, Kin, device=DEV, dtype=torch.bfloat16)
     expA[: nm * r] = A
     assert torch.equal(Acat, expA) and torch.equal(AcatT, expA.T)
@@ -328,6 +328,38 @@ def test_lora_pack():
     for i in range(nm):
         expB[i * Nmod:(i + 1) * Nmod, i * r:(i + 1) * r] = Bf[i]
     assert torch.equal(Bcat, expB)
+    assert torch.equal(BT, torch.cat([Bf[i].T for i in range(nm)], 0))
+
+
+@pytest.mark.parametrize("M,K,used", [(4800, 4096, 48), (300, 11008, 16), (77, 512, 32), (1, 256, 64)])
+def test_lora_skinny_down(M, K, used):
+    """u = s x A_cat^T: dense mode, partial n-tiles, rows M..M_out-1 and pad columns zeroed."""
+    Rp = 64
+    x = rnd(M + 5, K)
+    Acat = torch.zeros(Rp, K, device=DEV, dtype=torch.bfloat16)
+    Acat[:used] = rnd(used, K)
+    M_out = (M + 63) // 64 * 64
+    out = torch.full((M_out + 3, Rp), 7.0, device=DEV, dtype=torch.bfloat16)
+    nt = (used + 15) // 16
+    ops().lora_skinny(x, Acat, out, M, M_out, K, nt, 0, 2.0, b_rows=used)
+    ref = 2.0 * (x[:M].float() @ Acat.float().T)
+    assert relerr(out[:M].float(), ref) < 8e-3
+    assert torch.all(out[M:M_out] == 0) and torch.all(out[:M, 16 * nt:] == 0)
+    assert torch.all(out[M_out:] == 7.0)
+
+
+@pytest.mark.parametrize("M,nm,Nmod", [(4800, 3, 4096), (640, 2, 11008), (100, 1, 4096)])
+def test_lora_skinny_up_blockdiag(M, nm, Nmod):
+    """g = s dy B over the block-diagonal B_cat, via per-module B^T (r = 16)."""
+    r, Rp = 16, 64
+    dy = rnd(M, nm * Nmod)
+    Bf = rnd(nm, Nmod, r)
+    BT = torch.cat([Bf[i].T for i in range(nm)], 0).contiguous()
+    out = torch.empty(M, Rp, device=DEV, dtype=torch.bfloat16)
+    ops().lora_skinny(dy, BT, out, M, M, Nmod, nm, Nmod if nm > 1 else 0, 2.0)
+    ref = torch.cat([dy[:, i * Nmod:(i + 1) * Nmod].float() @ Bf[i].float() for i in range(nm)], 1) * 2.0
+    assert relerr(out[:, : nm * r].float(), ref) < 8e-3
+    assert torch.all(out[:, nm * r:] == 0)
 
 
 # -------------------------------------------------------------- optimizer

@@ -47,12 +47,17 @@ def main():
                 call("ospo_set_gemm_variant", v)
                 res[f"v{v}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
             res["hipblaslt"].append(timeit(lambda: torch.matmul(a, b.t(), out=ref)))
-        call("ospo_set_gemm_variant", 0)
-        ops.gemm_nt(a, b, out, a2=a2, b2=b2)
         exp = a.float() @ b.float().t() + (a2.float() @ b2.float().t() if k2 else 0)
-        err = float((out.float() - exp).norm() / exp.norm())
+        errs = {}
+        for v in VARIANTS:
+            call("ospo_set_gemm_variant", v)
+            out.zero_()
+            ops.gemm_nt(a, b, out, a2=a2, b2=b2)
+            errs[f"v{v}"] = float((out.float() - exp).norm() / exp.norm())
+        call("ospo_set_gemm_variant", 0)
+        del exp
         fl = 2.0 * m * n * k
-        line = {"shape": name, "M": m, "N": n, "K": k, "K2": k2, "tile": ops.gemm_nt_tile(m, n), "relerr": err}
+        line = {"shape": name, "M": m, "N": n, "K": k, "K2": k2, "tile": ops.gemm_nt_tile(m, n), "relerr": errs}
         for kk, ts in res.items():
             t = sorted(ts)[len(ts) // 2]
             line[kk] = {"ms": round(t, 4), "tflops": round(fl / t / 1e9, 1)}
