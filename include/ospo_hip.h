@@ -53,13 +53,21 @@ int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int
                       const void* bias, const void* residual, int ldr, void* C, int ldc,
                       hipStream_t stream);
 
-/* Tuning knob (process-global) selecting the NT GEMM schedule: 0 = register-double-
- * buffered fragments, 3-deep LDS-DMA ring (160-row tiles), XCD-aware tile order,
- * s_setprio (default); 1 = simple double-buffered; 2 = 0 without the XCD remap;
- * 3 = 0 with a 2-deep ring; 4 = 0 without s_setprio. */
+/* Split-K workspace for the GEMM's tail round (tiles % CUs leftover tiles are split
+ * along K into fp32 partial tiles, then summed + epilogued by a fixup launch).
+ * bytes >= 256 KiB x CU count uses the split everywhere it pays; NULL disables it.
+ * The library keeps the pointer: it must outlive every later GEMM call, and GEMMs
+ * sharing it must be stream-ordered. */
+int ospo_gemm_set_workspace(void* ws, size_t bytes);
+
+/* Tuning knob (process-global) selecting the NT GEMM schedule for N % 256 == 0:
+ * 0 = 256x256 8-phase ping-pong with counted vmcnt + split-K tail (default);
+ * 1 = simple double-buffered 256x256; 2 = simple 160x256; 3 = register-prefetch
+ * (v3); 4 = BK=32 LDS ring (v4); 5 = 8-phase without the split tail;
+ * 10-13 = ablations for profiling (results INVALID: no loads / no MFMA). */
 int ospo_set_gemm_variant(int variant);
 
-/* Row count of the tile ospo_gemm_nt_bf16 uses for an M x N output (256, 160 or 64). */
+/* Row count of the tile ospo_gemm_nt_bf16 uses for an M x N output (256 or 64). */
 int ospo_gemm_nt_tile(int M, int N);
 
 /* C[M,N] (fp32) += alpha * op(A)[M,K] . op(B)[N,K]^T, split over K into
@@ -185,10 +193,14 @@ int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int
  * 16*n_tiles..out_cols-1 of out are written zero.  n_tiles <= 4, K % 32 == 0.
  *   u = s x A_cat^T : A = x [M, K], Bt = A_cat [Rp, K], a_koff = 0
  *   g = s dy B      : A = dy [M, nmods*Nmod], Bt = BT [nmods*r, Nmod],
- *                     K = a_koff = Nmod, n_tiles = nmods (r == 16) */
+ *                     K = a_koff = Nmod, n_tiles = nmods (r == 16)
+ * K is split across workgroups; ws (>= ospo_lora_skinny_ws_bytes(M_out, K,
+ * n_tiles) bytes, 16-B aligned) holds the fp32 partials that a second launch
+ * sums.  Calls sharing a ws must be ordered (same stream). */
+size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles);
 int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out,
                      int K, int n_tiles, int a_koff, float scale, void* out, int ldo, int out_cols,
-                     hipStream_t stream);
+                     void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* ------------------------------------------------------------ optimizer ---
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip

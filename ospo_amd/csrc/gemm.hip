@@ -100,7 +100,9 @@ struct GemmArgs {
   int diag_nblk, diag_r;
 };
 
-template <int WM, int WN, int FM, int FN, bool AK, bool BKM, int EPI>
+// DBG (A/B decomposition only, results invalid): 1 = no global loads after the
+// prologue, 2 = no MFMA, 3 = global loads only (no LDS reads, no MFMA).
+template <int WM, int WN, int FM, int FN, bool AK, bool BKM, int EPI, int DBG = 0>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16;
@@ -156,12 +158,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) 
     __syncthreads();
     for (int t = t_begin; t < t_end; ++t) {
       const int buf = (t - t_begin) & 1;
-      if (t + 1 < t_end) stage(t + 1, buf ^ 1);
+      if (DBG != 1 && t + 1 < t_end) stage(t + 1, buf ^ 1);
       const char* la = smem + buf * STAGE;
       const char* lb = la + A_BYTES;
       const bool ext = t >= nt1;  // the K-extension tiles are always M/N-major
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < 2 && DBG != 3; ++s) {
         bf16x8 af[FM], bfr[FN];
         if (AK && !ext) {
 #pragma unroll
@@ -176,6 +178,13 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) 
         } else {
 #pragma unroll
           for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, false>(lb, wn * FN * 16 + j * 16, s, lane);
+        }
+        if (DBG == 2) {  // keep the reads alive without MFMA
+#pragma unroll
+          for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+          for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(bfr[j]));
+          continue;
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -255,14 +264,14 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) 
   }
 }
 
-template <int WM, int WN, int FM, int FN, bool AK, bool BKM, int EPI>
+template <int WM, int WN, int FM, int FN, bool AK, bool BKM, int EPI, int DBG = 0>
 int launch(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   if (a.N % BN) return OSPO_ERR_SHAPE;
   // K-major A: the tile loads columns up to roundup(M, BM) (must exist), stores are predicated on M
   if (AK && a.lda < ((a.M + BM - 1) / BM) * BM) return OSPO_ERR_SHAPE;
   dim3 grid(a.N / BN, (a.M + BM - 1) / BM, a.k_splits > 1 ? a.k_splits : 1);
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AK, BKM, EPI>), grid, dim3(WM * WN * 64), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AK, BKM, EPI, DBG>), grid, dim3(WM * WN * 64), 0, s, a);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
@@ -293,7 +302,7 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 //   read(t,1)->SB | MFMA(SA) | vmcnt(0) lgkmcnt(0) s_barrier | stage(t+2) | read(t+1,0)->SA | MFMA(SB)
 // Two LDS buffers; tile t+2 streams into tile t's buffer right after the barrier that
 // certifies every wave finished reading it.  Loads get one K-tile of slack.
-template <int FM, int STAGES, bool REMAP, bool PRIO, int WM = 2, int WN = 4, int FN = 4>
+template <int FM, int STAGES, bool REMAP, bool PRIO, int WM = 2, int WN = 4, int FN = 4, int DBG = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_nt_v3_kernel(const GemmArgs args, int tiles_m, int tiles_n) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
@@ -370,6 +379,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt_v3_kernel(const GemmArgs
     for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, false>(buf + A_BYTES, wn * FN * 16 + j * 16, s, lane);
   };
   auto mm = [&](const bf16x8 (&af)[FM], const bf16x8 (&bfr)[FN]) {
+    if (DBG == 2) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(bfr[j]));
+      return;
+    }
     if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -397,8 +413,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt_v3_kernel(const GemmArgs
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     // tile t's buffer is free (its fragments are in registers): refill it with tile t+STAGES
-    if (t + STAGES < nt) stage(t + STAGES, t % STAGES);
-    if (t + 1 < nt) rd(smem + ((t + 1) % STAGES) * STAGE, 0, aA, bA);
+    if (DBG != 1 && t + STAGES < nt) stage(t + STAGES, t % STAGES);
+    // unconditional (the last iteration re-reads a valid, unused buffer): a branch here
+    // makes the loop header merge 0 and 12 pending LDS reads and the waitcnt pass then
+    // drains lgkmcnt(0) before the next cluster, serialising the fragment prefetch
+    rd(smem + ((t + 1) % STAGES) * STAGE, 0, aA, bA);
     mm(aB, bB);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -618,31 +637,348 @@ int launch_v4(const GemmArgs& a, hipStream_t s) {
   return OSPO_OK;
 }
 
-template <int FM, int STAGES, bool REMAP, bool PRIO, int WM = 2, int WN = 4, int FN = 4>
+// ----------------------------------------------------------------------------
+// v5: 256 x 256 x 64 "8-phase" ping-pong (cdna_hip_programming.md, The 256^2 8-phase
+// template: T1 XCD remap, T2 swizzle, T3+T4 phases with counted vmcnt, T5 setprio).
+//  * Each K-tile = 4 phases; phase j computes one 128 x 128 C-quadrant (A-half ia,
+//    B-half ib) in the order (0,0) (0,1) (1,1) (1,0); wave w owns rows 64*(w>>2)
+//    and cols 32*(w&3) of every quadrant (16 MFMAs per phase) and reads only the
+//    fragments that change (12 / 4 / 8 / 4 ds_read_b128).
+//  * Waves 4-7 run one s_barrier behind waves 0-3: on every SIMD one wave's MFMA
+//    cluster overlaps the other wave's LDS reads + LDS-DMA issue.
+//  * LDS: 2 slots x {A0, A1, B0, B1} half-tiles of 128 rows x 64 k (16 KiB, 128-B
+//    rows, chunk ^ row&7).  Phase j of tile T stages one half-tile (2 glds / wave):
+//    j=0 B1(T+1), j=1 B0(T+1), j=2 A1(T+1), j=3 A0(T+2) -- each after the last read
+//    of the slot it overwrites has been retired (lgkmcnt(0) + a barrier).
+//  * Counted vmcnt, never 0 in the loop: before the first read of a half-tile each
+//    wave waits for its own DMA of it (vmcnt(2+2) before q0, vmcnt(6) before q2),
+//    placed just before the barrier that precedes the first reader.
+// Tile order: XCD-contiguous chunks of the data-parallel workgroups, GM = 4 row-tile groups.
+__device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0, int& n0) {
+  constexpr int GM = 4;
+  const int gsize = GM * tiles_n;
+  const int first_m = (L / gsize) * GM;
+  const int gm = min(tiles_m - first_m, GM);
+  const int within = L % gsize;
+  m0 = (first_m + within % gm) * 256;
+  n0 = (within / gm) * 256;
+}
+
+// Data-parallel + split-K tail: workgroups [0, dp) own whole tiles (XCD-remapped);
+// workgroups dp + u (u < tail * split) own K-range u % split of tail tile dp + u / split
+// and write an fp32 partial tile to ws (summed + epilogued by splitk_fixup_kernel).
+template <int DBG = 0>
+__global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
+                                                         int split, float* __restrict__ ws) {
+  constexpr int BM = 256, BN = 256, HALF = 16384, SLOT = 4 * HALF;  // half order in a slot: A0 A1 B0 B1
+  constexpr int CPITCH = BN * 2 + 16;
+  constexpr int LDS_BYTES = (2 * SLOT > BM * CPITCH) ? 2 * SLOT : BM * CPITCH;
+  static_assert(LDS_BYTES <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool g1 = wave >= 4;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  int m0, n0, tb, tcount, part = -1;
+  const int nt1 = args.K / BK, ntot = nt1 + args.K2 / BK;
+  {
+    const int wg = blockIdx.x;
+    if (wg < dp) {
+      const int xcd = wg & 7, slot = wg >> 3, q = dp >> 3, r = dp & 7;
+      const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+      v5_tile(L, tiles_m, tiles_n, m0, n0);
+      tb = 0;
+      tcount = ntot;
+    } else {
+      const int u = wg - dp, z = u % split;
+      part = u;
+      v5_tile(dp + u / split, tiles_m, tiles_n, m0, n0);
+      tb = (int)((long)ntot * z / split);
+      tcount = (int)((long)ntot * (z + 1) / split) - tb;
+    }
+  }
+  const int nt = tcount;  // K-tiles this workgroup runs; absolute tile = tb + local
+  const int Mlast = args.M - 1, Nlast = args.N - 1;
+  const int rr8 = lane >> 3, c8 = lane & 7;
+
+  // stage half-tile h (0 A0, 1 A1, 2 B0, 3 B1) of K-tile t: 16 pieces of 8 rows x 128 B, 2 per wave
+  auto stage_half = [&](int tl, int h) {  // tl: local K-tile index
+    if (DBG == 1 && tl >= 2) return;
+    char* dst = smem + (tl & 1) * SLOT + h * HALF;
+    const int t = tb + tl;
+    const bool ext = t >= nt1;
+    const bool isA = h < 2;
+    const bf16* base = isA ? (ext ? args.A2 : args.A) : (ext ? args.B2 : args.B);
+    const int ld = isA ? (ext ? args.lda2 : args.lda) : (ext ? args.ldb2 : args.ldb);
+    const int k0 = (ext ? t - nt1 : t) * BK;
+    const int row0 = (isA ? m0 : n0) + (h & 1) * 128;
+    const int last = isA ? Mlast : Nlast;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = wave * 2 + i;
+      const int row = p * 8 + rr8;
+      const int g = min(row0 + row, last);
+      glds16(base + (long)g * ld + k0 + ((c8 ^ (row & 7)) << 3), dst + p * 1024);
+    }
+  };
+
+  f32x4 acc[4][4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[2][2];
+
+  // prologue: tile 0 complete, A0 of tile 1 in flight
+  if (nt > 0) {
+    stage_half(0, 2); stage_half(0, 3); stage_half(0, 1); stage_half(0, 0);
+  }
+  if (nt > 1) stage_half(1, 0);
+  if (nt > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (g1) {  // the ping-pong offset
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  const int frow = lane & 15, fcol = lane >> 4;
+  for (int t = 0; t < nt; ++t) {
+    const char* slot = smem + (t & 1) * SLOT;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ia = (j >= 2) ? 1 : 0;
+      const int ib = (j == 1 || j == 2) ? 1 : 0;
+      // ---- R: fragments that change this phase, then one half-tile of staging
+      if (j == 0 || j == 2) {
+        const char* la = slot + ia * HALF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
+      }
+      {
+        const char* lb = slot + (2 + ib) * HALF;
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            bfr[n][s] = *reinterpret_cast<const bf16x8*>(lb + mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+      }
+      if (DBG != 1) {
+        if (j == 0 && t + 1 < nt) stage_half(t + 1, 3);
+        if (j == 1 && t + 1 < nt) stage_half(t + 1, 2);
+        if (j == 2 && t + 1 < nt) stage_half(t + 1, 1);
+        if (j == 3 && t + 2 < nt) stage_half(t + 2, 0);
+      }
+      // counted DMA waits before the barrier that precedes the first reader:
+      // into q2 of this tile: A1(t) (6 later glds when tile t+1 is staged);
+      // into q0 of tile t+1: A0(t+1), B0(t+1) (A1(t+1) + A0(t+2) later)
+      const bool wq2 = (j == 1), wq0 = (j == 3) && (t + 1 < nt);
+      const int nq2 = (t + 1 < nt) ? 6 : 0;
+      const int nq0 = (t + 2 < nt) ? 4 : 2;
+      if (g1) {
+        if (wq2) wait_vmcnt_exact(nq2);
+        if (wq0) wait_vmcnt_exact(nq0);
+      }
+      asm volatile("" ::: "memory");  // keep this phase's reads / DMA issue above the barrier
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- M: one C-quadrant x K = 64
+      if (DBG != 2) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              acc[j][i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[n][s], af[i][s], acc[j][i][n], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i][0]), "v"(af[i][1]));
+#pragma unroll
+        for (int n = 0; n < 2; ++n) asm volatile("" ::"v"(bfr[n][0]), "v"(bfr[n][1]));
+      }
+      if (!g1) {
+        if (wq2) wait_vmcnt_exact(nq2);
+        if (wq0) wait_vmcnt_exact(nq0);
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  if (!g1) {  // re-align the barrier count
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: quadrant j, frag (i, n): D[n][m] -> lane holds m = l16, n = 4g..4g+3
+  const int g = lane >> 4, l16 = lane & 15;
+  if (part >= 0) {  // split-K tail: raw fp32 partial tile [256][256]
+    float* wt = ws + (long)part * (BM * BN);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ia = (j >= 2) ? 1 : 0;
+      const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ml = ia * 128 + wm * 64 + i * 16 + l16;
+          const int nl = ib * 128 + wn * 32 + n * 16 + 4 * g;
+          *reinterpret_cast<f32x4*>(wt + ml * BN + nl) = acc[j][i][n];
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int ia = (j >= 2) ? 1 : 0;
+    const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int nl = ib * 128 + wn * 32 + n * 16 + 4 * g;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (args.bias) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) b4[qq] = bf2f(args.bias[n0 + nl + qq]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ml = ia * 128 + wm * 64 + i * 16 + l16;
+        const f32x4 v = acc[j][i][n];
+        uint2 pk;
+        pk.x = pack2(v[0] * args.alpha + b4[0], v[1] * args.alpha + b4[1]);
+        pk.y = pack2(v[2] * args.alpha + b4[2], v[3] * args.alpha + b4[3]);
+        *reinterpret_cast<uint2*>(smem + ml * CPITCH + nl * 2) = pk;
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  bf16* C = reinterpret_cast<bf16*>(args.C);
+  for (int c = threadIdx.x; c < BM * CPR; c += 512) {
+    const int r2 = c / CPR, cc = c % CPR;
+    const int m = m0 + r2;
+    if (m >= args.M) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + cc * 16);
+    if (args.res) {
+      const u32x4 rv = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + cc * 8);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float lo = bits2f(v[qq] & 0xffff) + bits2f(rv[qq] & 0xffff);
+        const float hi = bits2f(v[qq] >> 16) + bits2f(rv[qq] >> 16);
+        v[qq] = pack2(lo, hi);
+      }
+    }
+    *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8) = v;
+  }
+}
+
+// sum the split partials of each tail tile, apply alpha / bias / residual, write bf16
+__global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
+                                                           int split, const float* __restrict__ ws) {
+  const int tile = blockIdx.x >> 5, rblk = blockIdx.x & 31;
+  int m0, n0;
+  v5_tile(dp + tile, tiles_m, tiles_n, m0, n0);
+  const int r = rblk * 8 + (threadIdx.x >> 5), c = (threadIdx.x & 31) * 8;
+  const int m = m0 + r;
+  if (m >= args.M) return;
+  f32x4 lo = f32x4{0.f, 0.f, 0.f, 0.f}, hi = lo;
+  for (int z = 0; z < split; ++z) {
+    const float* p = ws + (long)(tile * split + z) * 65536 + r * 256 + c;
+    lo += *reinterpret_cast<const f32x4*>(p);
+    hi += *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    v[q] *= args.alpha;
+    if (args.bias) v[q] += bf2f(args.bias[n0 + c + q]);
+  }
+  u32x4 o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = pack2(v[2 * q], v[2 * q + 1]);
+  if (args.res) {  // residual added after the bf16 rounding of the product, as the main epilogue does
+    const u32x4 rv = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + c);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      o[q] = pack2(bits2f(o[q] & 0xffff) + bits2f(rv[q] & 0xffff), bits2f(o[q] >> 16) + bits2f(rv[q] >> 16));
+  }
+  *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(args.C) + (long)m * args.ldc + n0 + c) = o;
+}
+
+float* g_splitk_ws = nullptr;
+size_t g_splitk_ws_bytes = 0;
+int g_num_cus = 0;
+
+int num_cus() {
+  if (!g_num_cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_num_cus = n;
+  }
+  return g_num_cus;
+}
+
+template <int DBG = 0>
+int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
+  if (a.N % 256) return OSPO_ERR_SHAPE;
+  const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
+  const int ntot = a.K / BK + a.K2 / BK;
+  const int cus = num_cus();
+  int dp = tiles, split = 1, tail = 0;
+  if (allow_split && tiles > cus) {
+    tail = tiles % cus;
+    split = tail ? std::min(cus / tail, std::min(8, ntot / 4)) : 1;
+    const size_t need = (size_t)tail * split * 65536 * sizeof(float);
+    if (tail && split >= 2 && ntot >= 16 && g_splitk_ws && need <= g_splitk_ws_bytes) {
+      dp = tiles - tail;
+    } else {
+      split = 1;
+      tail = 0;
+    }
+  }
+  const int grid = dp + tail * split;
+  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split, g_splitk_ws);
+  OSPO_CHECK_LAUNCH();
+  if (tail) {
+    hipLaunchKernelGGL(splitk_fixup_kernel, dim3(tail * 32), dim3(256), 0, s, a, tm, tn, dp, split,
+                       (const float*)g_splitk_ws);
+    OSPO_CHECK_LAUNCH();
+  }
+  return OSPO_OK;
+}
+
+template <int FM, int STAGES, bool REMAP, bool PRIO, int WM = 2, int WN = 4, int FN = 4, int DBG = 0>
 int launch_v3(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   if (a.N % BN) return OSPO_ERR_SHAPE;
   const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
-  hipLaunchKernelGGL((gemm_nt_v3_kernel<FM, STAGES, REMAP, PRIO, WM, WN, FN>), dim3(tm * tn), dim3(64 * WM * WN), 0,
+  hipLaunchKernelGGL((gemm_nt_v3_kernel<FM, STAGES, REMAP, PRIO, WM, WN, FN, DBG>), dim3(tm * tn), dim3(64 * WM * WN), 0,
                      s, a, tm, tn);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
 
-int g_gemm_variant = 0;  // 0 = v3 (XCD remap, setprio), 1 = simple, 2 = v3 no remap, 3 = v3 no prio, 4 = 3-stage
+int g_gemm_variant = 0;  // 0 = 8-phase + split-K tail (default); others: A/B schedules, see dispatch
 
-// Pick the bf16 NT tile: minimise (waves of 256 CUs) x (relative time per tile).  A
-// 160 x 256 tile costs ~1.1x a 256 x 256 tile per row (more LDS-DMA issue per MFMA,
-// measured on the step's shapes), but 256-row tiles quantise badly at M ~ 5k, N = 4096
-// (304 tiles = 1.19 waves).
+// NT tile: 256 x 256 (8-phase, split-K tail) whenever N % 256 == 0, else the 64 x 64 simple kernel.
 int pick_nt_tile(int M, int N) {
-  if (N % 256) return 64;
-  const int cus = 256;
-  const long t256 = (long)((M + 255) / 256) * (N / 256);
-  const long t160 = (long)((M + 159) / 160) * (N / 256);
-  const double c256 = (double)((t256 + cus - 1) / cus) * 256.0;
-  const double c160 = (double)((t160 + cus - 1) / cus) * 160.0 * 1.1;
-  return c256 <= c160 ? 256 : 160;
+  (void)M;
+  return (N % 256) ? 64 : 256;
 }
 
 }  // namespace
@@ -663,29 +999,32 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
              M, N, K, K2, alpha, (const bf16*)bias, (const bf16*)residual, ldr, C, ldc, 1, 0, 0};
   const int tile = pick_nt_tile(M, N);
-  // default schedule per tile (tools/gemm_bench.py A/B on the step's shapes): 160-row
-  // tiles run fastest on the simple double-buffered loop, 256-row tiles on v3
-  if (g_gemm_variant == 1 || tile == 64 || (g_gemm_variant == 0 && tile == 160)) {
-    switch (tile) {
-      case 256: return launch<2, 4, 8, 4, false, false, EPI_BF16>(a, stream);
-      case 160: return launch<2, 4, 5, 4, false, false, EPI_BF16>(a, stream);
-      default: return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
-    }
-  }
+  if (tile == 64) return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
   switch (g_gemm_variant) {
-    case 2: return tile == 256 ? launch_v3<8, 2, false, true>(a, stream) : launch_v3<5, 3, false, true>(a, stream);
-    case 3: return tile == 256 ? launch_v3<8, 2, true, true>(a, stream) : launch_v3<5, 2, true, true>(a, stream);
-    case 4: return tile == 256 ? launch_v3<8, 2, true, false>(a, stream) : launch_v3<5, 3, true, false>(a, stream);
-    case 5:  // 4 waves (2 x 2), 128 x 128 / 80 x 128 per wave
-      return tile == 256 ? launch_v3<8, 2, true, true, 2, 2, 8>(a, stream) : launch_v3<5, 3, true, true, 2, 2, 8>(a, stream);
-    case 6: return tile == 256 ? launch_v4<8, 4>(a, stream) : launch_v4<5, 6>(a, stream);
-    case 7: return tile == 256 ? launch_v4<8, 3>(a, stream) : launch_v4<5, 4>(a, stream);
-    default: return tile == 256 ? launch_v3<8, 2, true, true>(a, stream) : launch_v3<5, 3, true, true>(a, stream);
+    // A/B alternatives (tools/gemm_bench.py); results identical, schedules differ
+    case 1: return launch<2, 4, 8, 4, false, false, EPI_BF16>(a, stream);            // simple double-buffered
+    case 2: return launch<2, 4, 5, 4, false, false, EPI_BF16>(a, stream);            // simple, 160 x 256
+    case 3: return launch_v3<8, 2, true, true>(a, stream);                           // v3 register-prefetch
+    case 4: return launch_v4<8, 3>(a, stream);                                       // v4 BK=32 ring
+    case 5: return launch_v5<0>(a, stream, false);                                   // 8-phase, no split tail
+    // decompositions (results invalid): 10 no loads / 11 no MFMA (simple); 12 no loads / 13 no MFMA (8-phase)
+    case 10: return launch<2, 4, 8, 4, false, false, EPI_BF16, 1>(a, stream);
+    case 11: return launch<2, 4, 8, 4, false, false, EPI_BF16, 2>(a, stream);
+    case 12: return launch_v5<1>(a, stream, false);
+    case 13: return launch_v5<2>(a, stream, false);
+    default: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
   }
 }
 
+extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {
+  if (bytes && (!ws || !aligned16(ws))) return OSPO_ERR_ARG;
+  g_splitk_ws = (float*)ws;
+  g_splitk_ws_bytes = ws ? bytes : 0;
+  return OSPO_OK;
+}
+
 extern "C" int ospo_set_gemm_variant(int v) {
-  if (v < 0 || v > 7) return OSPO_ERR_ARG;
+  if (v < 0 || v > 13 || (v > 5 && v < 10)) return OSPO_ERR_ARG;
   g_gemm_variant = v;
   return OSPO_OK;
 }

@@ -19,7 +19,7 @@ namespace {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
-constexpr int SK_WAVES = 8;
+constexpr int SK_WAVES = 4;
 constexpr int SK_U = 4;  // k-steps per register batch; two batches in flight per wave
 
 // One wave's share of the reduction: steps s = wave + i*SK_WAVES, i < n_i.
@@ -62,26 +62,33 @@ __device__ __forceinline__ void sk_loop(const bf16* arow, const bf16* const (&bp
 }
 
 // out[m][16j + c] = scale * sum_k A[m][j*a_koff + k] * Bt[16j + c][k]
+// grid (row blocks of 16, K splits).  Each workgroup reduces its K range; with
+// splits > 1 the fp32 partial tile goes to ws and skinny_reduce_kernel sums the
+// splits (a cross-workgroup handoff inside one launch would need an agent-scope
+// release, i.e. an L2 writeback per workgroup on gfx950 -- far dearer).
 template <int NT>
 __global__ __launch_bounds__(64 * SK_WAVES) void skinny_kernel(const bf16* __restrict__ A, int lda,
                                                                const bf16* __restrict__ Bt, int ldb, int b_rows,
                                                                int M, int M_out, int K, int a_koff, float scale,
-                                                               bf16* __restrict__ out, int ldo, int out_cols) {
+                                                               bf16* __restrict__ out, int ldo, int out_cols,
+                                                               f32x4* __restrict__ ws) {
   __shared__ f32x4 red[SK_WAVES][NT][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, g = lane >> 4;
-  const int m0 = blockIdx.x * 16;
+  const int rb = blockIdx.x, z = blockIdx.y, splits = gridDim.y;
+  const int m0 = rb * 16;
   int row = m0 + l16;
   row = row < M ? row : M - 1;
   const int nsteps = K >> 5;
-  const int n_i = (nsteps - wave + SK_WAVES - 1) / SK_WAVES;  // this wave's steps
+  const int s_begin = (int)((long)nsteps * z / splits), s_end = (int)((long)nsteps * (z + 1) / splits);
+  const int n_i = (s_end - s_begin - wave + SK_WAVES - 1) / SK_WAVES;  // this wave's steps
 
   f32x4 acc[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bf16* arow = A + (long)row * lda + 8 * g;
+  const bf16* arow = A + (long)row * lda + 8 * g + 32 * s_begin;
   if (a_koff == 0) {  // dense: one A fragment feeds every n-tile
     const bf16* bp[NT];
     bool bok[NT];
@@ -89,7 +96,7 @@ __global__ __launch_bounds__(64 * SK_WAVES) void skinny_kernel(const bf16* __res
     for (int j = 0; j < NT; ++j) {
       const int br = 16 * j + l16;
       bok[j] = br < b_rows;
-      bp[j] = Bt + (long)(bok[j] ? br : 0) * ldb + 8 * g;
+      bp[j] = Bt + (long)(bok[j] ? br : 0) * ldb + 8 * g + 32 * s_begin;
     }
     sk_loop<NT>(arow, bp, bok, wave, n_i, acc);
   } else {  // block-diagonal: n-tile j reduces over its own K block of A
@@ -97,7 +104,7 @@ __global__ __launch_bounds__(64 * SK_WAVES) void skinny_kernel(const bf16* __res
     for (int j = 0; j < NT; ++j) {
       const int br = 16 * j + l16;
       const bool ok1[1] = {br < b_rows};
-      const bf16* const bp1[1] = {Bt + (long)(ok1[0] ? br : 0) * ldb + 8 * g};
+      const bf16* const bp1[1] = {Bt + (long)(ok1[0] ? br : 0) * ldb + 8 * g + 32 * s_begin};
       f32x4 acc1[1] = {acc[j]};
       sk_loop<1>(arow + (long)j * a_koff, bp1, ok1, wave, n_i, acc1);
       acc[j] = acc1[0];
@@ -107,21 +114,26 @@ __global__ __launch_bounds__(64 * SK_WAVES) void skinny_kernel(const bf16* __res
 #pragma unroll
   for (int j = 0; j < NT; ++j) red[wave][j][lane] = acc[j];
   __syncthreads();
-  const int m = m0 + l16;
-  for (int j = wave; j < NT; j += SK_WAVES) {
-    f32x4 v = red[0][j][lane];
+  // wave j (< NT) owns n-tile j: sum the waves' partials
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (wave < NT) {
 #pragma unroll
-    for (int w = 1; w < SK_WAVES; ++w) v += red[w][j][lane];
-    if (m < M_out) {
-      uint2 pk;
-      if (m < M) {
-        pk.x = pack2(v[0] * scale, v[1] * scale);
-        pk.y = pack2(v[2] * scale, v[3] * scale);
-      } else {
-        pk.x = pk.y = 0u;
-      }
-      *reinterpret_cast<uint2*>(out + (long)m * ldo + 16 * j + 4 * g) = pk;
+    for (int w = 0; w < SK_WAVES; ++w) v += red[w][wave][lane];
+  }
+  if (splits > 1) {  // fp32 partial; skinny_reduce_kernel sums the splits
+    if (wave < NT) ws[((long)(z * gridDim.x + rb) * NT + wave) * 64 + lane] = v;
+    return;
+  }
+  const int m = m0 + l16;
+  if (wave < NT && m < M_out) {
+    uint2 pk;
+    if (m < M) {
+      pk.x = pack2(v[0] * scale, v[1] * scale);
+      pk.y = pack2(v[2] * scale, v[3] * scale);
+    } else {
+      pk.x = pk.y = 0u;
     }
+    *reinterpret_cast<uint2*>(out + (long)m * ldo + 16 * wave + 4 * g) = pk;
   }
   // zero padding columns 16*NT .. out_cols-1 of this row block
   const int pad = out_cols - 16 * NT;
@@ -131,27 +143,82 @@ __global__ __launch_bounds__(64 * SK_WAVES) void skinny_kernel(const bf16* __res
   }
 }
 
+// sum the split partials of one row block: block = NT waves, wave j = n-tile j
+template <int NT>
+__global__ __launch_bounds__(64 * NT) void skinny_reduce_kernel(const f32x4* __restrict__ ws, int splits, int RB,
+                                                               int M, int M_out, float scale, bf16* __restrict__ out,
+                                                               int ldo, int out_cols) {
+  const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;
+  const int rb = blockIdx.x, g = lane >> 4, l16 = lane & 15;
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < splits; ++z) v += ws[((long)(z * RB + rb) * NT + j) * 64 + lane];
+  const int m = rb * 16 + l16;
+  if (m < M_out) {
+    uint2 pk;
+    if (m < M) {
+      pk.x = pack2(v[0] * scale, v[1] * scale);
+      pk.y = pack2(v[2] * scale, v[3] * scale);
+    } else {
+      pk.x = pk.y = 0u;
+    }
+    *reinterpret_cast<uint2*>(out + (long)m * ldo + 16 * j + 4 * g) = pk;
+  }
+  const int pad = out_cols - 16 * NT;
+  for (int i = threadIdx.x; i < 16 * pad; i += 64 * NT) {
+    const int r = rb * 16 + i / pad;
+    if (r < M_out) out[(long)r * ldo + 16 * NT + i % pad] = f2bf(0.f);
+  }
+}
+
 }  // namespace
 
+// K splits: enough workgroups to keep every CU streaming (>= ~4 per CU), each
+// split >= 512 k; the workspace holds splits x row_blocks fp32 partial tiles.
+static int skinny_splits(int M_out, int K) {
+  const int rb = (M_out + 15) / 16;
+  int s = 1;
+  while (s < 16 && (long)rb * s < 1024 && K / (32 * (s * 2)) >= 16) s *= 2;
+  return s;
+}
+
+extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
+  const long rb = (M_out + 15) / 16;
+  const int sp = skinny_splits(M_out, K);
+  return (size_t)(sp > 1 ? sp : 0) * rb * n_tiles * 64 * sizeof(f32x4) + 16;
+}
+
 extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out, int K,
-                                int n_tiles, int a_koff, float scale, void* out, int ldo, int out_cols,
-                                hipStream_t stream) {
-  if (!A || !Bt || !out) return OSPO_ERR_ARG;
+                                int n_tiles, int a_koff, float scale, void* out, int ldo, int out_cols, void* ws,
+                                size_t ws_bytes, hipStream_t stream) {
+  if (!A || !Bt || !out || !ws) return OSPO_ERR_ARG;
   if (M <= 0 || M_out < M || K <= 0 || n_tiles < 1 || n_tiles > 4 || b_rows <= 0 || a_koff < 0) return OSPO_ERR_SHAPE;
   if (K % 32 || lda % 8 || ldb % 8 || a_koff % 8 || ldo % 4 || out_cols < 16 * n_tiles || ldo < out_cols)
     return OSPO_ERR_SHAPE;
   if (ldb < K || (a_koff == 0 && lda < K) || (a_koff > 0 && lda < (n_tiles - 1) * a_koff + K)) return OSPO_ERR_SHAPE;
-  if (!aligned16(A) || !aligned16(Bt) || ((uintptr_t)out & 7)) return OSPO_ERR_ALIGN;
-  const dim3 grid((M_out + 15) / 16), block(64 * SK_WAVES);
+  if (ws_bytes < ospo_lora_skinny_ws_bytes(M_out, K, n_tiles)) return OSPO_ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(Bt) || !aligned16(ws) || ((uintptr_t)out & 7)) return OSPO_ERR_ALIGN;
+  const int rbn = (M_out + 15) / 16;
+  const int sp = skinny_splits(M_out, K);
+  f32x4* part = (f32x4*)ws;
+  const dim3 grid(rbn, sp), block(64 * SK_WAVES);
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)Bt;
   bf16* o = (bf16*)out;
   switch (n_tiles) {
-    case 1: hipLaunchKernelGGL(skinny_kernel<1>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols); break;
-    case 2: hipLaunchKernelGGL(skinny_kernel<2>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols); break;
-    case 3: hipLaunchKernelGGL(skinny_kernel<3>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols); break;
-    default: hipLaunchKernelGGL(skinny_kernel<4>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols); break;
+    case 1: hipLaunchKernelGGL(skinny_kernel<1>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
+    case 2: hipLaunchKernelGGL(skinny_kernel<2>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
+    case 3: hipLaunchKernelGGL(skinny_kernel<3>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
+    default: hipLaunchKernelGGL(skinny_kernel<4>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
   }
   OSPO_CHECK_LAUNCH();
+  if (sp > 1) {
+    switch (n_tiles) {
+      case 1: hipLaunchKernelGGL(skinny_reduce_kernel<1>, dim3(rbn), dim3(64), 0, stream, part, sp, rbn, M, M_out, scale, o, ldo, out_cols); break;
+      case 2: hipLaunchKernelGGL(skinny_reduce_kernel<2>, dim3(rbn), dim3(128), 0, stream, part, sp, rbn, M, M_out, scale, o, ldo, out_cols); break;
+      case 3: hipLaunchKernelGGL(skinny_reduce_kernel<3>, dim3(rbn), dim3(192), 0, stream, part, sp, rbn, M, M_out, scale, o, ldo, out_cols); break;
+      default: hipLaunchKernelGGL(skinny_reduce_kernel<4>, dim3(rbn), dim3(256), 0, stream, part, sp, rbn, M, M_out, scale, o, ldo, out_cols); break;
+    }
+    OSPO_CHECK_LAUNCH();
+  }
   return OSPO_OK;
 }

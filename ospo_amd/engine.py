@@ -138,6 +138,7 @@ class SimPOEngine:
         self.pack_lora()
         self._alloc(max_pairs, max_text_len, n_img_tokens)
         self._rope_T = -1
+        self._side = torch.cuda.Stream(device=self.device)
 
     def ensure_capacity(self, pairs: int, text_len: int):
         """Grow the activation buffers when a batch exceeds them (ragged prompts)."""
@@ -182,7 +183,8 @@ class SimPOEngine:
         self.seq_logps = z(S, dt=F32)
         # backward scratch (shared by all layers)
         self.u32_flat = z(Mc * Rmax, dt=F32)
-        self.gsc_flat = z(Mc * Rmax)
+        # one g buffer per LoRA group: the side stream's dA/dB of a group may still read it
+        self.gsc = {name: z(Mc, g.Rp) for name, g in self.layout.groups.items()}
         self.dx = z(Mc, D)
         self.dxmid = z(Mc, D)
         self.dxn = z(Mc, D)
@@ -220,20 +222,32 @@ class SimPOEngine:
     def _u32(self, Rp: int) -> torch.Tensor:
         return self.u32_flat[: self.Mcap * Rp].view(self.Mcap, Rp)
 
+    def _skinny_ws(self, K: int, n_tiles: int) -> torch.Tensor:
+        """Split-K workspace of ospo_lora_skinny (grown on demand, never shared across streams)."""
+        need = ops.lora_skinny_ws_bytes(self.Mk, K, n_tiles)
+        ws = getattr(self, "_sk_ws", None)
+        if ws is None or ws.numel() * 4 < need:
+            ws = self._sk_ws = ops.lora_skinny_ws(self.Mk, K, max(n_tiles, 4), self.device)
+        return ws
+
     def _lora_down(self, x, Acat, out_bf16, M, nmods):
         """out = bf16(scale * x . Acat^T)  ([Mcap, Rp]; rows M..Mk-1 and unused columns zero)."""
         Rp, K = Acat.shape
         used = nmods * self.layout.r
-        ops.lora_skinny(x, Acat, out_bf16, M, self.Mk, K, (used + 15) // 16, 0, self.scale, b_rows=used)
+        nt = (used + 15) // 16
+        ops.lora_skinny(x, Acat, out_bf16, M, self.Mk, K, nt, 0, self.scale, b_rows=used, ws=self._skinny_ws(K, nt))
 
     def _lora_g(self, dy, g, Bcat, BT, M):
         """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows M..Mk-1 zero)."""
         r = self.layout.r
-        out = self.gsc_flat[: self.Mcap * g.Rp].view(self.Mcap, g.Rp)
+        out = self.gsc[g.name]
         if g.nmods == 1:
-            ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, (r + 15) // 16, 0, self.scale, b_rows=r)
+            nt = (r + 15) // 16
+            ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, nt, 0, self.scale, b_rows=r,
+                            ws=self._skinny_ws(g.Nmod, nt))
         elif r == 16:
-            ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, g.nmods, g.Nmod, self.scale)
+            ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, g.nmods, g.Nmod, self.scale,
+                            ws=self._skinny_ws(g.Nmod, g.nmods))
         else:  # block-diagonal with r != 16: split-K fp32 path
             K = Bcat.shape[0]
             u32 = self._u32(g.Rp)
@@ -329,42 +343,66 @@ class SimPOEngine:
         ops.rmsnorm_bwd(self.dxn[:M], self.x_final[:M], self.norm, self.rstd_f[:M], self.dx[:M])
         scale_attn = 1.0 / math.sqrt(hd)
         lay = self.layout
+        # LoRA weight grads (dA = g^T x, dB = dy^T u) of each group run on a side stream,
+        # under the dX GEMMs; events guard every buffer the side stream reads before the
+        # main stream rewrites it (g buffer per group, dy buffers, next layer).
+        main, side = torch.cuda.current_stream(self.device), self._side
+        side.wait_stream(main)
+        done = {}  # group -> event after its dA/dB were enqueued on the side stream
+
+        def guard(name):  # main must not rewrite what group `name`'s pending dA/dB read
+            ev = done.pop(name, None)
+            if ev is not None:
+                main.wait_event(ev)
+
+        def lora_grads_async(name, gs, x_in, dy, u, gbase):
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                self._lora_grads(gs, x_in, dy, u, lay.groups[name], gbase)
+            ev2 = torch.cuda.Event()
+            ev2.record(side)
+            done[name] = ev2
+
         for i in reversed(range(dims.n_layers)):
             a, lw, pk = self.acts[i], self.layers[i], self.packed[i]
             gbase = lay.layer_off(i)
             dx = self.dx  # gradient w.r.t. this layer's output (bf16)
             # ---- down_proj: out = xmid + h W_d^T + s (h A_d^T) B_d^T
-            g = lay.groups["down"]
             Acat, AcatT, Bcat, BT = pk["down"]
-            gs = self._lora_g(dx, g, Bcat, BT, M)
+            guard("down")
+            gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M)
             ops.gemm_nt(dx[:M], lw["downT"], self.dh[:M], a2=gs[:M], b2=AcatT)
-            self._lora_grads(gs, a["h"], dx, a["u_d"], g, gbase)
+            lora_grads_async("down", gs, a["h"], dx, a["u_d"], gbase)
+            guard("gu")  # dgu is rewritten here
             ops.swiglu_bwd(self.dh[:M], a["gu"][:M], self.dgu[:M])
             # ---- gate/up
-            g = lay.groups["gu"]
             Acat, AcatT, Bcat, BT = pk["gu"]
-            gs = self._lora_g(self.dgu, g, Bcat, BT, M)
+            gs = self._lora_g(self.dgu, lay.groups["gu"], Bcat, BT, M)
             ops.gemm_nt(self.dgu[:M], lw["guT"], self.dxn[:M], a2=gs[:M], b2=AcatT)
-            self._lora_grads(gs, a["xn2"], self.dgu, a["u_gu"], g, gbase)
+            lora_grads_async("gu", gs, a["xn2"], self.dgu, a["u_gu"], gbase)
+            guard("o")  # dxmid is rewritten here
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], self.dxmid[:M],
                             dres=dx[:M])
             # ---- o_proj
-            g = lay.groups["o"]
             Acat, AcatT, Bcat, BT = pk["o"]
-            gs = self._lora_g(self.dxmid, g, Bcat, BT, M)
+            gs = self._lora_g(self.dxmid, lay.groups["o"], Bcat, BT, M)
             ops.gemm_nt(self.dxmid[:M], lw["oT"], self.dattn[:M], a2=gs[:M], b2=AcatT)
-            self._lora_grads(gs, a["attn"], self.dxmid, a["u_o"], g, gbase)
+            lora_grads_async("o", gs, a["attn"], self.dxmid, a["u_o"], gbase)
             # ---- attention + RoPE
+            guard("qkv")  # dqkv is rewritten here
             ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, None,
                                self.dqkv, S, T, H, hd, scale_attn)
             ops.rope(self.dqkv, 0, D, S, T, H, hd, self.cos, self.sin, backward=True)
             # ---- q/k/v
-            g = lay.groups["qkv"]
             Acat, AcatT, Bcat, BT = pk["qkv"]
-            gs = self._lora_g(self.dqkv, g, Bcat, BT, M)
+            gs = self._lora_g(self.dqkv, lay.groups["qkv"], Bcat, BT, M)
             ops.gemm_nt(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT)
-            self._lora_grads(gs, a["xn1"], self.dqkv, a["u_qkv"], g, gbase)
+            lora_grads_async("qkv", gs, a["xn1"], self.dqkv, a["u_qkv"], gbase)
+            guard("down")  # dx (the down group's dy) is rewritten here
             ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M])
+        main.wait_stream(side)
 
     def _lora_grads(self, gs, x_in, dy, u, g, gbase):
         """dA = g_s^T . x_in  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal)."""

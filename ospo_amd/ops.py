@@ -74,6 +74,21 @@ def _ld(t: torch.Tensor) -> int:
 
 
 # ------------------------------------------------------------------ GEMM
+_GEMM_WS = {}
+
+
+def gemm_workspace(device=None) -> torch.Tensor:
+    """Process-lifetime split-K workspace of the NT GEMM (256 partial tiles = 64 MiB),
+    registered with the library on first use and never freed, so the library's pointer
+    cannot dangle.  One per device; GEMMs are issued on one stream per device."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    ws = _GEMM_WS.get(dev.index)
+    if ws is None:
+        ws = _GEMM_WS[dev.index] = torch.empty(256 * 65536, dtype=torch.float32, device=dev)
+        call("ospo_gemm_set_workspace", ws.data_ptr(), ws.numel() * 4)
+    return ws
+
+
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0,
             bias=None, residual=None) -> torch.Tensor:
     """out[M,N] = bf16(alpha*(a.b^T + a2.b2^T) + bias) [+ residual]  (nn.Linear layout b=[N,K])."""
@@ -88,6 +103,8 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
         K2 = a2.shape[1]
         if a2.shape[0] != M or b2.shape != (N, K2):
             raise ValueError("gemm_nt K-extension shape mismatch")
+    if not _GEMM_WS:
+        gemm_workspace(a.device)
     st = torch.cuda.current_stream()
     e0 = _TIMER.start(st) if _TIMER is not None else None
     call("ospo_gemm_nt_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K,
@@ -253,10 +270,23 @@ def lora_pack(A_flat, B_flat, nmods, r, Kin, Nmod, Rp, Acat, AcatT, Bcat, BT=Non
          _s())
 
 
-def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=None):
+def lora_skinny_ws_bytes(M_out, K, n_tiles) -> int:
+    return int(query("ospo_lora_skinny_ws_bytes", M_out, K, n_tiles))
+
+
+def lora_skinny_ws(M_out, K, n_tiles=4, device="cuda") -> torch.Tensor:
+    """Workspace for ospo_lora_skinny's split-K partials."""
+    n = lora_skinny_ws_bytes(M_out, K, n_tiles)
+    return torch.zeros((n + 15) // 16 * 4, dtype=torch.float32, device=device)
+
+
+def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=None, ws=None):
     """out[:M_out, :] (bf16) = scale * a . bt^T per 16-column n-tile (see ospo_lora_skinny)."""
+    if ws is None:
+        ws = lora_skinny_ws(M_out, K, n_tiles, a.device)
     call("ospo_lora_skinny", _p(a), _ld(a), _p(bt), _ld(bt), bt.shape[0] if b_rows is None else b_rows, M, M_out,
-         K, n_tiles, a_koff, float(scale), _p(out), _ld(out), out.shape[1], _s())
+         K, n_tiles, a_koff, float(scale), _p(out), _ld(out), out.shape[1], _p(ws), ws.numel() * ws.element_size(),
+         _s())
 
 
 # -------------------------------------------------------------- optimizer

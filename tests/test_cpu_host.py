@@ -27,7 +27,7 @@ def lib():
 
 def header_symbols():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(ospo_[a-z0-9_]+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(ospo_[a-z0-9_]+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_header_symbol(lib):
@@ -75,8 +75,8 @@ def test_validation_before_launch(lib):
     # logprob rows not a multiple of N
     rc = lib.ospo_logprob_fwd(P(a), 64, P(a), 10, 3, P(a), P(a), P(a), None)
     assert rc == 1
-    # nt tile heuristic: 160-row tiles at M ~ 4.8k (quantisation over 256 CUs)
-    assert lib.ospo_gemm_nt_tile(4800, 4096) == 160
+    # nt tile: 256 x 256 8-phase whenever N % 256 == 0 (split-K tail absorbs quantisation), else 64
+    assert lib.ospo_gemm_nt_tile(4800, 4096) == 256
     assert lib.ospo_gemm_nt_tile(4608, 16384) == 256
     assert lib.ospo_gemm_nt_tile(100, 192) == 64
 

@@ -341,11 +341,13 @@ def test_lora_skinny_down(M, K, used):
     M_out = (M + 63) // 64 * 64
     out = torch.full((M_out + 3, Rp), 7.0, device=DEV, dtype=torch.bfloat16)
     nt = (used + 15) // 16
-    ops().lora_skinny(x, Acat, out, M, M_out, K, nt, 0, 2.0, b_rows=used)
+    ws = ops().lora_skinny_ws(M_out, K, nt)
     ref = 2.0 * (x[:M].float() @ Acat.float().T)
-    assert relerr(out[:M].float(), ref) < 8e-3
-    assert torch.all(out[M:M_out] == 0) and torch.all(out[:M, 16 * nt:] == 0)
-    assert torch.all(out[M_out:] == 7.0)
+    for rep in range(2):  # second call reuses the workspace
+        ops().lora_skinny(x, Acat, out, M, M_out, K, nt, 0, 2.0, b_rows=used, ws=ws)
+        assert relerr(out[:M].float(), ref) < 8e-3
+        assert torch.all(out[M:M_out] == 0) and torch.all(out[:M, 16 * nt:] == 0)
+        assert torch.all(out[M_out:] == 7.0)
 
 
 @pytest.mark.parametrize("M,nm,Nmod", [(4800, 3, 4096), (640, 2, 11008), (100, 1, 4096)])

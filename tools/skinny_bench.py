@@ -21,7 +21,8 @@ def main():
         x = torch.randn(M, K, device="cuda").bfloat16()
         bt = torch.randn(16 * nt, kred, device="cuda").bfloat16()
         out = torch.empty(M, 64, device="cuda", dtype=torch.bfloat16)
-        f = lambda: ops.lora_skinny(x, bt, out, M, M, kred, nt, koff, 2.0)
+        ws = ops.lora_skinny_ws(M, kred, nt)
+        f = lambda: ops.lora_skinny(x, bt, out, M, M, kred, nt, koff, 2.0, ws=ws)
         for _ in range(3):
             f()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
