@@ -154,7 +154,9 @@ def main():
             traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                "kernel": f"{dom} (gemm_kernel MFMA bf16)", "launches": d["count"],
+                "traffic_note": "HBM+Infinity-Cache bytes per launch (2*FETCH_SIZE+WRITE_SIZE, profiles/gemm_pmc.json)",
+                "algorithmic_bytes_per_launch": round(d["bytes"] / d["count"]),
+                "kernel": f"{dom} (gemm_nt_v5_kernel 8-phase MFMA bf16 + split-K fixup)", "launches": d["count"],
                 "avg_launch_us": round(d["ms"] * 1e3 / d["count"], 2),
                 "step_mfma_frac": round(flops_pair * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)}
     line = {

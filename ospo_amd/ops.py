@@ -20,25 +20,26 @@ _TIMER = None
 
 class KernelTimer:
     def __init__(self):
-        self.recs = []  # (tag, algorithmic flops, start event, end event)
+        self.recs = []  # (tag, algorithmic flops, algorithmic bytes, start event, end event)
 
     def start(self, stream):
         e = torch.cuda.Event(enable_timing=True)
         e.record(stream)
         return e
 
-    def add(self, tag, flops, e0, stream):
+    def add(self, tag, flops, e0, stream, nbytes=0.0):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record(stream)
-        self.recs.append((tag, flops, e0, e1))
+        self.recs.append((tag, flops, nbytes, e0, e1))
 
     def summary(self):
-        """{tag: {count, flops, ms}} (call after synchronize)."""
+        """{tag: {count, flops, bytes, ms}} (call after synchronize)."""
         out = {}
-        for tag, fl, e0, e1 in self.recs:
-            d = out.setdefault(tag, {"count": 0, "flops": 0.0, "ms": 0.0})
+        for tag, fl, nb, e0, e1 in self.recs:
+            d = out.setdefault(tag, {"count": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0})
             d["count"] += 1
             d["flops"] += fl
+            d["bytes"] += nb
             d["ms"] += e0.elapsed_time(e1)
         return out
 
@@ -112,7 +113,9 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
          _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), st.cuda_stream)
     if e0 is not None:
         # algorithmic flops: the frozen product only (the LoRA K-extension is not counted)
-        _TIMER.add(f"gemm_nt_{gemm_nt_tile(M, N)}x{N if N < 256 else 256}", 2.0 * M * N * K, e0, st)
+        # algorithmic bytes: A, B, C once each (+ the bf16 residual read)
+        nbytes = 2.0 * (M * K + N * K + M * N + (M * N if residual is not None else 0))
+        _TIMER.add(f"gemm_nt_{gemm_nt_tile(M, N)}x{N if N < 256 else 256}", 2.0 * M * N * K, e0, st, nbytes)
     return out
 
 

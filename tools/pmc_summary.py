@@ -1,0 +1,65 @@
+"""Per-launch HBM bytes and MFMA busy of the bench's kernels from tools/gpu_pmc_bench.sh.
+
+HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: on gfx950
+FETCH_SIZE reports half the bytes of 16-B/lane streaming reads; WRITE_SIZE is exact),
+FETCH/WRITE_SIZE in KiB.  The NT GEMM's split-K fixup launches are charged to the GEMM
+(the bench times them inside the same launch window).  Writes profiles/gemm_pmc.json."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc_bench")
+
+
+def load(tag):
+    f = glob.glob(os.path.join(src, tag, "**", "*counter_collection.csv"), recursive=True)[0]
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    n = collections.Counter()
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"]
+        per[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        n[(k, r["Counter_Name"])] += 1
+    return per, n
+
+
+def short(k):
+    return k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+
+
+fetch, nf = load("FETCH_SIZE")
+write, nw = load("WRITE_SIZE")
+sq, ns = load("SQ_VALU_MFMA_BUSY_CYCLES")
+out = {}
+gemm = [k for k in fetch if "gemm_nt_v5_kernel" in k]
+fix = [k for k in fetch if "splitk_fixup" in k]
+launches = sum(nf[(k, "FETCH_SIZE")] for k in gemm)
+kib = sum(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"] for k in gemm + fix)
+busy = sum(sq[k]["SQ_VALU_MFMA_BUSY_CYCLES"] for k in sq if "gemm_nt_v5_kernel" in k)
+gui = sum(sq[k]["GRBM_GUI_ACTIVE"] for k in sq if "gemm_nt_v5_kernel" in k)
+# kernel wall time of the same dispatches (counter rows carry the dispatch timestamps)
+f = glob.glob(os.path.join(src, "SQ_VALU_MFMA_BUSY_CYCLES", "**", "*counter_collection.csv"), recursive=True)[0]
+durs = {}
+for r in csv.DictReader(open(f)):
+    if "gemm_nt_v5_kernel" in r["Kernel_Name"]:
+        durs[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+dur_s = sum(durs.values()) * 1e-9
+out["gemm_nt_256x256"] = {
+    "hbm_bytes_per_launch": round(kib * 1024 / launches),
+    "launches": int(launches),
+    "method": "2*FETCH_SIZE + WRITE_SIZE (KiB), gemm_nt_v5_kernel + splitk_fixup_kernel, averaged over launches",
+    # SQ_VALU_MFMA_BUSY_CYCLES: summed over the 1024 SIMDs (16 cycles per 16x16x32 bf16 MFMA);
+    # GRBM_GUI_ACTIVE: summed over the 8 XCDs (GRBM / wall time = 8 x the shader clock)
+    "effective_clock_ghz": round(gui / 8 / dur_s / 1e9, 3) if dur_s else None,
+    "mfma_busy_frac_of_active_cycles": round(busy / (gui / 8 * 1024), 4) if gui else None,
+    "mfma_busy_frac_at_2p4ghz_peak": round(busy / (dur_s * 2.4e9 * 1024), 4) if dur_s else None,
+}
+for k in sorted(set(fetch) | set(write), key=lambda k: -(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"]))[:15]:
+    n = max(nf[(k, "FETCH_SIZE")], 1)
+    out.setdefault("per_kernel_MiB_per_launch", {})[short(k)[:60]] = round(
+        (2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"]) / 1024 / n, 2)
+json.dump(out, open(os.path.join(ROOT, "profiles", "gemm_pmc.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))
