@@ -121,14 +121,17 @@ int ospo_swiglu_bwd(const void* dh, int ld_dh, const void* gu, int ld_gu, void* 
  * [S, H, T] (natural-log sum-exp of the scaled scores).  head_dim == 128.
  * bwd needs the workspace delta fp32 [S*H*T]; dq_acc_ws is reserved (ignored,
  * may be NULL -- dQ is accumulated in registers, no atomics).  dq/dk/dv are
- * written (bf16) into dqkv. */
+ * written (bf16) into dqkv.  With rope_cos/rope_sin (bf16 [T][head_dim/2], the
+ * ospo_rope_* tables) the RoPE backward is applied to dq and dk before the store
+ * (q/k in qkv are then the post-RoPE values); NULL for plain attention. */
 int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
                         int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
                         hipStream_t stream);
 int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col,
                         const void* o, int ld_o, const void* dout, int ld_do, const float* lse,
                         float* delta_ws, float* dq_acc_ws, void* dqkv, int ld_dqkv, int S, int T,
-                        int n_heads, int head_dim, float scale, hipStream_t stream);
+                        int n_heads, int head_dim, float scale, const void* rope_cos,
+                        const void* rope_sin, hipStream_t stream);
 
 /* ------------------------------------------------------- embed / gather ---
  * preprocess_batch (ospo/wrapper/train.py:224-239, 267-277) + concatenated_inputs

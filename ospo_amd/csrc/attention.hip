@@ -95,6 +95,25 @@ __device__ __forceinline__ bf16x8 pack_perm(const f32x4& a, const f32x4& b) {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
+// RoPE backward (transpose of the rotate-half rotation) on fp32 accumulators whose lane
+// holds d = 16dt + 4g + j, dt = 0..7: d < 64 pairs with d + 64 (dt + 4) in the same lane.
+// cs / sn: bf16 [T][64] tables, t = the row's position in its sequence.
+__device__ __forceinline__ void rope_bwd_acc(f32x4 (&v)[8], const bf16* cs, const bf16* sn, int t, int g) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const uint2 cw = *reinterpret_cast<const uint2*>(cs + (long)t * 64 + 16 * dt + 4 * g);
+    const uint2 sw = *reinterpret_cast<const uint2*>(sn + (long)t * 64 + 16 * dt + 4 * g);
+    const float c[4] = {bits2f(cw.x & 0xffff), bits2f(cw.x >> 16), bits2f(cw.y & 0xffff), bits2f(cw.y >> 16)};
+    const float sv[4] = {bits2f(sw.x & 0xffff), bits2f(sw.x >> 16), bits2f(sw.y & 0xffff), bits2f(sw.y >> 16)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = v[dt][j], b = v[dt + 4][j];
+      v[dt][j] = a * c[j] + b * sv[j];
+      v[dt + 4][j] = b * c[j] - a * sv[j];
+    }
+  }
+}
+
 // ============================================================== forward ====
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
                                                        bf16* __restrict__ out, int ldo, float* __restrict__ lse,
@@ -238,7 +257,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
                                                             int vc, const bf16* __restrict__ dout, int ldd,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
-                                                            int ldg, int T, int H, float scale) {
+                                                            int ldg, int T, int H, float scale,
+                                                            const bf16* __restrict__ rcs, const bf16* __restrict__ rsn) {
   // LDS: [Q | dO] x 2 buffers, then lse[2][64], delta[2][64]
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES + 4 * 64 * 4];
   float* Lsb = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
@@ -335,6 +355,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
 
   // lane holds [d = 16dt + 4g + j][key = l16]
   if (key_l < T) {
+    if (rcs) rope_bwd_acc(dk, rcs, rsn, key_l, g);
     bf16* kp = dqkv + (rowbase + key_l) * ldg + kc + h * HD;
     bf16* vp = dqkv + (rowbase + key_l) * ldg + vc + h * HD;
 #pragma unroll
@@ -356,7 +377,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
                                                           int vc, const bf16* __restrict__ dout, int ldd,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, bf16* __restrict__ dqkv,
-                                                          int ldg, int T, int H, float scale) {
+                                                          int ldg, int T, int H, float scale,
+                                                          const bf16* __restrict__ rcs, const bf16* __restrict__ rsn) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -436,6 +458,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   }
 
   if (qrow < T) {
+    if (rcs) rope_bwd_acc(dq, rcs, rsn, qrow, g);
     bf16* dp = dqkv + (rowbase + qrow) * ldg + qc + h * HD;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
@@ -467,13 +490,18 @@ extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k
 extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, const void* o,
                                    int ld_o, const void* dout, int ld_do, const float* lse, float* delta_ws,
                                    float* dq_acc_ws, void* dqkv, int ld_dqkv, int S, int T, int n_heads,
-                                   int head_dim, float scale, hipStream_t stream) {
+                                   int head_dim, float scale, const void* rope_cos, const void* rope_sin,
+                                   hipStream_t stream) {
   (void)dq_acc_ws;  // reserved (ABI v1 atomic-dQ workspace); may be NULL
   if (!qkv || !o || !dout || !lse || !delta_ws || !dqkv) return OSPO_ERR_ARG;
   if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
   if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || ld_do % 8 || ld_dqkv % 8) return OSPO_ERR_SHAPE;
   if (q_col % 8 || k_col % 8 || v_col % 8) return OSPO_ERR_SHAPE;
   if (!aligned16(qkv) || !aligned16(o) || !aligned16(dout) || !aligned16(dqkv)) return OSPO_ERR_ALIGN;
+  if ((rope_cos == nullptr) != (rope_sin == nullptr)) return OSPO_ERR_ARG;
+  if (rope_cos && (((uintptr_t)rope_cos & 7) || ((uintptr_t)rope_sin & 7))) return OSPO_ERR_ALIGN;
+  const bf16* rc = (const bf16*)rope_cos;
+  const bf16* rs = (const bf16*)rope_sin;
   const long rows = (long)S * T;
   const long items = rows * n_heads;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((items + 3) / 4), dim3(256), 0, stream, (const bf16*)o, ld_o,
@@ -481,11 +509,11 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
   OSPO_CHECK_LAUNCH();
   dim3 grid((T + KB - 1) / KB, n_heads, S);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
-                     v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale);
+                     v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
   OSPO_CHECK_LAUNCH();
   dim3 gq((T + QB - 1) / QB, n_heads, S);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
-                     (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale);
+                     (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

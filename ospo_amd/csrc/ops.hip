@@ -133,6 +133,116 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16* __restrict
   (void)gv;
 }
 
+// Wave-per-row forms (D <= 64 lanes x 16 chunks x 8 = 8192): every load of the row is
+// issued before the first use (IT x 16 B in flight per lane), the reduction is a
+// wave shuffle, 4 rows per workgroup -- ~3x the bytes in flight of the block form.
+template <int IT, bool FULL>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_w_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                            bf16* __restrict__ y, float* __restrict__ rstd, long M,
+                                                            int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nch = D >> 3;
+  const u32x4* xr = reinterpret_cast<const u32x4*>(x + row * D);
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  u32x4 v[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = it * 64 + lane;
+    if (FULL || c < nch) v[it] = xr[c];
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = it * 64 + lane;
+    if (FULL || c < nch) {
+      float f[8];
+      unpack8(v[it], f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss += f[q] * f[q];
+    }
+  }
+  const float r = rsqrtf(wave_sum(ss) / (float)D + eps);
+  // re-unpack in the second pass instead of keeping IT x 8 floats alive (occupancy)
+#pragma unroll
+  for (int it = 0; it < IT; ++it) asm volatile("" : "+v"(v[it]));
+  asm volatile("" ::: "memory");  // keep the w loads in this pass
+  u32x4* yr = reinterpret_cast<u32x4*>(y + row * D);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = it * 64 + lane;
+    if (FULL || c < nch) {
+      float f[8], g[8];
+      unpack8(v[it], f);
+      unpack8(wr[c], g);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) f[q] = g[q] * round_bf(f[q] * r);
+      yr[c] = pack8(f);
+    }
+  }
+  if (lane == 0) rstd[row] = r;
+}
+
+template <int IT, bool FULL>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                            const bf16* __restrict__ w, const float* __restrict__ rstd,
+                                                            const bf16* __restrict__ dres, bf16* __restrict__ dx,
+                                                            long M, int D) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nch = D >> 3;
+  const float r = rstd[row];
+  const u32x4* xr = reinterpret_cast<const u32x4*>(x + row * D);
+  const u32x4* dr = reinterpret_cast<const u32x4*>(dy + row * D);
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  const u32x4* rr = dres ? reinterpret_cast<const u32x4*>(dres + row * D) : nullptr;
+  u32x4 xv[IT], dv[IT], rv[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = it * 64 + lane;
+    if (FULL || c < nch) {
+      xv[it] = xr[c];
+      dv[it] = dr[c];
+      if (rr) rv[it] = rr[c];
+    }
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = it * 64 + lane;
+    if (FULL || c < nch) {
+      float f[8], d[8], ww[8];
+      unpack8(xv[it], f);
+      unpack8(dv[it], d);
+      unpack8(wr[c], ww);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dot += d[q] * ww[q] * f[q] * r;
+    }
+  }
+  const float mdot = wave_sum(dot) / (float)D;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) asm volatile("" : "+v"(xv[it]), "+v"(dv[it]));
+  asm volatile("" ::: "memory");
+  u32x4* outr = reinterpret_cast<u32x4*>(dx + row * D);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = it * 64 + lane;
+    if (FULL || c < nch) {
+      float f[8], d[8], ww[8], o[8];
+      unpack8(xv[it], f);
+      unpack8(dv[it], d);
+      unpack8(wr[c], ww);
+      float res[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (rr) unpack8(rv[it], res);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = res[q] + r * (d[q] * ww[q] - f[q] * r * mdot);
+      outr[c] = pack8(o);
+    }
+  }
+}
+
 // --------------------------------------------------------------------- RoPE
 // one thread = 8 rotation pairs (i..i+7, i+h..i+h+7) of one (row, head, q|k)
 template <bool BWD>
@@ -496,8 +606,17 @@ extern "C" int ospo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rs
   if (!x || !w || !y || !rstd) return OSPO_ERR_ARG;
   if (M <= 0 || D % 8 || D > 256 * 8 * RMS_MAXIT) return OSPO_ERR_SHAPE;
   if (!aligned16(x) || !aligned16(w) || !aligned16(y)) return OSPO_ERR_ALIGN;
-  hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3(M), dim3(256), 0, st, (const bf16*)x, (const bf16*)w, (bf16*)y, rstd,
-                     D, eps);
+  const int it = (D / 8 + 63) / 64;
+  const dim3 gw((M + 3) / 4);
+  const bf16 *xb = (const bf16*)x, *wb = (const bf16*)w;
+  const long Ml = M;
+  if (D == 4096) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<8, true>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
+  else if (D == 2048) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<4, true>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
+  else if (it <= 1) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<1, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
+  else if (it <= 2) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<2, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
+  else if (it <= 4) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<4, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
+  else if (it <= 8) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<8, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
+  else hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3(M), dim3(256), 0, st, xb, wb, (bf16*)y, rstd, D, eps);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
@@ -508,8 +627,17 @@ extern "C" int ospo_rmsnorm_bwd(const void* dy, const void* x, const void* w, co
   if (M <= 0 || D % 8 || D > 256 * 8 * RMS_MAXIT) return OSPO_ERR_SHAPE;
   if (!aligned16(dy) || !aligned16(x) || !aligned16(w) || !aligned16(dx) || (dres && !aligned16(dres)))
     return OSPO_ERR_ALIGN;
-  hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(M), dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, (const bf16*)w,
-                     rstd, (const bf16*)dres, (bf16*)dx, D);
+  const int it = (D / 8 + 63) / 64;
+  const dim3 gw((M + 3) / 4);
+  const bf16 *dyb = (const bf16*)dy, *xb = (const bf16*)x, *wb = (const bf16*)w, *rb = (const bf16*)dres;
+  const long Ml = M;
+  if (D == 4096) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<8, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
+  else if (D == 2048) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<4, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
+  else if (it <= 1) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<1, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
+  else if (it <= 2) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<2, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
+  else if (it <= 4) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<4, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
+  else if (it <= 8) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<8, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
+  else hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(M), dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, D);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

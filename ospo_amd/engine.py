@@ -393,8 +393,7 @@ class SimPOEngine:
             # ---- attention + RoPE
             guard("qkv")  # dqkv is rewritten here
             ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, None,
-                               self.dqkv, S, T, H, hd, scale_attn)
-            ops.rope(self.dqkv, 0, D, S, T, H, hd, self.cos, self.sin, backward=True)
+                               self.dqkv, S, T, H, hd, scale_attn, rope_cos=self.cos, rope_sin=self.sin)
             # ---- q/k/v
             Acat, AcatT, Bcat, BT = pk["qkv"]
             gs = self._lora_g(self.dqkv, lay.groups["qkv"], Bcat, BT, M)

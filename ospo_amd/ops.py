@@ -194,9 +194,12 @@ def flash_attn_fwd(qkv, q_col, k_col, v_col, o, lse, S, T, n_heads, head_dim, sc
     return o, lse
 
 
-def flash_attn_bwd(qkv, q_col, k_col, v_col, o, dout, lse, delta_ws, dq_ws, dqkv, S, T, n_heads, head_dim, scale):
+def flash_attn_bwd(qkv, q_col, k_col, v_col, o, dout, lse, delta_ws, dq_ws, dqkv, S, T, n_heads, head_dim, scale,
+                   rope_cos=None, rope_sin=None):
+    """Attention backward; with rope_cos/rope_sin the RoPE backward is fused into the dq/dk stores."""
     call("ospo_flash_attn_bwd", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(dout), _ld(dout),
-         _p(lse), _p(delta_ws), _p(dq_ws), _p(dqkv), _ld(dqkv), S, T, n_heads, head_dim, float(scale), _s())
+         _p(lse), _p(delta_ws), _p(dq_ws), _p(dqkv), _ld(dqkv), S, T, n_heads, head_dim, float(scale),
+         _p(rope_cos), _p(rope_sin), _s())
     return dqkv
 
 

@@ -221,6 +221,46 @@ def test_flash_attention(S, T, H):
         assert e < 2e-2, (nm, e)
 
 
+@pytest.mark.parametrize("S,T,H", [(2, 130, 2), (1, 600, 1)])
+def test_flash_attention_bwd_fused_rope(S, T, H):
+    """dq/dk with the RoPE backward fused into the stores == the unfused chain
+    (attention bwd, then ospo_rope_bwd), and both track fp32 autograd through
+    rope -> attention w.r.t. the PRE-RoPE q, k."""
+    hd = 128
+    D = H * hd
+    rows = S * T + 3
+    pre = rnd(rows, 3 * D)
+    cos, sin = ops().rope_tables(T, hd, 1e4, DEV)
+    qkv = pre.clone()
+    ops().rope(qkv, 0, D, S, T, H, hd, cos, sin)
+    o = torch.zeros(rows, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(S * H * T, device=DEV)
+    scale = 1 / math.sqrt(hd)
+    ops().flash_attn_fwd(qkv, 0, D, 2 * D, o, lse, S, T, H, hd, scale)
+    do = rnd(rows, D)
+    delta = torch.empty(S * H * T, device=DEV)
+    fused = torch.zeros(rows, 3 * D, device=DEV, dtype=torch.bfloat16)
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, fused, S, T, H, hd, scale,
+                         rope_cos=cos, rope_sin=sin)
+    plain = torch.zeros(rows, 3 * D, device=DEV, dtype=torch.bfloat16)
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, plain, S, T, H, hd, scale)
+    ops().rope(plain, 0, D, S, T, H, hd, cos, sin, backward=True)
+    assert relerr(fused[: S * T].float(), plain[: S * T].float()) < 8e-3
+    assert torch.equal(fused[: S * T, 2 * D:], plain[: S * T, 2 * D:])  # dv untouched by RoPE
+    # fp32 autograd through rope -> attention (scores rounded like the kernel)
+    c, s_ = O.rope_cos_sin(T, hd, 1e4, torch.bfloat16)
+    c, s_ = c.to(DEV).float(), s_.to(DEV).float()
+    src = pre[: S * T].float().view(S, T, 3, H, hd).permute(2, 0, 3, 1, 4).requires_grad_(True)
+    q = O.apply_rope(src[0], c, s_)
+    k = O.apply_rope(src[1], c, s_)
+    ref = attn_ref(q, k, src[2], scale)
+    ref.backward(do[: S * T].float().view(S, T, H, hd).transpose(1, 2))
+    g = src.grad.permute(1, 3, 0, 2, 4).reshape(S * T, 3 * D)
+    for i, nm in enumerate("qkv"):
+        e = relerr(fused[: S * T, i * D:(i + 1) * D].float(), g[:, i * D:(i + 1) * D])
+        assert e < 2e-2, (nm, e)
+
+
 # ------------------------------------------------------- embed / gather / gelu
 def test_assemble_and_aligner():
     B, Lt, N, D, V = 2, 5, 8, 256, 50
