@@ -185,9 +185,12 @@ int ospo_simpo_bwd(const float* logps, int B, float beta, float gamma_beta_ratio
  *   AcatT[Kin][Rp]   its transpose
  *   Bcat [nmods*Nmod][Rp] block-diagonal stacked lora_B
  *   BT   [nmods*r][Nmod]  per-module lora_B^T (optional, may be NULL)
- * Rp = roundup(nmods*r, 64). */
+ * Rp = roundup(nmods*r, 64).  n_layers layers in one launch: A_flat/B_flat
+ * advance by layer_stride elements per layer, the outputs are [n_layers][...]
+ * contiguous. */
 int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int Kin, int Nmod,
-                   int Rp, void* Acat, void* AcatT, void* Bcat, void* BT, hipStream_t stream);
+                   int Rp, void* Acat, void* AcatT, void* Bcat, void* BT, int n_layers,
+                   long layer_stride, hipStream_t stream);
 
 /* Skinny LoRA products (peft lora.Linear, y += s B(A x)) -- bf16 out, no
  * atomics.  For n-tile j < n_tiles (columns 16j .. 16j+15):

@@ -230,25 +230,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 }
 
 // ============================================================ backward =====
-// delta[s,h,t] = sum_d dO[t, h*HD + d] * O[t, h*HD + d]
-__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict__ o, int ldo,
-                                                         const bf16* __restrict__ dout, int ldd,
-                                                         float* __restrict__ delta, int S, int T, int H) {
-  const int lane = threadIdx.x & 63;
-  const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per (row, head)
-  if (item >= (long)S * T * H) return;
-  const int h = item % H;
-  const long row = item / H;
-  const int s = row / T, t = row % T;
-  const bf16* op = o + row * ldo + h * HD;
-  const bf16* dp = dout + row * ldd + h * HD;
-  const unsigned ov = reinterpret_cast<const unsigned*>(op)[lane];
-  const unsigned dv = reinterpret_cast<const unsigned*>(dp)[lane];
-  float acc = bits2f(ov & 0xffff) * bits2f(dv & 0xffff) + bits2f(ov >> 16) * bits2f(dv >> 16);
-  acc = wave_sum(acc);
-  if (lane == 0) delta[((long)s * H + h) * T + t] = acc;
-}
-
 // dK / dV: workgroup = 4 waves = 64 keys of one (sequence, head); each wave
 // owns 16 keys (K, V fragments in registers, dK^T dV^T accumulators) and
 // sweeps the query tiles at/after its block.  Q / dO tiles (+ lse, delta) are
@@ -375,8 +356,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
 // dQ lives in registers for the whole sweep: no atomics, no workspace.
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
                                                           int vc, const bf16* __restrict__ dout, int ldd,
+                                                          const bf16* __restrict__ o, int ldo,
                                                           const float* __restrict__ lse,
-                                                          const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                          float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                           int ldg, int T, int H, float scale,
                                                           const bf16* __restrict__ rcs, const bf16* __restrict__ rsn) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
@@ -390,17 +372,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const int qrow = qb * QB + wave * 16 + l16;
   const int qr_c = qrow < T ? qrow : T - 1;
   bf16x8 qf[4], of[4];
+  float dpart = 0.f;  // delta = rowsum(dO * O), this lane's 32 of the head's 128 columns
   {
     const bf16* qp = qkv + (rowbase + qr_c) * ldq + qc + h * HD;
     const bf16* op = dout + (rowbase + qr_c) * ldd + h * HD;
+    const bf16* oo = o + (rowbase + qr_c) * ldo + h * HD;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       qf[d] = *reinterpret_cast<const bf16x8*>(qp + 32 * d + 8 * g);
       of[d] = *reinterpret_cast<const bf16x8*>(op + 32 * d + 8 * g);
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(oo + 32 * d + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dpart += bf2f(of[d][i]) * bf2f(ov[i]);
     }
   }
+  dpart += __shfl_xor(dpart, 16, 64);
+  dpart += __shfl_xor(dpart, 32, 64);
+  const float del_q = dpart;
   const float lse_q = lse[((long)s * H + h) * T + qr_c];
-  const float del_q = delta[((long)s * H + h) * T + qr_c];
+  if (g == 0 && qrow < T) delta[((long)s * H + h) * T + qrow] = del_q;  // for the dK/dV kernel (launched next)
 
   f32x4 dq[8];
 #pragma unroll
@@ -502,18 +492,15 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
   if (rope_cos && (((uintptr_t)rope_cos & 7) || ((uintptr_t)rope_sin & 7))) return OSPO_ERR_ALIGN;
   const bf16* rc = (const bf16*)rope_cos;
   const bf16* rs = (const bf16*)rope_sin;
-  const long rows = (long)S * T;
-  const long items = rows * n_heads;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((items + 3) / 4), dim3(256), 0, stream, (const bf16*)o, ld_o,
-                     (const bf16*)dout, ld_do, delta_ws, S, T, n_heads);
+  // dQ first: it also produces delta = rowsum(dO * O) for the dK/dV kernel
+  dim3 gq((T + QB - 1) / QB, n_heads, S);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+                     (const bf16*)dout, ld_do, (const bf16*)o, ld_o, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads,
+                     scale, rc, rs);
   OSPO_CHECK_LAUNCH();
   dim3 grid((T + KB - 1) / KB, n_heads, S);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
                      v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
-  OSPO_CHECK_LAUNCH();
-  dim3 gq((T + QB - 1) / QB, n_heads, S);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
-                     (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

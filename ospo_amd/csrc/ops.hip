@@ -518,13 +518,22 @@ __global__ void simpo_bwd_kernel(const float* __restrict__ lp, int B, float beta
 }
 
 // ---------------------------------------------------------------- LoRA pack
+// blockIdx.y = layer: sources advance by layer_stride elements of the flat LoRA
+// buffer, destinations are [n_layers][...] contiguous
 __global__ void lora_pack_kernel(const bf16* __restrict__ Af, const bf16* __restrict__ Bf, int nmods, int r, int Kin,
                                  int Nmod, int Rp, bf16* __restrict__ Acat, bf16* __restrict__ AcatT,
-                                 bf16* __restrict__ Bcat, bf16* __restrict__ BT) {
+                                 bf16* __restrict__ Bcat, bf16* __restrict__ BT, long layer_stride) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long na = (long)Rp * Kin;
   const long nb = (long)nmods * Nmod * Rp;
   const int used = nmods * r;
+  const long l = blockIdx.y;
+  Af += l * layer_stride;
+  Bf += l * layer_stride;
+  Acat += l * na;
+  AcatT += l * na;
+  Bcat += l * nb;
+  if (BT) BT += l * (long)used * Nmod;
   if (tid < na) {
     const int j = tid / Kin, k = tid % Kin;
     const bf16 v = j < used ? Af[(long)j * Kin + k] : f2bf(0.f);
@@ -803,12 +812,16 @@ extern "C" int ospo_simpo_bwd(const float* logps, int B, float beta, float gbr, 
 }
 
 extern "C" int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int Kin, int Nmod, int Rp,
-                              void* Acat, void* AcatT, void* Bcat, void* BT, hipStream_t st) {
+                              void* Acat, void* AcatT, void* Bcat, void* BT, int n_layers, long layer_stride,
+                              hipStream_t st) {
   if (!A_flat || !B_flat || !Acat || !AcatT || !Bcat) return OSPO_ERR_ARG;
-  if (nmods <= 0 || r <= 0 || Kin <= 0 || Nmod <= 0 || Rp < nmods * r) return OSPO_ERR_SHAPE;
+  if (nmods <= 0 || r <= 0 || Kin <= 0 || Nmod <= 0 || Rp < nmods * r || n_layers < 1 || n_layers > 65535 ||
+      (n_layers > 1 && layer_stride <= 0))
+    return OSPO_ERR_SHAPE;
   const long n = std::max((long)Rp * Kin, (long)nmods * Nmod * Rp);
-  hipLaunchKernelGGL(lora_pack_kernel, dim3(blocks(n)), dim3(256), 0, st, (const bf16*)A_flat, (const bf16*)B_flat,
-                     nmods, r, Kin, Nmod, Rp, (bf16*)Acat, (bf16*)AcatT, (bf16*)Bcat, (bf16*)BT);
+  hipLaunchKernelGGL(lora_pack_kernel, dim3(blocks(n), n_layers), dim3(256), 0, st, (const bf16*)A_flat,
+                     (const bf16*)B_flat, nmods, r, Kin, Nmod, Rp, (bf16*)Acat, (bf16*)AcatT, (bf16*)Bcat, (bf16*)BT,
+                     layer_stride);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

@@ -125,16 +125,15 @@ class SimPOEngine:
         self.exp_avg_sq = torch.zeros(n, dtype=BF16, device=dev)
         self.opt_step = 0
         self._sumsq = torch.zeros(1, dtype=F32, device=dev)
-        # packed LoRA operands per layer / group
-        self.packed = []
-        for i in range(L):
-            d = {}
-            for gname, g in self.layout.groups.items():
-                d[gname] = (torch.zeros(g.Rp, g.Kin, dtype=BF16, device=dev),
-                            torch.zeros(g.Kin, g.Rp, dtype=BF16, device=dev),
-                            torch.zeros(g.nmods * g.Nmod, g.Rp, dtype=BF16, device=dev),
-                            torch.zeros(g.nmods * self.layout.r, g.Nmod, dtype=BF16, device=dev))
-            self.packed.append(d)
+        # packed LoRA operands, per group contiguous over layers ([L][...], one pack launch per group)
+        r = self.layout.r
+        self._packed_all = {
+            gname: (torch.zeros(max(L, 1), g.Rp, g.Kin, dtype=BF16, device=dev),
+                    torch.zeros(max(L, 1), g.Kin, g.Rp, dtype=BF16, device=dev),
+                    torch.zeros(max(L, 1), g.nmods * g.Nmod, g.Rp, dtype=BF16, device=dev),
+                    torch.zeros(max(L, 1), g.nmods * r, g.Nmod, dtype=BF16, device=dev))
+            for gname, g in self.layout.groups.items()}
+        self.packed = [{gname: tuple(t[i] for t in ts) for gname, ts in self._packed_all.items()} for i in range(L)]
         self.pack_lora()
         self._alloc(max_pairs, max_text_len, n_img_tokens)
         self._rope_T = -1
@@ -197,15 +196,17 @@ class SimPOEngine:
         self.dhsel = z(R, D)
 
     def pack_lora(self):
-        """Rebuild the packed A / A^T / block-diagonal B operands from the flat params."""
-        r = self.layout.r
-        for i in range(self.dims.n_layers):
-            base = self.layout.layer_off(i)
-            for gname, g in self.layout.groups.items():
-                Acat, AcatT, Bcat, BT = self.packed[i][gname]
-                A = self.lora[base + g.a_off: base + g.a_off + g.nmods * r * g.Kin]
-                B = self.lora[base + g.b_off: base + g.b_off + g.nmods * g.Nmod * r]
-                ops.lora_pack(A, B, g.nmods, r, g.Kin, g.Nmod, g.Rp, Acat, AcatT, Bcat, BT)
+        """Rebuild the packed A / A^T / block-diagonal B / B^T operands from the flat params
+        (one launch per module group, all layers)."""
+        L, r = self.dims.n_layers, self.layout.r
+        if L == 0:
+            return
+        for gname, g in self.layout.groups.items():
+            Acat, AcatT, Bcat, BT = self._packed_all[gname]
+            A = self.lora[g.a_off:]
+            B = self.lora[g.b_off:]
+            ops.lora_pack(A, B, g.nmods, r, g.Kin, g.Nmod, g.Rp, Acat, AcatT, Bcat, BT, n_layers=L,
+                          layer_stride=self.layout.per_layer)
 
     def lora_tensors(self) -> Dict[str, torch.Tensor]:
         return self.layout.from_flat(self.lora)

@@ -271,9 +271,9 @@ def simpo_bwd(logps, B, beta, gbr, ls, loss_type, g_loss, glogps):
 
 
 # ------------------------------------------------------------- LoRA pack
-def lora_pack(A_flat, B_flat, nmods, r, Kin, Nmod, Rp, Acat, AcatT, Bcat, BT=None):
+def lora_pack(A_flat, B_flat, nmods, r, Kin, Nmod, Rp, Acat, AcatT, Bcat, BT=None, n_layers=1, layer_stride=0):
     call("ospo_lora_pack", _p(A_flat), _p(B_flat), nmods, r, Kin, Nmod, Rp, _p(Acat), _p(AcatT), _p(Bcat), _p(BT),
-         _s())
+         n_layers, layer_stride, _s())
 
 
 def lora_skinny_ws_bytes(M_out, K, n_tiles) -> int:

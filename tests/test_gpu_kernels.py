@@ -369,6 +369,22 @@ def test_lora_pack():
         expB[i * Nmod:(i + 1) * Nmod, i * r:(i + 1) * r] = Bf[i]
     assert torch.equal(Bcat, expB)
     assert torch.equal(BT, torch.cat([Bf[i].T for i in range(nm)], 0))
+    # two layers in one launch: sources at a layer stride in a flat buffer, outputs [L][...]
+    na, nb = nm * r * Kin, nm * Nmod * r
+    stride = na + nb + 40
+    flat = torch.zeros(2 * stride, device=DEV, dtype=torch.bfloat16)
+    A2, B2 = rnd(nm * r, Kin), rnd(nm, Nmod, r)
+    for l, (a_, b_) in enumerate(((A, Bf), (A2, B2))):
+        flat[l * stride: l * stride + na] = a_.reshape(-1)
+        flat[l * stride + na: l * stride + na + nb] = b_.reshape(-1)
+    Ac2 = torch.empty(2, Rp, Kin, device=DEV, dtype=torch.bfloat16)
+    AT2 = torch.empty(2, Kin, Rp, device=DEV, dtype=torch.bfloat16)
+    Bc2 = torch.empty(2, nm * Nmod, Rp, device=DEV, dtype=torch.bfloat16)
+    BT2 = torch.empty(2, nm * r, Nmod, device=DEV, dtype=torch.bfloat16)
+    ops().lora_pack(flat, flat[na:], nm, r, Kin, Nmod, Rp, Ac2, AT2, Bc2, BT2, n_layers=2, layer_stride=stride)
+    assert torch.equal(Ac2[0], Acat) and torch.equal(AT2[0], AcatT) and torch.equal(Bc2[0], Bcat)
+    assert torch.equal(BT2[0], BT)
+    assert torch.equal(Ac2[1, : nm * r], A2) and torch.equal(BT2[1], torch.cat([B2[i].T for i in range(nm)], 0))
 
 
 @pytest.mark.parametrize("M,K,used", [(4800, 4096, 48), (300, 11008, 16), (77, 512, 32), (1, 256, 64)])
