@@ -53,6 +53,17 @@ int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int
                       const void* bias, const void* residual, int ldr, void* C, int ldc,
                       hipStream_t stream);
 
+/* ospo_gemm_nt_bf16 (alpha 1, no bias / residual, N % 256 == 0) with the RoPE
+ * forward (ospo_rope_fwd semantics: HF rotate-half, bf16 rounding per op) fused
+ * into the epilogue for output columns < rope_cols (a multiple of the 128-wide
+ * head; q|k of the fused qkv projection), position = row % T.  rope_cos/sin are
+ * the bf16 [T][64] tables.  Replaces q_proj/k_proj + apply_rotary_pos_emb
+ * (transformers 4.38 modeling_llama.py, reached from ospo/wrapper/train.py:352). */
+int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
+                           const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
+                           const void* rope_cos, const void* rope_sin, int T, int rope_cols,
+                           hipStream_t stream);
+
 /* Split-K workspace for the GEMM's tail round (tiles % CUs leftover tiles are split
  * along K into fp32 partial tiles, then summed + epilogued by a fixup launch).
  * bytes >= 256 KiB x CU count uses the split everywhere it pays; NULL disables it.

@@ -21,6 +21,7 @@ SIGNATURES = {
     "ospo_abi_version": [],
     "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P],
     "ospo_gemm_nt_tile": [I, I],
+    "ospo_gemm_nt_rope_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, P, I, I, P],
     "ospo_set_gemm_variant": [I],
     "ospo_gemm_set_workspace": [P, Z],
     "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],

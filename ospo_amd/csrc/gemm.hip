@@ -98,6 +98,10 @@ struct GemmArgs {
   void* C; int ldc;
   int k_splits;
   int diag_nblk, diag_r;
+  // fused RoPE (HF rotate-half, head_dim 128) on output columns < rope_cols, position = row % rope_T
+  const bf16* rope_cs = nullptr;
+  const bf16* rope_sn = nullptr;
+  int rope_T = 0, rope_cols = 0;
 };
 
 // DBG (A/B decomposition only, results invalid): 1 = no global loads after the
@@ -654,8 +658,9 @@ int launch_v4(const GemmArgs& a, hipStream_t s) {
 //    wave waits for its own DMA of it (vmcnt(2+2) before q0, vmcnt(6) before q2),
 //    placed just before the barrier that precedes the first reader.
 // Tile order: XCD-contiguous chunks of the data-parallel workgroups, GM = 4 row-tile groups.
-__device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0, int& n0) {
-  constexpr int GM = 4;
+int g_v5_gm = 4;  // row tiles per L2 group (A/B knob, variants 20-23)
+
+__device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0, int& n0, int GM = 4) {
   const int gsize = GM * tiles_n;
   const int first_m = (L / gsize) * GM;
   const int gm = min(tiles_m - first_m, GM);
@@ -669,7 +674,7 @@ __device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0
 // and write an fp32 partial tile to ws (summed + epilogued by splitk_fixup_kernel).
 template <int DBG = 0>
 __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
-                                                         int split, float* __restrict__ ws) {
+                                                         int split, float* __restrict__ ws, int GM) {
   constexpr int BM = 256, BN = 256, HALF = 16384, SLOT = 4 * HALF;  // half order in a slot: A0 A1 B0 B1
   constexpr int CPITCH = BN * 2 + 16;
   constexpr int LDS_BYTES = (2 * SLOT > BM * CPITCH) ? 2 * SLOT : BM * CPITCH;
@@ -688,13 +693,13 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
     if (wg < dp) {
       const int xcd = wg & 7, slot = wg >> 3, q = dp >> 3, r = dp & 7;
       const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-      v5_tile(L, tiles_m, tiles_n, m0, n0);
+      v5_tile(L, tiles_m, tiles_n, m0, n0, GM);
       tb = 0;
       tcount = ntot;
     } else {
       const int u = wg - dp, z = u % split;
       part = u;
-      v5_tile(dp + u / split, tiles_m, tiles_n, m0, n0);
+      v5_tile(dp + u / split, tiles_m, tiles_n, m0, n0, GM);
       tb = (int)((long)ntot * z / split);
       tcount = (int)((long)ntot * (z + 1) / split) - tb;
     }
@@ -873,6 +878,31 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
     const int m = m0 + r2;
     if (m >= args.M) continue;
     u32x4 v = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + cc * 16);
+    if (n0 + cc * 8 < args.rope_cols) {
+      // RoPE on the bf16-rounded product, rounding per op like HF: x*cos + rotate_half(x)*sin.
+      // The tile holds two whole heads, so the partner (+-64 columns) is in the same LDS row.
+      const int d = (cc * 8) & 127;
+      const bool lo = d < 64;
+      const u32x4 pv = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + (lo ? cc + 8 : cc - 8) * 16);
+      const int t = m % args.rope_T, dd = lo ? d : d - 64;
+      const u32x4 cw = *reinterpret_cast<const u32x4*>(args.rope_cs + (long)t * 64 + dd);
+      const u32x4 sw = *reinterpret_cast<const u32x4*>(args.rope_sn + (long)t * 64 + dd);
+      u32x4 o;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        float r[2];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int sh = 16 * hh;
+          const float x = bits2f((v[qq] >> sh) & 0xffff), p = bits2f((pv[qq] >> sh) & 0xffff);
+          const float cf = bits2f((cw[qq] >> sh) & 0xffff), sf = bits2f((sw[qq] >> sh) & 0xffff);
+          // lo half: x1*c + (-x2)*s ; hi half: x2*c + x1*s
+          r[hh] = lo ? round_bf(x * cf) + round_bf(-p * sf) : round_bf(x * cf) + round_bf(p * sf);
+        }
+        o[qq] = pack2(r[0], r[1]);
+      }
+      v = o;
+    }
     if (args.res) {
       const u32x4 rv = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + cc * 8);
 #pragma unroll
@@ -888,10 +918,10 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
 
 // sum the split partials of each tail tile, apply alpha / bias / residual, write bf16
 __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
-                                                           int split, const float* __restrict__ ws) {
+                                                           int split, const float* __restrict__ ws, int GM) {
   const int tile = blockIdx.x >> 5, rblk = blockIdx.x & 31;
   int m0, n0;
-  v5_tile(dp + tile, tiles_m, tiles_n, m0, n0);
+  v5_tile(dp + tile, tiles_m, tiles_n, m0, n0, GM);
   const int r = rblk * 8 + (threadIdx.x >> 5), c = (threadIdx.x & 31) * 8;
   const int m = m0 + r;
   if (m >= args.M) return;
@@ -940,7 +970,7 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   const int ntot = a.K / BK + a.K2 / BK;
   const int cus = num_cus();
   int dp = tiles, split = 1, tail = 0;
-  if (allow_split && tiles > cus) {
+  if (allow_split && a.rope_cols == 0 && tiles > cus) {
     tail = tiles % cus;
     split = tail ? std::min(cus / tail, std::min(8, ntot / 4)) : 1;
     const size_t need = (size_t)tail * split * 65536 * sizeof(float);
@@ -952,11 +982,11 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
     }
   }
   const int grid = dp + tail * split;
-  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split, g_splitk_ws);
+  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split, g_splitk_ws, g_v5_gm);
   OSPO_CHECK_LAUNCH();
   if (tail) {
     hipLaunchKernelGGL(splitk_fixup_kernel, dim3(tail * 32), dim3(256), 0, s, a, tm, tn, dp, split,
-                       (const float*)g_splitk_ws);
+                       (const float*)g_splitk_ws, g_v5_gm);
     OSPO_CHECK_LAUNCH();
   }
   return OSPO_OK;
@@ -1016,6 +1046,28 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   }
 }
 
+extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
+                                      const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
+                                      const void* rope_cos, const void* rope_sin, int T, int rope_cols,
+                                      hipStream_t stream) {
+  if (!A || !B || !C || !rope_cos || !rope_sin) return OSPO_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK || K2 < 0 || K2 % BK || N % 256 || T <= 0) return OSPO_ERR_SHAPE;
+  if (rope_cols < 0 || rope_cols % 128 || rope_cols > N) return OSPO_ERR_SHAPE;
+  if (K2 > 0 && (!A2 || !B2)) return OSPO_ERR_ARG;
+  if (lda < K || ldb < K || ldc < N || (lda % 8) || (ldb % 8) || (ldc % 8)) return OSPO_ERR_SHAPE;
+  if (K2 > 0 && (lda2 < K2 || ldb2 < K2 || lda2 % 8 || ldb2 % 8)) return OSPO_ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(B) || !aligned16(C) || !aligned16(rope_cos) || !aligned16(rope_sin) ||
+      (K2 > 0 && (!aligned16(A2) || !aligned16(B2))))
+    return OSPO_ERR_ALIGN;
+  GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
+             M, N, K, K2, 1.f, nullptr, nullptr, 0, C, ldc, 1, 0, 0};
+  a.rope_cs = (const bf16*)rope_cos;
+  a.rope_sn = (const bf16*)rope_sin;
+  a.rope_T = T;
+  a.rope_cols = rope_cols;
+  return launch_v5<0>(a, stream, false);
+}
+
 extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {
   if (bytes && (!ws || !aligned16(ws))) return OSPO_ERR_ARG;
   g_splitk_ws = (float*)ws;
@@ -1024,7 +1076,14 @@ extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {
 }
 
 extern "C" int ospo_set_gemm_variant(int v) {
+  if (v >= 20 && v <= 23) {  // L2 row-group size of the default schedule: 2, 8, 16, 4
+    const int gms[4] = {2, 8, 16, 4};
+    g_v5_gm = gms[v - 20];
+    g_gemm_variant = 0;
+    return OSPO_OK;
+  }
   if (v < 0 || v > 13 || (v > 5 && v < 10)) return OSPO_ERR_ARG;
+  g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;
 }

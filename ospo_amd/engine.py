@@ -299,8 +299,12 @@ class SimPOEngine:
             ops.rmsnorm_fwd(x[:M], lw["ln_in"], a["xn1"][:M], a["rstd1"][:M], dims.rms_eps)
             Acat, _, Bcat, _ = pk["qkv"]
             self._lora_down(a["xn1"], Acat, a["u_qkv"], M, lay.groups["qkv"].nmods)
-            ops.gemm_nt(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat)
-            ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
+            if (3 * D) % 256 == 0:  # q|k RoPE fused into the projection's epilogue
+                ops.gemm_nt(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat,
+                            rope=(self.cos, self.sin, T, 2 * D))
+            else:
+                ops.gemm_nt(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat)
+                ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
             ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn)
             Acat, _, Bcat, _ = pk["o"]
             self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods)

@@ -91,8 +91,9 @@ def gemm_workspace(device=None) -> torch.Tensor:
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0,
-            bias=None, residual=None) -> torch.Tensor:
-    """out[M,N] = bf16(alpha*(a.b^T + a2.b2^T) + bias) [+ residual]  (nn.Linear layout b=[N,K])."""
+            bias=None, residual=None, rope=None) -> torch.Tensor:
+    """out[M,N] = bf16(alpha*(a.b^T + a2.b2^T) + bias) [+ residual]  (nn.Linear layout b=[N,K]).
+    rope=(cos, sin, T, ncols): RoPE forward fused on output columns < ncols (ospo_gemm_nt_rope_bf16)."""
     for t, n in ((a, "a"), (b, "b"), (out, "out")):
         _chk(t, BF16, n)
     M, K = a.shape
@@ -108,9 +109,17 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
         gemm_workspace(a.device)
     st = torch.cuda.current_stream()
     e0 = _TIMER.start(st) if _TIMER is not None else None
-    call("ospo_gemm_nt_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K,
-         _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2, float(alpha),
-         _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), st.cuda_stream)
+    if rope is not None:
+        if bias is not None or residual is not None or alpha != 1.0:
+            raise ValueError("gemm_nt: rope excludes bias / residual / alpha")
+        cos, sin, T, ncols = rope
+        call("ospo_gemm_nt_rope_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K,
+             _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2,
+             _p(out), _ld(out), _p(cos), _p(sin), int(T), int(ncols), st.cuda_stream)
+    else:
+        call("ospo_gemm_nt_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K,
+             _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2, float(alpha),
+             _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), st.cuda_stream)
     if e0 is not None:
         # algorithmic flops: the frozen product only (the LoRA K-extension is not counted)
         # algorithmic bytes: A, B, C once each (+ the bf16 residual read)

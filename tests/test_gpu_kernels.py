@@ -136,6 +136,23 @@ def test_rmsnorm(M, D):
 
 
 # --------------------------------------------------------------------- RoPE
+@pytest.mark.parametrize("M,H,T", [(2 * 72, 2, 72), (300, 4, 150), (4800, 8, 600)])
+def test_gemm_rope_fused_equals_unfused(M, H, T):
+    """ospo_gemm_nt_rope_bf16 == gemm_nt then ospo_rope_fwd, bit for bit (same rounding points)."""
+    hd, K = 128, 512
+    D = H * hd
+    N = 3 * D if (3 * D) % 256 == 0 else 4 * D
+    a, b = rnd(M, K), rnd(N, K, s=0.05)
+    a2, b2 = rnd(M, 64), rnd(N, 64, s=0.05)
+    cos, sin = ops().rope_tables(T, hd, 1e4, DEV)
+    ref = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(a, b, ref, a2=a2, b2=b2)
+    ops().rope(ref, 0, D, M // T, T, H, hd, cos, sin)
+    out = torch.empty_like(ref)
+    ops().gemm_nt(a, b, out, a2=a2, b2=b2, rope=(cos, sin, T, 2 * D))
+    assert torch.equal(out, ref)
+
+
 def test_rope_fwd_bwd():
     S, T, H, hd = 2, 72, 3, 128
     D = H * hd
