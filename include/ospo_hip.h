@@ -205,19 +205,20 @@ int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int
 
 /* Skinny LoRA products (peft lora.Linear, y += s B(A x)) -- bf16 out, no
  * atomics.  For n-tile j < n_tiles (columns 16j .. 16j+15):
- *   out[m][16j+c] = scale * sum_{k<K} A[m][j*a_koff + k] * Bt[16j+c][k]
- * Bt rows >= b_rows read as zero; rows M..M_out-1 and columns
- * 16*n_tiles..out_cols-1 of out are written zero.  n_tiles <= 4, K % 32 == 0.
+ *   out[m][16j+c] = scale * sum_{k<K} A[m][(j / module_tiles) * a_koff + k] * Bt[16j+c][k]
+ * (a_koff = 0: dense, every tile reduces the same K columns of A).  Bt rows
+ * >= b_rows read as zero; rows M..M_out-1 and columns 16*n_tiles..out_cols-1
+ * of out are written zero.  n_tiles <= 16, K % 32 == 0.
  *   u = s x A_cat^T : A = x [M, K], Bt = A_cat [Rp, K], a_koff = 0
  *   g = s dy B      : A = dy [M, nmods*Nmod], Bt = BT [nmods*r, Nmod],
- *                     K = a_koff = Nmod, n_tiles = nmods (r == 16)
+ *                     K = a_koff = Nmod, module_tiles = r / 16
  * K is split across workgroups; ws (>= ospo_lora_skinny_ws_bytes(M_out, K,
  * n_tiles) bytes, 16-B aligned) holds the fp32 partials that a second launch
  * sums.  Calls sharing a ws must be ordered (same stream). */
 size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles);
 int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out,
-                     int K, int n_tiles, int a_koff, float scale, void* out, int ldo, int out_cols,
-                     void* ws, size_t ws_bytes, hipStream_t stream);
+                     int K, int n_tiles, int a_koff, int module_tiles, float scale, void* out, int ldo,
+                     int out_cols, void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* ------------------------------------------------------------ optimizer ---
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip

@@ -45,7 +45,7 @@ SIGNATURES = {
     "ospo_simpo_fwd": [P, I, F, F, F, I, P, P, P, P],
     "ospo_simpo_bwd": [P, I, F, F, F, I, P, P, P],
     "ospo_lora_pack": [P, P, I, I, I, I, I, P, P, P, P, I, L, P],
-    "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, F, P, I, I, P, Z, P],
+    "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, P],
     "ospo_lora_skinny_ws_bytes": [I, I, I],
     "ospo_sumsq": [P, L, P, P],
     "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],

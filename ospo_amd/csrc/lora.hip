@@ -187,23 +187,12 @@ extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
   return (size_t)(sp > 1 ? sp : 0) * rb * n_tiles * 64 * sizeof(f32x4) + 16;
 }
 
-extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out, int K,
-                                int n_tiles, int a_koff, float scale, void* out, int ldo, int out_cols, void* ws,
-                                size_t ws_bytes, hipStream_t stream) {
-  if (!A || !Bt || !out || !ws) return OSPO_ERR_ARG;
-  if (M <= 0 || M_out < M || K <= 0 || n_tiles < 1 || n_tiles > 4 || b_rows <= 0 || a_koff < 0) return OSPO_ERR_SHAPE;
-  if (K % 32 || lda % 8 || ldb % 8 || a_koff % 8 || ldo % 4 || out_cols < 16 * n_tiles || ldo < out_cols)
-    return OSPO_ERR_SHAPE;
-  if (ldb < K || (a_koff == 0 && lda < K) || (a_koff > 0 && lda < (n_tiles - 1) * a_koff + K)) return OSPO_ERR_SHAPE;
-  if (ws_bytes < ospo_lora_skinny_ws_bytes(M_out, K, n_tiles)) return OSPO_ERR_SHAPE;
-  if (!aligned16(A) || !aligned16(Bt) || !aligned16(ws) || ((uintptr_t)out & 7)) return OSPO_ERR_ALIGN;
+static int launch_skinny(const bf16* a, int lda, const bf16* b, int ldb, int b_rows, int M, int M_out, int K,
+                         int n_tiles, int a_koff, float scale, bf16* o, int ldo, int out_cols, f32x4* part,
+                         hipStream_t stream) {
   const int rbn = (M_out + 15) / 16;
   const int sp = skinny_splits(M_out, K);
-  f32x4* part = (f32x4*)ws;
   const dim3 grid(rbn, sp), block(64 * SK_WAVES);
-  const bf16* a = (const bf16*)A;
-  const bf16* b = (const bf16*)Bt;
-  bf16* o = (bf16*)out;
   switch (n_tiles) {
     case 1: hipLaunchKernelGGL(skinny_kernel<1>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
     case 2: hipLaunchKernelGGL(skinny_kernel<2>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
@@ -219,6 +208,49 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
       default: hipLaunchKernelGGL(skinny_reduce_kernel<4>, dim3(rbn), dim3(256), 0, stream, part, sp, rbn, M, M_out, scale, o, ldo, out_cols); break;
     }
     OSPO_CHECK_LAUNCH();
+  }
+  return OSPO_OK;
+}
+
+extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out, int K,
+                                int n_tiles, int a_koff, int module_tiles, float scale, void* out, int ldo,
+                                int out_cols, void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (!A || !Bt || !out || !ws) return OSPO_ERR_ARG;
+  if (M <= 0 || M_out < M || K <= 0 || n_tiles < 1 || n_tiles > 16 || b_rows <= 0 || a_koff < 0 || module_tiles < 1)
+    return OSPO_ERR_SHAPE;
+  if (K % 32 || lda % 8 || ldb % 8 || a_koff % 8 || ldo % 4 || out_cols < 16 * n_tiles || ldo < out_cols)
+    return OSPO_ERR_SHAPE;
+  if (a_koff > 0 && n_tiles % module_tiles) return OSPO_ERR_SHAPE;
+  const int nmods = a_koff > 0 ? n_tiles / module_tiles : 1;
+  if (ldb < K || (a_koff == 0 && lda < K) || (a_koff > 0 && lda < (nmods - 1) * a_koff + K)) return OSPO_ERR_SHAPE;
+  if (ws_bytes < ospo_lora_skinny_ws_bytes(M_out, K, n_tiles)) return OSPO_ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(Bt) || !aligned16(ws) || ((uintptr_t)out & 7)) return OSPO_ERR_ALIGN;
+  const bf16* a = (const bf16*)A;
+  const bf16* b = (const bf16*)Bt;
+  bf16* o = (bf16*)out;
+  f32x4* part = (f32x4*)ws;
+  if (a_koff > 0 && module_tiles == 1 && n_tiles <= 4)  // one launch: n-tile j reduces over block j of A
+    return launch_skinny(a, lda, b, ldb, b_rows, M, M_out, K, n_tiles, a_koff, scale, o, ldo, out_cols, part, stream);
+  // general form: per module (block-diagonal) or the whole matrix (dense), in chunks of <= 4 n-tiles;
+  // each chunk zero-pads only its own columns, the last one also the tail up to out_cols
+  for (int mi = 0; mi < nmods; ++mi) {
+    const int t0 = a_koff > 0 ? mi * module_tiles : 0, tn = a_koff > 0 ? module_tiles : n_tiles;
+    for (int c0 = 0; c0 < tn; c0 += 4) {
+      const int nt = tn - c0 < 4 ? tn - c0 : 4;
+      const int j0 = t0 + c0;
+      const bool last = (mi == nmods - 1) && (c0 + nt == tn);
+      const int oc = last ? out_cols - 16 * j0 : 16 * nt;
+      const int rc = b_rows - 16 * j0;
+      if (rc <= 0) {  // nothing left of B: zero the remaining columns via a chunk with all-zero rows
+        const int rs = launch_skinny(a + (a_koff > 0 ? (long)mi * a_koff : 0), lda, b, ldb, 1, M, M_out, K, 1, 0,
+                                     0.f, o + 16 * j0, ldo, oc, part, stream);
+        if (rs) return rs;
+        break;
+      }
+      const int rs = launch_skinny(a + (a_koff > 0 ? (long)mi * a_koff : 0), lda, b + (long)16 * j0 * ldb, ldb, rc, M,
+                                   M_out, K, nt, 0, scale, o + 16 * j0, ldo, oc, part, stream);
+      if (rs) return rs;
+    }
   }
   return OSPO_OK;
 }

@@ -228,7 +228,7 @@ class SimPOEngine:
         need = ops.lora_skinny_ws_bytes(self.Mk, K, n_tiles)
         ws = getattr(self, "_sk_ws", None)
         if ws is None or ws.numel() * 4 < need:
-            ws = self._sk_ws = ops.lora_skinny_ws(self.Mk, K, max(n_tiles, 4), self.device)
+            ws = self._sk_ws = ops.lora_skinny_ws(self.Mk, K, max(n_tiles, 8), self.device)
         return ws
 
     def _lora_down(self, x, Acat, out_bf16, M, nmods):
@@ -246,10 +246,11 @@ class SimPOEngine:
             nt = (r + 15) // 16
             ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, nt, 0, self.scale, b_rows=r,
                             ws=self._skinny_ws(g.Nmod, nt))
-        elif r == 16:
-            ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, g.nmods, g.Nmod, self.scale,
-                            ws=self._skinny_ws(g.Nmod, g.nmods))
-        else:  # block-diagonal with r != 16: split-K fp32 path
+        elif r % 16 == 0:  # block-diagonal: n-tile j reduces over module j // (r/16) of dy
+            nt = g.nmods * r // 16
+            ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, nt, g.Nmod, self.scale,
+                            ws=self._skinny_ws(g.Nmod, nt), module_tiles=r // 16)
+        else:  # block-diagonal with r % 16 != 0: split-K fp32 path
             K = Bcat.shape[0]
             u32 = self._u32(g.Rp)
             u32.zero_()

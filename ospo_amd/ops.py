@@ -295,13 +295,13 @@ def lora_skinny_ws(M_out, K, n_tiles=4, device="cuda") -> torch.Tensor:
     return torch.zeros((n + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
-def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=None, ws=None):
+def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=None, ws=None, module_tiles=1):
     """out[:M_out, :] (bf16) = scale * a . bt^T per 16-column n-tile (see ospo_lora_skinny)."""
     if ws is None:
         ws = lora_skinny_ws(M_out, K, n_tiles, a.device)
     call("ospo_lora_skinny", _p(a), _ld(a), _p(bt), _ld(bt), bt.shape[0] if b_rows is None else b_rows, M, M_out,
-         K, n_tiles, a_koff, float(scale), _p(out), _ld(out), out.shape[1], _p(ws), ws.numel() * ws.element_size(),
-         _s())
+         K, n_tiles, a_koff, module_tiles, float(scale), _p(out), _ld(out), out.shape[1], _p(ws),
+         ws.numel() * ws.element_size(), _s())
 
 
 # -------------------------------------------------------------- optimizer

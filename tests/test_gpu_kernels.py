@@ -404,10 +404,12 @@ def test_lora_pack():
     assert torch.equal(Ac2[1, : nm * r], A2) and torch.equal(BT2[1], torch.cat([B2[i].T for i in range(nm)], 0))
 
 
-@pytest.mark.parametrize("M,K,used", [(4800, 4096, 48), (300, 11008, 16), (77, 512, 32), (1, 256, 64)])
+@pytest.mark.parametrize("M,K,used", [(4800, 4096, 48), (300, 11008, 16), (77, 512, 32), (1, 256, 64),
+                                      (600, 4096, 96)])
 def test_lora_skinny_down(M, K, used):
-    """u = s x A_cat^T: dense mode, partial n-tiles, rows M..M_out-1 and pad columns zeroed."""
-    Rp = 64
+    """u = s x A_cat^T: dense mode, partial n-tiles, rows M..M_out-1 and pad columns zeroed
+    (96 used of Rp = 128: LoRA r = 32 on q|k|v, 6 n-tiles in two chunks)."""
+    Rp = 64 if used <= 64 else 128
     x = rnd(M + 5, K)
     Acat = torch.zeros(Rp, K, device=DEV, dtype=torch.bfloat16)
     Acat[:used] = rnd(used, K)
@@ -423,15 +425,17 @@ def test_lora_skinny_down(M, K, used):
         assert torch.all(out[M_out:] == 7.0)
 
 
-@pytest.mark.parametrize("M,nm,Nmod", [(4800, 3, 4096), (640, 2, 11008), (100, 1, 4096)])
-def test_lora_skinny_up_blockdiag(M, nm, Nmod):
-    """g = s dy B over the block-diagonal B_cat, via per-module B^T (r = 16)."""
-    r, Rp = 16, 64
+@pytest.mark.parametrize("M,nm,Nmod,r", [(4800, 3, 4096, 16), (640, 2, 11008, 16), (100, 1, 4096, 16),
+                                         (300, 3, 1024, 32), (200, 2, 2048, 32)])
+def test_lora_skinny_up_blockdiag(M, nm, Nmod, r):
+    """g = s dy B over the block-diagonal B_cat, via per-module B^T (r / 16 n-tiles per module)."""
+    Rp = (nm * r + 63) // 64 * 64
     dy = rnd(M, nm * Nmod)
     Bf = rnd(nm, Nmod, r)
     BT = torch.cat([Bf[i].T for i in range(nm)], 0).contiguous()
     out = torch.empty(M, Rp, device=DEV, dtype=torch.bfloat16)
-    ops().lora_skinny(dy, BT, out, M, M, Nmod, nm, Nmod if nm > 1 else 0, 2.0)
+    nt = nm * r // 16
+    ops().lora_skinny(dy, BT, out, M, M, Nmod, nt, Nmod if nm > 1 else 0, 2.0, module_tiles=r // 16)
     ref = torch.cat([dy[:, i * Nmod:(i + 1) * Nmod].float() @ Bf[i].float() for i in range(nm)], 1) * 2.0
     assert relerr(out[:, : nm * r].float(), ref) < 8e-3
     assert torch.all(out[:, nm * r:] == 0)

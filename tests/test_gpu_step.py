@@ -160,3 +160,25 @@ def test_engine_optimizer_step_matches_torch_adamw():
     mism = sum(int((new[k] != params[k]).sum()) for k in params)
     total = sum(p.numel() for p in params.values())
     assert mism / total < 0.01, (mism, total)
+
+
+@pytest.mark.parametrize("r", [32, 8])
+def test_step_lora_rank_variants_vs_oracle(r):
+    """configs/peft/lora.yaml trains at r = 32 (alpha 64): u with 6 n-tiles over Rp = 128,
+    g block-diagonal with 2 n-tiles per module.  r = 8 exercises the non-multiple-of-16
+    fallback.  Small dims, bf16, against the oracle."""
+    dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=2048,
+                       gen_head_dim=256, lora_r=r, lora_alpha=2 * r)
+    w = O.init_weights(dims, seed=11, dtype=torch.bfloat16, lora_b_std=1e-2)
+    g = torch.Generator().manual_seed(12)
+    B, N = 3, 64
+    text = [torch.randint(0, dims.vocab, (1, 10 - 2 * i), generator=g, dtype=torch.int32) for i in range(B)]
+    chosen = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    rejected = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    algo = {"beta": 10.0, "gamma_beta_ratio": 0.5, "label_smoothing": 0.0, "loss_type": "sigmoid"}
+    eng = build_engine(dims, w, B, 10, N)
+    logps, loss, grads = run_hip_step(eng, text, chosen, rejected, algo)
+    ora = O.simpo_step(text, chosen, rejected, w, dims, dtype=torch.bfloat16)
+    assert max(rel(logps[:B], ora.chosen_logps), rel(logps[B:], ora.rejected_logps)) < 1e-3
+    assert abs(loss - float(ora.loss)) / float(ora.loss) < 2e-3
+    assert max(rel(grads[k], ora.lora_grads[k]) for k in ora.lora_grads) < 5e-2
