@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--img-tokens", type=int, default=576)
     ap.add_argument("--layers", type=int, default=30)
     ap.add_argument("--lora-r", type=int, default=16)
+    # dropout 0 for parity runs, configs/peft/lora.yaml's 0.05 for throughput
+    ap.add_argument("--lora-dropout", type=float, default=0.05)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
     args = ap.parse_args()
@@ -104,7 +106,8 @@ def main():
                                      "lora_alpha": 2 * args.lora_r})
     B, Lt, N = args.pairs_per_gpu, args.text_len, args.img_tokens
     weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)  # identical on every rank (same seeds)
-    eng = SimPOEngine(dims, weights, device=dev, max_pairs=B, max_text_len=Lt, n_img_tokens=N)
+    eng = SimPOEngine(dims, weights, device=dev, max_pairs=B, max_text_len=Lt, n_img_tokens=N,
+                      lora_dropout=args.lora_dropout, dropout_seed=42)
     del weights
     torch.cuda.empty_cache()
     cfg = SimPOConfig()
@@ -165,7 +168,9 @@ def main():
         "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (random-init Janus-Pro-7B-shaped weights, random prompt/VQ token ids)",
         "config": {"workload": f"Janus-Pro-{'7B' if dims.n_layers == 30 else str(dims.n_layers) + 'L'} SimPO "
-                               f"train step, LoRA r={dims.lora_r}, {N} image tokens, {B} pairs/GPU",
+                               f"train step, LoRA r={dims.lora_r} dropout {args.lora_dropout}, {N} image tokens, "
+                               f"{B} pairs/GPU",
+                   "lora_dropout": args.lora_dropout,
                    "global_batch": global_batch, "seq_len": T, "parallelism": f"dp{world}",
                    "algorithmic_tflop_per_pair": round(flops_pair / 1e12, 3)},
         "roofline": roof,

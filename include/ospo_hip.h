@@ -64,6 +64,19 @@ int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M
                            const void* rope_cos, const void* rope_sin, int T, int rope_cols,
                            hipStream_t stream);
 
+/* LoRA-dropout backward of a frozen Linear with its adapter (peft lora.Linear,
+ * dropout before lora_A): C = A.B^T + mask (.) (A2.B2^T) / (1 - drop_p), with
+ * the forward's mask over the [M, N] input of the adapter (element (m, n) kept
+ * iff drop_hash(m*N + n, drop_seed) >= drop_p * 2^32, common.h), i.e.
+ * dX = dy.W + dropout'(g . A_cat).  N % 256 == 0, K2 > 0, no bias / residual. */
+int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
+                              const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
+                              unsigned drop_seed, float drop_p, hipStream_t stream);
+
+/* The LoRA dropout mask hash (host copy of the device function): element idx of an
+ * adapter input is kept iff ospo_dropout_hash(idx, seed) >= p * 2^32. */
+unsigned ospo_dropout_hash(unsigned idx, unsigned seed);
+
 /* Split-K workspace for the GEMM's tail round (tiles % CUs leftover tiles are split
  * along K into fp32 partial tiles, then summed + epilogued by a fixup launch).
  * bytes >= 256 KiB x CU count uses the split everywhere it pays; NULL disables it.
@@ -214,11 +227,16 @@ int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int
  *                     K = a_koff = Nmod, module_tiles = r / 16
  * K is split across workgroups; ws (>= ospo_lora_skinny_ws_bytes(M_out, K,
  * n_tiles) bytes, 16-B aligned) holds the fp32 partials that a second launch
- * sums.  Calls sharing a ws must be ordered (same stream). */
+ * sums.  Calls sharing a ws must be ordered (same stream).
+ * drop_p > 0 (dense mode only): peft lora_dropout on A -- element (m, k) is kept
+ * iff drop_hash(m*K + k, drop_seed) >= drop_p * 2^32 (common.h) and becomes
+ * bf16(A / (1 - drop_p)); the masked A is also written to xd [M, ld_xd] when xd
+ * is non-NULL (the dA = g^T . dropout(x) operand of the backward). */
 size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles);
 int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out,
                      int K, int n_tiles, int a_koff, int module_tiles, float scale, void* out, int ldo,
-                     int out_cols, void* ws, size_t ws_bytes, hipStream_t stream);
+                     int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed, float drop_p,
+                     void* xd, int ld_xd, hipStream_t stream);
 
 /* ------------------------------------------------------------ optimizer ---
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip

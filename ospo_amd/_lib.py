@@ -9,18 +9,20 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import c_float, c_int, c_long, c_size_t, c_void_p
+from ctypes import c_float, c_int, c_long, c_size_t, c_uint, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OSPO_HIP_LIB", os.path.join(_HERE, "libospo_hip.so"))
 
-P, I, L, F, Z = c_void_p, c_int, c_long, c_float, c_size_t
+P, I, L, F, Z, U = c_void_p, c_int, c_long, c_float, c_size_t, c_uint
 
 # name -> argtypes (restype is c_int = ospo_status unless listed in RESTYPES)
 SIGNATURES = {
     "ospo_abi_version": [],
+    "ospo_dropout_hash": [U, U],
     "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P],
     "ospo_gemm_nt_tile": [I, I],
+    "ospo_gemm_nt_dropout_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, U, F, P],
     "ospo_gemm_nt_rope_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, P, I, I, P],
     "ospo_set_gemm_variant": [I],
     "ospo_gemm_set_workspace": [P, Z],
@@ -45,13 +47,13 @@ SIGNATURES = {
     "ospo_simpo_fwd": [P, I, F, F, F, I, P, P, P, P],
     "ospo_simpo_bwd": [P, I, F, F, F, I, P, P, P],
     "ospo_lora_pack": [P, P, I, I, I, I, I, P, P, P, P, I, L, P],
-    "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, P],
+    "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, U, F, P, I, P],
     "ospo_lora_skinny_ws_bytes": [I, I, I],
     "ospo_sumsq": [P, L, P, P],
     "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],
 }
 
-RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t}
+RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 

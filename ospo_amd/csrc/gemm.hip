@@ -102,6 +102,10 @@ struct GemmArgs {
   const bf16* rope_cs = nullptr;
   const bf16* rope_sn = nullptr;
   int rope_T = 0, rope_cols = 0;
+  // LoRA dropout backward: C = A.B^T + mask (.) (A2.B2^T) / (1 - p), mask over [M, drop_ld]
+  uint32_t drop_seed = 0, drop_thresh = 0;
+  float drop_scale = 0.f;  // > 0: on
+  int drop_ld = 0;
 };
 
 // DBG (A/B decomposition only, results invalid): 1 = no global loads after the
@@ -672,7 +676,7 @@ __device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0
 // Data-parallel + split-K tail: workgroups [0, dp) own whole tiles (XCD-remapped);
 // workgroups dp + u (u < tail * split) own K-range u % split of tail tile dp + u / split
 // and write an fp32 partial tile to ws (summed + epilogued by splitk_fixup_kernel).
-template <int DBG = 0>
+template <int DBG = 0, bool DROP = false>
 __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
                                                          int split, float* __restrict__ ws, int GM) {
   constexpr int BM = 256, BN = 256, HALF = 16384, SLOT = 4 * HALF;  // half order in a slot: A0 A1 B0 B1
@@ -687,7 +691,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   const int wm = wave >> 2, wn = wave & 3;
 
   int m0, n0, tb, tcount, part = -1;
-  const int nt1 = args.K / BK, ntot = nt1 + args.K2 / BK;
+  const int nt1 = args.K / BK, nt2 = args.K2 / BK, ntot = nt1 + nt2;
   {
     const int wg = blockIdx.x;
     if (wg < dp) {
@@ -712,7 +716,9 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   auto stage_half = [&](int tl, int h) {  // tl: local K-tile index
     if (DBG == 1 && tl >= 2) return;
     char* dst = smem + (tl & 1) * SLOT + h * HALF;
-    const int t = tb + tl;
+    const int q = tb + tl;
+    // with dropout the LoRA extension tiles run FIRST so their (masked) sum can be scaled alone
+    const int t = DROP ? (q < nt2 ? nt1 + q : q - nt2) : q;
     const bool ext = t >= nt1;
     const bool isA = h < 2;
     const bf16* base = isA ? (ext ? args.A2 : args.A) : (ext ? args.B2 : args.B);
@@ -819,6 +825,28 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+    }
+    if constexpr (DROP) {
+      if (tb == 0 && t == nt2 - 1) {  // accumulators hold exactly A2.B2^T: apply the dropout mask
+        const int gq = lane >> 4, lq = lane & 15;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ia = (j >= 2) ? 1 : 0;
+          const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+              const uint32_t m = (uint32_t)(m0 + ia * 128 + wm * 64 + i * 16 + lq);
+              const uint32_t c = (uint32_t)(n0 + ib * 128 + wn * 32 + n * 16 + 4 * gq);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const bool keep = drop_hash(m * (uint32_t)args.drop_ld + c + e, args.drop_seed) >= args.drop_thresh;
+                acc[j][i][n][e] *= keep ? args.drop_scale : 0.f;
+              }
+            }
+        }
+      }
     }
   }
   if (!g1) {  // re-align the barrier count
@@ -963,7 +991,7 @@ int num_cus() {
   return g_num_cus;
 }
 
-template <int DBG = 0>
+template <int DBG = 0, bool DROP = false>
 int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
   const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
@@ -982,7 +1010,8 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
     }
   }
   const int grid = dp + tail * split;
-  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split, g_splitk_ws, g_v5_gm);
+  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split, g_splitk_ws,
+                     g_v5_gm);
   OSPO_CHECK_LAUNCH();
   if (tail) {
     hipLaunchKernelGGL(splitk_fixup_kernel, dim3(tail * 32), dim3(256), 0, s, a, tm, tn, dp, split,
@@ -1066,6 +1095,27 @@ extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int
   a.rope_T = T;
   a.rope_cols = rope_cols;
   return launch_v5<0>(a, stream, false);
+}
+
+extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
+                                         const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
+                                         unsigned drop_seed, float drop_p, hipStream_t stream) {
+  if (!A || !B || !C || !A2 || !B2) return OSPO_ERR_ARG;
+  if (drop_p < 0.f || drop_p >= 1.f) return OSPO_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK || K2 <= 0 || K2 % BK) return OSPO_ERR_SHAPE;
+  if (N % 256) return OSPO_ERR_UNSUPPORTED;
+  if ((long)M * N > 0xFFFFFFFFL) return OSPO_ERR_SHAPE;  // 32-bit mask index
+  if (lda < K || ldb < K || ldc < N || (lda % 8) || (ldb % 8) || (ldc % 8)) return OSPO_ERR_SHAPE;
+  if (lda2 < K2 || ldb2 < K2 || lda2 % 8 || ldb2 % 8) return OSPO_ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(B) || !aligned16(C) || !aligned16(A2) || !aligned16(B2)) return OSPO_ERR_ALIGN;
+  GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
+             M, N, K, K2, 1.f, nullptr, nullptr, 0, C, ldc, 1, 0, 0};
+  if (drop_p == 0.f) return launch_v5<0>(a, stream);
+  a.drop_seed = drop_seed;
+  a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
+  a.drop_scale = 1.f / (1.f - drop_p);
+  a.drop_ld = N;
+  return launch_v5<0, true>(a, stream);
 }
 
 extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {

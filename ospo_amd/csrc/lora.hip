@@ -22,12 +22,22 @@ namespace {
 constexpr int SK_WAVES = 4;
 constexpr int SK_U = 4;  // k-steps per register batch; two batches in flight per wave
 
+// LoRA dropout on the A operand (the adapter input x), dense mode only: the lane's
+// 8 elements of step s sit at columns k0 + 32 s .. +7 of row `row`; the masked
+// fragment is also stored to xd (the backward's dA operand) when `xd` is set.
+struct SkDrop {
+  uint32_t seed, thresh, rowidx;  // rowidx = row * ncols
+  float scale;
+  int k0;                         // absolute column of the lane at step 0
+  bf16* xd;                       // xd + row * ld (nullptr: do not store)
+};
+
 // One wave's share of the reduction: steps s = wave + i*SK_WAVES, i < n_i.
 // Register double-buffered batches keep 2*SK_U*(1+NTL) 1-KiB loads in flight
 // (addresses clamped, tail steps zeroed in A), no branches in the loop.
-template <int NTL>
+template <int NTL, bool DROP = false>
 __device__ __forceinline__ void sk_loop(const bf16* arow, const bf16* const (&bp)[NTL], const bool (&bok)[NTL],
-                                        int wave, int n_i, f32x4 (&acc)[NTL]) {
+                                        int wave, int n_i, f32x4 (&acc)[NTL], const SkDrop& dp = SkDrop{}) {
   if (n_i <= 0) return;
   bf16x8 a0[SK_U], b0[SK_U][NTL], a1[SK_U], b1[SK_U][NTL];
   auto load = [&](int batch, bf16x8 (&a)[SK_U], bf16x8 (&b)[SK_U][NTL]) {
@@ -44,7 +54,16 @@ __device__ __forceinline__ void sk_loop(const bf16* arow, const bf16* const (&bp
   auto consume = [&](int batch, const bf16x8 (&a)[SK_U], const bf16x8 (&b)[SK_U][NTL]) {
 #pragma unroll
     for (int u = 0; u < SK_U; ++u) {
-      const bf16x8 av = (batch * SK_U + u < n_i) ? a[u] : bf16x8{};
+      bf16x8 av = (batch * SK_U + u < n_i) ? a[u] : bf16x8{};
+      if constexpr (DROP) {
+        const int k = dp.k0 + 32 * (wave + (batch * SK_U + u) * SK_WAVES);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool keep = drop_hash(dp.rowidx + (uint32_t)(k + e), dp.seed) >= dp.thresh;
+          av[e] = keep ? f2bf(bf2f(av[e]) * dp.scale) : f2bf(0.f);
+        }
+        if (dp.xd && batch * SK_U + u < n_i) *reinterpret_cast<bf16x8*>(dp.xd + k) = av;
+      }
 #pragma unroll
       for (int j = 0; j < NTL; ++j)
         acc[j] = MFMA(bok[j] ? b[u][j] : bf16x8{}, av, acc[j]);  // D[n][m]: lane m = l16, n = 4g..4g+3
@@ -66,12 +85,14 @@ __device__ __forceinline__ void sk_loop(const bf16* arow, const bf16* const (&bp
 // splits > 1 the fp32 partial tile goes to ws and skinny_reduce_kernel sums the
 // splits (a cross-workgroup handoff inside one launch would need an agent-scope
 // release, i.e. an L2 writeback per workgroup on gfx950 -- far dearer).
-template <int NT>
+template <int NT, bool DROP>
 __global__ __launch_bounds__(64 * SK_WAVES) void skinny_kernel(const bf16* __restrict__ A, int lda,
                                                                const bf16* __restrict__ Bt, int ldb, int b_rows,
                                                                int M, int M_out, int K, int a_koff, float scale,
                                                                bf16* __restrict__ out, int ldo, int out_cols,
-                                                               f32x4* __restrict__ ws) {
+                                                               f32x4* __restrict__ ws, uint32_t dseed,
+                                                               uint32_t dthresh, float dscale, bf16* __restrict__ xd,
+                                                               int ldxd) {
   __shared__ f32x4 red[SK_WAVES][NT][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -98,7 +119,18 @@ __global__ __launch_bounds__(64 * SK_WAVES) void skinny_kernel(const bf16* __res
       bok[j] = br < b_rows;
       bp[j] = Bt + (long)(bok[j] ? br : 0) * ldb + 8 * g + 32 * s_begin;
     }
-    sk_loop<NT>(arow, bp, bok, wave, n_i, acc);
+    if constexpr (DROP) {
+      SkDrop dp;
+      dp.seed = dseed;
+      dp.thresh = dthresh;
+      dp.scale = dscale;
+      dp.rowidx = (uint32_t)row * (uint32_t)K;
+      dp.k0 = 32 * s_begin + 8 * g;
+      dp.xd = (xd && m0 + l16 < M) ? xd + (long)row * ldxd : nullptr;
+      sk_loop<NT, true>(arow, bp, bok, wave, n_i, acc, dp);
+    } else {
+      sk_loop<NT>(arow, bp, bok, wave, n_i, acc);
+    }
   } else {  // block-diagonal: n-tile j reduces over its own K block of A
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -187,17 +219,29 @@ extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
   return (size_t)(sp > 1 ? sp : 0) * rb * n_tiles * 64 * sizeof(f32x4) + 16;
 }
 
+struct SkDropArgs {
+  uint32_t seed = 0, thresh = 0;
+  float scale = 0.f;  // > 0: dropout on
+  bf16* xd = nullptr;
+  int ldxd = 0;
+};
+
+#define SK_LAUNCH(NTV, DV)                                                                                        \
+  hipLaunchKernelGGL((skinny_kernel<NTV, DV>), grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, \
+                     scale, o, ldo, out_cols, part, dr.seed, dr.thresh, dr.scale, dr.xd, dr.ldxd)
+
 static int launch_skinny(const bf16* a, int lda, const bf16* b, int ldb, int b_rows, int M, int M_out, int K,
                          int n_tiles, int a_koff, float scale, bf16* o, int ldo, int out_cols, f32x4* part,
-                         hipStream_t stream) {
+                         hipStream_t stream, const SkDropArgs& dr = SkDropArgs{}) {
   const int rbn = (M_out + 15) / 16;
   const int sp = skinny_splits(M_out, K);
   const dim3 grid(rbn, sp), block(64 * SK_WAVES);
+  const bool drop = dr.scale > 0.f;
   switch (n_tiles) {
-    case 1: hipLaunchKernelGGL(skinny_kernel<1>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
-    case 2: hipLaunchKernelGGL(skinny_kernel<2>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
-    case 3: hipLaunchKernelGGL(skinny_kernel<3>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
-    default: hipLaunchKernelGGL(skinny_kernel<4>, grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, scale, o, ldo, out_cols, part); break;
+    case 1: if (drop) SK_LAUNCH(1, true); else SK_LAUNCH(1, false); break;
+    case 2: if (drop) SK_LAUNCH(2, true); else SK_LAUNCH(2, false); break;
+    case 3: if (drop) SK_LAUNCH(3, true); else SK_LAUNCH(3, false); break;
+    default: if (drop) SK_LAUNCH(4, true); else SK_LAUNCH(4, false); break;
   }
   OSPO_CHECK_LAUNCH();
   if (sp > 1) {
@@ -214,8 +258,21 @@ static int launch_skinny(const bf16* a, int lda, const bf16* b, int ldb, int b_r
 
 extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out, int K,
                                 int n_tiles, int a_koff, int module_tiles, float scale, void* out, int ldo,
-                                int out_cols, void* ws, size_t ws_bytes, hipStream_t stream) {
+                                int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed, float drop_p, void* xd,
+                                int ld_xd, hipStream_t stream) {
   if (!A || !Bt || !out || !ws) return OSPO_ERR_ARG;
+  if (drop_p < 0.f || drop_p >= 1.f) return OSPO_ERR_ARG;
+  SkDropArgs dr;
+  if (drop_p > 0.f) {
+    if (a_koff != 0) return OSPO_ERR_UNSUPPORTED;  // dropout acts on the adapter input (dense u product)
+    if ((long)M * K > 0xFFFFFFFFL) return OSPO_ERR_SHAPE;  // 32-bit mask index
+    if (xd && (ld_xd < K || ld_xd % 8 || !aligned16(xd))) return OSPO_ERR_SHAPE;
+    dr.seed = drop_seed;
+    dr.thresh = (uint32_t)((double)drop_p * 4294967296.0);
+    dr.scale = 1.f / (1.f - drop_p);
+    dr.xd = (bf16*)xd;
+    dr.ldxd = ld_xd;
+  }
   if (M <= 0 || M_out < M || K <= 0 || n_tiles < 1 || n_tiles > 16 || b_rows <= 0 || a_koff < 0 || module_tiles < 1)
     return OSPO_ERR_SHAPE;
   if (K % 32 || lda % 8 || ldb % 8 || a_koff % 8 || ldo % 4 || out_cols < 16 * n_tiles || ldo < out_cols)
@@ -230,7 +287,8 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
   bf16* o = (bf16*)out;
   f32x4* part = (f32x4*)ws;
   if (a_koff > 0 && module_tiles == 1 && n_tiles <= 4)  // one launch: n-tile j reduces over block j of A
-    return launch_skinny(a, lda, b, ldb, b_rows, M, M_out, K, n_tiles, a_koff, scale, o, ldo, out_cols, part, stream);
+    return launch_skinny(a, lda, b, ldb, b_rows, M, M_out, K, n_tiles, a_koff, scale, o, ldo, out_cols, part, stream,
+                         dr);
   // general form: per module (block-diagonal) or the whole matrix (dense), in chunks of <= 4 n-tiles;
   // each chunk zero-pads only its own columns, the last one also the tail up to out_cols
   for (int mi = 0; mi < nmods; ++mi) {
@@ -248,7 +306,7 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
         break;
       }
       const int rs = launch_skinny(a + (a_koff > 0 ? (long)mi * a_koff : 0), lda, b + (long)16 * j0 * ldb, ldb, rc, M,
-                                   M_out, K, nt, 0, scale, o + 16 * j0, ldo, oc, part, stream);
+                                   M_out, K, nt, 0, scale, o + 16 * j0, ldo, oc, part, stream, dr);
       if (rs) return rs;
     }
   }

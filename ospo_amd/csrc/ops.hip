@@ -610,6 +610,9 @@ extern "C" const char* ospo_strerror(int s) {
 }
 extern "C" int ospo_abi_version(void) { return 1; }
 
+// host restatement of the device dropout hash (tests pin ospo_amd/dropout.py against it)
+extern "C" unsigned ospo_dropout_hash(unsigned idx, unsigned seed) { return drop_hash(idx, seed); }
+
 extern "C" int ospo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int M, int D, float eps,
                                 hipStream_t st) {
   if (!x || !w || !y || !rstd) return OSPO_ERR_ARG;

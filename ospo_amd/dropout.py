@@ -1,0 +1,48 @@
+"""LoRA dropout masks of the HIP path (peft lora.Linear: y = W x + s B A dropout(x),
+ospo/utils/model.py:50-57 with configs/peft/lora.yaml lora_dropout).
+
+The mask is counter based, so the forward (skinny u kernel) and the backward (dX
+GEMM epilogue, dA on the stored masked input) regenerate the same bits without
+storing them: element (m, k) of a [M, K] adapter input is kept iff
+drop_hash(m * K + k, seed) >= p * 2^32, kept values become bf16(x / (1 - p)).
+``drop_hash`` restates ``ospo_amd/csrc/common.h`` bit for bit (numpy uint32).
+
+One mask per adapter INPUT per layer and step: q/k/v share the mask of the
+attention-norm output and gate/up that of the MLP-norm output (their LoRA A's are
+fused into one product).  peft draws an independent mask per module; the
+per-module marginal distribution and the expectation are the same.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+GROUP_IDS = {"qkv": 0, "o": 1, "gu": 2, "down": 3}
+_M32 = np.uint32(0xFFFFFFFF)
+
+
+def drop_hash(idx, seed):
+    """uint32 hash of element index idx (array) under seed (int), as on the device."""
+    with np.errstate(over="ignore"):
+        x = np.asarray(idx, dtype=np.uint32) * np.uint32(0x9E3779B1) + np.uint32(seed & 0xFFFFFFFF)
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x7FEB352D)
+        x ^= x >> np.uint32(15)
+        x *= np.uint32(0x846CA68B)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def threshold(p: float) -> int:
+    return int(float(p) * 4294967296.0)
+
+
+def layer_seed(base: int, call: int, layer: int, group: str) -> int:
+    """Seed of one adapter input's mask: distinct per (base seed, forward call, layer, group)."""
+    h = drop_hash(np.uint32((call * 131 + layer * 8 + GROUP_IDS[group]) & 0xFFFFFFFF), base & 0xFFFFFFFF)
+    return int(drop_hash(h, 0x5BD1E995))
+
+
+def keep_mask(M: int, K: int, seed: int, p: float) -> np.ndarray:
+    """bool [M, K] keep mask of an adapter input (test / oracle use)."""
+    idx = np.arange(M * K, dtype=np.uint64).astype(np.uint32).reshape(M, K)
+    return drop_hash(idx, seed) >= np.uint32(threshold(p))

@@ -29,7 +29,7 @@ from typing import Dict, Optional
 
 import torch
 
-from . import ops
+from . import dropout, ops
 from .lora import LoraLayout, roundup
 
 BF16 = torch.bfloat16
@@ -75,11 +75,15 @@ class SimPOEngine:
     """Device-resident Janus-Pro SimPO policy (one per GPU / rank)."""
 
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_pairs: int = 4,
-                 max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0):
-        if lora_dropout and lora_dropout > 0:
-            raise NotImplementedError(
-                "lora_dropout > 0 is not on the built path yet (peft lora.Linear dropout on the adapter input); "
-                "set lora.lora_dropout=0.0 (the parity configuration) or lora.ignore_dropout=true")
+                 max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
+                 dropout_seed: int = 42):
+        if not 0.0 <= float(lora_dropout) < 1.0:
+            raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
+        # peft lora_dropout on the adapter inputs (ospo_amd/dropout.py: counter-based masks, one per input)
+        self.lora_dropout = float(lora_dropout)
+        self.training = True
+        self._drop_base = int(dropout_seed)
+        self._drop_call = 0
         if dims.head_dim != 128:
             raise ValueError("head_dim must be 128 (Janus-Pro)")
         if dims.d_model % 256 or dims.d_ff % 256 or dims.gen_head_dim % 256 or dims.img_vocab % 256:
@@ -164,6 +168,8 @@ class SimPOEngine:
                 "u_gu": z(Mc, self.layout.groups["gu"].Rp), "gu": z(Mc, 2 * Fd), "h": z(Mc, Fd),
                 "u_d": z(Mc, self.layout.groups["down"].Rp),
             })
+            if self.lora_dropout > 0:  # dropout(x) of each adapter input, the backward's dA operand
+                self.acts[-1].update({"xd_qkv": z(Mc, D), "xd_o": z(Mc, D), "xd_gu": z(Mc, D), "xd_d": z(Mc, Fd)})
         self.x_final = z(Mc, D)
         self.hf = z(Mc, D)
         self.rstd_f = z(Mc, dt=F32)
@@ -231,12 +237,20 @@ class SimPOEngine:
             ws = self._sk_ws = ops.lora_skinny_ws(self.Mk, K, max(n_tiles, 8), self.device)
         return ws
 
-    def _lora_down(self, x, Acat, out_bf16, M, nmods):
-        """out = bf16(scale * x . Acat^T)  ([Mcap, Rp]; rows M..Mk-1 and unused columns zero)."""
+    def _drop(self, layer: int, group: str):
+        """(seed, p) of one adapter input's dropout mask in the current step, or None."""
+        if self.lora_dropout <= 0 or not self.training:
+            return None
+        return (dropout.layer_seed(self._drop_base, self._drop_call, layer, group), self.lora_dropout)
+
+    def _lora_down(self, x, Acat, out_bf16, M, nmods, drop=None, xd=None):
+        """out = bf16(scale * dropout(x) . Acat^T)  ([Mcap, Rp]; rows M..Mk-1 and unused columns zero).
+        With drop=(seed, p) the masked x is also written to xd (the backward's dA operand)."""
         Rp, K = Acat.shape
         used = nmods * self.layout.r
         nt = (used + 15) // 16
-        ops.lora_skinny(x, Acat, out_bf16, M, self.Mk, K, nt, 0, self.scale, b_rows=used, ws=self._skinny_ws(K, nt))
+        ops.lora_skinny(x, Acat, out_bf16, M, self.Mk, K, nt, 0, self.scale, b_rows=used, ws=self._skinny_ws(K, nt),
+                        dropout=drop, xd=xd if drop else None)
 
     def _lora_g(self, dy, g, Bcat, BT, M):
         """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows M..Mk-1 zero)."""
@@ -277,6 +291,10 @@ class SimPOEngine:
                 raise ValueError(f"{name} out of range [0, {hi})")
         S, T = 2 * B, Lt + N
         M = S * T
+        if self.lora_dropout > 0 and self.training:
+            self._drop_call += 1  # fresh masks per forward; backward() reuses this call's
+            if M * max(self.dims.d_model, self.dims.d_ff) >= 2 ** 32:
+                raise ValueError("LoRA dropout mask index exceeds 32 bits")
         self.B, self.S, self.T, self.Lt, self.M = B, S, T, Lt, M
         self.Mk = roundup(M, 64)
         D, Fd, H, hd = dims.d_model, dims.d_ff, dims.n_heads, dims.head_dim
@@ -299,7 +317,7 @@ class SimPOEngine:
             x = a["x"]
             ops.rmsnorm_fwd(x[:M], lw["ln_in"], a["xn1"][:M], a["rstd1"][:M], dims.rms_eps)
             Acat, _, Bcat, _ = pk["qkv"]
-            self._lora_down(a["xn1"], Acat, a["u_qkv"], M, lay.groups["qkv"].nmods)
+            self._lora_down(a["xn1"], Acat, a["u_qkv"], M, lay.groups["qkv"].nmods, self._drop(i, "qkv"), a.get("xd_qkv"))
             if (3 * D) % 256 == 0:  # q|k RoPE fused into the projection's epilogue
                 ops.gemm_nt(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat,
                             rope=(self.cos, self.sin, T, 2 * D))
@@ -308,15 +326,15 @@ class SimPOEngine:
                 ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
             ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn)
             Acat, _, Bcat, _ = pk["o"]
-            self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods)
+            self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods, self._drop(i, "o"), a.get("xd_o"))
             ops.gemm_nt(a["attn"][:M], lw["o"], a["xmid"][:M], a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
             ops.rmsnorm_fwd(a["xmid"][:M], lw["ln_post"], a["xn2"][:M], a["rstd2"][:M], dims.rms_eps)
             Acat, _, Bcat, _ = pk["gu"]
-            self._lora_down(a["xn2"], Acat, a["u_gu"], M, lay.groups["gu"].nmods)
+            self._lora_down(a["xn2"], Acat, a["u_gu"], M, lay.groups["gu"].nmods, self._drop(i, "gu"), a.get("xd_gu"))
             ops.gemm_nt(a["xn2"][:M], lw["gu"], a["gu"][:M], a2=a["u_gu"][:M], b2=Bcat)
             ops.swiglu_fwd(a["gu"][:M], a["h"][:M])
             Acat, _, Bcat, _ = pk["down"]
-            self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods)
+            self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods, self._drop(i, "down"), a.get("xd_d"))
             xn = self.acts[i + 1]["x"] if i + 1 < dims.n_layers else self.x_final
             ops.gemm_nt(a["h"][:M], lw["down"], xn[:M], a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
         ops.rmsnorm_fwd(self.x_final[:M], self.norm, self.hf[:M], self.rstd_f[:M], dims.rms_eps)
@@ -379,23 +397,26 @@ class SimPOEngine:
             Acat, AcatT, Bcat, BT = pk["down"]
             guard("down")
             gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M)
-            ops.gemm_nt(dx[:M], lw["downT"], self.dh[:M], a2=gs[:M], b2=AcatT)
-            lora_grads_async("down", gs, a["h"], dx, a["u_d"], gbase)
+            dr = self._drop(i, "down")
+            ops.gemm_nt(dx[:M], lw["downT"], self.dh[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            lora_grads_async("down", gs, a["xd_d"] if dr else a["h"], dx, a["u_d"], gbase)
             guard("gu")  # dgu is rewritten here
             ops.swiglu_bwd(self.dh[:M], a["gu"][:M], self.dgu[:M])
             # ---- gate/up
             Acat, AcatT, Bcat, BT = pk["gu"]
             gs = self._lora_g(self.dgu, lay.groups["gu"], Bcat, BT, M)
-            ops.gemm_nt(self.dgu[:M], lw["guT"], self.dxn[:M], a2=gs[:M], b2=AcatT)
-            lora_grads_async("gu", gs, a["xn2"], self.dgu, a["u_gu"], gbase)
+            dr = self._drop(i, "gu")
+            ops.gemm_nt(self.dgu[:M], lw["guT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            lora_grads_async("gu", gs, a["xd_gu"] if dr else a["xn2"], self.dgu, a["u_gu"], gbase)
             guard("o")  # dxmid is rewritten here
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], self.dxmid[:M],
                             dres=dx[:M])
             # ---- o_proj
             Acat, AcatT, Bcat, BT = pk["o"]
             gs = self._lora_g(self.dxmid, lay.groups["o"], Bcat, BT, M)
-            ops.gemm_nt(self.dxmid[:M], lw["oT"], self.dattn[:M], a2=gs[:M], b2=AcatT)
-            lora_grads_async("o", gs, a["attn"], self.dxmid, a["u_o"], gbase)
+            dr = self._drop(i, "o")
+            ops.gemm_nt(self.dxmid[:M], lw["oT"], self.dattn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            lora_grads_async("o", gs, a["xd_o"] if dr else a["attn"], self.dxmid, a["u_o"], gbase)
             # ---- attention + RoPE
             guard("qkv")  # dqkv is rewritten here
             ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, None,
@@ -403,8 +424,9 @@ class SimPOEngine:
             # ---- q/k/v
             Acat, AcatT, Bcat, BT = pk["qkv"]
             gs = self._lora_g(self.dqkv, lay.groups["qkv"], Bcat, BT, M)
-            ops.gemm_nt(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT)
-            lora_grads_async("qkv", gs, a["xn1"], self.dqkv, a["u_qkv"], gbase)
+            dr = self._drop(i, "qkv")
+            ops.gemm_nt(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            lora_grads_async("qkv", gs, a["xd_qkv"] if dr else a["xn1"], self.dqkv, a["u_qkv"], gbase)
             guard("down")  # dx (the down group's dy) is rewritten here
             ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M])
         main.wait_stream(side)

@@ -147,7 +147,7 @@ def get_model(mode: str = "train", dtype=torch.bfloat16, config=None, device=Non
                 w[f"layers.{i}.{p}.lora_B"] = torch.zeros(out_f, r, dtype=torch.bfloat16)
     bs = max_pairs or int(get(config, "dataset.train.batch_size", 4))
     engine = SimPOEngine(dims, w, device=device, max_pairs=bs, max_text_len=max_text_len, n_img_tokens=n_img_tokens,
-                         lora_dropout=dropout)
+                         lora_dropout=dropout, dropout_seed=seed)
     del w
     tokenizer = load_tokenizer(get(config, "model.tokenizer_path"), vocab=dims.vocab)
     lora_cfg = {"lora_rank": r, "lora_alpha": alpha, "lora_dropout": dropout, "target_modules": targets}

@@ -91,9 +91,10 @@ def gemm_workspace(device=None) -> torch.Tensor:
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0,
-            bias=None, residual=None, rope=None) -> torch.Tensor:
+            bias=None, residual=None, rope=None, dropout=None) -> torch.Tensor:
     """out[M,N] = bf16(alpha*(a.b^T + a2.b2^T) + bias) [+ residual]  (nn.Linear layout b=[N,K]).
-    rope=(cos, sin, T, ncols): RoPE forward fused on output columns < ncols (ospo_gemm_nt_rope_bf16)."""
+    rope=(cos, sin, T, ncols): RoPE forward fused on output columns < ncols (ospo_gemm_nt_rope_bf16).
+    dropout=(seed, p): the a2.b2^T term is masked like the adapter input's dropout (ospo_gemm_nt_dropout_bf16)."""
     for t, n in ((a, "a"), (b, "b"), (out, "out")):
         _chk(t, BF16, n)
     M, K = a.shape
@@ -109,7 +110,12 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
         gemm_workspace(a.device)
     st = torch.cuda.current_stream()
     e0 = _TIMER.start(st) if _TIMER is not None else None
-    if rope is not None:
+    if dropout is not None and dropout[1] > 0:
+        if bias is not None or residual is not None or alpha != 1.0 or rope is not None or a2 is None:
+            raise ValueError("gemm_nt: dropout needs a2/b2 and excludes bias / residual / alpha / rope")
+        call("ospo_gemm_nt_dropout_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K, _p(a2), _ld(a2), _p(b2), _ld(b2),
+             K2, _p(out), _ld(out), int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]), st.cuda_stream)
+    elif rope is not None:
         if bias is not None or residual is not None or alpha != 1.0:
             raise ValueError("gemm_nt: rope excludes bias / residual / alpha")
         cos, sin, T, ncols = rope
@@ -295,13 +301,17 @@ def lora_skinny_ws(M_out, K, n_tiles=4, device="cuda") -> torch.Tensor:
     return torch.zeros((n + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
-def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=None, ws=None, module_tiles=1):
-    """out[:M_out, :] (bf16) = scale * a . bt^T per 16-column n-tile (see ospo_lora_skinny)."""
+def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=None, ws=None, module_tiles=1,
+                dropout=None, xd=None):
+    """out[:M_out, :] (bf16) = scale * a . bt^T per 16-column n-tile (see ospo_lora_skinny).
+    dropout=(seed, p): LoRA dropout on a (dense mode); the masked a is written to xd if given."""
     if ws is None:
         ws = lora_skinny_ws(M_out, K, n_tiles, a.device)
+    seed, p = dropout if dropout is not None else (0, 0.0)
     call("ospo_lora_skinny", _p(a), _ld(a), _p(bt), _ld(bt), bt.shape[0] if b_rows is None else b_rows, M, M_out,
          K, n_tiles, a_koff, module_tiles, float(scale), _p(out), _ld(out), out.shape[1], _p(ws),
-         ws.numel() * ws.element_size(), _s())
+         ws.numel() * ws.element_size(), int(seed) & 0xFFFFFFFF, float(p), _p(xd), _ld(xd) if xd is not None else 0,
+         _s())
 
 
 # -------------------------------------------------------------- optimizer

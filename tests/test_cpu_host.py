@@ -27,7 +27,7 @@ def lib():
 
 def header_symbols():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(ospo_[a-z0-9_]+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int|unsigned|size_t|const char\*)\s+(ospo_[a-z0-9_]+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_header_symbol(lib):
@@ -188,3 +188,19 @@ def test_checkpoint_roundtrip_cpu(tmp_path):
     opt2 = FusedLoraAdamW(e2, 4e-5, (0.9, 0.95), 1e-8, 0.0, 1.0)
     load_checkpoint(p, e2, opt2, ConstantLR(opt2))
     assert torch.equal(e2.lora, e.lora) and torch.equal(e2.exp_avg_sq, e.exp_avg_sq) and e2.opt_step == 7
+
+
+def test_dropout_hash_host_c_and_numpy_agree(lib):
+    """ospo_amd/dropout.py restates the device mask hash bit for bit; keep rate ~ 1 - p."""
+    import numpy as np
+    from ospo_amd import dropout as D
+    rng = np.random.default_rng(0)
+    idx = rng.integers(0, 2 ** 32, 2000, dtype=np.uint64).astype(np.uint32)
+    seeds = rng.integers(0, 2 ** 32, 2000, dtype=np.uint64).astype(np.uint32)
+    ref = np.array([lib.ospo_dropout_hash(int(i), int(s)) for i, s in zip(idx, seeds)], dtype=np.uint32)
+    assert np.array_equal(ref, np.array([D.drop_hash(i, int(s)) for i, s in zip(idx, seeds)], dtype=np.uint32))
+    m = D.keep_mask(512, 4096, D.layer_seed(42, 1, 0, "qkv"), 0.05)
+    assert abs(m.mean() - 0.95) < 2e-3
+    m2 = D.keep_mask(512, 4096, D.layer_seed(42, 1, 0, "o"), 0.05)
+    assert 0.90 < (m == m2).mean() < 0.91  # independent masks agree where both keep or both drop
+    assert D.layer_seed(42, 1, 3, "gu") != D.layer_seed(42, 2, 3, "gu")

@@ -425,6 +425,41 @@ def test_lora_skinny_down(M, K, used):
         assert torch.all(out[M_out:] == 7.0)
 
 
+@pytest.mark.parametrize("M,K,used", [(600, 4096, 48), (77, 11008, 16)])
+def test_lora_skinny_dropout(M, K, used):
+    """u = s dropout(x) A^T with the counter-based mask; xd = dropout(x) stored for the backward."""
+    import numpy as np
+    from ospo_amd import dropout as Dm
+    p, seed = 0.05, 123457
+    Rp = 64
+    x = rnd(M, K)
+    Acat = torch.zeros(Rp, K, device=DEV, dtype=torch.bfloat16)
+    Acat[:used] = rnd(used, K)
+    out = torch.empty(M, Rp, device=DEV, dtype=torch.bfloat16)
+    xd = torch.full((M, K), 3.0, device=DEV, dtype=torch.bfloat16)
+    ops().lora_skinny(x, Acat, out, M, M, K, (used + 15) // 16, 0, 2.0, b_rows=used, dropout=(seed, p), xd=xd)
+    keep = torch.from_numpy(Dm.keep_mask(M, K, seed, p)).to(DEV)
+    ref_xd = torch.where(keep, (x.float() / (1 - p)).to(torch.bfloat16), torch.zeros((), dtype=torch.bfloat16,
+                                                                                           device=DEV))
+    assert torch.equal(xd, ref_xd)
+    ref = 2.0 * (ref_xd.float() @ Acat.float().T)
+    assert relerr(out.float(), ref) < 8e-3
+
+
+@pytest.mark.parametrize("M,N,K,K2", [(300, 512, 256, 64), (4800, 4096, 4096, 64), (600, 1024, 512, 128)])
+def test_gemm_dropout_backward(M, N, K, K2):
+    """dX = dy.W + mask (.) (g.A) / (1-p): the K-extension is masked like the adapter input."""
+    from ospo_amd import dropout as Dm
+    p, seed = 0.05, 998877
+    a, b = rnd(M, K), rnd(N, K, s=0.05)
+    a2, b2 = rnd(M, K2), rnd(N, K2, s=0.05)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(seed, p))
+    keep = torch.from_numpy(Dm.keep_mask(M, N, seed, p)).to(DEV)
+    ref = a.float() @ b.float().T + keep.float() / (1 - p) * (a2.float() @ b2.float().T)
+    assert relerr(out.float(), ref) < 4e-3
+
+
 @pytest.mark.parametrize("M,nm,Nmod,r", [(4800, 3, 4096, 16), (640, 2, 11008, 16), (100, 1, 4096, 16),
                                          (300, 3, 1024, 32), (200, 2, 2048, 32)])
 def test_lora_skinny_up_blockdiag(M, nm, Nmod, r):

@@ -182,3 +182,38 @@ def test_step_lora_rank_variants_vs_oracle(r):
     assert max(rel(logps[:B], ora.chosen_logps), rel(logps[B:], ora.rejected_logps)) < 1e-3
     assert abs(loss - float(ora.loss)) / float(ora.loss) < 2e-3
     assert max(rel(grads[k], ora.lora_grads[k]) for k in ora.lora_grads) < 5e-2
+
+
+def test_step_lora_dropout_vs_oracle_with_replayed_masks():
+    """configs/peft/lora.yaml: lora_dropout 0.05.  The HIP path's counter-based masks
+    (ospo_amd/dropout.py) are replayed into the oracle, which then computes peft's
+    dropout(x) exactly: forward log-probs, loss and every LoRA grad must match."""
+    from ospo_amd import dropout as Dm
+    p = 0.05
+    dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=2048,
+                       gen_head_dim=256, lora_r=16, lora_alpha=32, lora_dropout=p)
+    w = O.init_weights(dims, seed=21, dtype=torch.bfloat16, lora_b_std=1e-2)
+    g = torch.Generator().manual_seed(22)
+    B, N = 2, 64
+    text = [torch.randint(0, dims.vocab, (1, 8 - 2 * i), generator=g, dtype=torch.int32) for i in range(B)]
+    chosen = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    rejected = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    algo = {"beta": 10.0, "gamma_beta_ratio": 0.5, "label_smoothing": 0.0, "loss_type": "sigmoid"}
+    from ospo_amd.engine import ModelDims, SimPOEngine
+    eng = SimPOEngine(ModelDims.from_any(dims), w, device="cuda", max_pairs=B, max_text_len=8, n_img_tokens=N,
+                      lora_dropout=p, dropout_seed=7)
+    logps, loss, grads = run_hip_step(eng, text, chosen, rejected, algo)
+    call = eng._drop_call
+    M = 2 * B * (8 + N)
+    kin = {"qkv": dims.d_model, "o": dims.d_model, "gu": dims.d_model, "down": dims.d_ff}
+    masks = {(i, grp): torch.from_numpy(Dm.keep_mask(M, kin[grp], Dm.layer_seed(7, call, i, grp), p))
+             for i in range(dims.n_layers) for grp in kin}
+    ora = O.simpo_step(text, chosen, rejected, w, dims, dtype=torch.bfloat16, dropout_masks=masks)
+    assert max(rel(logps[:B], ora.chosen_logps), rel(logps[B:], ora.rejected_logps)) < 1e-3
+    assert abs(loss - float(ora.loss)) / float(ora.loss) < 2e-3
+    ge = max(rel(grads[k], ora.lora_grads[k]) for k in ora.lora_grads)
+    assert ge < 5e-2, ge
+    # without replaying the masks the grads differ: the mask is really applied
+    plain = O.simpo_step(text, chosen, rejected, w, O.JanusDims(**{**dims.__dict__, "lora_dropout": 0.0}),
+                         dtype=torch.bfloat16)
+    assert max(rel(grads[k], plain.lora_grads[k]) for k in plain.lora_grads) > 0.05
