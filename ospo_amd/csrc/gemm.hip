@@ -16,6 +16,8 @@
 //    fusing alpha, bias and the bf16 residual add of the decoder layer.
 //  * The LoRA update x.A^T.B^T*s is one more K segment (A2 = s*u, B2 = packed
 //    block-diagonal lora_B), so the adapter costs Rp/K extra MFMAs, no pass.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -759,7 +761,8 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   }
 
   const int frow = lane & 15, fcol = lane >> 4;
-  for (int t = 0; t < nt; ++t) {
+  // one K-tile = 4 phases; a lambda so the dropout variant can peel its extension tiles
+  auto run_tile = [&](int t) {
     const char* slot = smem + (t & 1) * SLOT;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -826,8 +829,14 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
+  };
+  // with dropout the LoRA extension tiles come first (stage_half's order); their masked sum is
+  // scaled once between the two loops, outside the hot loop's register allocation
+  const int pre = (DROP && tb == 0) ? (nt2 < nt ? nt2 : nt) : 0;
+  for (int t = 0; t < pre; ++t) run_tile(t);
+  if (pre > 0) {
     if constexpr (DROP) {
-      if (tb == 0 && t == nt2 - 1) {  // accumulators hold exactly A2.B2^T: apply the dropout mask
+      {  // accumulators hold exactly A2.B2^T: apply the dropout mask
         const int gq = lane >> 4, lq = lane & 15;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -849,6 +858,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       }
     }
   }
+  for (int t = pre; t < nt; ++t) run_tile(t);
   if (!g1) {  // re-align the barrier count
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1160,8 +1170,18 @@ extern "C" int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void
   if (!a_kmajor && !b_kmajor) return launch<2, 2, 2, 2, false, false, EPI_F32_ATOMIC>(a, stream);
   if (!a_kmajor && b_kmajor) return launch<2, 2, 2, 2, false, true, EPI_F32_ATOMIC>(a, stream);
   if (a_kmajor && !b_kmajor) return OSPO_ERR_UNSUPPORTED;
-  // both K-major (LoRA weight gradients)
-  if (wideN && !tallM) return launch<2, 4, 2, 4, true, true, EPI_F32_ATOMIC>(a, stream);   // 64 x 256
-  if (tallM && !wideN) return launch<4, 2, 4, 2, true, true, EPI_F32_ATOMIC>(a, stream);   // 256 x 64
+  // both K-major (LoRA weight gradients): big tiles only when they alone fill the chip,
+  // otherwise 64 x 64 tiles (parallelism from tiles, not from more fp32-atomic K splits)
+  const long ks = a.k_splits > 1 ? a.k_splits : 1;
+  static const bool legacy = getenv("OSPO_F32ACC_LEGACY") != nullptr;  // A/B of the tile rule only
+  if (legacy) {
+    if (wideN && !tallM) return launch<2, 4, 2, 4, true, true, EPI_F32_ATOMIC>(a, stream);
+    if (tallM && !wideN) return launch<4, 2, 4, 2, true, true, EPI_F32_ATOMIC>(a, stream);
+    return launch<2, 2, 2, 2, true, true, EPI_F32_ATOMIC>(a, stream);
+  }
+  if (wideN && !tallM && (long)(N / 256) * ((M + 63) / 64) * ks >= 384)
+    return launch<2, 4, 2, 4, true, true, EPI_F32_ATOMIC>(a, stream);   // 64 x 256
+  if (tallM && !wideN && (long)(M / 256) * ((N + 63) / 64) * ks >= 384)
+    return launch<4, 2, 4, 2, true, true, EPI_F32_ATOMIC>(a, stream);   // 256 x 64
   return launch<2, 2, 2, 2, true, true, EPI_F32_ATOMIC>(a, stream);
 }

@@ -432,17 +432,17 @@ class SimPOEngine:
         main.wait_stream(side)
 
     def _lora_grads(self, gs, x_in, dy, u, g, gbase):
-        """dA = g_s^T . x_in  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal)."""
+        """dA = g_s^T . x_in  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal).
+        Only the nmods*r used columns of g enter dA (no atomics of padding rows); 8 K splits."""
         r = self.layout.r
         Mk = self.Mk
+        used = g.nmods * r
         a_off = gbase + g.a_off
-        dA = self.grads[a_off: a_off + g.nmods * r * g.Kin].view(g.nmods * r, g.Kin)
-        ks = max(1, min(Mk // 512, 16))
-        ops.gemm_f32acc(gs[:Mk], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True, k_splits=ks)
+        dA = self.grads[a_off: a_off + used * g.Kin].view(used, g.Kin)
+        ops.gemm_f32acc(gs[:Mk, :used], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True, k_splits=8)
         b_off = gbase + g.b_off
         dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
-        ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=max(1, min(Mk // 1024, 8)),
-                        diag=(g.Nmod, r))
+        ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=8, diag=(g.Nmod, r))
 
     # ------------------------------------------------------------ optimizer
     def grad_norm_sq(self) -> torch.Tensor:

@@ -91,6 +91,9 @@ def test_gemm_nt_rejects_bad_shapes():
     (True, True, 64, 512, 640, 5),       # dA = g^T x
     (True, True, 1024, 64, 640, 4),      # dB = dy^T u
     (True, True, 128, 128, 256, 1),
+    (True, True, 128, 4096, 1280, 12),  # 64 x 256 tiles (grid >= 384)
+    (True, True, 4096, 64, 640, 8),     # 256 x 64 tiles
+    (True, True, 256, 1024, 640, 8),    # 64 x 64 fallback
 ])
 def test_gemm_f32acc_layouts(a_k, b_k, M, N, K, splits):
     A = ints(K, M) if a_k else ints(M, K)
@@ -101,6 +104,18 @@ def test_gemm_f32acc_layouts(a_k, b_k, M, N, K, splits):
     ops().gemm_f32acc(A, B, out, a_kmajor=a_k, b_kmajor=b_k, k_splits=splits, alpha=2.0)
     ref = 0.5 + 2.0 * (Aop @ Bop.T)
     assert torch.equal(out, ref), (out - ref).abs().max()
+
+
+def test_gemm_f32acc_dA_used_rows_of_padded_g():
+    """dA = g[:, :used]^T x with g padded to Rp = 64 columns: only the used rows are written."""
+    K, Rp, used, N = 4800, 64, 48, 4096
+    g = ints(K, Rp)
+    x = ints(K, N)
+    out = torch.full((used + 1, N), 7.0, device=DEV, dtype=torch.float32)
+    ops().gemm_f32acc(g[:, :used], x, out[:used], a_kmajor=True, b_kmajor=True, k_splits=8)
+    ref = 7.0 + g[:, :used].float().T @ x.float()
+    assert torch.equal(out[:used], ref)
+    assert torch.all(out[used] == 7.0)
 
 
 def test_gemm_f32acc_blockdiag_scatter():

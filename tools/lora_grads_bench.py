@@ -1,0 +1,52 @@
+"""A/B the LoRA weight-gradient products (dA = g^T x, dB = dy^T u) on one layer's
+shapes (Janus-Pro-7B, 4 pairs, T = 600): legacy (Rp rows, 9/4 splits, big tiles) vs
+current (used rows, 8 splits, grid-aware tiles).  Run twice: with and without
+OSPO_F32ACC_LEGACY=1 (the C tile rule is read once per process)."""
+import json
+import os
+import sys
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ospo_amd import ops
+
+Mk, D, F, r, Rp = 4864, 4096, 11008, 16, 64
+GROUPS = [("qkv", 3, D, D), ("o", 1, D, D), ("gu", 2, D, F), ("down", 1, F, D)]  # name, nmods, Kin, Nmod
+legacy = os.environ.get("OSPO_F32ACC_LEGACY") is not None
+
+
+def main():
+    torch.manual_seed(0)
+    tot = 0.0
+    for name, nm, kin, nmod in GROUPS:
+        g = (torch.randn(Mk, Rp, device="cuda") * 0.1).bfloat16()
+        x = torch.randn(Mk, kin, device="cuda").bfloat16()
+        dy = torch.randn(Mk, nm * nmod, device="cuda").bfloat16()
+        u = (torch.randn(Mk, Rp, device="cuda") * 0.1).bfloat16()
+        used = nm * r
+        dA = torch.zeros(Rp if legacy else used, kin, device="cuda")
+        dB = torch.zeros(nm * nmod, r, device="cuda")
+
+        def run():
+            if legacy:
+                ops.gemm_f32acc(g, x, dA, a_kmajor=True, b_kmajor=True, k_splits=min(Mk // 512, 16))
+                ops.gemm_f32acc(dy, u, dB, a_kmajor=True, b_kmajor=True, k_splits=min(Mk // 1024, 8), diag=(nmod, r))
+            else:
+                ops.gemm_f32acc(g[:, :used], x, dA, a_kmajor=True, b_kmajor=True, k_splits=8)
+                ops.gemm_f32acc(dy, u, dB, a_kmajor=True, b_kmajor=True, k_splits=8, diag=(nmod, r))
+        for _ in range(3):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 20 * 1e3
+        tot += us
+        print(json.dumps({"group": name, "legacy": legacy, "dA+dB_us": round(us, 1)}), flush=True)
+    print(json.dumps({"legacy": legacy, "per_layer_us": round(tot, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
