@@ -20,6 +20,8 @@
 // LDS images are [row][128 x bf16] (256-B rows) with 16-B chunk swizzle
 // chunk ^ 2*(row & 7): conflict-free for both the ds_read_b128 row reads and
 // the ds_read_b64_tr_b16 column reads (CDNA4 LDS banking, 64 x 4 B banks).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -38,12 +40,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, char* lds_dst_uniform) 
 }
 
 // Stage 64 rows x 128 bf16 (rows row0.., clamped to [0, row_lim)) of a strided
-// buffer into an LDS image.  4 waves x 4 pieces of 1 KiB (4 rows each).
+// buffer into an LDS image: 16 pieces of 1 KiB (4 rows each) over the NW waves.
+template <int NW>
 __device__ __forceinline__ void stage64(const bf16* base, int ld, int row0, int row_lim, int col0, char* lds,
                                         int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = wave * 4 + i;
+  for (int p = wave; p < 16; p += NW) {
     const int row = p * 4 + (lane >> 4);
     const int ch = (lane & 15) ^ aswz(row);
     int gr = row0 + row;
@@ -71,6 +73,43 @@ __device__ __forceinline__ bf16x8 frag_tr_perm(const char* lds, int kbase, int c
   i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(lds + r2 * ROWB + ((x ^ aswz(r2)) << 4) + h));
   i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// Inline-asm form of frag_tr_perm: the two ds_read_b64_tr_b16 are invisible to the
+// compiler's waitcnt pass, which otherwise (a) drains vmcnt(0) before every transposed
+// read -- it cannot tell them from the in-flight LDS-DMA of the next tile -- and (b)
+// issues one read pair per MFMA behind lgkmcnt(0).  Callers issue a batch, then
+// trp_wait() the whole batch once (registers tied, then a sched_barrier).
+__device__ __forceinline__ uint32_t lds_u32(const char* p) {
+  return (uint32_t)(uintptr_t)((LDS_AS const char*)p);
+}
+__device__ __forceinline__ void trp_issue(const char* lds, int kbase, int c0, int lane, i16x4& lo, i16x4& hi) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int r1 = kbase + 4 * g + q;
+  const int r2 = r1 + 16;
+  const int x = (c0 >> 3) + (p >> 1);
+  const int h = (p & 1) << 3;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(lds_u32(lds + r1 * ROWB + ((x ^ aswz(r1)) << 4) + h)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(lds_u32(lds + r2 * ROWB + ((x ^ aswz(r2)) << 4) + h)));
+}
+__device__ __forceinline__ bf16x8 trp_join(const i16x4& lo, const i16x4& hi) {
+  i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// wait for 4 transposed fragments (8 reads): all registers tied to the wait
+__device__ __forceinline__ void trp_wait4(i16x4 (&lo)[4], i16x4 (&hi)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]),
+                 "+v"(hi[3])::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// wait for 8 transposed fragments (16 reads): all registers tied to the wait
+__device__ __forceinline__ void trp_wait8(i16x4 (&lo)[8], i16x4 (&hi)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(lo[4]), "+v"(lo[5]), "+v"(lo[6]),
+                 "+v"(lo[7]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3]), "+v"(hi[4]), "+v"(hi[5]),
+                 "+v"(hi[6]), "+v"(hi[7])::"memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // Same, natural k order (element j <- row kbase + 8g + j): for the dQ = dS.K product.
@@ -115,7 +154,8 @@ __device__ __forceinline__ void rope_bwd_acc(f32x4 (&v)[8], const bf16* cs, cons
 }
 
 // ============================================================== forward ====
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
+template <int NW, int DBG = 0>  // DBG 1: no K/V loads after the first tile (ablation, results invalid)
+__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
                                                        bf16* __restrict__ out, int ldo, float* __restrict__ lse,
                                                        int T, int H, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
@@ -128,7 +168,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   const int rows_lim_seq = T;  // clamp inside the sequence
 
   // this lane's query row
-  const int qrow = qb * QB + wave * 16 + l16;
+  constexpr int RB = 16 * NW;  // query rows per workgroup
+  const int qrow = qb * RB + wave * 16 + l16;
   const int qr_c = qrow < T ? qrow : T - 1;
   bf16x8 qf[4];
   {
@@ -142,21 +183,22 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -1e30f, l_run = 0.f;
 
-  const int n_kv = qb + 1;  // causal: key tiles 0..qb
+  const int last = (qb * RB + RB - 1 < T ? qb * RB + RB - 1 : T - 1);
+  const int n_kv = last / KB + 1;  // causal: key tiles up to the block's last row
   const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
   const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
 
-  stage64(kbase, ldq, 0, rows_lim_seq, 0, smem, wave, lane);
-  stage64(vbase, ldq, 0, rows_lim_seq, 0, smem + TILE_BYTES, wave, lane);
+  stage64<NW>(kbase, ldq, 0, rows_lim_seq, 0, smem, wave, lane);
+  stage64<NW>(vbase, ldq, 0, rows_lim_seq, 0, smem + TILE_BYTES, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int kt = 0; kt < n_kv; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < n_kv) {
+    if (DBG == 0 && kt + 1 < n_kv) {
       char* nb = smem + (buf ^ 1) * 2 * TILE_BYTES;
-      stage64(kbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nb, wave, lane);
-      stage64(vbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nb + TILE_BYTES, wave, lane);
+      stage64<NW>(kbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nb, wave, lane);
+      stage64<NW>(vbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nb + TILE_BYTES, wave, lane);
     }
     const char* Ks = smem + buf * 2 * TILE_BYTES;
     const char* Vs = Ks + TILE_BYTES;
@@ -169,8 +211,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int d = 0; d < 4; ++d) st[t] = MFMA(frag_row(Ks, 16 * t, d, lane), qf[d], st[t]);
     }
-    // scale + mask, tile max
-    const bool diag = (kt == qb) || ((kt + 1) * KB > T);
+    // scale + mask, tile max (tiles that may hold a key beyond some row of the block)
+    const bool diag = (kt * KB + KB - 1 > qb * RB) || ((kt + 1) * KB > T);
     float tmax = -1e30f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -204,12 +246,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] *= alpha;
 
-    // O^T[d][q] += V^T[d][key] . P^T[key][q]
+    // O^T[d][q] += V^T[d][key] . P^T[key][q]: V^T fragments in batches of 4 (asm reads: no
+    // vmcnt drain of the in-flight next tile, 4 LDS waits per tile instead of 16)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const bf16x8 pb = pack_perm(st[2 * u], st[2 * u + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[dt] = MFMA(frag_tr_perm(Vs, 32 * u, 16 * dt, lane), pb, o[dt]);
+      for (int d0 = 0; d0 < 8; d0 += 4) {
+        i16x4 vlo[4], vhi[4];
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) trp_issue(Vs, 32 * u, 16 * (d0 + dd), lane, vlo[dd], vhi[dd]);
+        trp_wait4(vlo, vhi);
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) o[d0 + dd] = MFMA(trp_join(vlo[dd], vhi[dd]), pb, o[d0 + dd]);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -234,7 +284,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 // owns 16 keys (K, V fragments in registers, dK^T dV^T accumulators) and
 // sweeps the query tiles at/after its block.  Q / dO tiles (+ lse, delta) are
 // double-buffered in LDS through global_load_lds; no atomics.
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
                                                             int vc, const bf16* __restrict__ dout, int ldd,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
@@ -250,8 +301,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
   const int g = lane >> 4, l16 = lane & 15;
   const long rowbase = (long)s * T;
   const int nq = (T + QB - 1) / QB;
-
-  const int key_l = kb * KB + wave * 16 + l16;
+  constexpr int KBW = 16 * NW;  // keys per workgroup
+  const int key_l = kb * KBW + wave * 16 + l16;
   const int key_c = key_l < T ? key_l : T - 1;
   bf16x8 kf[4], vf[4];
   {
@@ -274,8 +325,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
 
   auto stage = [&](int qt, int b) {
     char* Qs = smem + b * 2 * TILE_BYTES;
-    stage64(qbase, ldq, qt * QB, T, 0, Qs, wave, lane);
-    stage64(obase, ldd, qt * QB, T, 0, Qs + TILE_BYTES, wave, lane);
+    stage64<NW>(qbase, ldq, qt * QB, T, 0, Qs, wave, lane);
+    stage64<NW>(obase, ldd, qt * QB, T, 0, Qs + TILE_BYTES, wave, lane);
     if (wave < 2) {  // 64 lanes x 4 B: lse (wave 0) / delta (wave 1) of the tile's 64 queries
       int q = qt * QB + lane;
       q = q < T ? q : T - 1;
@@ -284,12 +335,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
     }
   };
 
-  stage(kb, 0);
+  const int qt0 = (kb * KBW) / QB;  // first query tile with a row >= the block's first key
+  stage(qt0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int qt = kb; qt < nq; ++qt) {
-    const int b = (qt - kb) & 1;
+  for (int qt = qt0; qt < nq; ++qt) {
+    const int b = (qt - qt0) & 1;
     if (qt + 1 < nq) stage(qt + 1, b ^ 1);
     const char* Qs = smem + b * 2 * TILE_BYTES;
     const char* Os = Qs + TILE_BYTES;
@@ -354,7 +406,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
 // the lanes; sweeps key tiles 0..qb with K / V double-buffered in LDS.
 // dS^T[key][q] = P^T (dP^T - delta), dP^T = V . dO^T; dQ^T[d][q] += K^T[d][key] . dS^T.
 // dQ lives in registers for the whole sweep: no atomics, no workspace.
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
                                                           int vc, const bf16* __restrict__ dout, int ldd,
                                                           const bf16* __restrict__ o, int ldo,
                                                           const float* __restrict__ lse,
@@ -369,7 +422,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const int g = lane >> 4, l16 = lane & 15;
   const long rowbase = (long)s * T;
 
-  const int qrow = qb * QB + wave * 16 + l16;
+  constexpr int RB = 16 * NW;
+  const int qrow = qb * RB + wave * 16 + l16;
   const int qr_c = qrow < T ? qrow : T - 1;
   bf16x8 qf[4], of[4];
   float dpart = 0.f;  // delta = rowsum(dO * O), this lane's 32 of the head's 128 columns
@@ -396,11 +450,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
   for (int i = 0; i < 8; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int n_kv = qb + 1;
+  const int last = (qb * RB + RB - 1 < T ? qb * RB + RB - 1 : T - 1);
+  const int n_kv = last / KB + 1;
   const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
   const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
-  stage64(kbase, ldq, 0, T, 0, smem, wave, lane);
-  stage64(vbase, ldq, 0, T, 0, smem + TILE_BYTES, wave, lane);
+  stage64<NW>(kbase, ldq, 0, T, 0, smem, wave, lane);
+  stage64<NW>(vbase, ldq, 0, T, 0, smem + TILE_BYTES, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -408,8 +463,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     const int buf = kt & 1;
     if (kt + 1 < n_kv) {
       char* nb = smem + (buf ^ 1) * 2 * TILE_BYTES;
-      stage64(kbase, ldq, (kt + 1) * KB, T, 0, nb, wave, lane);
-      stage64(vbase, ldq, (kt + 1) * KB, T, 0, nb + TILE_BYTES, wave, lane);
+      stage64<NW>(kbase, ldq, (kt + 1) * KB, T, 0, nb, wave, lane);
+      stage64<NW>(vbase, ldq, (kt + 1) * KB, T, 0, nb + TILE_BYTES, wave, lane);
     }
     const char* Ks = smem + buf * 2 * TILE_BYTES;
     const char* Vs = Ks + TILE_BYTES;
@@ -425,7 +480,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         dpt[t] = MFMA(frag_row(Vs, 16 * t, d, lane), of[d], dpt[t]);
       }
     }
-    const bool diag = (kt == qb) || ((kt + 1) * KB > T);
+    const bool diag = (kt * KB + KB - 1 > qb * RB) || ((kt + 1) * KB > T);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -460,6 +515,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   }
 }
 
+// waves per workgroup (16 query rows / keys each): 8 shares every staged K/V (Q/dO)
+// tile between twice the rows; OSPO_ATTN_WAVES=4 selects the 64-row form (A/B)
+int attn_waves() {
+  static const int nw = [] {
+    const char* e = getenv("OSPO_ATTN_WAVES");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  return nw;
+}
+
 }  // namespace
 
 extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
@@ -470,8 +535,11 @@ extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k
   if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || q_col % 8 || k_col % 8 || v_col % 8)
     return OSPO_ERR_SHAPE;
   if (!aligned16(qkv) || !aligned16(o)) return OSPO_ERR_ALIGN;
-  dim3 grid((T + QB - 1) / QB, n_heads, S);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+  const int nw = attn_waves();
+  dim3 grid((T + 16 * nw - 1) / (16 * nw), n_heads, S);
+  static const bool dbg = getenv("OSPO_ATTN_DBG") != nullptr;  // ablation only
+  auto kfn = dbg ? attn_fwd_kernel<8, 1> : (nw == 8 ? attn_fwd_kernel<8, 0> : attn_fwd_kernel<4, 0>);
+  hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                      (bf16*)o, ld_o, lse, T, n_heads, scale);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
@@ -493,13 +561,14 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
   const bf16* rc = (const bf16*)rope_cos;
   const bf16* rs = (const bf16*)rope_sin;
   // dQ first: it also produces delta = rowsum(dO * O) for the dK/dV kernel
-  dim3 gq((T + QB - 1) / QB, n_heads, S);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+  const int nw = attn_waves();
+  dim3 gq((T + 16 * nw - 1) / (16 * nw), n_heads, S);
+  hipLaunchKernelGGL(nw == 8 ? attn_bwd_dq_kernel<8> : attn_bwd_dq_kernel<4>, gq, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                      (const bf16*)dout, ld_do, (const bf16*)o, ld_o, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads,
                      scale, rc, rs);
   OSPO_CHECK_LAUNCH();
-  dim3 grid((T + KB - 1) / KB, n_heads, S);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+  dim3 grid((T + 16 * nw - 1) / (16 * nw), n_heads, S);
+  hipLaunchKernelGGL(nw == 8 ? attn_bwd_dkdv_kernel<8> : attn_bwd_dkdv_kernel<4>, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
                      v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
