@@ -55,6 +55,47 @@ class GradAllReduce:
         flat.mul_(1.0 / self.world)
         return flat
 
+    # ---- overlapped form: buckets launched as the backward finishes layers
+    def begin(self, flat: torch.Tensor):
+        """Start a step: ``push`` contiguous ranges as they become final, then ``finish``."""
+        self._flat, self._works, self._pend = flat, [], None
+
+    def push(self, lo: int, hi: int):
+        """Elements [lo, hi) of the flat buffer are final on the CURRENT stream.  Adjacent
+        ranges are merged until a bucket is full, then all-reduced asynchronously (the
+        collective waits for the current stream's work so far, not for the whole backward)."""
+        if self.world <= 1:
+            return
+        if self._pend is None:
+            self._pend = [lo, hi]
+        elif hi == self._pend[0]:      # backward walks layers in reverse: ranges grow downwards
+            self._pend[0] = lo
+        elif lo == self._pend[1]:
+            self._pend[1] = hi
+        else:
+            self._flush()
+            self._pend = [lo, hi]
+        if self._pend[1] - self._pend[0] >= self.bucket:
+            self._flush()
+
+    def _flush(self):
+        if self._pend is not None:
+            lo, hi = self._pend
+            self._works.append(dist.all_reduce(self._flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
+            self._pend = None
+
+    def finish(self):
+        """Launch the last bucket, make the current stream wait for every collective, average."""
+        if self.world <= 1:
+            return self._flat
+        self._flush()
+        for w in self._works:
+            w.wait()
+        self._works = []
+        self._flat.mul_(1.0 / self.world)
+        return self._flat
+
 
 def broadcast_(t: torch.Tensor, src: int = 0, group=None):
     if dist.is_initialized() and dist.get_world_size(group) > 1:

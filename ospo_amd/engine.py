@@ -351,8 +351,11 @@ class SimPOEngine:
     def zero_grad(self):
         self.grads.zero_()
 
-    def backward(self, g_seq: torch.Tensor):
-        """g_seq fp32 [2B] = dL/d seq_logps.  Accumulates LoRA grads into self.grads."""
+    def backward(self, g_seq: torch.Tensor, on_layer_grads=None):
+        """g_seq fp32 [2B] = dL/d seq_logps.  Accumulates LoRA grads into self.grads.
+        on_layer_grads(lo, hi): called (on the side stream, after that layer's dA/dB were
+        enqueued) when grads[lo:hi] of a layer are final -- e.g. GradAllReduce.push, so the
+        data-parallel all-reduce overlaps the rest of the backward."""
         dims = self.dims
         S, T, Lt, M, Mk, N = self.S, self.T, self.Lt, self.M, self.Mk, self.N
         D, Fd, H, hd = dims.d_model, dims.d_ff, dims.n_heads, dims.head_dim
@@ -429,6 +432,9 @@ class SimPOEngine:
             lora_grads_async("qkv", gs, a["xd_qkv"] if dr else a["xn1"], self.dqkv, a["u_qkv"], gbase)
             guard("down")  # dx (the down group's dy) is rewritten here
             ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M])
+            if on_layer_grads is not None:
+                with torch.cuda.stream(side):  # this layer's dA/dB are the last side-stream work so far
+                    on_layer_grads(gbase, gbase + lay.per_layer)
         main.wait_stream(side)
 
     def _lora_grads(self, gs, x_in, dy, u, g, gbase):

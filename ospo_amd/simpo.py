@@ -64,9 +64,14 @@ def train_step(engine, text_ids, chosen_ids, rejected_ids, cfg: SimPOConfig, buf
     losses, mean, rewards = simpo_forward(logps, B, cfg, buf)
     glogps = simpo_backward(logps, B, cfg, buf)
     engine.zero_grad()
-    engine.backward(glogps)
-    if allreduce is not None:
-        allreduce(engine.grads)
+    if allreduce is not None and hasattr(allreduce, "begin"):
+        allreduce.begin(engine.grads)  # layer buckets all-reduced while the backward runs on
+        engine.backward(glogps, on_layer_grads=allreduce.push)
+        allreduce.finish()
+    else:
+        engine.backward(glogps)
+        if allreduce is not None:
+            allreduce(engine.grads)
     if optimizer:
         engine.optimizer_step(cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay, cfg.max_norm)
     return {"loss": mean, "losses": losses, "logps": logps, "rewards": rewards}

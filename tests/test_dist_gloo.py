@@ -35,6 +35,14 @@ def _worker(rank, world, port, q):
         odist.GradAllReduce(world, bucket_elems=128)(flat)
         exp = torch.arange(1000, dtype=torch.float32) * (1 + 2) / 2
         ok1 = torch.allclose(flat, exp)
+        # (1b) the overlapped form: ranges pushed in reverse-layer order, merged into buckets
+        ar = odist.GradAllReduce(world, bucket_elems=300)
+        flat2 = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+        ar.begin(flat2)
+        for lo in range(900, -1, -100):  # ten "layers" of 100, last layer first
+            ar.push(lo, lo + 100)
+        ar.finish()
+        ok1 = ok1 and torch.allclose(flat2, exp)
         # (2) DP SimPO grads == union-batch grads
         from tests import fixtures as FX
         from ospo_amd.lora import LoraLayout

@@ -1,0 +1,97 @@
+"""Overlapped data-parallel all-reduce on the GPU path: two ranks (gloo, both on the
+box's single GPU) run the HIP SimPO step on one pair each; the per-layer buckets
+all-reduced while the backward runs (engine.backward(on_layer_grads=...)) must equal
+the post-backward all-reduce and the union-batch gradient of a single engine over
+both pairs, within fp32 reduction-order noise (the LoRA weight-gradient kernels add
+split-K partials with fp32 atomics, so two backward passes are not bitwise equal)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs():
+    from oracle import simpo_ref as O
+    dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=2048,
+                       gen_head_dim=256, lora_r=16, lora_alpha=32)
+    w = O.init_weights(dims, seed=31, dtype=torch.bfloat16, lora_b_std=1e-2)
+    g = torch.Generator().manual_seed(32)
+    text = torch.randint(0, dims.vocab, (2, 6), generator=g, dtype=torch.int32)
+    chosen = torch.randint(0, dims.img_vocab, (2, 64), generator=g, dtype=torch.int32)
+    rejected = torch.randint(0, dims.img_vocab, (2, 64), generator=g, dtype=torch.int32)
+    return dims, w, text, chosen, rejected
+
+
+def _grads(eng, text, chosen, rejected, allreduce=None, overlap=False):
+    from ospo_amd.simpo import SimPOConfig, SimPOLossBuffers, simpo_backward, simpo_forward
+    B = chosen.shape[0]
+    cfg, buf = SimPOConfig(), SimPOLossBuffers(B, "cuda")
+    logps = eng.forward(text.cuda(), chosen.cuda(), rejected.cuda())
+    simpo_forward(logps, B, cfg, buf)
+    glogps = simpo_backward(logps, B, cfg, buf)
+    eng.zero_grad()
+    if overlap:
+        allreduce.begin(eng.grads)
+        eng.backward(glogps, on_layer_grads=allreduce.push)
+        allreduce.finish()
+    else:
+        eng.backward(glogps)
+        if allreduce is not None:
+            allreduce(eng.grads)
+    torch.cuda.synchronize()
+    return eng.grads.detach().cpu().clone()
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    from ospo_amd import dist as odist
+    from ospo_amd.engine import ModelDims, SimPOEngine
+    odist.init(backend="gloo")
+    try:
+        dims, w, text, chosen, rejected = _inputs()
+        eng = SimPOEngine(ModelDims.from_any(dims), w, device="cuda", max_pairs=1, max_text_len=6, n_img_tokens=64)
+        sl = slice(rank, rank + 1)
+        ar = odist.GradAllReduce(world, bucket_elems=20000)  # several buckets per step
+        g_over = _grads(eng, text[sl], chosen[sl], rejected[sl], ar, overlap=True)
+        g_post = _grads(eng, text[sl], chosen[sl], rejected[sl], ar, overlap=False)
+        q.put((rank, g_over, g_post))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_allreduce_equals_post_backward_and_union_batch():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
+    for _, g_over, g_post in res:
+        assert rel(g_over, g_post) < 1e-5
+    assert torch.equal(res[0][1], res[1][1])  # one all-reduce result, identical on every rank
+    from ospo_amd.engine import ModelDims, SimPOEngine
+    dims, w, text, chosen, rejected = _inputs()
+    eng = SimPOEngine(ModelDims.from_any(dims), w, device="cuda", max_pairs=2, max_text_len=6, n_img_tokens=64)
+    g_union = _grads(eng, text, chosen, rejected)
+    err = rel(res[0][1], g_union)
+    assert err < 1e-4, err
