@@ -238,6 +238,26 @@ int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows
                      int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed, float drop_p,
                      void* xd, int ld_xd, hipStream_t stream);
 
+/* ------------------------------------------------------------ MXFP8 variant ---
+ * BASELINE config 5 / SURVEY §8f rank 1: the frozen Linears of the SimPO step
+ * (q|k|v, o, gate|up, down; forward and dX backward -- the products that
+ * ospo_gemm_nt_bf16 / _rope_ / _dropout_ run in bf16, reached from
+ * ospo/wrapper/train.py:352 and PL's backward) with CDNA4 block-scaled fp8
+ * MFMA (OCP MX: e4m3 elements, one E8M0 scale per 32 values along K).
+ * ospo_quant_mx8: X bf16 [M, K] -> Q e4m3 [M, ldq bytes] + S (ospo_mx8_scale_bytes(M, K)
+ * bytes, the tile layout documented in ospo_amd/csrc/mx8.hip).  K % 128 == 0.
+ * ospo_gemm_nt_mx8: C = bf16(alpha * (deq(A8) . deq(B8)^T + A2 . B2^T) + bias) [+ residual],
+ * A8/B8 from ospo_quant_mx8 (lda/ldb in bytes), the LoRA K-extension A2/B2 in bf16
+ * (as ospo_gemm_nt_bf16).  rope_cols > 0: RoPE epilogue (as ospo_gemm_nt_rope_bf16);
+ * drop_p > 0: masked extension (as ospo_gemm_nt_dropout_bf16).  N % 256 == 0. */
+size_t ospo_mx8_scale_bytes(int M, int K);
+int ospo_quant_mx8(const void* X, int ldx, int M, int K, void* Q, int ldq, void* S, hipStream_t stream);
+int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, int ldb, const void* Bsc,
+                     int M, int N, int K, const void* A2, int lda2, const void* B2, int ldb2, int K2,
+                     float alpha, const void* bias, const void* residual, int ldr, void* C, int ldc,
+                     const void* rope_cos, const void* rope_sin, int rope_T, int rope_cols,
+                     unsigned drop_seed, float drop_p, hipStream_t stream);
+
 /* ------------------------------------------------------------ optimizer ---
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip
  * (ospo/utils/train.py:30, gradient_clip_val) + torch AdamW

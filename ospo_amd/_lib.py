@@ -25,6 +25,9 @@ SIGNATURES = {
     "ospo_gemm_nt_dropout_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, U, F, P],
     "ospo_gemm_nt_rope_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, P, I, I, P],
     "ospo_set_gemm_variant": [I],
+    "ospo_mx8_scale_bytes": [I, I],
+    "ospo_quant_mx8": [P, I, I, I, P, I, P, P],
+    "ospo_gemm_nt_mx8": [P, I, P, P, I, P, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P, P, I, I, U, F, P],
     "ospo_gemm_set_workspace": [P, Z],
     "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],
     "ospo_f32_to_bf16": [P, P, L, F, P],
@@ -53,7 +56,7 @@ SIGNATURES = {
     "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],
 }
 
-RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
+RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 

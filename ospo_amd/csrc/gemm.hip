@@ -17,6 +17,7 @@
 //  * The LoRA update x.A^T.B^T*s is one more K segment (A2 = s*u, B2 = packed
 //    block-diagonal lora_B), so the adapter costs Rp/K extra MFMAs, no pass.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -88,6 +89,25 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int r0, int s, int 
   }
 }
 
+// v_mfma_scale_f32_16x16x128_f8f6f4 on e4m3 operands (cbsz = blgp = 0); OPSEL picks the scale
+// byte of each lane's 32-bit scale register and must be an immediate, hence the switch (it folds
+// away under the unrolled callers).
+template <int OA, int OB>
+__device__ __forceinline__ f32x4 mx_mfma_t(const i32x8& a, const i32x8& b, const f32x4& c, uint32_t sa, uint32_t sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, OA, (int)sa, OB, (int)sb);
+}
+__device__ __forceinline__ f32x4 mx_mfma(const i32x8& a, const i32x8& b, const f32x4& c, int oa, uint32_t sa, int ob,
+                                         uint32_t sb) {
+#define MXC(x, y) \
+  case x * 4 + y: return mx_mfma_t<x, y>(a, b, c, sa, sb);
+  switch (oa * 4 + ob) {
+    MXC(0, 0) MXC(0, 1) MXC(0, 2) MXC(0, 3) MXC(1, 0) MXC(1, 1) MXC(1, 2) MXC(1, 3)
+    MXC(2, 0) MXC(2, 1) MXC(2, 2) MXC(2, 3) MXC(3, 0) MXC(3, 1) MXC(3, 2) MXC(3, 3)
+    default: return c;
+  }
+#undef MXC
+}
+
 enum { EPI_BF16 = 0, EPI_F32_ATOMIC = 1 };
 
 struct GemmArgs {
@@ -108,6 +128,10 @@ struct GemmArgs {
   uint32_t drop_seed = 0, drop_thresh = 0;
   float drop_scale = 0.f;  // > 0: on
   int drop_ld = 0;
+  // MXFP8 main operands (gemm_nt_v5_kernel<.., MX = true>): A / B are e4m3 bytes, lda / ldb
+  // in BYTES; sa / sb the E8M0 block scales in ospo_quant_mx8's tile layout (mx8.hip).
+  const uint32_t* sa = nullptr;
+  const uint32_t* sb = nullptr;
 };
 
 // DBG (A/B decomposition only, results invalid): 1 = no global loads after the
@@ -678,12 +702,25 @@ __device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0
 // Data-parallel + split-K tail: workgroups [0, dp) own whole tiles (XCD-remapped);
 // workgroups dp + u (u < tail * split) own K-range u % split of tail tile dp + u / split
 // and write an fp32 partial tile to ws (summed + epilogued by splitk_fixup_kernel).
-template <int DBG = 0, bool DROP = false>
+//
+// MX = true: the main K-tiles are MXFP8 (e4m3 bytes, 128 k per tile = the same 128-B LDS rows
+// as 64 bf16) and run v_mfma_scale_f32_16x16x128_f8f6f4 -- 8 MFMAs per phase at twice the bf16
+// rate per clock.  Its operand layout (measured, tools/mx8_probe.hip): lane l holds row l & 15,
+// bytes 0-15 = k 16g..16g+15 and bytes 16-31 = k 64+16g.., g = l >> 4 -- i.e. exactly the two
+// ds_read_b128 fragments of the bf16 k-substeps s = 0, 1; the scale of lane l is that of
+// (row l & 15, 32-k block l >> 4), byte chosen by OPSEL.  The E8M0 scales of K-tile t stream into
+// LDS with the data: one 4-B LDS-DMA per wave (waves 0-3: A's four 64-row groups, 4-7: B's),
+// issued with B1 of the tile before, so the counted waits cover them.  The LoRA K-extension
+// tiles stay bf16 (16 bf16 MFMAs per phase).
+template <int DBG = 0, bool DROP = false, bool MX = false>
 __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
                                                          int split, float* __restrict__ ws, int GM) {
   constexpr int BM = 256, BN = 256, HALF = 16384, SLOT = 4 * HALF;  // half order in a slot: A0 A1 B0 B1
+  constexpr int SC_SLOT = 2048;                                       // MX: 1 KiB A + 1 KiB B scales
+  constexpr int SC_BASE = 2 * SLOT;
   constexpr int CPITCH = BN * 2 + 16;
-  constexpr int LDS_BYTES = (2 * SLOT > BM * CPITCH) ? 2 * SLOT : BM * CPITCH;
+  constexpr int MAIN_BYTES = 2 * SLOT + (MX ? 2 * SC_SLOT : 0);
+  constexpr int LDS_BYTES = (MAIN_BYTES > BM * CPITCH) ? MAIN_BYTES : BM * CPITCH;
   static_assert(LDS_BYTES <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
@@ -693,7 +730,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   const int wm = wave >> 2, wn = wave & 3;
 
   int m0, n0, tb, tcount, part = -1;
-  const int nt1 = args.K / BK, nt2 = args.K2 / BK, ntot = nt1 + nt2;
+  const int nt1 = MX ? args.K / 128 : args.K / BK, nt2 = args.K2 / BK, ntot = nt1 + nt2;
   {
     const int wg = blockIdx.x;
     if (wg < dp) {
@@ -714,26 +751,53 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   const int Mlast = args.M - 1, Nlast = args.N - 1;
   const int rr8 = lane >> 3, c8 = lane & 7;
 
-  // stage half-tile h (0 A0, 1 A1, 2 B0, 3 B1) of K-tile t: 16 pieces of 8 rows x 128 B, 2 per wave
+  // with dropout the LoRA extension tiles run FIRST so their (masked) sum can be scaled alone
+  auto abs_tile = [&](int tl) {
+    const int q = tb + tl;
+    return DROP ? (q < nt2 ? nt1 + q : q - nt2) : q;
+  };
+  // stage half-tile h (0 A0, 1 A1, 2 B0, 3 B1) of K-tile t: 16 pieces of 8 rows x 128 B, 2 per wave.
+  // A K-tile row is 128 bytes in both formats (64 bf16 or 128 e4m3), so staging is byte-generic.
   auto stage_half = [&](int tl, int h) {  // tl: local K-tile index
     if (DBG == 1 && tl >= 2) return;
     char* dst = smem + (tl & 1) * SLOT + h * HALF;
-    const int q = tb + tl;
-    // with dropout the LoRA extension tiles run FIRST so their (masked) sum can be scaled alone
-    const int t = DROP ? (q < nt2 ? nt1 + q : q - nt2) : q;
+    const int t = abs_tile(tl);
     const bool ext = t >= nt1;
     const bool isA = h < 2;
-    const bf16* base = isA ? (ext ? args.A2 : args.A) : (ext ? args.B2 : args.B);
-    const int ld = isA ? (ext ? args.lda2 : args.lda) : (ext ? args.ldb2 : args.ldb);
-    const int k0 = (ext ? t - nt1 : t) * BK;
     const int row0 = (isA ? m0 : n0) + (h & 1) * 128;
     const int last = isA ? Mlast : Nlast;
+    if constexpr (MX) {
+      const char* base = reinterpret_cast<const char*>(isA ? (ext ? args.A2 : args.A) : (ext ? args.B2 : args.B));
+      const int ldB = (isA ? (ext ? args.lda2 : args.lda) : (ext ? args.ldb2 : args.ldb)) * (ext ? 2 : 1);
+      const int kb = (ext ? t - nt1 : t) * 128;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = wave * 2 + i;
-      const int row = p * 8 + rr8;
-      const int g = min(row0 + row, last);
-      glds16(base + (long)g * ld + k0 + ((c8 ^ (row & 7)) << 3), dst + p * 1024);
+      for (int i = 0; i < 2; ++i) {
+        const int p = wave * 2 + i;
+        const int row = p * 8 + rr8;
+        const int g = min(row0 + row, last);
+        glds16(base + (long)g * ldB + kb + ((c8 ^ (row & 7)) << 4), dst + p * 1024);
+      }
+    } else {
+      const bf16* base = isA ? (ext ? args.A2 : args.A) : (ext ? args.B2 : args.B);
+      const int ld = isA ? (ext ? args.lda2 : args.lda) : (ext ? args.ldb2 : args.ldb);
+      const int k0 = (ext ? t - nt1 : t) * BK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int p = wave * 2 + i;
+        const int row = p * 8 + rr8;
+        const int g = min(row0 + row, last);
+        glds16(base + (long)g * ld + k0 + ((c8 ^ (row & 7)) << 3), dst + p * 1024);
+      }
+    }
+  };
+  // MX: the E8M0 scales of K-tile tl (one 4-B LDS-DMA per wave; extension tiles load a valid, unused tile)
+  auto stage_scales = [&](int tl) {
+    if constexpr (MX) {
+      const int t = min(abs_tile(tl), nt1 - 1);
+      const uint32_t* src = wave < 4 ? args.sa + ((long)(m0 / 64 + wave) * nt1 + t) * 64
+                                     : args.sb + ((long)(n0 / 64 + wave - 4) * nt1 + t) * 64;
+      __builtin_amdgcn_global_load_lds(src + lane, (LDS_AS void*)(smem + SC_BASE + (tl & 1) * SC_SLOT + wave * 256), 4,
+                                       0, 0);
     }
   };
 
@@ -745,9 +809,11 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bfr[2][2];
+  i32x8 a8[4], b8[2];  // MX tiles: both k-halves of a fragment in one 8-register operand
 
   // prologue: tile 0 complete, A0 of tile 1 in flight
   if (nt > 0) {
+    stage_scales(0);
     stage_half(0, 2); stage_half(0, 3); stage_half(0, 1); stage_half(0, 0);
   }
   if (nt > 1) stage_half(1, 0);
@@ -762,22 +828,50 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
 
   const int frow = lane & 15, fcol = lane >> 4;
   // one K-tile = 4 phases; a lambda so the dropout variant can peel its extension tiles
-  auto run_tile = [&](int t) {
+  // mxt: an MXFP8 main tile (compile-time, so each loop below keeps one MFMA form and its
+  // accumulators in place; a per-phase runtime branch made the compiler copy them)
+  auto run_tile = [&](int t, auto mxt) __attribute__((always_inline)) {
     const char* slot = smem + (t & 1) * SLOT;
+    constexpr bool mx_tile = MX && decltype(mxt)::value;
+    uint32_t scA[2] = {0u, 0u}, scB[2] = {0u, 0u};
+    if constexpr (mx_tile) {  // staged with tile t-1's B1 (or in the prologue): landed per the q0 wait + barriers
+      const char* sc = smem + SC_BASE + (t & 1) * SC_SLOT;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        scA[h] = *reinterpret_cast<const uint32_t*>(sc + (h * 2 + wm) * 256 + lane * 4);
+        scB[h] = *reinterpret_cast<const uint32_t*>(sc + 1024 + (h * 2 + (wn >> 1)) * 256 + lane * 4) >>
+                 (16 * (wn & 1));
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int ia = (j >= 2) ? 1 : 0;
       const int ib = (j == 1 || j == 2) ? 1 : 0;
       // ---- R: fragments that change this phase, then one half-tile of staging
-      if (j == 0 || j == 2) {
-        const char* la = slot + ia * HALF;
+      if constexpr (mx_tile) {
+        if (j == 0 || j == 2) {
+          const char* la = slot + ia * HALF;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i) {
+            a8[i].lo = *reinterpret_cast<const i32x4*>(la + mmaj_off(wm * 64 + i * 16 + frow, fcol));
+            a8[i].hi = *reinterpret_cast<const i32x4*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 + fcol));
+          }
+        }
+        const char* lb = slot + (2 + ib) * HALF;
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
-            af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
-      }
-      {
+        for (int n = 0; n < 2; ++n) {
+          b8[n].lo = *reinterpret_cast<const i32x4*>(lb + mmaj_off(wn * 32 + n * 16 + frow, fcol));
+          b8[n].hi = *reinterpret_cast<const i32x4*>(lb + mmaj_off(wn * 32 + n * 16 + frow, 4 + fcol));
+        }
+      } else {
+        if (j == 0 || j == 2) {
+          const char* la = slot + ia * HALF;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
+        }
         const char* lb = slot + (2 + ib) * HALF;
 #pragma unroll
         for (int n = 0; n < 2; ++n)
@@ -786,16 +880,17 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
             bfr[n][s] = *reinterpret_cast<const bf16x8*>(lb + mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
       }
       if (DBG != 1) {
+        if (j == 0 && t + 1 < nt) stage_scales(t + 1);
         if (j == 0 && t + 1 < nt) stage_half(t + 1, 3);
         if (j == 1 && t + 1 < nt) stage_half(t + 1, 2);
         if (j == 2 && t + 1 < nt) stage_half(t + 1, 1);
         if (j == 3 && t + 2 < nt) stage_half(t + 2, 0);
       }
       // counted DMA waits before the barrier that precedes the first reader:
-      // into q2 of this tile: A1(t) (6 later glds when tile t+1 is staged);
+      // into q2 of this tile: A1(t) (6 later glds when tile t+1 is staged, +1 scale DMA with MX);
       // into q0 of tile t+1: A0(t+1), B0(t+1) (A1(t+1) + A0(t+2) later)
       const bool wq2 = (j == 1), wq0 = (j == 3) && (t + 1 < nt);
-      const int nq2 = (t + 1 < nt) ? 6 : 0;
+      const int nq2 = (t + 1 < nt) ? (MX ? 7 : 6) : 0;
       const int nq0 = (t + 2 < nt) ? 4 : 2;
       if (g1) {
         if (wq2) wait_vmcnt_exact(nq2);
@@ -806,7 +901,21 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       // ---- M: one C-quadrant x K = 64
-      if (DBG != 2) {
+      if constexpr (DBG != 2 && mx_tile) {
+        // one scaled MFMA per (i, n) over the whole 128-k tile; first operand B (SWAP layout)
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) acc[j][i][n] = mx_mfma(b8[n], a8[i], acc[j][i][n], n, scB[ib], i, scA[ia]);
+        // pin the cluster inside its phase: the scaled-MFMA builtin is not convergent, so without a
+        // use here the compiler sinks it past the barriers (merging phases, spilling)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[j][i][n]));
+        __builtin_amdgcn_s_setprio(0);
+      } else if (DBG != 2) {
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -832,8 +941,10 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   };
   // with dropout the LoRA extension tiles come first (stage_half's order); their masked sum is
   // scaled once between the two loops, outside the hot loop's register allocation
+  using MXT = std::integral_constant<bool, true>;
+  using BFT = std::integral_constant<bool, false>;
   const int pre = (DROP && tb == 0) ? (nt2 < nt ? nt2 : nt) : 0;
-  for (int t = 0; t < pre; ++t) run_tile(t);
+  for (int t = 0; t < pre; ++t) run_tile(t, BFT{});
   if (pre > 0) {
     if constexpr (DROP) {
       {  // accumulators hold exactly A2.B2^T: apply the dropout mask
@@ -858,7 +969,13 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       }
     }
   }
-  for (int t = pre; t < nt; ++t) run_tile(t);
+  if constexpr (MX) {  // main (fp8) tiles, then any bf16 extension tiles of this K-range
+    const int main_end = DROP ? nt : min(nt, max(pre, nt1 - tb));
+    for (int t = pre; t < main_end; ++t) run_tile(t, MXT{});
+    for (int t = main_end; t < nt; ++t) run_tile(t, BFT{});
+  } else {
+    for (int t = pre; t < nt; ++t) run_tile(t, BFT{});
+  }
   if (!g1) {  // re-align the barrier count
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1001,18 +1118,20 @@ int num_cus() {
   return g_num_cus;
 }
 
-template <int DBG = 0, bool DROP = false>
+template <int DBG = 0, bool DROP = false, bool MX = false>
 int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
   const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
-  const int ntot = a.K / BK + a.K2 / BK;
+  const int ntot = (MX ? a.K / 128 : a.K / BK) + a.K2 / BK;
   const int cus = num_cus();
   int dp = tiles, split = 1, tail = 0;
   if (allow_split && a.rope_cols == 0 && tiles > cus) {
     tail = tiles % cus;
     split = tail ? std::min(cus / tail, std::min(8, ntot / 4)) : 1;
     const size_t need = (size_t)tail * split * 65536 * sizeof(float);
-    if (tail && split >= 2 && ntot >= 16 && g_splitk_ws && need <= g_splitk_ws_bytes) {
+    // (with dropout every extension tile must sit in K-range 0, which applies the mask)
+    const bool drop_ok = !DROP || (long)(a.K2 / BK) * split <= ntot;
+    if (tail && split >= 2 && ntot >= 16 && drop_ok && g_splitk_ws && need <= g_splitk_ws_bytes) {
       dp = tiles - tail;
     } else {
       split = 1;
@@ -1020,8 +1139,8 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
     }
   }
   const int grid = dp + tail * split;
-  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split, g_splitk_ws,
-                     g_v5_gm);
+  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP, MX>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split,
+                     g_splitk_ws, g_v5_gm);
   OSPO_CHECK_LAUNCH();
   if (tail) {
     hipLaunchKernelGGL(splitk_fixup_kernel, dim3(tail * 32), dim3(256), 0, s, a, tm, tn, dp, split,
@@ -1126,6 +1245,48 @@ extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, 
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = N;
   return launch_v5<0, true>(a, stream);
+}
+
+extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, int ldb, const void* Bsc,
+                                int M, int N, int K, const void* A2, int lda2, const void* B2, int ldb2, int K2,
+                                float alpha, const void* bias, const void* residual, int ldr, void* C, int ldc,
+                                const void* rope_cos, const void* rope_sin, int rope_T, int rope_cols,
+                                unsigned drop_seed, float drop_p, hipStream_t stream) {
+  if (!A8 || !Asc || !B8 || !Bsc || !C) return OSPO_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || K % 128 || K2 < 0 || K2 % BK) return OSPO_ERR_SHAPE;
+  if (N % 256) return OSPO_ERR_UNSUPPORTED;
+  if (K2 > 0 && (!A2 || !B2)) return OSPO_ERR_ARG;
+  if (lda < K || ldb < K || ldc < N || (lda % 16) || (ldb % 16) || (ldc % 8)) return OSPO_ERR_SHAPE;
+  if (K2 > 0 && (lda2 < K2 || ldb2 < K2 || lda2 % 8 || ldb2 % 8)) return OSPO_ERR_SHAPE;
+  if (residual && (ldr < N || ldr % 8)) return OSPO_ERR_SHAPE;
+  if (!aligned16(A8) || !aligned16(B8) || !aligned16(C) || !aligned16(Asc) || !aligned16(Bsc) ||
+      (residual && !aligned16(residual)) || (K2 > 0 && (!aligned16(A2) || !aligned16(B2))))
+    return OSPO_ERR_ALIGN;
+  const bool rope = rope_cols > 0, drop = drop_p > 0.f;
+  if (drop_p < 0.f || drop_p >= 1.f) return OSPO_ERR_ARG;
+  if (rope && (!rope_cos || !rope_sin || rope_T <= 0 || rope_cols % 128 || rope_cols > N || bias || residual ||
+               alpha != 1.f || drop))
+    return OSPO_ERR_ARG;
+  if (drop && (K2 <= 0 || bias || residual || alpha != 1.f || (long)M * N > 0xFFFFFFFFL)) return OSPO_ERR_ARG;
+  GemmArgs a{(const bf16*)A8, (const bf16*)B8, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
+             M, N, K, K2, alpha, (const bf16*)bias, (const bf16*)residual, ldr, C, ldc, 1, 0, 0};
+  a.sa = (const uint32_t*)Asc;
+  a.sb = (const uint32_t*)Bsc;
+  if (rope) {
+    a.rope_cs = (const bf16*)rope_cos;
+    a.rope_sn = (const bf16*)rope_sin;
+    a.rope_T = rope_T;
+    a.rope_cols = rope_cols;
+    return launch_v5<0, false, true>(a, stream, false);
+  }
+  if (drop) {
+    a.drop_seed = drop_seed;
+    a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
+    a.drop_scale = 1.f / (1.f - drop_p);
+    a.drop_ld = N;
+    return launch_v5<0, true, true>(a, stream);
+  }
+  return launch_v5<0, false, true>(a, stream);
 }
 
 extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {

@@ -134,6 +134,69 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
     return out
 
 
+# ------------------------------------------------------------ MXFP8 (config 5)
+class MX8:
+    """An MXFP8 operand on the device: e4m3 bytes q [rows, K] + E8M0 scales in the GEMM's tile
+    layout (include/ospo_hip.h ospo_quant_mx8).  Preallocate once and refill with quant_mx8."""
+
+    def __init__(self, rows: int, K: int, device):
+        if K % 128:
+            raise ValueError("MX8: K must be a multiple of 128")
+        self.rows, self.K = rows, K
+        self.q = torch.empty(rows, K, dtype=torch.uint8, device=device)
+        nbytes = query("ospo_mx8_scale_bytes", rows, K)
+        self.s = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        self.m = 0  # rows filled by the last quant_mx8
+
+    @classmethod
+    def of(cls, x: torch.Tensor) -> "MX8":
+        t = cls(x.shape[0], x.shape[1], x.device)
+        return quant_mx8(x, t)
+
+
+def quant_mx8(x: torch.Tensor, out: MX8) -> MX8:
+    """out <- MXFP8(x), x bf16 [M, K] (M <= out.rows)."""
+    _chk(x, BF16, "x")
+    M, K = x.shape
+    if K != out.K or M > out.rows:
+        raise ValueError(f"quant_mx8: x{tuple(x.shape)} does not fit MX8[{out.rows}, {out.K}]")
+    call("ospo_quant_mx8", _p(x), _ld(x), M, K, _p(out.q), out.q.stride(0), _p(out.s), _s())
+    out.m = M
+    return out
+
+
+def gemm_nt_mx8(a: MX8, b: MX8, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0, bias=None,
+                residual=None, rope=None, dropout=None) -> torch.Tensor:
+    """out[M, N] = bf16(alpha*(deq(a).deq(b)^T + a2.b2^T) + bias) [+ residual] on block-scaled fp8 MFMA;
+    M = a.m rows (the last quant_mx8), b = the weight [N, K].  rope / dropout as gemm_nt."""
+    _chk(out, BF16, "out")
+    M, N, K = a.m, b.m, a.K
+    if b.K != K or out.shape[0] != M or out.shape[1] != N:
+        raise ValueError(f"gemm_nt_mx8 shape mismatch a[{M},{K}] b[{N},{b.K}] out{tuple(out.shape)}")
+    K2 = 0
+    if a2 is not None:
+        K2 = a2.shape[1]
+        if a2.shape[0] != M or b2.shape != (N, K2):
+            raise ValueError("gemm_nt_mx8 K-extension shape mismatch")
+    if not _GEMM_WS:
+        gemm_workspace(out.device)
+    cos = sin = None
+    T = ncols = 0
+    if rope is not None:
+        cos, sin, T, ncols = rope
+    seed, p = (0, 0.0) if dropout is None else (int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]))
+    st = torch.cuda.current_stream()
+    e0 = _TIMER.start(st) if _TIMER is not None else None
+    call("ospo_gemm_nt_mx8", _p(a.q), a.q.stride(0), _p(a.s), _p(b.q), b.q.stride(0), _p(b.s), M, N, K,
+         _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2, float(alpha),
+         _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out),
+         _p(cos), _p(sin), int(T), int(ncols), seed, p, st.cuda_stream)
+    if e0 is not None:
+        nbytes = 1.0 * (M * K + N * K) + 2.0 * (M * N + (M * N if residual is not None else 0))
+        _TIMER.add("gemm_nt_mx8_256x256", 2.0 * M * N * K, e0, st, nbytes)
+    return out
+
+
 def gemm_f32acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a_kmajor: bool, b_kmajor: bool,
                 k_splits: int = 1, alpha: float = 1.0, diag: Optional[tuple] = None) -> torch.Tensor:
     """out[M,N] (fp32) += alpha * op(a) . op(b)^T.

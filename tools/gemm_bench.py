@@ -16,7 +16,8 @@ SHAPES = [  # name, M, N, K, K2
     ("down_fwd", M, 4096, 11008, 64), ("down_dx", M, 11008, 4096, 64), ("gu_dx", M, 4096, 22016, 64),
     ("qkv_dx", M, 4096, 12288, 64), ("gh2_fwd", 4608, 16384, 4096, 0), ("gh2_dx", 4608, 4096, 16384, 0),
 ]
-VARIANTS = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1").split(",") if v != ""]
+MX8 = os.environ.get("GB_MX8", "0") == "1"  # also time the block-scaled fp8 GEMM (+ its A quantization)
 ROUNDS, ITERS = 5, 10
 
 
@@ -42,7 +43,13 @@ def main():
         ref = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
         res = {f"v{v}": [] for v in VARIANTS}
         res["hipblaslt"] = []
+        if MX8:
+            a8, b8 = ops.MX8.of(a), ops.MX8.of(b)
+            res["mx8"], res["mx8_quantA"] = [], []
         for _ in range(ROUNDS):
+            if MX8:
+                res["mx8"].append(timeit(lambda: ops.gemm_nt_mx8(a8, b8, out, a2=a2, b2=b2)))
+                res["mx8_quantA"].append(timeit(lambda: ops.quant_mx8(a, a8)))
             for v in VARIANTS:
                 call("ospo_set_gemm_variant", v)
                 res[f"v{v}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
@@ -61,6 +68,8 @@ def main():
         for kk, ts in res.items():
             t = sorted(ts)[len(ts) // 2]
             line[kk] = {"ms": round(t, 4), "tflops": round(fl / t / 1e9, 1)}
+            if kk == "mx8_quantA":
+                line[kk] = {"ms": round(t, 4), "GBps": round(3.0 * m * k / t / 1e6, 1)}
         print(json.dumps(line), flush=True)
 
 
