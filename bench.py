@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_FP8_TFLOPS = 5000.0   # MI355X dense fp8 (MX-scaled e4m3) MFMA, same table
 METRIC = "preference-pairs/sec (whole node), Janus-Pro-7B SimPO @576 img tokens, 1/2/4/8 GPU"
 
 
@@ -91,6 +92,8 @@ def main():
     ap.add_argument("--lora-r", type=int, default=16)
     # dropout 0 for parity runs, configs/peft/lora.yaml's 0.05 for throughput
     ap.add_argument("--lora-dropout", type=float, default=0.05)
+    # BASELINE config 5: the frozen decoder Linears on MXFP8 block-scaled fp8 MFMA (use with --lora-r 32)
+    ap.add_argument("--linear-dtype", choices=("bf16", "mx8"), default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
     args = ap.parse_args()
@@ -107,7 +110,7 @@ def main():
     B, Lt, N = args.pairs_per_gpu, args.text_len, args.img_tokens
     weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)  # identical on every rank (same seeds)
     eng = SimPOEngine(dims, weights, device=dev, max_pairs=B, max_text_len=Lt, n_img_tokens=N,
-                      lora_dropout=args.lora_dropout, dropout_seed=42)
+                      lora_dropout=args.lora_dropout, dropout_seed=42, linear_dtype=args.linear_dtype)
     del weights
     torch.cuda.empty_cache()
     cfg = SimPOConfig()
@@ -155,22 +158,25 @@ def main():
         pmc = os.path.join(ROOT, "profiles", "gemm_pmc.json")
         if os.path.exists(pmc):
             traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
-        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+        mx = dom.startswith("gemm_nt_mx8")
+        peak = PEAK_FP8_TFLOPS if mx else PEAK_BF16_TFLOPS
+        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_note": "HBM+Infinity-Cache bytes per launch (2*FETCH_SIZE+WRITE_SIZE, profiles/gemm_pmc.json)",
                 "algorithmic_bytes_per_launch": round(d["bytes"] / d["count"]),
-                "kernel": f"{dom} (gemm_nt_v5_kernel 8-phase MFMA bf16 + split-K fixup)", "launches": d["count"],
+                "kernel": f"{dom} (gemm_nt_v5_kernel 8-phase MFMA {'MXFP8 e4m3' if mx else 'bf16'} + split-K fixup)",
+                "launches": d["count"],
                 "avg_launch_us": round(d["ms"] * 1e3 / d["count"], 2),
                 "step_mfma_frac": round(flops_pair * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)}
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16",
+        "vs_baseline": None, "dtype": "bf16" if args.linear_dtype == "bf16" else "mxfp8-e4m3 linears, bf16 rest",
         "data": "synthetic (random-init Janus-Pro-7B-shaped weights, random prompt/VQ token ids)",
         "config": {"workload": f"Janus-Pro-{'7B' if dims.n_layers == 30 else str(dims.n_layers) + 'L'} SimPO "
                                f"train step, LoRA r={dims.lora_r} dropout {args.lora_dropout}, {N} image tokens, "
-                               f"{B} pairs/GPU",
-                   "lora_dropout": args.lora_dropout,
+                               f"{B} pairs/GPU" + (", MXFP8 decoder Linears (config 5)" if args.linear_dtype == "mx8" else ""),
+                   "lora_dropout": args.lora_dropout, "linear_dtype": args.linear_dtype,
                    "global_batch": global_batch, "seq_len": T, "parallelism": f"dp{world}",
                    "algorithmic_tflop_per_pair": round(flops_pair / 1e12, 3)},
         "roofline": roof,

@@ -175,11 +175,16 @@ def apply_rope(x, cos, sin):
     return x * cos + rotate_half(x) * sin
 
 
-def lora_linear(x, W, A, B, scale, dropout_p: float = 0.0, training: bool = True, mask=None):
+def lora_linear(x, W, A, B, scale, dropout_p: float = 0.0, training: bool = True, mask=None, mx8: bool = False):
     """peft 0.7.1 lora.Linear.forward: base(x) + lora_B(lora_A(dropout(x))) * scaling.
     ``mask`` (bool, x's shape): an explicit keep mask (kept -> x / (1 - p) in x's dtype), so the
-    HIP path's counter-based masks can be replayed; without it torch's F.dropout draws one."""
-    y = F.linear(x, W)
+    HIP path's counter-based masks can be replayed; without it torch's F.dropout draws one.
+    ``mx8``: the frozen base product in MXFP8 (BASELINE config 5, oracle/mx8_ref.py)."""
+    if mx8:
+        from oracle.mx8_ref import mx8_linear
+        y = mx8_linear(x, W)
+    else:
+        y = F.linear(x, W)
     if A is None:
         return y
     if dropout_p > 0 and training and mask is not None:
@@ -203,7 +208,7 @@ _GROUP = {"q_proj": "qkv", "k_proj": "qkv", "v_proj": "qkv", "o_proj": "o", "gat
           "down_proj": "down"}
 
 
-def decoder_layer(x, w, i, dims: JanusDims, cos, sin, lora: bool = True, training=True, masks=None):
+def decoder_layer(x, w, i, dims: JanusDims, cos, sin, lora: bool = True, training=True, masks=None, mx8=False):
     S, T, D = x.shape
     H, hd = dims.n_heads, dims.head_dim
     s = dims.lora_scale
@@ -215,7 +220,7 @@ def decoder_layer(x, w, i, dims: JanusDims, cos, sin, lora: bool = True, trainin
         mk = masks.get((i, _GROUP[p])) if masks else None
         if mk is not None:
             mk = mk.reshape(h.shape)
-        return lora_linear(h, w[pfx + p], A, B, s, dims.lora_dropout, training, mk)
+        return lora_linear(h, w[pfx + p], A, B, s, dims.lora_dropout, training, mk, mx8)
 
     res = x
     h = rmsnorm(x, w[pfx + "input_layernorm"], dims.rms_eps)
@@ -231,14 +236,14 @@ def decoder_layer(x, w, i, dims: JanusDims, cos, sin, lora: bool = True, trainin
     return res + m
 
 
-def llama_hidden(inputs_embeds, w, dims: JanusDims, lora=True, training=True, masks=None):
+def llama_hidden(inputs_embeds, w, dims: JanusDims, lora=True, training=True, masks=None, mx8=False):
     """LlamaModel forward over inputs_embeds -> final-normed hidden state
     (== ``outputs.hidden_states[-1]`` at train.py:356).  masks: {(layer, group): keep mask}."""
     T = inputs_embeds.shape[1]
     cos, sin = rope_cos_sin(T, dims.head_dim, dims.rope_theta, inputs_embeds.dtype)
     x = inputs_embeds
     for i in range(dims.n_layers):
-        x = decoder_layer(x, w, i, dims, cos, sin, lora, training, masks)
+        x = decoder_layer(x, w, i, dims, cos, sin, lora, training, masks, mx8)
     return rmsnorm(x, w["norm"], dims.rms_eps)
 
 
@@ -329,7 +334,7 @@ class StepOut:
 
 def simpo_step(text_tokens, chosen_ids, rejected_ids, w, dims: JanusDims, dtype=torch.bfloat16,
                beta=10.0, gamma_beta_ratio=0.5, label_smoothing=0.0, loss_type="sigmoid",
-               backward: bool = True, training: bool = True, dropout_masks=None) -> StepOut:
+               backward: bool = True, training: bool = True, dropout_masks=None, mx8: bool = False) -> StepOut:
     """One SimPO step: preprocess -> concatenated forward -> logps -> loss
     (train.py:399-445) -> backward to the LoRA tensors (autograd)."""
     w = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in w.items()}
@@ -343,7 +348,7 @@ def simpo_step(text_tokens, chosen_ids, rejected_ids, w, dims: JanusDims, dtype=
     B = chosen_ids.shape[0]
     with torch.set_grad_enabled(backward):
         h = llama_hidden(cb["concatenated_inputs_embeds"], w, dims, lora=True, training=training,
-                         masks=dropout_masks)
+                         masks=dropout_masks, mx8=mx8)
         logits = gen_head(h, w)
         logps = get_batch_logps(logits, cb["concatenated_labels"])
         c, r = logps[:B], logps[B:]

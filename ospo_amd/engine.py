@@ -76,9 +76,14 @@ class SimPOEngine:
 
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_pairs: int = 4,
                  max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
-                 dropout_seed: int = 42):
+                 dropout_seed: int = 42, linear_dtype: str = "bf16"):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
+        if linear_dtype not in ("bf16", "mx8"):
+            raise ValueError(f"linear_dtype must be 'bf16' or 'mx8', got {linear_dtype!r}")
+        # "mx8": the frozen decoder Linears (q|k|v, o, gate|up, down; forward and dX) run as MXFP8
+        # block-scaled fp8 MFMA GEMMs (BASELINE config 5; oracle/mx8_ref.py defines the arithmetic)
+        self.linear_dtype = linear_dtype
         # peft lora_dropout on the adapter inputs (ospo_amd/dropout.py: counter-based masks, one per input)
         self.lora_dropout = float(lora_dropout)
         self.training = True
@@ -108,6 +113,9 @@ class SimPOEngine:
             }
             for k in ("qkv", "o", "gu", "down"):
                 lay[k + "T"] = lay[k].t().contiguous()
+                if linear_dtype == "mx8":  # fp8 copies replace the bf16 ones (quantized once: frozen)
+                    lay[k] = ops.MX8.of(lay[k])
+                    lay[k + "T"] = ops.MX8.of(lay[k + "T"])
             self.layers.append(lay)
         self.norm = _dev(w["norm"], dev)
         self.gh_w1, self.gh_b1 = _dev(w["gen_head.w1"], dev), _dev(w["gen_head.b1"], dev)
@@ -200,6 +208,8 @@ class SimPOEngine:
         self.delta_ws = z(S * H * Tm, dt=F32)
         self.dz = z(R, Dg)
         self.dhsel = z(R, D)
+        # MXFP8 activation operands, one per contraction size (main-stream GEMMs only, reused in order)
+        self._mx = {K: ops.MX8(Mc, K, dev) for K in {D, Fd, 2 * Fd, 3 * D}} if self.linear_dtype == "mx8" else {}
 
     def pack_lora(self):
         """Rebuild the packed A / A^T / block-diagonal B / B^T operands from the flat params
@@ -213,6 +223,14 @@ class SimPOEngine:
             B = self.lora[g.b_off:]
             ops.lora_pack(A, B, g.nmods, r, g.Kin, g.Nmod, g.Rp, Acat, AcatT, Bcat, BT, n_layers=L,
                           layer_stride=self.layout.per_layer)
+
+    def _lin(self, x: torch.Tensor, w, out: torch.Tensor, **kw) -> torch.Tensor:
+        """A frozen decoder Linear (+ LoRA K-extension / bias / residual / RoPE / dropout epilogues):
+        the bf16 MFMA GEMM, or in mx8 mode: quantize x (MXFP8, one pass) + the block-scaled fp8 GEMM."""
+        if self.linear_dtype == "mx8":
+            a = ops.quant_mx8(x, self._mx[x.shape[1]])
+            return ops.gemm_nt_mx8(a, w, out, **kw)
+        return ops.gemm_nt(x, w, out, **kw)
 
     def lora_tensors(self) -> Dict[str, torch.Tensor]:
         return self.layout.from_flat(self.lora)
@@ -319,24 +337,24 @@ class SimPOEngine:
             Acat, _, Bcat, _ = pk["qkv"]
             self._lora_down(a["xn1"], Acat, a["u_qkv"], M, lay.groups["qkv"].nmods, self._drop(i, "qkv"), a.get("xd_qkv"))
             if (3 * D) % 256 == 0:  # q|k RoPE fused into the projection's epilogue
-                ops.gemm_nt(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat,
-                            rope=(self.cos, self.sin, T, 2 * D))
+                self._lin(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat,
+                          rope=(self.cos, self.sin, T, 2 * D))
             else:
-                ops.gemm_nt(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat)
+                self._lin(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat)
                 ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
             ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn)
             Acat, _, Bcat, _ = pk["o"]
             self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods, self._drop(i, "o"), a.get("xd_o"))
-            ops.gemm_nt(a["attn"][:M], lw["o"], a["xmid"][:M], a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
+            self._lin(a["attn"][:M], lw["o"], a["xmid"][:M], a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
             ops.rmsnorm_fwd(a["xmid"][:M], lw["ln_post"], a["xn2"][:M], a["rstd2"][:M], dims.rms_eps)
             Acat, _, Bcat, _ = pk["gu"]
             self._lora_down(a["xn2"], Acat, a["u_gu"], M, lay.groups["gu"].nmods, self._drop(i, "gu"), a.get("xd_gu"))
-            ops.gemm_nt(a["xn2"][:M], lw["gu"], a["gu"][:M], a2=a["u_gu"][:M], b2=Bcat)
+            self._lin(a["xn2"][:M], lw["gu"], a["gu"][:M], a2=a["u_gu"][:M], b2=Bcat)
             ops.swiglu_fwd(a["gu"][:M], a["h"][:M])
             Acat, _, Bcat, _ = pk["down"]
             self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods, self._drop(i, "down"), a.get("xd_d"))
             xn = self.acts[i + 1]["x"] if i + 1 < dims.n_layers else self.x_final
-            ops.gemm_nt(a["h"][:M], lw["down"], xn[:M], a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
+            self._lin(a["h"][:M], lw["down"], xn[:M], a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
         ops.rmsnorm_fwd(self.x_final[:M], self.norm, self.hf[:M], self.rstd_f[:M], dims.rms_eps)
         # gen_head on the N positions that predict image tokens: t = Lt-1 .. T-2 (train.py:385-391)
         ops.gather_rows(self.hf, S, T, Lt - 1, N, self.hsel[:R])
@@ -401,7 +419,7 @@ class SimPOEngine:
             guard("down")
             gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M)
             dr = self._drop(i, "down")
-            ops.gemm_nt(dx[:M], lw["downT"], self.dh[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(dx[:M], lw["downT"], self.dh[:M], a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("down", gs, a["xd_d"] if dr else a["h"], dx, a["u_d"], gbase)
             guard("gu")  # dgu is rewritten here
             ops.swiglu_bwd(self.dh[:M], a["gu"][:M], self.dgu[:M])
@@ -409,7 +427,7 @@ class SimPOEngine:
             Acat, AcatT, Bcat, BT = pk["gu"]
             gs = self._lora_g(self.dgu, lay.groups["gu"], Bcat, BT, M)
             dr = self._drop(i, "gu")
-            ops.gemm_nt(self.dgu[:M], lw["guT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(self.dgu[:M], lw["guT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("gu", gs, a["xd_gu"] if dr else a["xn2"], self.dgu, a["u_gu"], gbase)
             guard("o")  # dxmid is rewritten here
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], self.dxmid[:M],
@@ -418,7 +436,7 @@ class SimPOEngine:
             Acat, AcatT, Bcat, BT = pk["o"]
             gs = self._lora_g(self.dxmid, lay.groups["o"], Bcat, BT, M)
             dr = self._drop(i, "o")
-            ops.gemm_nt(self.dxmid[:M], lw["oT"], self.dattn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(self.dxmid[:M], lw["oT"], self.dattn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("o", gs, a["xd_o"] if dr else a["attn"], self.dxmid, a["u_o"], gbase)
             # ---- attention + RoPE
             guard("qkv")  # dqkv is rewritten here
@@ -428,7 +446,7 @@ class SimPOEngine:
             Acat, AcatT, Bcat, BT = pk["qkv"]
             gs = self._lora_g(self.dqkv, lay.groups["qkv"], Bcat, BT, M)
             dr = self._drop(i, "qkv")
-            ops.gemm_nt(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("qkv", gs, a["xd_qkv"] if dr else a["xn1"], self.dqkv, a["u_qkv"], gbase)
             guard("down")  # dx (the down group's dy) is rewritten here
             ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M])

@@ -217,3 +217,57 @@ def test_step_lora_dropout_vs_oracle_with_replayed_masks():
     plain = O.simpo_step(text, chosen, rejected, w, O.JanusDims(**{**dims.__dict__, "lora_dropout": 0.0}),
                          dtype=torch.bfloat16)
     assert max(rel(grads[k], plain.lora_grads[k]) for k in plain.lora_grads) > 0.05
+
+
+def _mx8_case(dims, seed, B, Lt, N):
+    w = O.init_weights(dims, seed=seed, dtype=torch.bfloat16, lora_b_std=1e-2)
+    g = torch.Generator().manual_seed(seed + 1)
+    text = [torch.randint(0, dims.vocab, (1, Lt - i), generator=g, dtype=torch.int32) for i in range(B)]
+    chosen = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    rejected = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    algo = {"beta": 10.0, "gamma_beta_ratio": 0.5, "label_smoothing": 0.0, "loss_type": "sigmoid"}
+    from ospo_amd.engine import ModelDims, SimPOEngine
+    eng = SimPOEngine(ModelDims.from_any(dims), w, device="cuda", max_pairs=B, max_text_len=Lt, n_img_tokens=N,
+                      linear_dtype="mx8")
+    logps, loss, grads = run_hip_step(eng, text, chosen, rejected, algo)
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    ora = O.simpo_step(text, chosen, rejected, w, dims, dtype=torch.bfloat16, mx8=True)
+    bf = O.simpo_step(text, chosen, rejected, w, dims, dtype=torch.bfloat16, backward=False)
+    e = max(rel(logps[:B], ora.chosen_logps), rel(logps[B:], ora.rejected_logps))
+    e_bf = max(rel(logps[:B], bf.chosen_logps), rel(logps[B:], bf.rejected_logps))
+    el = abs(loss - float(ora.loss)) / float(ora.loss)
+    ge = {k: rel(grads[k], ora.lora_grads[k]) for k in ora.lora_grads}
+    # the noise floor of fp8 gradients: the oracle's own bf16 and fp32 runs of the same fp8 step differ
+    # because bf16-level differences in a quantizer's input flip ~1/16 of the fp8 roundings they touch
+    o32 = O.simpo_step(text, chosen, rejected, w, dims, dtype=torch.float32, mx8=True)
+    floor = {k: rel(o32.lora_grads[k], ora.lora_grads[k]) for k in ora.lora_grads}
+    ratio = {k: ge[k] / max(floor[k], 5e-2) for k in ge}
+    print(f"\nmx8 D{dims.d_model}: logp rel err vs mx8 oracle {e:.2e} (vs bf16 oracle {e_bf:.2e}); "
+          f"loss {loss:.6f} vs {float(ora.loss):.6f} ({el:.2e}); max grad rel err {max(ge.values()):.2e}, "
+          f"oracle bf16-vs-fp32 grad floor {max(floor.values()):.2e}, max err/max(floor, 5e-2) {max(ratio.values()):.2f}")
+    return logps, loss, e, el, ratio, ora, B
+
+
+def test_step_mx8_small_vs_oracle():
+    """BASELINE config 5 arithmetic (MXFP8 frozen Linears, bf16 LoRA) against the oracle's
+    fp8 mode (oracle/mx8_ref.py: same quantizer, fp32 products of the dequantized operands).
+    The two paths quantize bf16 activations that differ by bf16 rounding noise, so an
+    occasional block lands on a different fp8 code; log-probs are held to 1e-3 relative as in
+    bf16, the loss to 3e-3, and each LoRA grad to 1.5x the larger of 5e-2 and the fp8 noise floor
+    (the oracle's own bf16-vs-fp32 difference on the same fp8 step)."""
+    dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=2048,
+                       gen_head_dim=256, lora_r=16, lora_alpha=32)
+    logps, loss, e, el, ratio, ora, B = _mx8_case(dims, 31, 3, 10, 64)
+    assert e < 1e-3
+    assert abs(float(O.simpo_loss(logps[:B], logps[B:])[0].mean()) - loss) < 1e-5
+    assert el < 3e-3
+    assert max(ratio.values()) < 1.5, sorted(ratio.items(), key=lambda kv: -kv[1])[:3]
+
+
+def test_step_mx8_full_size_7b_shapes_two_layers():
+    """Config 5 at Janus-Pro-7B shapes (D 4096, F 11008, 32 heads, T = 600), 2 layers, 2 pairs."""
+    dims = O.JanusDims(n_layers=2, lora_r=16, lora_alpha=32)
+    logps, loss, e, el, ratio, ora, B = _mx8_case(dims, 41, 2, 24, 576)
+    assert e < 1e-3
+    assert el < 3e-3
+    assert max(ratio.values()) < 1.5, sorted(ratio.items(), key=lambda kv: -kv[1])[:3]
