@@ -146,8 +146,12 @@ def get_model(mode: str = "train", dtype=torch.bfloat16, config=None, device=Non
                 w[f"layers.{i}.{p}.lora_A"] = ((torch.rand(r, in_f, generator=g) * 2 - 1) * b).to(torch.bfloat16)
                 w[f"layers.{i}.{p}.lora_B"] = torch.zeros(out_f, r, dtype=torch.bfloat16)
     bs = max_pairs or int(get(config, "dataset.train.batch_size", 4))
+    # BASELINE config 5: MXFP8 frozen decoder Linears (model.linear_dtype: mx8, or experiment.precision: fp8)
+    linear_dtype = str(get(config, "model.linear_dtype", "bf16") or "bf16").lower()
+    if str(get(config, "experiment.precision", "bf16")).lower() in ("fp8", "mx8"):
+        linear_dtype = "mx8"
     engine = SimPOEngine(dims, w, device=device, max_pairs=bs, max_text_len=max_text_len, n_img_tokens=n_img_tokens,
-                         lora_dropout=dropout, dropout_seed=seed)
+                         lora_dropout=dropout, dropout_seed=seed, linear_dtype=linear_dtype)
     del w
     tokenizer = load_tokenizer(get(config, "model.tokenizer_path"), vocab=dims.vocab)
     lora_cfg = {"lora_rank": r, "lora_alpha": alpha, "lora_dropout": dropout, "target_modules": targets}

@@ -35,7 +35,8 @@ def main(config):
         os.makedirs(config["base"]["save_path"], exist_ok=True)
     seed_everything(int(get(config, "experiment.seed", 42)))
     prec = get(config, "experiment.precision", "bf16")
-    dtype = torch.bfloat16 if prec in ("bf16", None, "auto") else torch.float32
+    # fp8 / mx8: bf16 activations, MXFP8 frozen Linears (get_model reads the same key)
+    dtype = torch.bfloat16 if prec in ("bf16", None, "auto", "fp8", "mx8") else torch.float32
     model, chat_processor, image_processor, tokenizer = get_model(mode="train", dtype=dtype, config=config,
                                                                   seed=int(get(config, "experiment.seed", 42)))
     dl = train_dataloader(config, tokenizer, rank=rank, world=world, img_vocab=model.engine.dims.img_vocab)
