@@ -80,6 +80,73 @@ def cpu_baseline(Lt=24, N=576):
                       f"scaled to 30 layers = {t_pair:.1f}s/pair"}
 
 
+def t2i_bytes_per_step(dims, R, T_keys):
+    """Algorithmic HBM bytes of one decode step: every weight once (decoder
+    Linears, gen_head, aligner W2; bf16), the KV cache read by attention (K and V of T_keys
+    positions per row, layer and head), the new K/V written, activations negligible."""
+    D, Fd, L, H = dims.d_model, dims.d_ff, dims.n_layers, dims.n_heads
+    w = L * (4 * D * D + 3 * D * Fd) + D * dims.gen_head_dim + dims.gen_head_dim * dims.img_vocab + D * D
+    kv = L * R * H * 128 * 2 * (T_keys + 1)
+    return 2.0 * (w + kv)
+
+
+def bench_t2i(args):
+    """BASELINE config 4: step-3 AR T2I sampling, Janus-Pro-7B, 576 tokens, cfg 5, parallel_size 16
+    (32 cond/uncond rows), hipGraph-captured decode.  One 'step' = one generate() call."""
+    from ospo_amd.engine import JANUS_PRO_7B, synthetic_weights
+    from ospo_amd.generate import T2IGenerator
+    dev = torch.device("cuda", 0)
+    dims = JANUS_PRO_7B.__class__(**{**JANUS_PRO_7B.__dict__, "n_layers": args.layers})
+    B, N, Lp = args.t2i_batch, args.img_tokens, args.t2i_prompt_len
+    w = synthetic_weights(dims, dev, seed=0, lora_seed=1)
+    gen = T2IGenerator(dims, w, device=dev, max_batch=B, max_prompt_len=Lp, n_img_tokens=N, cfg_weight=5.0,
+                       temperature=1.0)
+    del w
+    torch.cuda.empty_cache()
+    g = torch.Generator().manual_seed(0)
+    prompts = [torch.randint(0, dims.vocab, (int(torch.randint(Lp // 2, Lp + 1, (1,), generator=g)),),
+                             generator=g).tolist() for _ in range(B)]
+    for i in range(args.warmup):
+        gen.generate(prompts, seed=i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        tok = gen.generate(prompts, seed=100 + i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # decode-step roofline: graph replays of one step timed with HIP events on the replay stream
+    R = 2 * B
+    gen.pos.fill_(Lp + N // 2)
+    gen.step.fill_(N)  # past the last token: the sampler writes nothing, the rest runs as usual
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 50
+    e0.record(st)
+    for _ in range(reps):
+        gen._graph.replay()
+    e1.record(st)
+    torch.cuda.synchronize()
+    step_ms = e0.elapsed_time(e1) / reps
+    nbytes = t2i_bytes_per_step(dims, R, Lp + N // 2 + reps // 2)
+    achieved = nbytes / (step_ms * 1e-3) / 1e9
+    value = B * args.steps / dt
+    line = {
+        "metric": "images/sec, Janus-Pro-7B step-3 T2I sampling (576 tokens, cfg 5, parallel_size 16)",
+        "value": round(value, 3), "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init Janus-Pro-7B weights, random prompt ids)",
+        "config": {"workload": f"Janus-Pro-{'7B' if dims.n_layers == 30 else str(dims.n_layers) + 'L'} T2I sampling, "
+                               f"{B} prompts x (cond, uncond), {N} image tokens, hipGraph decode step",
+                   "prompt_len_max": Lp, "decode_steps": N - 1, "tokens_per_s": round(value * N, 1)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(achieved / 8000.0, 4), "traffic": None,
+                     "kernel": "decode step (hipGraph: 30 x (4 decode_gemv + attn_cache + norms) + gen_head + sampler)",
+                     "algorithmic_bytes_per_step": round(nbytes), "avg_step_us": round(step_ms * 1e3, 1)},
+        "tokens_checksum": int(tok.long().sum().item()),
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,9 +161,14 @@ def main():
     ap.add_argument("--lora-dropout", type=float, default=0.05)
     # BASELINE config 5: the frozen decoder Linears on MXFP8 block-scaled fp8 MFMA (use with --lora-r 32)
     ap.add_argument("--linear-dtype", choices=("bf16", "mx8"), default="bf16")
+    ap.add_argument("--workload", choices=("simpo", "t2i"), default="simpo")  # t2i: BASELINE config 4
+    ap.add_argument("--t2i-batch", type=int, default=16)       # parallel_size: prompts (x2 rows with CFG)
+    ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
     args = ap.parse_args()
+    if args.workload == "t2i":
+        return bench_t2i(args)
 
     from ospo_amd import dist as odist
     from ospo_amd import ops

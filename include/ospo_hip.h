@@ -258,6 +258,38 @@ int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, i
                      const void* rope_cos, const void* rope_sin, int rope_T, int rope_cols,
                      unsigned drop_seed, float drop_p, hipStream_t stream);
 
+/* ------------------------------------------------------ step-3 T2I decode ---
+ * BASELINE config 4 / SURVEY §8f rank 2: the sampling loop of
+ * ospo/wrapper/image_generation.py:132-171 (= ospo/inference.py:122-163) over a KV cache,
+ * R = 2B rows (row 2b = prompt b, row 2b+1 its unconditional copy), captured once in a
+ * hipGraph (ospo_amd/generate.py).  Step-dependent state is read from device counters
+ * (pos_dev = position of the current query, step_dev = image-token index).
+ * ospo_decode_gemv: out[r][n] = act(x[r] . W[n] + bias[n]) (+ residual[r][n]), R <= 64 rows,
+ *   W [N, ldw] (nn.Linear layout), act = GELU(erf) when gelu; ws >= ospo_decode_gemv_ws_bytes.
+ * ospo_kv_store: q|k|v rows [R][nq] (position pos0 + i, pos0 = *pos_dev or 0): optional
+ *   rotate-half RoPE on q and k, k / v into the caches [R][H][Tmax][head_dim], q to q_out.
+ * ospo_attn_cache: causal attention of query (r, i) over cached keys [start[r], pos0 + i]
+ *   (left padding as the reference's attention mask), HF eager bf16 rounding points.
+ * ospo_cfg_sample: logits rows (2b, 2b+1) -> guided bf16 logits, bf16 softmax(l / T), inverse-CDF
+ *   token with uniform u[step][b] -> tokens[b][step], next_ids[2b] = next_ids[2b+1].
+ * ospo_embed_rows: out[i] = table[ids[i]] (get_input_embeddings for the prompt).
+ * ospo_decode_advance: ++*pos_dev, ++*step_dev. */
+size_t ospo_decode_gemv_ws_bytes(int R, int N, int K);
+int ospo_decode_gemv(const void* W, int ldw, const void* X, int ldx, int R, int N, int K, const void* bias,
+                     int gelu, const void* residual, int ldr, void* out, int ldo, void* ws, size_t ws_bytes,
+                     hipStream_t stream);
+int ospo_kv_store(void* qkv, int ld, int R, int nq, const int* pos_dev, int rope, const void* rope_cos,
+                  const void* rope_sin, void* k_cache, void* v_cache, int n_heads, int head_dim, int Tmax,
+                  void* q_out, int ld_q, hipStream_t stream);
+int ospo_attn_cache(const void* q, int ldq, const void* k_cache, const void* v_cache, int R, int nq, int n_heads,
+                    int head_dim, int Tmax, const int* start, const int* pos_dev, float scale, void* out, int ldo,
+                    hipStream_t stream);
+int ospo_cfg_sample(const void* logits, int ldl, int V, int B, float cfg_weight, float temperature, const float* u,
+                    const int* step_dev, int n_steps, int* tokens, int* next_ids, float* probs_out,
+                    hipStream_t stream);
+int ospo_embed_rows(const int* ids, long n, const void* table, int vocab, int D, void* out, hipStream_t stream);
+int ospo_decode_advance(int* pos_dev, int* step_dev, hipStream_t stream);
+
 /* ------------------------------------------------------------ optimizer ---
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip
  * (ospo/utils/train.py:30, gradient_clip_val) + torch AdamW

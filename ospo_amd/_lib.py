@@ -52,11 +52,18 @@ SIGNATURES = {
     "ospo_lora_pack": [P, P, I, I, I, I, I, P, P, P, P, I, L, P],
     "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, U, F, P, I, P],
     "ospo_lora_skinny_ws_bytes": [I, I, I],
+    "ospo_decode_gemv_ws_bytes": [I, I, I],
+    "ospo_decode_gemv": [P, I, P, I, I, I, I, P, I, P, I, P, I, P, Z, P],
+    "ospo_kv_store": [P, I, I, I, P, I, P, P, P, P, I, I, I, P, I, P],
+    "ospo_attn_cache": [P, I, P, P, I, I, I, I, I, P, P, F, P, I, P],
+    "ospo_cfg_sample": [P, I, I, I, F, F, P, P, I, P, P, P, P],
+    "ospo_embed_rows": [P, L, P, I, I, P, P],
+    "ospo_decode_advance": [P, P, P],
     "ospo_sumsq": [P, L, P, P],
     "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],
 }
 
-RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_dropout_hash": c_uint}
+RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 

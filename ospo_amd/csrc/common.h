@@ -43,6 +43,20 @@ __device__ __forceinline__ unsigned pack2(float lo, float hi) {
   return (unsigned)f2bits(lo) | ((unsigned)f2bits(hi) << 16);
 }
 
+__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = bits2f(v[q] & 0xffff);
+    f[2 * q + 1] = bits2f(v[q] >> 16);
+  }
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = pack2(f[2 * q], f[2 * q + 1]);
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

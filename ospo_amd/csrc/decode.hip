@@ -1,0 +1,478 @@
+// Step-3 autoregressive text-to-image sampling on gfx950 (BASELINE config 4):
+// the decode loop of ospo/wrapper/image_generation.py:132-171 (= ospo/inference.py:122-163) --
+// Janus-Pro LLM over a KV cache for 2B rows (B prompts x {cond, uncond}), gen_head on the last
+// position, classifier-free guidance, softmax(logits / T) and one sampled VQ token per image per
+// step, fed back through prepare_gen_img_embeds.
+//
+// MI355X-first shape of the step (R = 2B <= 64 rows):
+//  * every Linear is a weight stream (R rows against [N, K] weights): decode_gemv runs the
+//    register-direct skinny MFMA loop of skinny.h with the WEIGHT as the 16-row operand and the
+//    R activation rows as <= 4 small tiles, so each weight byte is loaded once, 16 B per lane,
+//    with 2 x 4 batches of loads in flight per wave; split-K partials only when the weight has
+//    too few 16-row blocks to fill 256 CUs;
+//  * attention reads the KV cache [R][H][Tmax][128] row-contiguous per (row, head): one
+//    workgroup per (query, head), keys range [pad_start[r], pos] (the reference's left padding
+//    is an attention mask, positions run 0..T-1 through it);
+//  * all step-dependent state (position, step index) lives in a device counter, so the whole
+//    step is captured once in a hipGraph and replayed (ospo_amd/generate.py);
+//  * sampling is inverse-CDF on the bf16 probabilities with a uniform per image and step,
+//    summed in a fixed order (64-element chunks, then the 256 chunk sums) that
+//    oracle/generate_ref.py restates, so a token is a deterministic function of (logits, u).
+#include "common.h"
+#include "skinny.h"
+
+namespace {
+
+constexpr int HD = 128;  // head_dim (Janus-Pro)
+
+// -------------------------------------------------------------------- GEMV
+// out[r][n] = act(x[r] . W[n] + bias[n]) (+ res[r][n]);  act = GELU(erf) of the bf16-rounded
+// pre-activation when gelu (vision_head's first Linear).
+__device__ __forceinline__ void gemv_store(float v, int r, int n, const bf16* bias, int gelu, const bf16* res,
+                                           int ldr, bf16* out, int ldo) {
+  float y = v + (bias ? bf2f(bias[n]) : 0.f);
+  if (gelu) y = gelu_erf(round_bf(y));
+  if (res) y = round_bf(y) + bf2f(res[(long)r * ldr + n]);
+  out[(long)r * ldo + n] = f2bf(y);
+}
+
+template <int NT>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemv_kernel(const bf16* __restrict__ W, int ldw,
+                                                             const bf16* __restrict__ X, int ldx, int R, int K,
+                                                             const bf16* __restrict__ bias, int gelu,
+                                                             const bf16* __restrict__ res, int ldr,
+                                                             bf16* __restrict__ out, int ldo,
+                                                             f32x4* __restrict__ ws) {
+  __shared__ f32x4 red[SK_WAVES][NT][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int nb = blockIdx.x, z = blockIdx.y, splits = gridDim.y;
+  const int n = nb * 16 + l16;
+  const int nsteps = K >> 5;
+  const int s_begin = (int)((long)nsteps * z / splits), s_end = (int)((long)nsteps * (z + 1) / splits);
+  const int n_i = (s_end - s_begin - wave + SK_WAVES - 1) / SK_WAVES;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16* wrow = W + (long)n * ldw + 8 * g + 32 * s_begin;
+  const bf16* bp[NT];
+  bool bok[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int r = 16 * j + l16;
+    bok[j] = r < R;
+    bp[j] = X + (long)(bok[j] ? r : 0) * ldx + 8 * g + 32 * s_begin;
+  }
+  sk_loop<NT>(wrow, bp, bok, wave, n_i, acc);  // acc[j][q] = sum_k W[n][k] x[16j + 4g + q][k]
+#pragma unroll
+  for (int j = 0; j < NT; ++j) red[wave][j][lane] = acc[j];
+  __syncthreads();
+  if (wave >= NT) return;
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 0; w < SK_WAVES; ++w) v += red[w][wave][lane];
+  if (splits > 1) {
+    ws[((long)(z * gridDim.x + nb) * NT + wave) * 64 + lane] = v;
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 16 * wave + 4 * g + q;
+    if (r < R) gemv_store(v[q], r, n, bias, gelu, res, ldr, out, ldo);
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(64 * NT) void gemv_reduce_kernel(const f32x4* __restrict__ ws, int splits, int NB, int R,
+                                                            const bf16* __restrict__ bias, int gelu,
+                                                            const bf16* __restrict__ res, int ldr,
+                                                            bf16* __restrict__ out, int ldo) {
+  const int lane = threadIdx.x & 63, j = threadIdx.x >> 6, nb = blockIdx.x;
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < splits; ++z) v += ws[((long)(z * NB + nb) * NT + j) * 64 + lane];
+  const int n = nb * 16 + (lane & 15), g = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 16 * j + 4 * g + q;
+    if (r < R) gemv_store(v[q], r, n, bias, gelu, res, ldr, out, ldo);
+  }
+}
+
+// ------------------------------------------------------- KV cache write
+// rows [R][nq] of qkv (q|k|v, H heads of 128 each): position p = pos0 + i (pos0 = *pos_dev, or 0).
+// rope: HF rotate-half on q and k at position p, rounded per op like the eager bf16 path
+// (ops.hip rope_kernel); q is written to q_out (else left in place), k / v to the caches.
+__global__ void kv_store_kernel(bf16* __restrict__ qkv, int ld, int R, int nq, const int* __restrict__ pos_dev,
+                                int rope, const bf16* __restrict__ cs, const bf16* __restrict__ sn,
+                                bf16* __restrict__ kc, bf16* __restrict__ vc, int H, int Tmax,
+                                bf16* __restrict__ q_out, int ldq) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)R * nq * H * 8;  // 8 chunks of 8 rotation pairs per head
+  if (tid >= total) return;
+  const int ch = tid & 7;
+  const int h = (int)((tid >> 3) % H);
+  const long ri = (tid >> 3) / H;
+  const int r = (int)(ri / nq), i = (int)(ri % nq);
+  const int p = (pos_dev ? *pos_dev : 0) + i;
+  if (p >= Tmax) return;
+  bf16* row = qkv + ri * ld;
+  const int D = H * HD;
+  float c[8], s[8];
+  if (rope) {
+    unpack8(*reinterpret_cast<const u32x4*>(cs + (long)p * 64 + ch * 8), c);
+    unpack8(*reinterpret_cast<const u32x4*>(sn + (long)p * 64 + ch * 8), s);
+  }
+  const long cbase = (((long)r * H + h) * Tmax + p) * HD + ch * 8;
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {  // 0 = q, 1 = k
+    bf16* base = row + which * D + h * HD + ch * 8;
+    u32x4 v1 = *reinterpret_cast<const u32x4*>(base), v2 = *reinterpret_cast<const u32x4*>(base + 64);
+    if (rope) {
+      float a[8], b[8], o1[8], o2[8];
+      unpack8(v1, a);
+      unpack8(v2, b);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        o1[q] = round_bf(a[q] * c[q]) + round_bf(-b[q] * s[q]);
+        o2[q] = round_bf(b[q] * c[q]) + round_bf(a[q] * s[q]);
+      }
+      v1 = pack8(o1);
+      v2 = pack8(o2);
+    }
+    if (which == 0) {
+      if (q_out) {
+        bf16* qo = q_out + ri * ldq + h * HD + ch * 8;
+        *reinterpret_cast<u32x4*>(qo) = v1;
+        *reinterpret_cast<u32x4*>(qo + 64) = v2;
+      } else if (rope) {
+        *reinterpret_cast<u32x4*>(base) = v1;
+        *reinterpret_cast<u32x4*>(base + 64) = v2;
+      }
+    } else {
+      *reinterpret_cast<u32x4*>(kc + cbase) = v1;
+      *reinterpret_cast<u32x4*>(kc + cbase + 64) = v2;
+    }
+  }
+  const bf16* vsrc = row + 2 * D + h * HD + ch * 8;
+  *reinterpret_cast<u32x4*>(vc + cbase) = *reinterpret_cast<const u32x4*>(vsrc);
+  *reinterpret_cast<u32x4*>(vc + cbase + 64) = *reinterpret_cast<const u32x4*>(vsrc + 64);
+}
+
+// ------------------------------------------------------------ attention
+// one workgroup (256 threads) per (query row, head): keys [start[r], p], p = pos0 + i.
+// HF eager bf16: s = bf16(bf16(q.k) * scale); fp32 softmax over the unmasked keys (masked keys
+// get finfo.min and contribute exactly 0); P rounded to bf16; o = bf16(sum P v) with fp32 sums.
+constexpr int ATT_MAXT = 2048;
+__global__ __launch_bounds__(256) void attn_cache_kernel(const bf16* __restrict__ q, int ldq,
+                                                         const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+                                                         int H, int Tmax, const int* __restrict__ start,
+                                                         const int* __restrict__ pos_dev, int nq, float scale,
+                                                         bf16* __restrict__ out, int ldo) {
+  __shared__ float sc[ATT_MAXT];
+  __shared__ float red[8];
+  __shared__ float2 part[4][64];
+  const int ri = blockIdx.x, h = blockIdx.y;
+  const int r = ri / nq, i = ri % nq;
+  const int p = (pos_dev ? *pos_dev : 0) + i;
+  const int s0 = start[r];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  bf16* orow = out + (long)ri * ldo + h * HD;
+  if (p < s0 || p >= Tmax) {  // a padded query position: never consumed (its key is masked for everyone)
+    if (wave == 0) reinterpret_cast<uint32_t*>(orow)[lane] = 0u;
+    return;
+  }
+  const int L = p - s0 + 1;
+  const uint32_t qv = reinterpret_cast<const uint32_t*>(q + (long)ri * ldq + h * HD)[lane];
+  const float q0 = bits2f(qv & 0xffff), q1 = bits2f(qv >> 16);
+  const long hb = ((long)r * H + h) * Tmax;
+  const uint32_t* kb = reinterpret_cast<const uint32_t*>(kc + (hb + s0) * HD) + lane;
+  // scores: wave w takes keys w, w+4, ...; 8 keys' loads in flight before the reductions
+  for (int k0 = wave * 8; k0 < L; k0 += 32) {
+    uint32_t kv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = min(k0 + u, L - 1);
+      kv[u] = kb[(long)k * (HD / 2)];
+    }
+    float d[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) d[u] = wave_sum(q0 * bits2f(kv[u] & 0xffff) + q1 * bits2f(kv[u] >> 16));
+    if (lane < 8 && k0 + lane < L) {
+      float dv = d[0];
+#pragma unroll
+      for (int u = 1; u < 8; ++u) dv = (lane == u) ? d[u] : dv;
+      sc[k0 + lane] = round_bf(round_bf(dv) * scale);
+    }
+  }
+  __syncthreads();
+  float m = -INFINITY;
+  for (int k = threadIdx.x; k < L; k += 256) m = fmaxf(m, sc[k]);
+  m = wave_max(m);
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+  for (int k = threadIdx.x; k < L; k += 256) {
+    const float e = __expf(sc[k] - m);
+    sc[k] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  if (lane == 0) red[4 + wave] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  // o[2d..2d+1] = sum_k bf16(e_k / sum) v[k][2d..]: thread (kg = wave, d = lane), keys kg, kg+4, ...
+  const uint32_t* vb = reinterpret_cast<const uint32_t*>(vc + (hb + s0) * HD) + lane;
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll 8
+  for (int k = wave; k < L; k += 4) {
+    const float pk = round_bf(sc[k] * inv);
+    const uint32_t vv = vb[(long)k * (HD / 2)];
+    a0 += pk * bits2f(vv & 0xffff);
+    a1 += pk * bits2f(vv >> 16);
+  }
+  part[wave][lane] = make_float2(a0, a1);
+  __syncthreads();
+  if (wave == 0) {
+    float o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      o0 += part[w][lane].x;
+      o1 += part[w][lane].y;
+    }
+    reinterpret_cast<uint32_t*>(orow)[lane] = pack2(o0, o1);
+  }
+}
+
+// --------------------------------------------------------- CFG + sampling
+// one workgroup per image b: logits rows 2b (cond) and 2b+1 (uncond) [V] bf16 (train.py-style
+// interleaving of image_generation.py:132-141, 156-157).  l = bf16(lu + bf16(w * bf16(lc - lu))),
+// l = bf16(l / T); p = bf16(softmax(l)) (fp32 inside, like torch's bf16 softmax); token = first j
+// with cumsum(p)_j > u * sum(p), sums in 64-element chunks (thread t owns chunk t) then the
+// chunk sums in order (a rounding overshoot takes the last token with mass).  V <= 256 * 64.
+// torch.multinomial draws from the same distribution with its own generator; the uniform here
+// comes from a seeded device buffer, so a run is reproducible and checkable token by token.
+constexpr int SMP_CHUNK = 64;
+__global__ __launch_bounds__(256) void cfg_sample_kernel(const bf16* __restrict__ logits, int ldl, int V, float cfg_w,
+                                                         float temp, const float* __restrict__ u,
+                                                         int B, const int* __restrict__ step_dev, int n_steps,
+                                                         int* __restrict__ tokens, int* __restrict__ next_ids,
+                                                         float* __restrict__ probs_out) {
+  __shared__ float csum[256];
+  __shared__ float red[8];
+  __shared__ int pick[2];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int step = step_dev ? *step_dev : 0;
+  if (step >= n_steps) return;
+  const bf16* lc = logits + (long)(2 * b) * ldl;
+  const bf16* lu = logits + (long)(2 * b + 1) * ldl;
+  const int j0 = t * SMP_CHUNK;
+  const int nj = max(0, min(SMP_CHUNK, V - j0));
+  float l[SMP_CHUNK];
+  float m = -INFINITY;
+#pragma unroll 8
+  for (int q = 0; q < SMP_CHUNK; ++q) {
+    float v = -INFINITY;
+    if (q < nj) {
+      const float c = bf2f(lc[j0 + q]), un = bf2f(lu[j0 + q]);
+      v = round_bf(un + round_bf(cfg_w * round_bf(c - un)));
+      if (temp != 1.f) v = round_bf(v / temp);
+    }
+    l[q] = v;
+    m = fmaxf(m, v);
+  }
+  m = wave_max(m);
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float s = 0.f;
+#pragma unroll 8
+  for (int q = 0; q < SMP_CHUNK; ++q) {
+    const float e = q < nj ? expf(l[q] - m) : 0.f;
+    l[q] = e;
+    s += e;
+  }
+  s = wave_sum(s);
+  __syncthreads();
+  if (lane == 0) red[4 + wave] = s;
+  __syncthreads();
+  const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  float cs = 0.f;
+#pragma unroll 8
+  for (int q = 0; q < SMP_CHUNK; ++q) {
+    const float pq = q < nj ? round_bf(l[q] * inv) : 0.f;
+    l[q] = pq;
+    cs += pq;
+    if (probs_out && q < nj) probs_out[(long)b * V + j0 + q] = pq;
+  }
+  csum[t] = cs;
+  __syncthreads();
+  if (t == 0) {  // the chunk sums in order: total and the chunk holding the target
+    float tot = 0.f;
+    for (int c = 0; c < 256; ++c) tot += csum[c];
+    const float target = u[(long)step * B + b] * tot;
+    float run = 0.f, run_last = 0.f;
+    int c = 0, last = 0;
+    for (; c < 256; ++c) {
+      if (run + csum[c] > target) break;
+      if (csum[c] > 0.f) {
+        last = c;
+        run_last = run;
+      }
+      run += csum[c];
+    }
+    if (c == 256) {  // target at the very top (rounding): the last chunk with mass
+      c = last;
+      run = run_last;
+    }
+    pick[0] = c;
+    red[0] = run;
+    red[1] = target;
+  }
+  __syncthreads();
+  if (t == pick[0]) {
+    float run = red[0];
+    const float target = red[1];
+    int tok = -1, last = j0;
+    for (int q = 0; q < nj; ++q) {
+      if (l[q] > 0.f) last = j0 + q;
+      run += l[q];
+      if (run > target) {
+        tok = j0 + q;
+        break;
+      }
+    }
+    if (tok < 0) tok = last;  // u * total at the very top of the chunk (rounding): its last nonzero
+    tokens[(long)b * n_steps + step] = tok;
+    next_ids[2 * b] = tok;
+    next_ids[2 * b + 1] = tok;
+  }
+}
+
+__global__ void embed_rows_kernel(const int* __restrict__ ids, long n, const bf16* __restrict__ table, int V, int D,
+                                  bf16* __restrict__ out) {
+  const int cpr = D / 8;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= n * cpr) return;
+  const long r = tid / cpr;
+  const int c = tid % cpr;
+  const int id = min(max(ids[r], 0), V - 1);  // the host validates ids; clamped so they cannot fault
+  reinterpret_cast<u32x4*>(out + r * D)[c] = reinterpret_cast<const u32x4*>(table + (long)id * D)[c];
+}
+
+__global__ void advance_kernel(int* pos, int* step) {
+  if (threadIdx.x == 0) {
+    *pos += 1;
+    *step += 1;
+  }
+}
+
+int gemv_splits(int nblocks, int K) {
+  int s = 1;
+  while (nblocks * s < 1024 && (K >> 5) / (2 * s) >= 8 * SK_WAVES) s *= 2;
+  return s;
+}
+
+}  // namespace
+
+extern "C" size_t ospo_decode_gemv_ws_bytes(int R, int N, int K) {
+  if (R <= 0 || R > 64 || N <= 0 || N % 16 || K <= 0) return 0;
+  const int nt = (R + 15) / 16, nb = N / 16;
+  return (size_t)gemv_splits(nb, K) * nb * nt * 64 * sizeof(f32x4);
+}
+
+extern "C" int ospo_decode_gemv(const void* W, int ldw, const void* X, int ldx, int R, int N, int K, const void* bias,
+                                int gelu, const void* residual, int ldr, void* out, int ldo, void* ws, size_t ws_bytes,
+                                hipStream_t stream) {
+  if (!W || !X || !out) return OSPO_ERR_ARG;
+  if (R <= 0 || R > 64 || N <= 0 || N % 16 || K <= 0 || K % 32) return OSPO_ERR_SHAPE;
+  if (ldw < K || ldx < K || ldo < N || ldw % 8 || ldx % 8 || (residual && (ldr < N))) return OSPO_ERR_SHAPE;
+  if (!aligned16(W) || !aligned16(X)) return OSPO_ERR_ALIGN;
+  const int nt = (R + 15) / 16, nb = N / 16;
+  const int splits = gemv_splits(nb, K);
+  if (splits > 1 && (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws))) return OSPO_ERR_ARG;
+  const bf16 *w = (const bf16*)W, *x = (const bf16*)X, *bs = (const bf16*)bias, *rs = (const bf16*)residual;
+  bf16* o = (bf16*)out;
+  f32x4* wsp = (f32x4*)ws;
+  const dim3 grid(nb, splits);
+#define GEMV(NT_)                                                                                                   \
+  hipLaunchKernelGGL((gemv_kernel<NT_>), grid, dim3(64 * SK_WAVES), 0, stream, w, ldw, x, ldx, R, K, bs, gelu, rs, ldr, \
+                     o, ldo, wsp);                                                                                  \
+  if (splits > 1)                                                                                                   \
+    hipLaunchKernelGGL((gemv_reduce_kernel<NT_>), dim3(nb), dim3(64 * NT_), 0, stream, wsp, splits, nb, R, bs, gelu,   \
+                       rs, ldr, o, ldo);
+  switch (nt) {
+    case 1: GEMV(1) break;
+    case 2: GEMV(2) break;
+    case 3: GEMV(3) break;
+    default: GEMV(4) break;
+  }
+#undef GEMV
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_kv_store(void* qkv, int ld, int R, int nq, const int* pos_dev, int rope, const void* rope_cos,
+                             const void* rope_sin, void* k_cache, void* v_cache, int n_heads, int head_dim, int Tmax,
+                             void* q_out, int ld_q, hipStream_t stream) {
+  if (!qkv || !k_cache || !v_cache) return OSPO_ERR_ARG;
+  if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
+  if (R <= 0 || nq <= 0 || n_heads <= 0 || Tmax <= 0 || ld < 3 * n_heads * HD || ld % 8) return OSPO_ERR_SHAPE;
+  if (rope && (!rope_cos || !rope_sin)) return OSPO_ERR_ARG;
+  if (q_out && (ld_q < n_heads * HD || ld_q % 8)) return OSPO_ERR_SHAPE;
+  if (!aligned16(qkv) || !aligned16(k_cache) || !aligned16(v_cache) || (q_out && !aligned16(q_out)))
+    return OSPO_ERR_ALIGN;
+  const long total = (long)R * nq * n_heads * 8;
+  hipLaunchKernelGGL(kv_store_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, (bf16*)qkv, ld, R,
+                     nq, pos_dev, rope, (const bf16*)rope_cos, (const bf16*)rope_sin, (bf16*)k_cache, (bf16*)v_cache,
+                     n_heads, Tmax, (bf16*)q_out, ld_q);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_attn_cache(const void* q, int ldq, const void* k_cache, const void* v_cache, int R, int nq,
+                               int n_heads, int head_dim, int Tmax, const int* start, const int* pos_dev, float scale,
+                               void* out, int ldo, hipStream_t stream) {
+  if (!q || !k_cache || !v_cache || !start || !out) return OSPO_ERR_ARG;
+  if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
+  if (R <= 0 || nq <= 0 || n_heads <= 0 || Tmax <= 0 || Tmax > ATT_MAXT) return OSPO_ERR_SHAPE;
+  if (ldq < n_heads * HD || ldo < n_heads * HD || ldq % 2 || ldo % 2) return OSPO_ERR_SHAPE;
+  hipLaunchKernelGGL(attn_cache_kernel, dim3(R * nq, n_heads), dim3(256), 0, stream, (const bf16*)q, ldq,
+                     (const bf16*)k_cache, (const bf16*)v_cache, n_heads, Tmax, start, pos_dev, nq, scale, (bf16*)out,
+                     ldo);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_cfg_sample(const void* logits, int ldl, int V, int B, float cfg_weight, float temperature,
+                               const float* u, const int* step_dev, int n_steps, int* tokens, int* next_ids,
+                               float* probs_out, hipStream_t stream) {
+  if (!logits || !u || !tokens || !next_ids) return OSPO_ERR_ARG;
+  if (V <= 0 || V > 256 * SMP_CHUNK || B <= 0 || ldl < V || n_steps <= 0) return OSPO_ERR_SHAPE;
+  if (!(temperature > 0.f)) return OSPO_ERR_ARG;
+  hipLaunchKernelGGL(cfg_sample_kernel, dim3(B), dim3(256), 0, stream, (const bf16*)logits, ldl, V, cfg_weight,
+                     temperature, u, B, step_dev, n_steps, tokens, next_ids, probs_out);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_decode_advance(int* pos_dev, int* step_dev, hipStream_t stream) {
+  if (!pos_dev || !step_dev) return OSPO_ERR_ARG;
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, stream, pos_dev, step_dev);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_embed_rows(const int* ids, long n, const void* table, int vocab, int D, void* out,
+                               hipStream_t stream) {
+  if (!ids || !table || !out) return OSPO_ERR_ARG;
+  if (n <= 0 || vocab <= 0 || D <= 0 || D % 8) return OSPO_ERR_SHAPE;
+  if (!aligned16(table) || !aligned16(out)) return OSPO_ERR_ALIGN;
+  const long total = n * (D / 8);
+  hipLaunchKernelGGL(embed_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, ids, n,
+                     (const bf16*)table, vocab, D, (bf16*)out);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}

@@ -26,19 +26,6 @@ __device__ __forceinline__ float block_max256(float v, float* red) {
   return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    f[2 * q] = bits2f(v[q] & 0xffff);
-    f[2 * q + 1] = bits2f(v[q] >> 16);
-  }
-}
-__device__ __forceinline__ u32x4 pack8(const float* f) {
-  u32x4 v;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = pack2(f[2 * q], f[2 * q + 1]);
-  return v;
-}
 
 constexpr int RMS_MAXIT = 8;  // D <= 256 threads * 8 it * 8 = 16384
 

@@ -1,0 +1,247 @@
+"""Step-3 text-to-image sampling on the MI355X (BASELINE config 4).
+
+The loop of ``ospo/wrapper/image_generation.py:109-171`` (``JanusProImageGenWrapper.generate_image``;
+the same loop is ``ospo/inference.py:110-163``), run over a KV cache:
+
+* the B prompts are left-padded with ``pad_id`` to one length Lp; row 2b is prompt b, row 2b+1 its
+  unconditional copy with every token but the first and the last replaced by ``pad_id``
+  (image_generation.py:132-141); padding is an attention mask, positions run 0..T-1 through it
+  (HF 4.38 ``LlamaModel`` builds position ids from ``past_key_values_length`` only);
+* step 0 is the prompt (prefill), steps 1..n-1 one token each; every step takes gen_head on the last
+  position, ``logits = uncond + cfg_weight * (cond - uncond)``, ``softmax(logits / temperature)`` and
+  samples one VQ id per image (:156-165), which ``prepare_gen_img_embeds`` turns into the next
+  input for both rows of the pair (:166-169).
+
+MI355X-first structure: the prefill reuses the training kernels (256x256 MFMA GEMM with the RoPE
+epilogue, RMSNorm, SwiGLU); each decode step is weight streaming (``ospo_decode_gemv``) plus cached
+attention (``ospo_attn_cache``); every step-dependent value is a device counter, so one decode step is
+captured as a hipGraph (``torch.cuda.CUDAGraph`` over the HIP launches) and replayed n-1 times.
+Sampling: inverse CDF on the bf16 probabilities with a seeded uniform per image and step
+(``ospo_cfg_sample``) -- the distribution ``torch.multinomial`` draws from, with a generator whose
+draws the oracle can replay.  The VQ pixel decoder (``decode_code``) is the VQ row of §8f (rank 3);
+``generate`` returns the image-token ids.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import ops
+from .engine import ModelDims
+
+BF16 = torch.bfloat16
+PAD_ID = 100015  # "<｜▁pad▁｜>" of the Janus-Pro tokenizer (VLChatProcessor.pad_id)
+
+
+def _dev(t, device):
+    return t.to(device=device, dtype=BF16).contiguous()
+
+
+class T2IGenerator:
+    """Device-resident Janus-Pro sampler (one per GPU).  ``weights``: the names of
+    ``engine.synthetic_weights`` / ``oracle.simpo_ref.init_weights``; LoRA A/B present in them are
+    merged (W + s B A, as ``inference.py`` merges the trained adapter before sampling)."""
+
+    def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_batch: int = 16,
+                 max_prompt_len: int = 64, n_img_tokens: int = 576, cfg_weight: float = 5.0,
+                 temperature: float = 1.0, pad_id: int = PAD_ID):
+        if dims.head_dim != 128:
+            raise ValueError("head_dim must be 128 (Janus-Pro)")
+        if 2 * max_batch > 64:
+            raise ValueError("at most 32 prompts per batch (64 cond/uncond rows)")
+        if not temperature > 0:
+            raise ValueError("temperature must be > 0")
+        self.dims, self.device = dims, torch.device(device)
+        self.cfg_weight, self.temperature, self.pad_id = float(cfg_weight), float(temperature), int(pad_id)
+        self.n_img = n_img_tokens
+        D, Fd, L, H = dims.d_model, dims.d_ff, dims.n_layers, dims.n_heads
+        dev, w = self.device, weights
+        s = dims.lora_scale
+
+        def merged(name):
+            W = w[name].to(device=dev, dtype=torch.float32)
+            A, B = w.get(name + ".lora_A"), w.get(name + ".lora_B")
+            if A is not None and B is not None:
+                W = W + s * (B.to(dev, torch.float32) @ A.to(dev, torch.float32))
+            return W.to(BF16)
+
+        self.embed = _dev(w["embed_tokens"], dev)
+        self.layers = []
+        for i in range(L):
+            p = f"layers.{i}."
+            self.layers.append({
+                "ln_in": _dev(w[p + "input_layernorm"], dev), "ln_post": _dev(w[p + "post_attention_layernorm"], dev),
+                "qkv": torch.cat([merged(p + "q_proj"), merged(p + "k_proj"), merged(p + "v_proj")], 0).contiguous(),
+                "o": merged(p + "o_proj").contiguous(),
+                "gu": torch.cat([merged(p + "gate_proj"), merged(p + "up_proj")], 0).contiguous(),
+                "down": merged(p + "down_proj").contiguous(),
+            })
+        self.norm = _dev(w["norm"], dev)
+        self.gh_w1, self.gh_b1 = _dev(w["gen_head.w1"], dev), _dev(w["gen_head.b1"], dev)
+        self.gh_w2, self.gh_b2 = _dev(w["gen_head.w2"], dev), _dev(w["gen_head.b2"], dev)
+        self.al_w1, self.al_b1 = _dev(w["gen_aligner.w1"], dev), _dev(w["gen_aligner.b1"], dev)
+        self.al_w2, self.al_b2 = _dev(w["gen_aligner.w2"], dev), _dev(w["gen_aligner.b2"], dev)
+        self.gen_embed = _dev(w["gen_embed"], dev)
+        # ---- KV cache and decode-step buffers (R = 2 * max_batch rows)
+        self.max_batch, self.max_prompt = max_batch, max_prompt_len
+        self.Tmax = max_prompt_len + n_img_tokens
+        R = 2 * max_batch
+        z = lambda *sh, dt=BF16: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
+        self.kc = [z(R, H, self.Tmax, 128) for _ in range(L)]
+        self.vc = [z(R, H, self.Tmax, 128) for _ in range(L)]
+        V, Dg = dims.img_vocab, dims.gen_head_dim
+        self.x, self.xn, self.qkv, self.q = z(R, D), z(R, D), z(R, 3 * D), z(R, D)
+        self.attn, self.xmid, self.xn2 = z(R, D), z(R, D), z(R, D)
+        self.gu, self.h, self.xo = z(R, 2 * Fd), z(R, Fd), z(R, D)
+        self.hf, self.zg, self.logits, self.e1 = z(R, D), z(R, Dg), z(R, V), z(R, D)
+        self.rstd = z(R, dt=torch.float32)
+        self.next_ids = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.start = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.pos = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.tokens = torch.zeros(max_batch, n_img_tokens, dtype=torch.int32, device=dev)
+        self.u = torch.zeros(n_img_tokens * max_batch, dtype=torch.float32, device=dev)  # [n, B] of this batch
+        shapes = [(3 * D, D), (D, D), (2 * Fd, D), (D, Fd), (Dg, D), (V, Dg), (D, D)]
+        self.gws = torch.empty(max(ops.query("ospo_decode_gemv_ws_bytes", R, n, k) for n, k in shapes) // 4 + 4,
+                               dtype=torch.float32, device=dev)
+        self.cos, self.sin = ops.rope_tables(self.Tmax, 128, dims.rope_theta, dev)
+        self._graph = None
+        self._graph_B = None
+        self.probs = None  # [n, B, V] fp32 when record_probs
+
+    # ------------------------------------------------------------------ prefill
+    def _prompt_rows(self, prompts: Sequence[Sequence[int]]):
+        """Token matrix [2B, Lp] and pad lengths exactly as image_generation.py:124-141."""
+        B = len(prompts)
+        Lp = max(len(p) for p in prompts)
+        toks = torch.full((2 * B, Lp), self.pad_id, dtype=torch.int32)
+        start = torch.zeros(2 * B, dtype=torch.int32)
+        for i in range(2 * B):
+            ids = torch.tensor(list(prompts[i // 2]), dtype=torch.int32)
+            pad = Lp - ids.numel()
+            toks[i, pad:] = ids
+            start[i] = pad
+            if i % 2 != 0:
+                toks[i, pad + 1: Lp - 1] = self.pad_id
+        return toks, start, Lp
+
+    def _prefill(self, toks: torch.Tensor, Lp: int):
+        dims, dev = self.dims, self.device
+        D, Fd, H = dims.d_model, dims.d_ff, dims.n_heads
+        R = toks.shape[0]
+        M = R * Lp
+        ids = toks.reshape(-1).to(dev)
+        z = lambda *sh, dt=BF16: torch.empty(*sh, dtype=dt, device=dev)  # noqa: E731
+        x, xn, qkv, attn = z(M, D), z(M, D), z(M, 3 * D), z(M, D)
+        xmid, gu, h, rstd = z(M, D), z(M, 2 * Fd), z(M, Fd), z(M, dt=torch.float32)
+        ops.embed_rows(ids, self.embed, x)
+        cos, sin = self.cos[:Lp].contiguous(), self.sin[:Lp].contiguous()
+        scale = 1.0 / math.sqrt(128)
+        for i, lw in enumerate(self.layers):
+            ops.rmsnorm_fwd(x, lw["ln_in"], xn, rstd, dims.rms_eps)
+            if (3 * D) % 256 == 0:  # q|k RoPE in the projection epilogue; position = row % Lp
+                ops.gemm_nt(xn, lw["qkv"], qkv, rope=(cos, sin, Lp, 2 * D))
+            else:
+                ops.gemm_nt(xn, lw["qkv"], qkv)
+                ops.rope(qkv, 0, D, R, Lp, H, 128, cos, sin)
+            ops.kv_store(qkv, R, Lp, None, self.kc[i], self.vc[i], H, self.Tmax)
+            ops.attn_cache(qkv, self.kc[i], self.vc[i], R, Lp, H, self.Tmax, self.start, None, scale, attn)
+            ops.gemm_nt(attn, lw["o"], xmid, residual=x)
+            ops.rmsnorm_fwd(xmid, lw["ln_post"], xn, rstd, dims.rms_eps)
+            ops.gemm_nt(xn, lw["gu"], gu)
+            ops.swiglu_fwd(gu, h)
+            ops.gemm_nt(h, lw["down"], x, residual=xmid)
+        last = x.view(R, Lp, D)[:, Lp - 1].contiguous()
+        self._head_and_sample(last, R)
+
+    # ---------------------------------------------------------------- one step
+    def _head_and_sample(self, last: torch.Tensor, R: int):
+        """gen_head on the last position, CFG + sampling, next input embeds (aligner)."""
+        dims = self.dims
+        ops.rmsnorm_fwd(last, self.norm, self.hf[:R], self.rstd[:R], dims.rms_eps)
+        ops.decode_gemv(self.hf[:R], self.gh_w1, self.zg[:R], bias=self.gh_b1, gelu=True, ws=self.gws)
+        ops.decode_gemv(self.zg[:R], self.gh_w2, self.logits[:R], bias=self.gh_b2, ws=self.gws)
+        B = R // 2
+        probs = None
+        if self.probs is not None:
+            probs = self.probs[self._host_step]
+        ops.cfg_sample(self.logits[:R], B, self.cfg_weight, self.temperature, self.u, self.step, self.n_img,
+                       self.tokens[:B], self.next_ids[:R], probs)
+        ops.gen_aligner_in(self.next_ids[:R], self.gen_embed, self.al_w1, self.al_b1, self.e1[:R])
+        ops.decode_gemv(self.e1[:R], self.al_w2, self.x[:R], bias=self.al_b2, ws=self.gws)
+        ops.decode_advance(self.pos, self.step)
+
+    def _decode_step(self, R: int):
+        """One token for every row at position *pos: the layer stack ping-pongs the residual
+        stream between self.x and self.xo; the aligner writes the next input into self.x."""
+        dims = self.dims
+        H = dims.n_heads
+        scale = 1.0 / math.sqrt(128)
+        g = self.gws
+        x, xo = self.x[:R], self.xo[:R]
+        for i, lw in enumerate(self.layers):
+            ops.rmsnorm_fwd(x, lw["ln_in"], self.xn[:R], self.rstd[:R], dims.rms_eps)
+            ops.decode_gemv(self.xn[:R], lw["qkv"], self.qkv[:R], ws=g)
+            ops.kv_store(self.qkv[:R], R, 1, self.pos, self.kc[i], self.vc[i], H, self.Tmax, rope=(self.cos, self.sin),
+                         q_out=self.q[:R])
+            ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos, scale,
+                           self.attn[:R])
+            ops.decode_gemv(self.attn[:R], lw["o"], self.xmid[:R], residual=x, ws=g)
+            ops.rmsnorm_fwd(self.xmid[:R], lw["ln_post"], self.xn2[:R], self.rstd[:R], dims.rms_eps)
+            ops.decode_gemv(self.xn2[:R], lw["gu"], self.gu[:R], ws=g)
+            ops.swiglu_fwd(self.gu[:R], self.h[:R])
+            ops.decode_gemv(self.h[:R], lw["down"], xo, residual=self.xmid[:R], ws=g)
+            x, xo = xo, x
+        self._head_and_sample(x, R)
+
+    # ----------------------------------------------------------------- generate
+    def uniforms(self, seed: int, B: int) -> torch.Tensor:
+        """The sampler's uniforms [n_img_tokens, B] for a seed (set_seed(seed) in the reference
+        seeds torch.multinomial; here a CPU generator seeds the inverse-CDF draws)."""
+        g = torch.Generator(device="cpu").manual_seed(int(seed))
+        return torch.rand(self.n_img, B, generator=g)
+
+    @torch.inference_mode()
+    def generate(self, prompts: Sequence[Sequence[int]], seed: int = 0, use_graph: bool = True,
+                 record_probs: bool = False) -> torch.Tensor:
+        """prompts: B lists of token ids (tokenizer.encode of the formatted prompt, BOS included).
+        Returns the image-token ids int32 [B, n_img_tokens] (on the device)."""
+        dims = self.dims
+        B = len(prompts)
+        if not 1 <= B <= self.max_batch:
+            raise ValueError(f"batch of {B} prompts, capacity {self.max_batch}")
+        for p in prompts:
+            if not 1 <= len(p) <= self.max_prompt:
+                raise ValueError(f"prompt length {len(p)} outside [1, {self.max_prompt}]")
+            if min(p) < 0 or max(p) >= dims.vocab:
+                raise ValueError(f"token id out of range [0, {dims.vocab})")
+        R = 2 * B
+        toks, start, Lp = self._prompt_rows(prompts)
+        self.u.zero_()
+        self.u[: self.n_img * B].copy_(self.uniforms(seed, B).reshape(-1))
+        self.start[:R].copy_(start)
+        self.pos.fill_(Lp)      # the first decoded token sits at position Lp
+        self.step.fill_(0)
+        self.tokens.zero_()
+        self.probs = (torch.zeros(self.n_img, B, dims.img_vocab, dtype=torch.float32, device=self.device)
+                      if record_probs else None)
+        self._host_step = 0
+        self._prefill(toks, Lp)          # step 0 (+ advance: pos = Lp, step = 1 after it)
+        self.pos.fill_(Lp)
+        n_rest = self.n_img - 1
+        if use_graph and not record_probs:
+            if self._graph is None or self._graph_B != B:
+                torch.cuda.synchronize(self.device)
+                self._graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._graph):
+                    self._decode_step(R)
+                self._graph_B = B
+            for _ in range(n_rest):
+                self._graph.replay()
+        else:
+            for s in range(n_rest):
+                self._host_step = s + 1
+                self._decode_step(R)
+        return self.tokens[:B]

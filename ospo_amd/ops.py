@@ -385,3 +385,51 @@ def sumsq(g, out):
 def adamw_clip(p, g, m, v, lr, beta1, beta2, eps, wd, step, sumsq_buf, max_norm):
     call("ospo_adamw_clip", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
          float(eps), float(wd), int(step), _p(sumsq_buf), float(max_norm), _s())
+
+
+# ------------------------------------------------------ step-3 T2I decode (config 4)
+def decode_gemv_ws(R: int, N: int, K: int, device) -> torch.Tensor:
+    nbytes = query("ospo_decode_gemv_ws_bytes", R, N, K)
+    return torch.empty(max(nbytes // 4, 4), dtype=torch.float32, device=device)
+
+
+def decode_gemv(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu: bool = False, residual=None,
+                ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[R, N] = act(x . w^T + bias) (+ residual), R <= 64 (weight-streaming decode GEMV)."""
+    for t, n in ((x, "x"), (w, "w"), (out, "out")):
+        _chk(t, BF16, n)
+    R, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K or out.shape != (R, N):
+        raise ValueError(f"decode_gemv shape mismatch x{tuple(x.shape)} w{tuple(w.shape)} out{tuple(out.shape)}")
+    call("ospo_decode_gemv", _p(w), _ld(w), _p(x), _ld(x), R, N, K, _p(bias), int(gelu), _p(residual),
+         _ld(residual) if residual is not None else 0, _p(out), _ld(out), _p(ws), 0 if ws is None else ws.numel() * 4,
+         _s())
+    return out
+
+
+def kv_store(qkv, R, nq, pos_dev, k_cache, v_cache, n_heads, Tmax, *, rope=None, q_out=None):
+    cos, sin = rope if rope is not None else (None, None)
+    call("ospo_kv_store", _p(qkv), _ld(qkv), R, nq, _p(pos_dev), int(rope is not None), _p(cos), _p(sin), _p(k_cache),
+         _p(v_cache), n_heads, 128, Tmax, _p(q_out), _ld(q_out) if q_out is not None else 0, _s())
+
+
+def attn_cache(q, k_cache, v_cache, R, nq, n_heads, Tmax, start, pos_dev, scale, out):
+    call("ospo_attn_cache", _p(q), _ld(q), _p(k_cache), _p(v_cache), R, nq, n_heads, 128, Tmax, _p(start),
+         _p(pos_dev), float(scale), _p(out), _ld(out), _s())
+    return out
+
+
+def cfg_sample(logits, B, cfg_weight, temperature, u, step_dev, n_steps, tokens, next_ids, probs_out=None):
+    V = logits.shape[1]
+    call("ospo_cfg_sample", _p(logits), _ld(logits), V, B, float(cfg_weight), float(temperature), _p(u), _p(step_dev),
+         n_steps, _p(tokens), _p(next_ids), _p(probs_out), _s())
+
+
+def embed_rows(ids, table, out):
+    call("ospo_embed_rows", _p(ids), ids.numel(), _p(table), table.shape[0], table.shape[1], _p(out), _s())
+    return out
+
+
+def decode_advance(pos_dev, step_dev):
+    call("ospo_decode_advance", _p(pos_dev), _p(step_dev), _s())
