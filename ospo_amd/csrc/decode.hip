@@ -21,6 +21,8 @@
 #include "common.h"
 #include "skinny.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int HD = 128;  // head_dim (Janus-Pro)
@@ -96,6 +98,93 @@ __global__ __launch_bounds__(64 * NT) void gemv_reduce_kernel(const f32x4* __res
   for (int q = 0; q < 4; ++q) {
     const int r = 16 * j + 4 * g + q;
     if (r < R) gemv_store(v[q], r, n, bias, gelu, res, ldr, out, ldo);
+  }
+}
+
+// GEMV v2: a workgroup owns 64 weight rows (wave w: rows 16w..16w+15) x a K range; the R <= 32
+// activation rows of each 512-k chunk are staged once in LDS (one 1-KiB LDS-DMA per row, pitch
+// 1040 B so the 16 fragment rows of a ds_read_b128 land in distinct banks) and shared by the four
+// waves, while each wave streams its 16 weight rows with all of the chunk's loads (16 x 1 KiB) in
+// flight at once.  v1 above re-read x from L2 for every 16 weight rows (2x the weight traffic).
+constexpr int G2_ROWS = 64, G2_KC = 512, G2_PITCH = G2_KC * 2 + 16;
+template <int NT>
+__global__ __launch_bounds__(256) void gemv2_kernel(const bf16* __restrict__ W, int ldw, const bf16* __restrict__ X,
+                                                    int ldx, int R, int K, int kper, const bf16* __restrict__ bias,
+                                                    int gelu, const bf16* __restrict__ res, int ldr,
+                                                    bf16* __restrict__ out, int ldo, f32x4* __restrict__ ws) {
+  __shared__ __attribute__((aligned(16))) char xs[16 * NT * G2_PITCH];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int n = blockIdx.x * G2_ROWS + wave * 16 + l16;
+  const int z = blockIdx.y, splits = gridDim.y;
+  const int k_begin = z * kper, k_end = min(K, k_begin + kper);
+  const bf16* wrow = W + (long)n * ldw;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = k_begin; kc < k_end; kc += G2_KC) {
+    const int nsteps = min(G2_KC, k_end - kc) >> 5;
+    // stage x rows [0, 16 NT) x [kc, kc + 512): wave w takes rows w, w+4, ...
+    for (int r = wave; r < 16 * NT; r += 4) {
+      const int rr = r < R ? r : R - 1;  // rows >= R are masked at the fragment
+      const int col = min(kc + 8 * lane, K - 8);
+      __builtin_amdgcn_global_load_lds(X + (long)rr * ldx + col, (LDS_AS void*)(xs + r * G2_PITCH), 16, 0, 0);
+    }
+    asm volatile("" ::: "memory");  // the x DMA is issued before the weight loads (the vmcnt below counts on it)
+    bf16x8 wv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = kc + 32 * min(s, nsteps - 1) + 8 * g;
+      wv[s] = *reinterpret_cast<const bf16x8*>(wrow + k);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the x DMA (issued first) has landed
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < nsteps) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          bf16x8 xf = *reinterpret_cast<const bf16x8*>(xs + (16 * j + l16) * G2_PITCH + (32 * s + 8 * g) * 2);
+          if (16 * j + l16 >= R) xf = bf16x8{};
+          acc[j] = MFMA(xf, wv[s], acc[j]);  // D[x row 4g+q][w row l16]
+        }
+      }
+    }
+    __syncthreads();  // every wave done with the chunk before it is restaged
+  }
+  const int nb = n >> 4;
+  if (splits > 1) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) ws[((long)(z * (gridDim.x * 4) + nb) * NT + j) * 64 + lane] = acc[j];
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * j + 4 * g + q;
+      if (r < R) gemv_store(acc[j][q], r, n, bias, gelu, res, ldr, out, ldo);
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void gemv2_reduce_kernel(const f32x4* __restrict__ ws, int splits, int NB, int R,
+                                                           const bf16* __restrict__ bias, int gelu,
+                                                           const bf16* __restrict__ res, int ldr,
+                                                           bf16* __restrict__ out, int ldo) {
+  const int lane = threadIdx.x & 63, nb = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (nb >= NB) return;
+  const int n = nb * 16 + (lane & 15), g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < splits; ++z) v += ws[((long)(z * NB + nb) * NT + j) * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * j + 4 * g + q;
+      if (r < R) gemv_store(v[q], r, n, bias, gelu, res, ldr, out, ldo);
+    }
   }
 }
 
@@ -374,13 +463,32 @@ int gemv_splits(int nblocks, int K) {
   while (nblocks * s < 1024 && (K >> 5) / (2 * s) >= 8 * SK_WAVES) s *= 2;
   return s;
 }
+int g_gemv_variant = 2;  // 1 = skinny-loop GEMV, 2 = LDS-shared x (default); A/B knob
+// v2 K split: ~1024 workgroups, at least one 512-k chunk each; returns k per split (multiple of 32)
+int gemv2_kper(int N, int K) {
+  const int groups = N / G2_ROWS;
+  int splits = (1024 + groups - 1) / groups;
+  splits = std::max(1, std::min(splits, K / G2_KC));
+  int kper = (K + splits - 1) / splits;
+  return (kper + 31) / 32 * 32;
+}
 
 }  // namespace
 
 extern "C" size_t ospo_decode_gemv_ws_bytes(int R, int N, int K) {
   if (R <= 0 || R > 64 || N <= 0 || N % 16 || K <= 0) return 0;
   const int nt = (R + 15) / 16, nb = N / 16;
-  return (size_t)gemv_splits(nb, K) * nb * nt * 64 * sizeof(f32x4);
+  const size_t v1 = (size_t)gemv_splits(nb, K) * nb * nt * 64 * sizeof(f32x4);
+  if (N % G2_ROWS || K % 32) return v1;
+  const int kper = gemv2_kper(N, K);
+  const size_t v2 = (size_t)((K + kper - 1) / kper) * nb * nt * 64 * sizeof(f32x4);
+  return std::max(v1, v2);
+}
+
+extern "C" int ospo_set_gemv_variant(int v) {
+  if (v != 1 && v != 2) return OSPO_ERR_ARG;
+  g_gemv_variant = v;
+  return OSPO_OK;
 }
 
 extern "C" int ospo_decode_gemv(const void* W, int ldw, const void* X, int ldx, int R, int N, int K, const void* bias,
@@ -391,11 +499,31 @@ extern "C" int ospo_decode_gemv(const void* W, int ldw, const void* X, int ldx, 
   if (ldw < K || ldx < K || ldo < N || ldw % 8 || ldx % 8 || (residual && (ldr < N))) return OSPO_ERR_SHAPE;
   if (!aligned16(W) || !aligned16(X)) return OSPO_ERR_ALIGN;
   const int nt = (R + 15) / 16, nb = N / 16;
-  const int splits = gemv_splits(nb, K);
-  if (splits > 1 && (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws))) return OSPO_ERR_ARG;
   const bf16 *w = (const bf16*)W, *x = (const bf16*)X, *bs = (const bf16*)bias, *rs = (const bf16*)residual;
   bf16* o = (bf16*)out;
   f32x4* wsp = (f32x4*)ws;
+  if (g_gemv_variant == 2 && R <= 32 && N % G2_ROWS == 0 && K >= 8) {
+    const int kper = gemv2_kper(N, K);
+    const int splits = (K + kper - 1) / kper;
+    if (splits > 1 && (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws))) return OSPO_ERR_ARG;
+    const dim3 grid(N / G2_ROWS, splits);
+#define GEMV2(NT_)                                                                                              \
+  hipLaunchKernelGGL((gemv2_kernel<NT_>), grid, dim3(256), 0, stream, w, ldw, x, ldx, R, K, kper, bs, gelu, rs, ldr, \
+                     o, ldo, wsp);                                                                              \
+  if (splits > 1)                                                                                               \
+    hipLaunchKernelGGL((gemv2_reduce_kernel<NT_>), dim3((nb + 3) / 4), dim3(256), 0, stream, wsp, splits, nb, R, bs,  \
+                       gelu, rs, ldr, o, ldo);
+    if (nt == 1) {
+      GEMV2(1)
+    } else {
+      GEMV2(2)
+    }
+#undef GEMV2
+    OSPO_CHECK_LAUNCH();
+    return OSPO_OK;
+  }
+  const int splits = gemv_splits(nb, K);
+  if (splits > 1 && (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws))) return OSPO_ERR_ARG;
   const dim3 grid(nb, splits);
 #define GEMV(NT_)                                                                                                   \
   hipLaunchKernelGGL((gemv_kernel<NT_>), grid, dim3(64 * SK_WAVES), 0, stream, w, ldw, x, ldx, R, K, bs, gelu, rs, ldr, \
