@@ -60,6 +60,7 @@ SIGNATURES = {
     "ospo_embed_rows": [P, L, P, I, I, P, P],
     "ospo_decode_advance": [P, P, P],
     "ospo_set_gemv_variant": [I],
+    "ospo_set_skinny_variant": [I],
     "ospo_sumsq": [P, L, P, P],
     "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],
 }

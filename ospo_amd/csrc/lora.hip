@@ -140,6 +140,131 @@ __global__ __launch_bounds__(64 * NT) void skinny_reduce_kernel(const f32x4* __r
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v2: 64 activation rows per workgroup (wave w: rows 16w..16w+15) streamed with a whole chunk of
+// loads in flight per wave, the small LoRA operand (Bt rows of this launch's tiles) staged once
+// per chunk in LDS and shared by the four waves -- v1 re-read it from L2 for every 16 rows, which
+// was (n_tiles x) the activation traffic.  Dense (u, forward, optional dropout on A) or
+// block-diagonal (g, backward: grid z = module, its tiles reduce over its own K block of A).
+// Split-K partials: fp32 [split][M_pad][16 * n_tiles] + skinny2_reduce_kernel.
+template <int NT>
+struct Sk2Cfg {
+  static constexpr int KC = NT <= 2 ? 512 : (NT <= 4 ? 256 : 128);  // k per LDS chunk
+  static constexpr int PITCH = 2 * KC + 16;                           // 16-row fragment reads hit distinct banks
+  static constexpr int STEPS = KC / 32;
+};
+
+template <int NT, bool DROP>
+__global__ __launch_bounds__(256) void skinny2_kernel(const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bt,
+                                                      int ldb, int b_rows, int M, int M_out, int K, int kper,
+                                                      int a_koff, int tiles_total, float scale, bf16* __restrict__ out,
+                                                      int ldo, int out_cols, float* __restrict__ ws, int M_pad,
+                                                      uint32_t dseed, uint32_t dthresh, float dscale,
+                                                      bf16* __restrict__ xd, int ldxd) {
+  using C = Sk2Cfg<NT>;
+  __shared__ __attribute__((aligned(16))) char bs[16 * NT * C::PITCH];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int m = blockIdx.x * 64 + wave * 16 + l16;
+  const int mr = m < M ? m : M - 1;
+  const int z = blockIdx.y, splits = gridDim.y, mod = blockIdx.z;
+  const int tbase = mod * NT;                              // first output tile of this workgroup
+  const bf16* arow = A + (long)mr * lda + (long)mod * a_koff;
+  const int k_begin = z * kper, k_end = min(K, k_begin + kper);
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = k_begin; kc < k_end; kc += C::KC) {
+    const int nsteps = min(C::KC, k_end - kc) >> 5;
+    // stage Bt rows [16 tbase, 16 (tbase + NT)) x [kc, kc + KC): one LDS-DMA per (row, 1 KiB piece)
+    constexpr int PIECES = C::KC / 512 > 0 ? C::KC / 512 : 1, LANES = C::KC >= 512 ? 64 : C::KC / 8;
+    for (int t = wave; t < 16 * NT * PIECES; t += 4) {
+      const int r = t / PIECES, pc = t % PIECES;
+      const int br = min(16 * tbase + r, b_rows - 1);  // rows >= b_rows are masked at the fragment
+      const int col = min(kc + pc * 512 + 8 * lane, K - 8);
+      if (LANES == 64 || lane < LANES)  // a row image is 2 KC bytes: lanes past it must not write the next row's
+        __builtin_amdgcn_global_load_lds(Bt + (long)br * ldb + col, (LDS_AS void*)(bs + r * C::PITCH + pc * 1024),
+                                         16, 0, 0);
+    }
+    asm volatile("" ::: "memory");  // the Bt DMA is issued before the activation loads (counted below)
+    bf16x8 av[C::STEPS];
+#pragma unroll
+    for (int s = 0; s < C::STEPS; ++s) {
+      const int k = kc + 32 * min(s, nsteps - 1) + 8 * g;
+      av[s] = *reinterpret_cast<const bf16x8*>(arow + k);
+    }
+    if constexpr (C::STEPS >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if constexpr (C::STEPS >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < C::STEPS; ++s) {
+      if (s < nsteps) {
+        bf16x8 a = av[s];
+        if constexpr (DROP) {
+          const int k0 = kc + 32 * s + 8 * g;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const bool keep = drop_hash((uint32_t)mr * (uint32_t)K + (uint32_t)(k0 + e), dseed) >= dthresh;
+            a[e] = keep ? f2bf(bf2f(a[e]) * dscale) : f2bf(0.f);
+          }
+          if (xd && m < M) *reinterpret_cast<bf16x8*>(xd + (long)m * ldxd + k0) = a;
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          bf16x8 bfr = *reinterpret_cast<const bf16x8*>(bs + (16 * j + l16) * C::PITCH + (32 * s + 8 * g) * 2);
+          if (16 * (tbase + j) + l16 >= b_rows) bfr = bf16x8{};
+          acc[j] = MFMA(bfr, a, acc[j]);  // D[c = 16 j + 4 g + q][m = l16]
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int ctot = 16 * tiles_total;
+  if (splits > 1) {
+    if (m < M_pad) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        *reinterpret_cast<f32x4*>(ws + ((long)z * M_pad + m) * ctot + 16 * (tbase + j) + 4 * g) = acc[j];
+    }
+    return;
+  }
+  if (m < M_out) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      uint2 pk;
+      if (m < M) {
+        pk.x = pack2(acc[j][0] * scale, acc[j][1] * scale);
+        pk.y = pack2(acc[j][2] * scale, acc[j][3] * scale);
+      } else {
+        pk.x = pk.y = 0u;
+      }
+      *reinterpret_cast<uint2*>(out + (long)m * ldo + 16 * (tbase + j) + 4 * g) = pk;
+    }
+    if (mod == gridDim.z - 1 && g == 0) {  // zero the padding columns of this lane's row
+      for (int c = ctot; c < out_cols; ++c) out[(long)m * ldo + c] = f2bf(0.f);
+    }
+  }
+}
+
+// out[m][c] = bf16(scale * sum_z ws[z][m][c]) for c < ctot, 0 for ctot <= c < out_cols; rows >= M zero
+__global__ void skinny2_reduce_kernel(const float* __restrict__ ws, int splits, int M, int M_out, int M_pad, int ctot,
+                                      float scale, bf16* __restrict__ out, int ldo, int out_cols) {
+  const int cq = out_cols / 4;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (long)M_out * cq) return;
+  const int m = (int)(tid / cq), c = (int)(tid % cq) * 4;
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (m < M && c < ctot) {
+    for (int z = 0; z < splits; ++z) v += *reinterpret_cast<const f32x4*>(ws + ((long)z * M_pad + m) * ctot + c);
+  }
+  uint2 pk;
+  pk.x = pack2(v[0] * scale, v[1] * scale);
+  pk.y = pack2(v[2] * scale, v[3] * scale);
+  *reinterpret_cast<uint2*>(out + (long)m * ldo + c) = pk;
+}
+
 }  // namespace
 
 // K splits: enough workgroups to keep every CU streaming (>= ~4 per CU), each
@@ -151,18 +276,75 @@ static int skinny_splits(int M_out, int K) {
   return s;
 }
 
-extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
-  const long rb = (M_out + 15) / 16;
-  const int sp = skinny_splits(M_out, K);
-  return (size_t)(sp > 1 ? sp : 0) * rb * n_tiles * 64 * sizeof(f32x4) + 16;
-}
-
 struct SkDropArgs {
   uint32_t seed = 0, thresh = 0;
   float scale = 0.f;  // > 0: dropout on
   bf16* xd = nullptr;
   int ldxd = 0;
 };
+
+static int g_skinny_variant = 2;  // 1 = 16-row skinny loop, 2 = 64-row LDS-shared (default); A/B knob
+
+// v2 K split: ~1024 workgroups over (64-row blocks x modules), each split >= one chunk
+static int skinny2_kper(int M_out, int K, int nz, int KC) {
+  const int blocks = (M_out + 63) / 64 * nz;
+  int splits = (1024 + blocks - 1) / blocks;
+  splits = splits < 1 ? 1 : splits;
+  const int maxs = K / KC > 0 ? K / KC : 1;
+  splits = splits > maxs ? maxs : splits;
+  const int kper = (K + splits - 1) / splits;
+  return (kper + 31) / 32 * 32;
+}
+
+extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
+  const long rb = (M_out + 15) / 16;
+  const int sp = skinny_splits(M_out, K);
+  const size_t v1 = (size_t)(sp > 1 ? sp : 0) * rb * n_tiles * 64 * sizeof(f32x4) + 16;
+  // v2: the worst case over its tilings (KC = 128 .. 512, one module or n_tiles modules)
+  size_t v2 = 0;
+  for (int nz = 1; nz <= n_tiles; nz = nz * 2 > n_tiles && nz < n_tiles ? n_tiles : nz * 2) {
+    for (int KC = 128; KC <= 512; KC *= 2) {
+      const int kper = skinny2_kper(M_out, K, nz, KC);
+      const size_t sp2 = (K + kper - 1) / kper;
+      const size_t b = sp2 > 1 ? sp2 * (size_t)((M_out + 63) / 64 * 64) * 16 * n_tiles * 4 : 0;
+      v2 = b > v2 ? b : v2;
+    }
+    if (nz == n_tiles) break;
+  }
+  return (v1 > v2 ? v1 : v2) + 16;
+}
+
+extern "C" int ospo_set_skinny_variant(int v) {
+  if (v != 1 && v != 2) return OSPO_ERR_ARG;
+  g_skinny_variant = v;
+  return OSPO_OK;
+}
+
+template <int NT>
+static int launch_skinny2(const bf16* a, int lda, const bf16* b, int ldb, int b_rows, int M, int M_out, int K,
+                          int a_koff, int nz, int tiles_total, float scale, bf16* o, int ldo, int out_cols, float* part,
+                          size_t ws_bytes, hipStream_t stream, const SkDropArgs& dr) {
+  const int kper = skinny2_kper(M_out, K, nz, Sk2Cfg<NT>::KC);
+  const int splits = (K + kper - 1) / kper;
+  const int M_pad = (M_out + 63) / 64 * 64;
+  if (splits > 1 && ws_bytes < (size_t)splits * M_pad * 16 * tiles_total * 4) return OSPO_ERR_SHAPE;
+  const dim3 grid(M_pad / 64, splits, nz);
+  if (dr.scale > 0.f)
+    hipLaunchKernelGGL((skinny2_kernel<NT, true>), grid, dim3(256), 0, stream, a, lda, b, ldb, b_rows, M, M_out, K,
+                       kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad, dr.seed, dr.thresh, dr.scale,
+                       dr.xd, dr.ldxd);
+  else
+    hipLaunchKernelGGL((skinny2_kernel<NT, false>), grid, dim3(256), 0, stream, a, lda, b, ldb, b_rows, M, M_out, K,
+                       kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad, 0u, 0u, 0.f, nullptr, 0);
+  OSPO_CHECK_LAUNCH();
+  if (splits > 1) {
+    const long n = (long)M_out * (out_cols / 4);
+    hipLaunchKernelGGL(skinny2_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, part, splits,
+                       M, M_out, M_pad, 16 * tiles_total, scale, o, ldo, out_cols);
+    OSPO_CHECK_LAUNCH();
+  }
+  return OSPO_OK;
+}
 
 #define SK_LAUNCH(NTV, DV)                                                                                        \
   hipLaunchKernelGGL((skinny_kernel<NTV, DV>), grid, block, 0, stream, a, lda, b, ldb, b_rows, M, M_out, K, a_koff, \
@@ -224,6 +406,21 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
   const bf16* b = (const bf16*)Bt;
   bf16* o = (bf16*)out;
   f32x4* part = (f32x4*)ws;
+  if (g_skinny_variant == 2 && out_cols % 4 == 0 && K >= 128) {
+    // dense: one workgroup column over all n-tiles; block-diagonal: grid z = module
+    const int nz = a_koff > 0 ? nmods : 1;
+    const int nt = a_koff > 0 ? module_tiles : n_tiles;
+    float* p2 = (float*)ws;
+    switch (nt) {
+      case 1: return launch_skinny2<1>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 2: return launch_skinny2<2>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 3: return launch_skinny2<3>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 4: return launch_skinny2<4>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 6: return launch_skinny2<6>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 8: return launch_skinny2<8>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      default: break;  // other tile counts: v1 below
+    }
+  }
   if (a_koff > 0 && module_tiles == 1 && n_tiles <= 4)  // one launch: n-tile j reduces over block j of A
     return launch_skinny(a, lda, b, ldb, b_rows, M, M_out, K, n_tiles, a_koff, scale, o, ldo, out_cols, part, stream,
                          dr);
