@@ -147,6 +147,74 @@ def bench_t2i(args):
     print(json.dumps(line), flush=True)
 
 
+def vq_flops_per_image(H=384, W=384):
+    """Algorithmic FLOPs of the VQ-16 encoder + quant_conv on one H x W image: every convolution
+    2 * Ho * Wo * Cout * Cin * KH * KW, the AttnBlock products 2 * 2 * n^2 * C (n = tokens)."""
+    ch, mult = 128, (1, 1, 2, 2, 4)
+    h, w = H, W
+    f = 2 * h * w * ch * 3 * 9  # conv_in
+    cin = ch
+    for i, m in enumerate(mult):
+        cout = ch * m
+        for j in range(2):
+            f += 2 * h * w * cout * cin * 9 + 2 * h * w * cout * cout * 9
+            if cin != cout:
+                f += 2 * h * w * cout * cin
+            cin = cout
+            if i == len(mult) - 1:
+                f += 4 * 2 * h * w * cin * cin + 4 * (h * w) ** 2 * cin
+        if i != len(mult) - 1:
+            h, w = h // 2, w // 2
+            f += 2 * h * w * cin * cin * 9
+    f += 2 * (2 * h * w * cin * cin * 9) * 2 + 4 * 2 * h * w * cin * cin + 4 * (h * w) ** 2 * cin  # mid
+    f += 2 * h * w * 256 * cin * 9 + 2 * h * w * 8 * 256  # conv_out, quant_conv
+    return f
+
+
+def bench_vq(args):
+    """VQ-16 image tokenizer (gen_vision_model.encode), fp32, 384 px, a batch of
+    images per call; value = images/s.  Roofline: f32 MFMA (157.3 TF dense, MI355X_MICROARCH.md)."""
+    from ospo_amd.vq import VQEncoder
+    from oracle import vq_ref as V  # weights only: seeded init under the reference's names
+    dev = torch.device("cuda", 0)
+    w = V.init_vq_weights(0)
+    enc = VQEncoder(w, device=dev)
+    B = args.vq_batch
+    g = torch.Generator().manual_seed(0)
+    x = (torch.rand(B, 3, 384, 384, generator=g) * 2 - 1).to(dev)
+    for _ in range(args.warmup):
+        enc.encode(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ids = enc.encode(x)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    value = B * args.steps / dt
+    fl = vq_flops_per_image()
+    achieved = value * fl / 1e12
+    line = {
+        "metric": "images/sec, Janus-Pro VQ-16 tokenizer encode (384 px -> 576 ids), fp32",
+        "value": round(value, 2), "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded VQ-16 weights, random pixels)",
+        "config": {"workload": f"VQ-16 encode + quantize, {B} images of 384x384 per call",
+                   "algorithmic_gflop_per_image": round(fl / 1e9, 1)},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": 157.3, "unit": "TFLOP/s",
+                     "frac": round(achieved / 157.3, 4), "traffic": None,
+                     "kernel": "whole encode (conv_f32_kernel implicit GEMM on v_mfma_f32_32x32x2_f32 dominates)"},
+        "ids_checksum": int(ids.long().sum().item()),
+    }
+    if not args.no_cpu_baseline:
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
+        t0 = time.perf_counter()
+        V.encode_ref(x[:1].cpu(), w)
+        tc = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": round(1.0 / tc, 4), "unit": "images/s", "cores": torch.get_num_threads(),
+                                "kind": "port", "sample": f"1 image, oracle/vq_ref.py encode_ref fp32 ({tc:.2f} s)"}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,7 +229,8 @@ def main():
     ap.add_argument("--lora-dropout", type=float, default=0.05)
     # BASELINE config 5: the frozen decoder Linears on MXFP8 block-scaled fp8 MFMA (use with --lora-r 32)
     ap.add_argument("--linear-dtype", choices=("bf16", "mx8"), default="bf16")
-    ap.add_argument("--workload", choices=("simpo", "t2i"), default="simpo")  # t2i: BASELINE config 4
+    ap.add_argument("--workload", choices=("simpo", "t2i", "vq"), default="simpo")  # t2i: config 4; vq: §8f-3
+    ap.add_argument("--vq-batch", type=int, default=16)
     ap.add_argument("--t2i-batch", type=int, default=16)       # parallel_size: prompts (x2 rows with CFG)
     ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -169,6 +238,8 @@ def main():
     args = ap.parse_args()
     if args.workload == "t2i":
         return bench_t2i(args)
+    if args.workload == "vq":
+        return bench_vq(args)
 
     from ospo_amd import dist as odist
     from ospo_amd import ops

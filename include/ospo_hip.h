@@ -294,6 +294,33 @@ int ospo_set_skinny_variant(int v);
 /* A/B knob of the decode GEMV schedule: 1 = skinny loop, 2 = LDS-shared activations (default). */
 int ospo_set_gemv_variant(int v);
 
+/* ------------------------------------------------------- VQ image tokenizer ---
+ * janus/models/vq_model.py Encoder (:46-124) + quant_conv + VectorQuantizer
+ * (:236-282) = gen_vision_model.encode, called per image at ospo/wrapper/train.py:246-264.  fp32
+ * (the ids must be exact), NHWC activations, conv weights [Cout][KH][KW][Cin].
+ * ospo_vq_conv2d: out = conv(x) + bias (+ residual); zero padding pad_t/pad_l on top/left and
+ *   whatever (Ho, Wo, stride) reach past the bottom/right (Downsample's (0,1,0,1) pad).
+ * ospo_vq_bmm_nt: out[b] = x[b] . w[b]^T ([n_rows, K] x [n_cols, K]), AttnBlock's q.k^T and p.v^T.
+ * ospo_vq_groupnorm: GroupNorm(G, eps) over [B][HW][C] (+ swish), ws >= ospo_vq_groupnorm_ws_bytes.
+ * ospo_vq_softmax_rows: in place, rows of softmax(x * scale).
+ * ospo_vq_transpose: [B][R][C] -> [B][C][R].
+ * ospo_vq_l2norm_rows: F.normalize(x, dim=-1) of [n][d].
+ * ospo_vq_quantize: ids[v] = argmin_c |zn_v|^2 + |e_c|^2 - 2 zn_v.e_c (first index on ties),
+ *   zn = F.normalize(z), e = the normalised codebook; dmin (optional) = the minimum. */
+int ospo_vq_conv2d(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int KH, int KW,
+                   int stride, int pad_t, int pad_l, int Ho, int Wo, const float* bias, const float* residual,
+                   float* out, hipStream_t stream);
+int ospo_vq_bmm_nt(const float* x, const float* w, int B, int n_rows, int n_cols, int K, float* out,
+                   hipStream_t stream);
+size_t ospo_vq_groupnorm_ws_bytes(int B, int G);
+int ospo_vq_groupnorm(const float* x, int B, int HW, int C, int G, const float* gamma, const float* beta,
+                      float eps, int swish, float* out, void* ws, size_t ws_bytes, hipStream_t stream);
+int ospo_vq_softmax_rows(float* x, int rows, int cols, float scale, hipStream_t stream);
+int ospo_vq_transpose(const float* x, int B, int R, int C, float* out, hipStream_t stream);
+int ospo_vq_l2norm_rows(const float* x, long n, int d, float* out, hipStream_t stream);
+int ospo_vq_quantize(const float* z, long n, int e_dim, const float* codebook_l2, int n_codes, int* ids,
+                     float* dmin, hipStream_t stream);
+
 /* ------------------------------------------------------------ optimizer ---
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip
  * (ospo/utils/train.py:30, gradient_clip_val) + torch AdamW

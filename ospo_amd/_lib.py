@@ -61,11 +61,19 @@ SIGNATURES = {
     "ospo_decode_advance": [P, P, P],
     "ospo_set_gemv_variant": [I],
     "ospo_set_skinny_variant": [I],
+    "ospo_vq_conv2d": [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, P, P, P],
+    "ospo_vq_bmm_nt": [P, P, I, I, I, I, P, P],
+    "ospo_vq_groupnorm_ws_bytes": [I, I],
+    "ospo_vq_groupnorm": [P, I, I, I, I, P, P, F, I, P, P, Z, P],
+    "ospo_vq_softmax_rows": [P, I, I, F, P],
+    "ospo_vq_transpose": [P, I, I, I, P, P],
+    "ospo_vq_l2norm_rows": [P, L, I, P, P],
+    "ospo_vq_quantize": [P, L, I, P, I, P, P, P],
     "ospo_sumsq": [P, L, P, P],
     "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],
 }
 
-RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
+RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 

@@ -1,0 +1,161 @@
+"""VQ image tokenizer on the MI355X: Janus-Pro's ``gen_vision_model.encode``
+(``janus/models/vq_model.py``: Encoder :46-124, quant_conv, VectorQuantizer :236-282) -- pixels to the
+VQ ids the SimPO step consumes (``ospo/wrapper/train.py:246-264`` encodes each chosen / rejected
+image; here once, into a token cache, see ``build_token_cache``).
+
+fp32 on the HIP kernels of ``csrc/vq.hip`` (f32-MFMA implicit-GEMM convolutions, GroupNorm, the
+AttnBlock as two batched products + softmax, the quantizer); activations NHWC.  No fallback: the
+library must be present.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ._lib import call, query
+
+F32 = torch.float32
+VQ16 = dict(ch=128, ch_mult=(1, 1, 2, 2, 4), num_res_blocks=2, z_channels=256, n_codes=16384, e_dim=8,
+            in_channels=3)
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class VQEncoder:
+    """Device-resident VQ-16 encoder.  ``weights``: the reference's state_dict names
+    (``encoder.*``, ``quant_conv.*``, ``quantize.embedding.weight``), any float dtype."""
+
+    def __init__(self, weights: Dict[str, torch.Tensor], device="cuda", cfg=VQ16):
+        self.cfg, self.device = cfg, torch.device(device)
+        self.w = {}
+        for k, v in weights.items():
+            if not (k.startswith("encoder.") or k.startswith("quant_conv.") or k == "quantize.embedding.weight"):
+                continue
+            t = v.detach().to(device=self.device, dtype=F32)
+            if t.dim() == 4:  # conv [Cout, Cin, KH, KW] -> [Cout, KH, KW, Cin]
+                t = t.permute(0, 2, 3, 1)
+            self.w[k] = t.contiguous()
+        cb = self.w["quantize.embedding.weight"]
+        self.codebook = torch.empty_like(cb)
+        call("ospo_vq_l2norm_rows", _p(cb), cb.shape[0], cb.shape[1], _p(self.codebook), _s())
+        self.gn_ws = torch.empty(query("ospo_vq_groupnorm_ws_bytes", 64, 32) // 4 + 4, dtype=F32, device=self.device)
+
+    # -------------------------------------------------------------- pieces
+    def _conv(self, x, name, stride=1, pad=1, Ho=None, Wo=None, residual=None):
+        B, H, W, Cin = x.shape
+        wt, b = self.w[name + ".weight"], self.w.get(name + ".bias")
+        Cout, KH, KW, _ = wt.shape
+        Ho = Ho or (H + 2 * pad - KH) // stride + 1
+        Wo = Wo or (W + 2 * pad - KW) // stride + 1
+        out = torch.empty(B, Ho, Wo, Cout, dtype=F32, device=self.device)
+        call("ospo_vq_conv2d", _p(x), B, H, W, Cin, _p(wt), Cout, KH, KW, stride, pad, pad, Ho, Wo, _p(b),
+             _p(residual), _p(out), _s())
+        return out
+
+    def _gn(self, x, name, swish):
+        B, H, W, C = x.shape
+        out = torch.empty_like(x)
+        if B > 64:
+            raise ValueError("at most 64 images per encode call")
+        call("ospo_vq_groupnorm", _p(x), B, H * W, C, 32, _p(self.w[name + ".weight"]), _p(self.w[name + ".bias"]),
+             1e-6, int(swish), _p(out), _p(self.gn_ws), self.gn_ws.numel() * 4, _s())
+        return out
+
+    def _res(self, x, p, cin, cout):
+        h = self._conv(self._gn(x, p + ".norm1", True), p + ".conv1")
+        h = self._gn(h, p + ".norm2", True)
+        sc = self._conv(x, p + ".nin_shortcut", pad=0) if cin != cout else x
+        return self._conv(h, p + ".conv2", residual=sc)
+
+    def _attn(self, x, p):
+        B, H, W, C = x.shape
+        n = H * W
+        h = self._gn(x, p + ".norm", False)
+        q, k, v = (self._conv(h, p + "." + m, pad=0) for m in ("q", "k", "v"))
+        s = torch.empty(B, n, n, dtype=F32, device=self.device)
+        call("ospo_vq_bmm_nt", _p(q), _p(k), B, n, n, C, _p(s), _s())
+        call("ospo_vq_softmax_rows", _p(s), B * n, n, float(int(C) ** (-0.5)), _s())
+        vt = torch.empty(B, C, n, dtype=F32, device=self.device)
+        call("ospo_vq_transpose", _p(v), B, n, C, _p(vt), _s())
+        o = torch.empty(B, n, C, dtype=F32, device=self.device)
+        call("ospo_vq_bmm_nt", _p(s), _p(vt), B, n, C, n, _p(o), _s())
+        return self._conv(o.view(B, H, W, C), p + ".proj_out", pad=0, residual=x)
+
+    # -------------------------------------------------------------- encode
+    @torch.inference_mode()
+    def encode(self, pixels: torch.Tensor, return_z: bool = False):
+        """pixels fp32 [B, 3, H, W] in [-1, 1] (H, W multiples of 16) -> ids int32 [B, (H/16)(W/16)]
+        (+ z, the quant_conv output NHWC, and each token's minimum distance when return_z)."""
+        cfg = self.cfg
+        if pixels.dim() != 4 or pixels.shape[1] != cfg["in_channels"]:
+            raise ValueError(f"pixels must be [B, {cfg['in_channels']}, H, W], got {tuple(pixels.shape)}")
+        B, _, H, W = pixels.shape
+        if H % 16 or W % 16:
+            raise ValueError("H and W must be multiples of 16 (4 stride-2 downsamples)")
+        x = pixels.to(device=self.device, dtype=F32).permute(0, 2, 3, 1).contiguous()
+        ch, mult, nrb = cfg["ch"], cfg["ch_mult"], cfg["num_res_blocks"]
+        x = self._conv(x, "encoder.conv_in")
+        in_mult = (1,) + tuple(mult)
+        block_in = ch
+        for i, m in enumerate(mult):  # Encoder.forward :107-116
+            block_in, block_out = ch * in_mult[i], ch * m
+            for j in range(nrb):
+                x = self._res(x, f"encoder.conv_blocks.{i}.res.{j}", block_in, block_out)
+                block_in = block_out
+                if i == len(mult) - 1:
+                    x = self._attn(x, f"encoder.conv_blocks.{i}.attn.{j}")
+            if i != len(mult) - 1:  # Downsample: pad (0, 1, 0, 1), 3x3 stride 2, no implicit padding
+                Hc, Wc = x.shape[1], x.shape[2]
+                x = self._conv(x, f"encoder.conv_blocks.{i}.downsample.conv", stride=2, pad=0, Ho=Hc // 2, Wo=Wc // 2)
+        x = self._res(x, "encoder.mid.0", block_in, block_in)
+        x = self._attn(x, "encoder.mid.1")
+        x = self._res(x, "encoder.mid.2", block_in, block_in)
+        x = self._gn(x, "encoder.norm_out", True)
+        x = self._conv(x, "encoder.conv_out")
+        z = self._conv(x, "quant_conv", pad=0)  # [B, h, w, e]
+        n = z.shape[0] * z.shape[1] * z.shape[2]
+        ids = torch.empty(n, dtype=torch.int32, device=self.device)
+        dmin = torch.empty(n, dtype=F32, device=self.device) if return_z else None
+        call("ospo_vq_quantize", _p(z), n, cfg["e_dim"], _p(self.codebook), self.codebook.shape[0], _p(ids), _p(dmin),
+             _s())
+        ids = ids.view(B, -1)
+        return (ids, z, dmin.view(B, -1)) if return_z else ids
+
+
+def build_token_cache(encoder: VQEncoder, items: Iterable, out_path: str, size: int = 384, batch: int = 16):
+    """items: (key, image path) pairs -> ``out_path`` .npz of int32 VQ ids per key (the
+    ``dataset.train.token_cache`` the SimPO dataloader reads: keys "{item_id}/chosen|rejected").
+    Pixels: VLMImageProcessor with the gen processor's mean = std = 0.5 (bicubic resize to size)."""
+    from PIL import Image
+    keys, pix, out = [], [], {}
+
+    def flush():
+        if not keys:
+            return
+        ids = encoder.encode(torch.stack(pix)).cpu().numpy()
+        for k, row in zip(keys, ids):
+            out[k] = row.astype(np.int32)
+        keys.clear()
+        pix.clear()
+
+    for key, path in items:
+        im = Image.open(path).convert("RGB")
+        if im.size != (size, size):
+            im = im.resize((size, size), Image.BICUBIC)
+        a = torch.from_numpy(np.asarray(im, dtype=np.uint8).copy()).permute(2, 0, 1).float() / 255.0
+        keys.append(key)
+        pix.append((a - 0.5) / 0.5)
+        if len(keys) == batch:
+            flush()
+    flush()
+    np.savez_compressed(out_path, **out)
+    return out

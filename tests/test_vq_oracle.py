@@ -1,0 +1,35 @@
+"""CPU: the VQ tokenizer oracle (oracle/vq_ref.py) against the vectors the reference's own
+janus/models/vq_model.py produced (tests/golden/make_golden_vq.py): identical ids, z to fp32 noise."""
+import os
+
+import numpy as np
+import torch
+
+from oracle import vq_ref as V
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "vq_golden.npz")
+
+
+def test_vq_oracle_matches_reference_golden():
+    z = np.load(GOLD)
+    w = V.init_vq_weights(int(z["seed"]))
+    torch.set_num_threads(max(1, min(8, torch.get_num_threads())))
+    for i in range(3):
+        u8 = torch.from_numpy(z[f"img{i}_u8"])
+        x = (u8.permute(2, 0, 1).float()[None] / 255.0 - 0.5) / 0.5
+        ids, zq, margin = V.encode_ref(x, w)
+        assert torch.equal(ids.reshape(-1), torch.from_numpy(z[f"img{i}_ids"]))
+        ref = torch.from_numpy(z[f"img{i}_z"])
+        assert float((zq[0] - ref).abs().max() / ref.abs().max()) < 1e-4
+
+
+def test_vq_weight_names_and_plan():
+    w = V.init_vq_weights(0)
+    assert w["encoder.conv_in.weight"].shape == (128, 3, 3, 3)
+    assert w["encoder.conv_blocks.2.res.0.nin_shortcut.weight"].shape == (256, 128, 1, 1)
+    assert w["encoder.conv_blocks.4.attn.1.proj_out.weight"].shape == (512, 512, 1, 1)
+    assert w["quant_conv.weight"].shape == (8, 256, 1, 1)
+    cb = w["quantize.embedding.weight"]
+    assert cb.shape == (16384, 8) and torch.allclose(cb.norm(dim=1), torch.ones(16384), atol=1e-6)
+    kinds = [k for k, *_ in V.encoder_plan()]
+    assert kinds.count("down") == 4 and kinds.count("attn") == 3 and kinds.count("res") == 12
