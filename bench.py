@@ -174,10 +174,9 @@ def vq_flops_per_image(H=384, W=384):
 def bench_vq(args):
     """VQ-16 image tokenizer (gen_vision_model.encode), fp32, 384 px, a batch of
     images per call; value = images/s.  Roofline: f32 MFMA (157.3 TF dense, MI355X_MICROARCH.md)."""
-    from ospo_amd.vq import VQEncoder
-    from oracle import vq_ref as V  # weights only: seeded init under the reference's names
+    from ospo_amd.vq import VQEncoder, synthetic_vq_weights
     dev = torch.device("cuda", 0)
-    w = V.init_vq_weights(0)
+    w = synthetic_vq_weights(0)
     enc = VQEncoder(w, device=dev)
     B = args.vq_batch
     g = torch.Generator().manual_seed(0)
@@ -206,6 +205,7 @@ def bench_vq(args):
         "ids_checksum": int(ids.long().sum().item()),
     }
     if not args.no_cpu_baseline:
+        from oracle import vq_ref as V
         torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
         t0 = time.perf_counter()
         V.encode_ref(x[:1].cpu(), w)

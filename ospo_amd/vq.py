@@ -159,3 +159,105 @@ def build_token_cache(encoder: VQEncoder, items: Iterable, out_path: str, size: 
     flush()
     np.savez_compressed(out_path, **out)
     return out
+
+
+def load_vq_weights(path: Optional[str], seed: int = 0) -> Dict[str, torch.Tensor]:
+    """VQ-16 weights from a safetensors file (``gen_vision_model.*`` keys of a Janus-Pro checkpoint, or
+    bare ``encoder.* / quant_conv.* / quantize.*``), else seeded synthetic ones (no checkpoint offline)."""
+    if path:
+        from safetensors.torch import load_file
+        sd = load_file(path)
+        out = {}
+        for k, v in sd.items():
+            k2 = k[len("gen_vision_model."):] if k.startswith("gen_vision_model.") else k
+            if k2.startswith(("encoder.", "quant_conv.", "quantize.embedding")):
+                out[k2] = v
+        if "quantize.embedding.weight" not in out:
+            raise ValueError(f"{path}: no VQ weights (gen_vision_model.* / encoder.*) found")
+        return out
+    print(f"[ospo_amd.vq] no VQ weights given: seeded synthetic VQ-16 weights (seed {seed})")
+    return synthetic_vq_weights(seed)
+
+
+def synthetic_vq_weights(seed: int = 0, cfg=VQ16) -> Dict[str, torch.Tensor]:
+    """Random VQ-16 weights under the reference's state_dict names (fan-in scaled convs, unit-norm codebook)."""
+    g = torch.Generator().manual_seed(int(seed))
+    w: Dict[str, torch.Tensor] = {}
+    ch, mult = cfg["ch"], cfg["ch_mult"]
+
+    def conv(name, cin, cout, k):
+        w[name + ".weight"] = torch.randn(cout, cin, k, k, generator=g) / math.sqrt(cin * k * k)
+        w[name + ".bias"] = torch.randn(cout, generator=g) * 0.02
+
+    def norm(name, c):
+        w[name + ".weight"] = 1.0 + torch.randn(c, generator=g) * 0.05
+        w[name + ".bias"] = torch.randn(c, generator=g) * 0.05
+
+    def res(p, cin, cout):
+        norm(p + ".norm1", cin)
+        conv(p + ".conv1", cin, cout, 3)
+        norm(p + ".norm2", cout)
+        conv(p + ".conv2", cout, cout, 3)
+        if cin != cout:
+            conv(p + ".nin_shortcut", cin, cout, 1)
+
+    def attn(p, c):
+        norm(p + ".norm", c)
+        for n in ("q", "k", "v", "proj_out"):
+            conv(p + "." + n, c, c, 1)
+
+    conv("encoder.conv_in", cfg["in_channels"], ch, 3)
+    in_mult = (1,) + tuple(mult)
+    block_in = ch
+    for i, m in enumerate(mult):
+        block_in, block_out = ch * in_mult[i], ch * m
+        for j in range(cfg["num_res_blocks"]):
+            res(f"encoder.conv_blocks.{i}.res.{j}", block_in, block_out)
+            block_in = block_out
+            if i == len(mult) - 1:
+                attn(f"encoder.conv_blocks.{i}.attn.{j}", block_in)
+        if i != len(mult) - 1:
+            conv(f"encoder.conv_blocks.{i}.downsample.conv", block_in, block_in, 3)
+    res("encoder.mid.0", block_in, block_in)
+    attn("encoder.mid.1", block_in)
+    res("encoder.mid.2", block_in, block_in)
+    norm("encoder.norm_out", block_in)
+    conv("encoder.conv_out", block_in, cfg["z_channels"], 3)
+    conv("quant_conv", cfg["z_channels"], cfg["e_dim"], 1)
+    cb = (torch.rand(cfg["n_codes"], cfg["e_dim"], generator=g) * 2 - 1) / cfg["n_codes"]
+    w["quantize.embedding.weight"] = cb / cb.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    return w
+
+
+def main(argv=None):
+    """python -m ospo_amd.vq --data-path train.json --out token_cache.npz [--weights vq.safetensors]
+    [--path-map OLD=NEW]: the step-5 dataset's chosen / rejected images (ospo/dataclass/train_dataset.py:
+    79-97) -> ``dataset.train.token_cache`` (keys "{item_id}/chosen|rejected")."""
+    import argparse
+    import json
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data-path", required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--weights", default=None)
+    ap.add_argument("--path-map", action="append", default=[])
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args(argv)
+    maps = [m.split("=", 1) for m in a.path_map]
+
+    def remap(p):
+        for old, new in maps:
+            if p.startswith(old):
+                return new + p[len(old):]
+        return p
+    items = []
+    for ex in json.load(open(a.data_path)):
+        items.append((f"{ex['item_id']}/chosen", remap(ex["chosen"])))
+        items.append((f"{ex['item_id']}/rejected", remap(ex["rejected"])))
+    enc = VQEncoder(load_vq_weights(a.weights, a.seed))
+    out = build_token_cache(enc, items, a.out, batch=a.batch)
+    print(f"[ospo_amd.vq] {len(out)} images -> {a.out}")
+
+
+if __name__ == "__main__":
+    main()

@@ -123,3 +123,24 @@ def test_encoder_matches_reference_golden_ids():
               f"id mismatches {int((ids.cpu().long().view(-1) != ref_ids).sum())}")
         assert relerr(zz, ref_z) < 1e-5
         assert torch.equal(ids.cpu().long().view(-1), ref_ids)
+
+
+def test_token_cache_cli_reads_step5_json(tmp_path):
+    """python -m ospo_amd.vq over a step-5 train.json: PNG -> VLMImageProcessor pixels -> ids, keyed
+    "{item_id}/chosen|rejected" as the SimPO dataloader reads them (ospo_amd/data.py)."""
+    import json
+    from PIL import Image
+    from ospo_amd import vq
+    z = np.load(GOLD)
+    png = tmp_path / "img.png"
+    Image.fromarray(z["img2_u8"]).save(png)
+    data = [{"item_id": "0000042", "prompt": "a cat", "chosen": "/old/root/img.png", "rejected": str(png)}]
+    jp = tmp_path / "train.json"
+    jp.write_text(json.dumps(data))
+    out = tmp_path / "cache.npz"
+    vq.main(["--data-path", str(jp), "--out", str(out), "--seed", str(int(z["seed"])),
+             "--path-map", f"/old/root={tmp_path}"])
+    cache = np.load(out)
+    assert sorted(cache.files) == ["0000042/chosen", "0000042/rejected"]
+    for k in cache.files:
+        assert np.array_equal(cache[k].astype(np.int64), z["img2_ids"])
