@@ -61,6 +61,7 @@ SIGNATURES = {
     "ospo_decode_advance": [P, P, P],
     "ospo_set_gemv_variant": [I],
     "ospo_set_skinny_variant": [I],
+    "ospo_gemm_force_split": [I],
     "ospo_vq_conv2d": [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, P, P, P],
     "ospo_vq_bmm_nt": [P, P, I, I, I, I, P, P],
     "ospo_vq_groupnorm_ws_bytes": [I, I],

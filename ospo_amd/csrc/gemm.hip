@@ -1095,6 +1095,35 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
   u32x4 o;
 #pragma unroll
   for (int q = 0; q < 4; ++q) o[q] = pack2(v[2 * q], v[2 * q + 1]);
+  if (n0 + c < args.rope_cols) {
+    // RoPE as the main epilogue does it: on the bf16-rounded products, partner column +-64 of the head
+    // (the tile holds whole heads, so the partner's partials are in the same partial tiles)
+    const int d = c & 127;
+    const bool lo_half = d < 64;
+    const int pc = lo_half ? c + 64 : c - 64, dd = lo_half ? d : d - 64;
+    f32x4 plo = f32x4{0.f, 0.f, 0.f, 0.f}, phi = plo;
+    for (int z = 0; z < split; ++z) {
+      const float* pp = ws + (long)(tile * split + z) * 65536 + r * 256 + pc;
+      plo += *reinterpret_cast<const f32x4*>(pp);
+      phi += *reinterpret_cast<const f32x4*>(pp + 4);
+    }
+    const float pv[8] = {plo[0], plo[1], plo[2], plo[3], phi[0], phi[1], phi[2], phi[3]};
+    const int t = m % args.rope_T;
+    const u32x4 cw = *reinterpret_cast<const u32x4*>(args.rope_cs + (long)t * 64 + dd);
+    const u32x4 sw = *reinterpret_cast<const u32x4*>(args.rope_sn + (long)t * 64 + dd);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float rr[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int sh = 16 * hh;
+        const float x = round_bf(v[2 * q + hh]), pr = round_bf(pv[2 * q + hh] * args.alpha);
+        const float cf = bits2f((cw[q] >> sh) & 0xffff), sf = bits2f((sw[q] >> sh) & 0xffff);
+        rr[hh] = lo_half ? round_bf(x * cf) + round_bf(-pr * sf) : round_bf(x * cf) + round_bf(pr * sf);
+      }
+      o[q] = pack2(rr[0], rr[1]);
+    }
+  }
   if (args.res) {  // residual added after the bf16 rounding of the product, as the main epilogue does
     const u32x4 rv = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + c);
 #pragma unroll
@@ -1107,6 +1136,7 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
 float* g_splitk_ws = nullptr;
 size_t g_splitk_ws_bytes = 0;
 int g_num_cus = 0;
+int g_force_split = 0;  // test / A-B knob: > 0 forces that split of the tail round (still bounded below)
 
 int num_cus() {
   if (!g_num_cus) {
@@ -1125,9 +1155,25 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   const int ntot = (MX ? a.K / 128 : a.K / BK) + a.K2 / BK;
   const int cus = num_cus();
   int dp = tiles, split = 1, tail = 0;
-  if (allow_split && a.rope_cols == 0 && tiles > cus) {
+  if (allow_split && tiles > cus) {
     tail = tiles % cus;
-    split = tail ? std::min(cus / tail, std::min(8, ntot / 4)) : 1;
+    // The tail round as pieces of 1/s of a tile: ceil(tail s / cus) waves of T / s, plus the fp32 partials
+    // (256 KiB per piece, written here and read by the fixup: ~0.13 us each at ~4 TB/s).  T = one tile's
+    // K loop, ~1.9 us per bf16 K-tile (2.3 per MX K-tile) at the measured 8-phase rate.  s = 1: a full T.
+    split = 1;
+    if (tail) {
+      const double T = ntot * (MX ? 2.3 : 1.9);
+      double best = T;
+      const int sp_max = std::min(std::min(8, ntot / 4), (int)(g_splitk_ws_bytes / (65536 * sizeof(float)) / tail));
+      for (int sp = 2; sp <= sp_max; ++sp) {
+        const double cost = (double)((tail * sp + cus - 1) / cus) / sp * T + 0.13 * tail * sp;
+        if (cost < best - 1e-9) {
+          best = cost;
+          split = sp;
+        }
+      }
+      if (g_force_split > 0) split = std::max(1, std::min(g_force_split, sp_max));
+    }
     const size_t need = (size_t)tail * split * 65536 * sizeof(float);
     // (with dropout every extension tile must sit in K-range 0, which applies the mask)
     const bool drop_ok = !DROP || (long)(a.K2 / BK) * split <= ntot;
@@ -1204,6 +1250,12 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   }
 }
 
+extern "C" int ospo_gemm_force_split(int s) {
+  if (s < 0 || s > 8) return OSPO_ERR_ARG;
+  g_force_split = s;
+  return OSPO_OK;
+}
+
 extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                                       const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
                                       const void* rope_cos, const void* rope_sin, int T, int rope_cols,
@@ -1223,7 +1275,7 @@ extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int
   a.rope_sn = (const bf16*)rope_sin;
   a.rope_T = T;
   a.rope_cols = rope_cols;
-  return launch_v5<0>(a, stream, false);
+  return launch_v5<0>(a, stream);  // split-K tail fixups apply the RoPE epilogue too
 }
 
 extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
@@ -1277,7 +1329,7 @@ extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const 
     a.rope_sn = (const bf16*)rope_sin;
     a.rope_T = rope_T;
     a.rope_cols = rope_cols;
-    return launch_v5<0, false, true>(a, stream, false);
+    return launch_v5<0, false, true>(a, stream);
   }
   if (drop) {
     a.drop_seed = drop_seed;

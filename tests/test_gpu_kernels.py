@@ -512,3 +512,34 @@ def test_clip_adamw_matches_torch():
     tol = torch.maximum(ref.float().abs() * 2 ** -7 * 1.01, torch.full_like(ref.float(), 1.5 * 4e-5 * 2))
     assert bool(((p.float() - ref.float()).abs() <= tol).all())
     assert (p != ref).float().mean().item() < 0.02
+
+
+@pytest.mark.parametrize("split", [2, 3, 4])
+def test_gemm_split_tail_equals_unsplit(split):
+    """Split-K tail tiles (partials + fixup, RoPE and residual epilogues applied in the fixup) give the
+    same bf16 output as the unsplit kernel: exact integers so the fp32 partial order cannot matter."""
+    from ospo_amd._lib import call
+    M, H, T, K = 4800, 16, 600, 1024
+    D = H * 128
+    N = 3 * D                                     # 19 x 24 = 456 tiles: a tail round of 200 tiles
+    a, b = ints(M, K), ints(N, K, lo=-1, hi=2)
+    a2, b2 = ints(M, 64), ints(N, 64, lo=-1, hi=2)
+    cos, sin = ops().rope_tables(T, 128, 1e4, DEV)
+    res = ints(M, N)
+    outs = {}
+    try:
+        for s in (1, split):
+            call("ospo_gemm_force_split", s if s > 1 else 0)   # 0: the cost model keeps this shape unsplit
+            o1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops().gemm_nt(a, b, o1, a2=a2, b2=b2, rope=(cos, sin, T, 2 * D))
+            o2 = torch.empty_like(o1)
+            ops().gemm_nt(a, b, o2, a2=a2, b2=b2, residual=res)
+            outs[s] = (o1, o2)
+    finally:
+        call("ospo_gemm_force_split", 0)
+    ref = torch.empty_like(outs[1][1])
+    ops().gemm_nt(a, b, ref, a2=a2, b2=b2)
+    ops().rope(ref, 0, D, M // T, T, H, 128, cos, sin)
+    assert torch.equal(outs[split][0], ref)
+    assert torch.equal(outs[split][0], outs[1][0])
+    assert torch.equal(outs[split][1], outs[1][1])

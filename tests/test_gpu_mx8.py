@@ -142,3 +142,27 @@ def test_gemm_mx8_rejects_bad_shapes():
              200, None, 0, None, 0, 0, 1.0, None, None, 0, out.data_ptr(), 256, None, None, 0, 0, 0, 0.0, None)
     with pytest.raises(ValueError):  # MX8 operand K mismatch
         ops().gemm_nt_mx8(a, ops().MX8.of(rnd(256, 384)), out)
+
+
+def test_gemm_mx8_split_tail_rope_equals_unsplit():
+    """MX8 rope GEMM with a forced split-K tail (RoPE applied in the fixup) == the unsplit kernel, on
+    codes whose products are exact (power-of-two scales, small integers)."""
+    from ospo_amd._lib import call
+    M, H, T, K = 4800, 16, 600, 1024
+    D = H * 128
+    x = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    w = torch.randint(-1, 2, (3 * D, K), device=DEV).to(torch.bfloat16)
+    a2 = torch.randint(-3, 4, (M, 64), device=DEV).to(torch.bfloat16)
+    b2 = torch.randint(-1, 2, (3 * D, 64), device=DEV).to(torch.bfloat16)
+    cos, sin = ops().rope_tables(T, 128, 10000.0, DEV)
+    xa, wb = ops().MX8.of(x), ops().MX8.of(w)
+    outs = []
+    try:
+        for s in (0, 3):
+            call("ospo_gemm_force_split", s)
+            o = torch.empty(M, 3 * D, device=DEV, dtype=torch.bfloat16)
+            ops().gemm_nt_mx8(xa, wb, o, a2=a2, b2=b2, rope=(cos, sin, T, 2 * D))
+            outs.append(o)
+    finally:
+        call("ospo_gemm_force_split", 0)
+    assert torch.equal(outs[0], outs[1])

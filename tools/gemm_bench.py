@@ -18,6 +18,7 @@ SHAPES = [  # name, M, N, K, K2
 ]
 VARIANTS = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1").split(",") if v != ""]
 MX8 = os.environ.get("GB_MX8", "0") == "1"  # also time the block-scaled fp8 GEMM (+ its A quantization)
+SPLITS = [int(v) for v in os.environ.get("GB_SPLITS", "").split(",") if v != ""]  # forced tail splits (v0)
 ROUNDS, ITERS = 5, 10
 
 
@@ -43,6 +44,8 @@ def main():
         ref = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
         res = {f"v{v}": [] for v in VARIANTS}
         res["hipblaslt"] = []
+        for sp in SPLITS:
+            res[f"split{sp}"] = []
         if MX8:
             a8, b8 = ops.MX8.of(a), ops.MX8.of(b)
             res["mx8"], res["mx8_quantA"] = [], []
@@ -54,6 +57,10 @@ def main():
                 call("ospo_set_gemm_variant", v)
                 res[f"v{v}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
             res["hipblaslt"].append(timeit(lambda: torch.matmul(a, b.t(), out=ref)))
+            for sp in SPLITS:
+                call("ospo_gemm_force_split", sp)
+                res[f"split{sp}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
+            call("ospo_gemm_force_split", 0)
         exp = a.float() @ b.float().t() + (a2.float() @ b2.float().t() if k2 else 0)
         errs = {}
         for v in VARIANTS:
