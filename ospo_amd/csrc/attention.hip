@@ -21,6 +21,7 @@
 // chunk ^ 2*(row & 7): conflict-free for both the ds_read_b128 row reads and
 // the ds_read_b64_tr_b16 column reads (CDNA4 LDS banking, 64 x 4 B banks).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -134,6 +135,41 @@ __device__ __forceinline__ bf16x8 pack_perm(const f32x4& a, const f32x4& b) {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
+constexpr float L2E = 1.4426950408889634f;  // exp(x) = exp2(x * log2 e): v_exp_f32 is a base-2 exponential
+
+// Two f32 -> bf16 (RNE) in one v_cvt_pk_bf16_f32, back to f32.
+__device__ __forceinline__ void bf_round2(float& a, float& b) {
+  const bf16x2 r = __builtin_convertvector((f32x2){a, b}, bf16x2);
+  const unsigned u = __builtin_bit_cast(unsigned, r);
+  a = __uint_as_float(u << 16);
+  b = __uint_as_float(u & 0xffff0000u);
+}
+// HF eager bf16 scores (modeling_llama.py: matmul output, then * 1/sqrt(d), each rounded to bf16)
+__device__ __forceinline__ void hf_scores2(float& a, float& b, float scale) {
+  bf_round2(a, b);
+  a *= scale;
+  b *= scale;
+  bf_round2(a, b);
+}
+// Reductions over the 4 lane groups (lanes l, l^16, l^32, l^48) with the CDNA4 half-row swaps
+// (VALU, no LDS round trip like ds_bpermute); every lane gets the same bits (a+b == b+a).
+__device__ __forceinline__ float grp_max(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  const unsigned w = __float_as_uint(x);
+  const auto q = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float grp_sum(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  const unsigned w = __float_as_uint(x);
+  const auto q = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
 // RoPE backward (transpose of the rotate-half rotation) on fp32 accumulators whose lane
 // holds d = 16dt + 4g + j, dt = 0..7: d < 64 pairs with d + 64 (dt + 4) in the same lane.
 // cs / sn: bf16 [T][64] tables, t = the row's position in its sequence.
@@ -161,8 +197,10 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int qb = gridDim.x - 1 - blockIdx.x;  // longest key sweep first
-  const int h = blockIdx.y, s = blockIdx.z;
+  // grid (H, S, blocks): workgroups dispatch in linear order, so every head's longest key sweep
+  // (the last query block) goes first across the whole chip, then the next longest (LPT order)
+  const int qb = gridDim.z - 1 - blockIdx.z;
+  const int h = blockIdx.x, s = blockIdx.y;
   const int g = lane >> 4, l16 = lane & 15;
   const long rowbase = (long)s * T;
   const int rows_lim_seq = T;  // clamp inside the sequence
@@ -193,7 +231,12 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+  const int lim = qrow < T ? qrow : T - 1;  // last key this row attends to (padding rows: T - 1)
+  // One K/V tile.  DIAG (the tiles that may hold a key after some row of the block, or past T):
+  // masked scores become -inf, which v_exp_f32 maps to 0 -- no per-element branch or compare
+  // outside those tiles.
   for (int kt = 0; kt < n_kv; ++kt) {
+    const bool diag = (kt * KB + KB - 1 > qb * RB) || ((kt + 1) * KB > T);
     const int buf = kt & 1;
     if (DBG == 0 && kt + 1 < n_kv) {
       char* nb = smem + (buf ^ 1) * 2 * TILE_BYTES;
@@ -211,36 +254,35 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
 #pragma unroll
       for (int d = 0; d < 4; ++d) st[t] = MFMA(frag_row(Ks, 16 * t, d, lane), qf[d], st[t]);
     }
-    // scale + mask, tile max (tiles that may hold a key beyond some row of the block)
-    const bool diag = (kt * KB + KB - 1 > qb * RB) || ((kt + 1) * KB > T);
-    float tmax = -1e30f;
+    // element (t, j) is key kt*KB + 4g + 16t + j; off the diagonal no element is masked
+    const int rel = diag ? lim - (kt * KB + 4 * g) : 64;
+    float tmax = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float v = round_bf(round_bf(st[t][j]) * scale);  // HF eager bf16: matmul out, then * scale, each rounded
-        if (diag) {
-          const int key = kt * KB + 16 * t + 4 * g + j;
-          if (key > qrow || key >= T) v = -1e30f;
-        }
-        st[t][j] = v;
-        tmax = fmaxf(tmax, v);
+      for (int j = 0; j < 4; j += 2) {
+        float a = st[t][j], b = st[t][j + 1];
+        hf_scores2(a, b, scale);
+        a = (16 * t + j > rel) ? -INFINITY : a;
+        b = (16 * t + j + 1 > rel) ? -INFINITY : b;
+        st[t][j] = a;
+        st[t][j + 1] = b;
+        tmax = fmaxf(tmax, fmaxf(a, b));
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float alpha = __expf(m_run - m_new);
+    tmax = grp_max(tmax);
+    const float m_new = fmaxf(m_run, tmax);  // finite: m_run starts at -1e30
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * L2E);
+    const float mb = m_new * L2E;
     float psum = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = (st[t][j] <= -1e29f) ? 0.f : __expf(st[t][j] - m_new);
+        const float p = __builtin_amdgcn_exp2f(fmaf(st[t][j], L2E, -mb));
         st[t][j] = p;
         psum += p;
       }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
+    psum = grp_sum(psum);
     l_run = l_run * alpha + psum;
     m_run = m_new;
 #pragma unroll
@@ -297,7 +339,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int kb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;  // kb = 0 (longest sweep) dispatched first
+  const int kb = blockIdx.z, h = blockIdx.x, s = blockIdx.y;  // kb = 0 (longest sweeps) dispatched first, chip-wide
   const int g = lane >> 4, l16 = lane & 15;
   const long rowbase = (long)s * T;
   const int nq = (T + QB - 1) / QB;
@@ -340,7 +382,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int qt = qt0; qt < nq; ++qt) {
+  auto tile = [&](const int qt, auto diag_c) {
+    constexpr bool DIAG = decltype(diag_c)::value;
     const int b = (qt - qt0) & 1;
     if (qt + 1 < nq) stage(qt + 1, b ^ 1);
     const char* Qs = smem + b * 2 * TILE_BYTES;
@@ -360,16 +403,26 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
         dp[a] = MFMA(frag_row(Os, 16 * a, d, lane), vf[d], dp[a]);
       }
     }
+    // element (a, j) is query qt*QB + 4g + 16a + j: masked below the key (causal) or at / past T
+    const int lo = key_l - (qt * QB + 4 * g), hi = T - (qt * QB + 4 * g);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4; j += 2) {
+        float x = sv[a][j], y = sv[a][j + 1];
+        hf_scores2(x, y, scale);
+        if (DIAG) {
+          const int e = 16 * a + j;
+          x = (e < lo || e >= hi) ? -INFINITY : x;
+          y = (e + 1 < lo || e + 1 >= hi) ? -INFINITY : y;
+        }
         const int ql = 16 * a + 4 * g + j;
-        const int q = qt * QB + ql;
-        float p = __expf(round_bf(round_bf(sv[a][j]) * scale) - Ls[ql]);
-        if (q >= T || key_l > q || key_l >= T) p = 0.f;
-        sv[a][j] = p;
-        dp[a][j] = p * (dp[a][j] - Dl[ql]) * scale;
+        const float px = __builtin_amdgcn_exp2f((x - Ls[ql]) * L2E);
+        const float py = __builtin_amdgcn_exp2f((y - Ls[ql + 1]) * L2E);
+        sv[a][j] = px;
+        sv[a][j + 1] = py;
+        dp[a][j] = px * (dp[a][j] - Dl[ql]) * scale;
+        dp[a][j + 1] = py * (dp[a][j + 1] - Dl[ql + 1]) * scale;
       }
     // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . (scale dS)[q][key]
 #pragma unroll
@@ -384,6 +437,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  };
+  // keys >= T (clamped copies of key T-1) are never stored, so only causality and the T edge mask
+  for (int qt = qt0; qt < nq; ++qt) {
+    if (qt * QB < kb * KBW + KBW || (qt + 1) * QB > T)
+      tile(qt, std::true_type{});
+    else
+      tile(qt, std::false_type{});
   }
 
   // lane holds [d = 16dt + 4g + j][key = l16]
@@ -417,8 +477,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int qb = gridDim.x - 1 - blockIdx.x;  // longest sweep first
-  const int h = blockIdx.y, s = blockIdx.z;
+  const int qb = gridDim.z - 1 - blockIdx.z;  // longest sweeps first, chip-wide (see the forward)
+  const int h = blockIdx.x, s = blockIdx.y;
   const int g = lane >> 4, l16 = lane & 15;
   const long rowbase = (long)s * T;
 
@@ -440,9 +500,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
       for (int i = 0; i < 8; ++i) dpart += bf2f(of[d][i]) * bf2f(ov[i]);
     }
   }
-  dpart += __shfl_xor(dpart, 16, 64);
-  dpart += __shfl_xor(dpart, 32, 64);
-  const float del_q = dpart;
+  const float del_q = grp_sum(dpart);
   const float lse_q = lse[((long)s * H + h) * T + qr_c];
   if (g == 0 && qrow < T) delta[((long)s * H + h) * T + qrow] = del_q;  // for the dK/dV kernel (launched next)
 
@@ -459,7 +517,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int kt = 0; kt < n_kv; ++kt) {
+  const int lim = qrow < T ? qrow : T - 1;
+  const float lse_b = lse_q * L2E;
+  auto tile = [&](const int kt, auto diag_c) {
+    constexpr bool DIAG = decltype(diag_c)::value;
     const int buf = kt & 1;
     if (kt + 1 < n_kv) {
       char* nb = smem + (buf ^ 1) * 2 * TILE_BYTES;
@@ -480,17 +541,21 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
         dpt[t] = MFMA(frag_row(Vs, 16 * t, d, lane), of[d], dpt[t]);
       }
     }
-    const bool diag = (kt * KB + KB - 1 > qb * RB) || ((kt + 1) * KB > T);
+    const int rel = lim - (kt * KB + 4 * g);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float p = __expf(round_bf(round_bf(st[t][j]) * scale) - lse_q);
-        if (diag) {
-          const int key = kt * KB + 16 * t + 4 * g + j;
-          if (key > qrow || key >= T) p = 0.f;
+      for (int j = 0; j < 4; j += 2) {
+        float a = st[t][j], b = st[t][j + 1];
+        hf_scores2(a, b, scale);
+        if (DIAG) {
+          a = (16 * t + j > rel) ? -INFINITY : a;
+          b = (16 * t + j + 1 > rel) ? -INFINITY : b;
         }
-        st[t][j] = p * (dpt[t][j] - del_q) * scale;
+        const float pa = __builtin_amdgcn_exp2f(fmaf(a, L2E, -lse_b));
+        const float pb = __builtin_amdgcn_exp2f(fmaf(b, L2E, -lse_b));
+        st[t][j] = pa * (dpt[t][j] - del_q) * scale;
+        st[t][j + 1] = pb * (dpt[t][j + 1] - del_q) * scale;
       }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -500,6 +565,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  };
+  for (int kt = 0; kt < n_kv; ++kt) {
+    if ((kt * KB + KB - 1 > qb * RB) || ((kt + 1) * KB > T))
+      tile(kt, std::true_type{});
+    else
+      tile(kt, std::false_type{});
   }
 
   if (qrow < T) {
@@ -536,7 +607,7 @@ extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k
     return OSPO_ERR_SHAPE;
   if (!aligned16(qkv) || !aligned16(o)) return OSPO_ERR_ALIGN;
   const int nw = attn_waves();
-  dim3 grid((T + 16 * nw - 1) / (16 * nw), n_heads, S);
+  dim3 grid(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
   static const bool dbg = getenv("OSPO_ATTN_DBG") != nullptr;  // ablation only
   auto kfn = dbg ? attn_fwd_kernel<8, 1> : (nw == 8 ? attn_fwd_kernel<8, 0> : attn_fwd_kernel<4, 0>);
   hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
@@ -562,12 +633,12 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
   const bf16* rs = (const bf16*)rope_sin;
   // dQ first: it also produces delta = rowsum(dO * O) for the dK/dV kernel
   const int nw = attn_waves();
-  dim3 gq((T + 16 * nw - 1) / (16 * nw), n_heads, S);
+  dim3 gq(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
   hipLaunchKernelGGL(nw == 8 ? attn_bwd_dq_kernel<8> : attn_bwd_dq_kernel<4>, gq, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                      (const bf16*)dout, ld_do, (const bf16*)o, ld_o, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads,
                      scale, rc, rs);
   OSPO_CHECK_LAUNCH();
-  dim3 grid((T + 16 * nw - 1) / (16 * nw), n_heads, S);
+  dim3 grid(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
   hipLaunchKernelGGL(nw == 8 ? attn_bwd_dkdv_kernel<8> : attn_bwd_dkdv_kernel<4>, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
                      v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
   OSPO_CHECK_LAUNCH();
