@@ -429,10 +429,20 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
     for (int u = 0; u < 2; ++u) {
       const bf16x8 pb = pack_perm(sv[2 * u], sv[2 * u + 1]);
       const bf16x8 sb = pack_perm(dp[2 * u], dp[2 * u + 1]);
+      // transposed fragments through the asm reads in batches of 2 + 2: the builtin form makes the
+      // compiler drain vmcnt(0) (the next tile's DMA) before the first of them
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        dv[dt] = MFMA(frag_tr_perm(Os, 32 * u, 16 * dt, lane), pb, dv[dt]);
-        dk[dt] = MFMA(frag_tr_perm(Qs, 32 * u, 16 * dt, lane), sb, dk[dt]);
+      for (int d0 = 0; d0 < 8; d0 += 2) {
+        i16x4 lo[4], hi[4];
+        trp_issue(Os, 32 * u, 16 * d0, lane, lo[0], hi[0]);
+        trp_issue(Os, 32 * u, 16 * (d0 + 1), lane, lo[1], hi[1]);
+        trp_issue(Qs, 32 * u, 16 * d0, lane, lo[2], hi[2]);
+        trp_issue(Qs, 32 * u, 16 * (d0 + 1), lane, lo[3], hi[3]);
+        trp_wait4(lo, hi);
+        dv[d0] = MFMA(trp_join(lo[0], hi[0]), pb, dv[d0]);
+        dv[d0 + 1] = MFMA(trp_join(lo[1], hi[1]), pb, dv[d0 + 1]);
+        dk[d0] = MFMA(trp_join(lo[2], hi[2]), sb, dk[d0]);
+        dk[d0 + 1] = MFMA(trp_join(lo[3], hi[3]), sb, dk[d0 + 1]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -561,7 +571,14 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
     for (int u = 0; u < 2; ++u) {
       const bf16x8 sb = pack_perm(st[2 * u], st[2 * u + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) dq[dt] = MFMA(frag_tr_perm(Ks, 32 * u, 16 * dt, lane), sb, dq[dt]);
+      for (int d0 = 0; d0 < 8; d0 += 4) {  // asm transposed reads: no vmcnt drain of the next tile's DMA
+        i16x4 lo[4], hi[4];
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) trp_issue(Ks, 32 * u, 16 * (d0 + dd), lane, lo[dd], hi[dd]);
+        trp_wait4(lo, hi);
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) dq[d0 + dd] = MFMA(trp_join(lo[dd], hi[dd]), sb, dq[d0 + dd]);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
