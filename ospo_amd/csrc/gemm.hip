@@ -1079,228 +1079,6 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   epi_rows<512>(args, smem, m0, n0);
 }
 
-__device__ __forceinline__ uint32_t w4_lds_u32(const void* p) {
-  return (uint32_t)(uintptr_t)((LDS_AS const char*)p);
-}
-// acc += b . a^T on v_mfma_f32_16x16x32_bf16, accumulator pinned in AGPRs (in-place chain: the
-// hardware forwards srcC, no wait states)
-__device__ __forceinline__ void w4_mfma(f32x4& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
-}
-// After the lgkmcnt wait that covers a batch of w4_ds_read: redefine all 16 destination registers
-// here, so the compiler keeps them allocated (and uncopied) from the read to this point -- an asm
-// load's output is written asynchronously, which the compiler cannot know.
-__device__ __forceinline__ void w4_tie(bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
-  asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
-               "+v"(fa[7]));
-  asm volatile("" : "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]), "+v"(fb[4]), "+v"(fb[5]), "+v"(fb[6]),
-               "+v"(fb[7]));
-}
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-__device__ __forceinline__ void w4_mfma32(f32x16& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
-}
-__device__ __forceinline__ void w4_ds_read4k(bf16x8& dst, uint32_t base, int i) {
-  switch (i) {
-#define W4R(k) \
-  case k: asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(4096 * k)); break;
-    W4R(0) W4R(1) W4R(2) W4R(3)
-#undef W4R
-  }
-}
-__device__ __forceinline__ void w4_ds_read1k(bf16x8& dst, uint32_t base, int i) {
-  switch (i) {
-#define W4R(k) \
-  case k: asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(1024 * k)); break;
-    W4R(0) W4R(1) W4R(2) W4R(3) W4R(4) W4R(5) W4R(6) W4R(7)
-#undef W4R
-  }
-}
-// fragment read at base + 2048 i (invisible to the compiler's waitcnt pass: callers wait lgkmcnt,
-// then w4_tie the destinations)
-__device__ __forceinline__ void w4_ds_read(bf16x8& dst, uint32_t base, int i) {
-  switch (i) {
-#define W4R(k) \
-  case k: asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(2048 * k)); break;
-    W4R(0) W4R(1) W4R(2) W4R(3) W4R(4) W4R(5) W4R(6) W4R(7)
-#undef W4R
-  }
-}
-
-// ----------------------------------------------------------------------------
-// w4: 256 x 256 x 64 with FOUR waves, one per SIMD; wave w owns the 128 x 128 quadrant (w >> 1,
-// w & 1) for the whole K loop (256 fp32 accumulators per lane: the AGPR half of the unified
-// register file).  Per K-tile a wave reads 32 fragments (8 A + 8 B per 32-k substep) for 128
-// MFMAs -- half the LDS reads per MFMA of the 8-wave ping-pong -- and there is one barrier per
-// K-tile, placed between the two substeps:
-//   read(t,1) | MFMA(t,0) | vmcnt(0) barrier | stage(t+2) -> slot t | read(t+1,0) | MFMA(t,1)
-// Same LDS image, tile order, split-K tail and epilogue as v5.
-template <int DBG = 0>
-__global__ __launch_bounds__(256) void gemm_nt_w4_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
-                                                         int split, float* __restrict__ ws, int GM) {
-  constexpr int BM = 256, BN = 256, HALF = 16384, SLOT = 4 * HALF;  // v5's image: A0 A1 B0 B1, [128][64 k]
-  constexpr int CPITCH = BN * 2 + 16;
-  constexpr int LDS_BYTES = (2 * SLOT > BM * CPITCH) ? 2 * SLOT : BM * CPITCH;
-  static_assert(LDS_BYTES <= 163840, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ia = wave >> 1, ib = wave & 1;
-
-  int m0, n0, tb, tcount, part = -1;
-  const int nt1 = args.K / BK, nt2 = args.K2 / BK, ntot = nt1 + nt2;
-  {
-    const int wg = blockIdx.x;
-    if (wg < dp) {
-      const int xcd = wg & 7, slot = wg >> 3, q = dp >> 3, r = dp & 7;
-      const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-      v5_tile(L, tiles_m, tiles_n, m0, n0, GM);
-      tb = 0;
-      tcount = ntot;
-    } else {
-      const int u = wg - dp, z = u % split;
-      part = u;
-      v5_tile(dp + u / split, tiles_m, tiles_n, m0, n0, GM);
-      tb = (int)((long)ntot * z / split);
-      tcount = (int)((long)ntot * (z + 1) / split) - tb;
-    }
-  }
-  const int nt = tcount;
-  const int Mlast = args.M - 1, Nlast = args.N - 1;
-  const int rr8 = lane >> 3, c8 = lane & 7;
-
-  // one of the 16 LDS-DMA pieces of K-tile tl this wave issues (half-tile pc >> 2, row group pc & 3)
-  auto stage_piece = [&](int tl, int pc) __attribute__((always_inline)) {
-    if (DBG == 1 && tl >= 2) return;
-    char* dst = smem + (tl & 1) * SLOT;
-    const int t = tb + min(tl, nt - 1);  // past the end: a harmless reload into a slot no one reads again
-    const bool ext = t >= nt1;
-    const int k0 = (ext ? t - nt1 : t) * BK;
-    const int h = pc >> 2, i = pc & 3;
-    const bool isA = h < 2;
-    const bf16* base = isA ? (ext ? args.A2 : args.A) : (ext ? args.B2 : args.B);
-    const int ld = isA ? (ext ? args.lda2 : args.lda) : (ext ? args.ldb2 : args.ldb);
-    const int row0 = (isA ? m0 : n0) + (h & 1) * 128;
-    const int last = isA ? Mlast : Nlast;
-    const int p = wave * 4 + i;
-    const int row = p * 8 + rr8;
-    const int g = min(row0 + row, last);
-    glds16(base + (long)g * ld + k0 + ((c8 ^ (row & 7)) << 3), dst + h * HALF + p * 1024);
-  };
-
-  // 32x32x16 MFMAs: the wave's 128 x 128 quadrant is 4 x 4 blocks of 32 x 32 (16 fp32 per lane
-  // each, 256 in all, pinned in AGPRs).  Per K-tile: 4 k-steps of 16; per phase (32 k) 2 k-steps:
-  // 8 A + 8 B fragment reads (row l & 31 of a 32-row block, 16-B chunk 2 ks + (l >> 5)), 32 MFMAs.
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][n][e] = 0.f;
-  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];  // [ks-in-phase * 4 + block]
-  const int frow = lane & 31, fhi = lane >> 5;
-  const uint32_t lds0 = w4_lds_u32(smem);
-  uint32_t fbase[2][4];  // [A / B][k-step of the K-tile]: + 4096 per 32-row block
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int sw = ((2 * ks + fhi) ^ (frow & 7)) << 4;
-    fbase[0][ks] = lds0 + ia * HALF + frow * 128 + sw;
-    fbase[1][ks] = lds0 + (2 + ib) * HALF + frow * 128 + sw;
-  }
-  // r = 0..15 of a phase: k-step ks2 = r >> 3, then A block, B block alternating
-  auto read_one = [&](int slot, int ph, int r, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) __attribute__((always_inline)) {
-    const int ks2 = r >> 3, blk = (r >> 1) & 3;
-    const int ks = 2 * ph + ks2;
-    const uint32_t a = (r & 1 ? fbase[1][ks] : fbase[0][ks]) + slot * SLOT;
-    if (r & 1) w4_ds_read4k(fb[ks2 * 4 + blk], a, blk);
-    else w4_ds_read4k(fa[ks2 * 4 + blk], a, blk);
-  };
-  auto phase = [&](const bf16x8 (&fa)[8], const bf16x8 (&fb)[8], int rslot, int rph, bf16x8 (&ra)[8],
-                   bf16x8 (&rb)[8], auto dma_c, int dtile) __attribute__((always_inline)) {
-    constexpr bool DMA = decltype(dma_c)::value;
-#pragma clang loop unroll(full)
-    for (int q = 0; q < 32; ++q) {
-      const int ks2 = q >> 4, i = (q >> 2) & 3, n = q & 3;
-      if constexpr (DBG != 2) w4_mfma32(acc[i][n], fb[ks2 * 4 + n], fa[ks2 * 4 + i]);
-      // 16 reads in the first 24 MFMAs (2 per 3), 16 DMA pieces spread over all 32
-      if (q < 24 && (q % 3) != 2) read_one(rslot, rph, (q / 3) * 2 + (q % 3), ra, rb);
-      if constexpr (DMA) {
-        if ((q & 1) == 0) stage_piece(dtile, q >> 1);
-      }
-    }
-  };
-
-  if (nt > 0)
-#pragma clang loop unroll(full)
-    for (int pc = 0; pc < 16; ++pc) stage_piece(0, pc);
-  if (nt > 1)
-#pragma clang loop unroll(full)
-    for (int pc = 0; pc < 16; ++pc) stage_piece(1, pc);
-  if (nt > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-#pragma clang loop unroll(full)
-  for (int r = 0; r < 16; ++r) read_one(0, 0, r, fa0, fb0);
-  for (int t = 0; t < nt; ++t) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    w4_tie(fa0, fb0);
-    phase(fa0, fb0, t & 1, 1, fa1, fb1, std::false_type{}, 0);  // MFMA (t, k 0-31) || read (t, k 32-63)
-    // tile t+1 landed (own DMA), every wave has read slot t: refill it with tile t + 2
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    w4_tie(fa1, fb1);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    phase(fa1, fb1, (t + 1) & 1, 0, fa0, fb0, std::true_type{}, t + 2);  // || read (t+1, k 0-31) || DMA (t+2)
-  }
-  // the last MFMA's result is read by plain code below: cover the MFMA -> read hazard; the
-  // last phase's (unused) reads land before their registers can be reused
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  w4_tie(fa0, fb0);
-  __syncthreads();
-
-  // block (i, n): lane holds row m = 32 i + (l & 31) of the quadrant and, for q = 0..3, the 4
-  // columns 32 n + 8 q + 4 (l >> 5) .. +3 (accumulator elements 4q .. 4q+3)
-  if (part >= 0) {  // split-K tail: raw fp32 partial tile [256][256]
-    float* wt = ws + (long)part * (BM * BN);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int ml = ia * 128 + i * 32 + frow;
-          const int nl = ib * 128 + n * 32 + q * 8 + 4 * fhi;
-          *reinterpret_cast<f32x4*>(wt + ml * BN + nl) =
-              f32x4{acc[i][n][4 * q], acc[i][n][4 * q + 1], acc[i][n][4 * q + 2], acc[i][n][4 * q + 3]};
-        }
-    return;
-  }
-#pragma unroll
-  for (int n = 0; n < 4; ++n)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int nl = ib * 128 + n * 32 + q * 8 + 4 * fhi;
-      float b4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (args.bias) {
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) b4[qq] = bf2f(args.bias[n0 + nl + qq]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ml = ia * 128 + i * 32 + frow;
-        uint2 pk;
-        pk.x = pack2(acc[i][n][4 * q] * args.alpha + b4[0], acc[i][n][4 * q + 1] * args.alpha + b4[1]);
-        pk.y = pack2(acc[i][n][4 * q + 2] * args.alpha + b4[2], acc[i][n][4 * q + 3] * args.alpha + b4[3]);
-        *reinterpret_cast<uint2*>(smem + ml * CPITCH + nl * 2) = pk;
-      }
-    }
-  __syncthreads();
-  epi_rows<256>(args, smem, m0, n0);
-}
-
 // sum the split partials of each tail tile, apply alpha / bias / residual, write bf16
 __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
                                                            int split, const float* __restrict__ ws, int GM) {
@@ -1378,7 +1156,7 @@ int num_cus() {
   return g_num_cus;
 }
 
-template <int DBG = 0, bool DROP = false, bool MX = false, bool W4 = false>
+template <int DBG = 0, bool DROP = false, bool MX = false>
 int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
   const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
@@ -1415,14 +1193,8 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
     }
   }
   const int grid = dp + tail * split;
-  if constexpr (W4) {
-    static_assert(!DROP && !MX, "w4: plain bf16 only");
-    hipLaunchKernelGGL((gemm_nt_w4_kernel<DBG>), dim3(grid), dim3(256), 0, s, a, tm, tn, dp, split, g_splitk_ws,
-                       g_v5_gm);
-  } else {
-    hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP, MX>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split,
-                       g_splitk_ws, g_v5_gm);
-  }
+  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP, MX>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split,
+                     g_splitk_ws, g_v5_gm);
   OSPO_CHECK_LAUNCH();
   if (tail) {
     hipLaunchKernelGGL(splitk_fixup_kernel, dim3(tail * 32), dim3(256), 0, s, a, tm, tn, dp, split,
@@ -1477,9 +1249,6 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 3: return launch_v3<8, 2, true, true>(a, stream);                           // v3 register-prefetch
     case 4: return launch_v4<8, 3>(a, stream);                                       // v4 BK=32 ring
     case 5: return launch_v5<0>(a, stream, false);                                   // 8-phase, no split tail
-    case 6: return launch_v5<0, false, false, true>(a, stream, true);                // w4 + split-K tail
-    case 7: return launch_v5<1, false, false, true>(a, stream, false);               // w4, no loads (ablation)
-    case 8: return launch_v5<2, false, false, true>(a, stream, false);               // w4, no MFMA (ablation)
     // decompositions (results invalid): 10 no loads / 11 no MFMA (simple); 12 no loads / 13 no MFMA (8-phase)
     case 10: return launch<2, 4, 8, 4, false, false, EPI_BF16, 1>(a, stream);
     case 11: return launch<2, 4, 8, 4, false, false, EPI_BF16, 2>(a, stream);
@@ -1594,7 +1363,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || v > 13 || v == 9) return OSPO_ERR_ARG;
+  if (v < 0 || v > 13 || (v > 5 && v < 10)) return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;
