@@ -294,8 +294,11 @@ int ospo_decode_advance(int* pos_dev, int* step_dev, hipStream_t stream);
 int ospo_gemm_force_split(int s);
 /* A/B knob of the LoRA skinny products: 1 = 16-row loop, 2 = 64-row LDS-shared (default). */
 int ospo_set_skinny_variant(int v);
-/* A/B knob of the decode GEMV schedule: 1 = skinny loop, 2 = LDS-shared activations (default). */
+/* A/B knob of the decode GEMV schedule: 1 = skinny loop, 2 = LDS-shared activations,
+ * 3 = the same with 128 weight rows per workgroup and power-of-two K splits (default). */
 int ospo_set_gemv_variant(int v);
+/* A/B knob: force the K-split count of GEMV schedules 2 / 3 (0 = automatic). */
+int ospo_set_gemv_splits(int s);
 
 /* ------------------------------------------------------- VQ image tokenizer ---
  * janus/models/vq_model.py Encoder (:46-124) + quant_conv + VectorQuantizer

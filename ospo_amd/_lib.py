@@ -60,6 +60,7 @@ SIGNATURES = {
     "ospo_embed_rows": [P, L, P, I, I, P, P],
     "ospo_decode_advance": [P, P, P],
     "ospo_set_gemv_variant": [I],
+    "ospo_set_gemv_splits": [I],
     "ospo_set_skinny_variant": [I],
     "ospo_gemm_force_split": [I],
     "ospo_vq_conv2d": [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, P, P, P],

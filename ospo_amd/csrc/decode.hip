@@ -107,6 +107,7 @@ __global__ __launch_bounds__(64 * NT) void gemv_reduce_kernel(const f32x4* __res
 // waves, while each wave streams its 16 weight rows with all of the chunk's loads (16 x 1 KiB) in
 // flight at once.  v1 above re-read x from L2 for every 16 weight rows (2x the weight traffic).
 constexpr int G2_ROWS = 64, G2_KC = 512, G2_PITCH = G2_KC * 2 + 16;
+constexpr int G2_MAX_SPLITS = 16;  // gemv2/3_kper cap the split count (K / 512 <= 16 up to K = 8192)
 template <int NT>
 __global__ __launch_bounds__(256) void gemv2_kernel(const bf16* __restrict__ W, int ldw, const bf16* __restrict__ X,
                                                     int ldx, int R, int K, int kper, const bf16* __restrict__ bias,
@@ -178,14 +179,85 @@ __global__ __launch_bounds__(256) void gemv2_reduce_kernel(const f32x4* __restri
   const int n = nb * 16 + (lane & 15), g = lane >> 4;
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
+    // every split's partial in flight at once, then summed in split order
+    f32x4 p[G2_MAX_SPLITS];
+#pragma unroll
+    for (int z = 0; z < G2_MAX_SPLITS; ++z)
+      if (z < splits) p[z] = ws[((long)(z * NB + nb) * NT + j) * 64 + lane];
     f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < splits; ++z) v += ws[((long)(z * NB + nb) * NT + j) * 64 + lane];
+#pragma unroll
+    for (int z = 0; z < G2_MAX_SPLITS; ++z)
+      if (z < splits) v += p[z];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = 16 * j + 4 * g + q;
       if (r < R) gemv_store(v[q], r, n, bias, gelu, res, ldr, out, ldo);
     }
   }
+}
+
+// GEMV v3: v2's schedule with 8 waves = 128 weight rows per workgroup: half the x staging per
+// weight byte.  Split partials as v2 (summed by gemv2_reduce_kernel).
+constexpr int G3_WAVES = 8, G3_ROWS = 16 * G3_WAVES;
+template <int NT>
+__global__ __launch_bounds__(64 * G3_WAVES) void gemv3_kernel(const bf16* __restrict__ W, int ldw,
+                                                              const bf16* __restrict__ X, int ldx, int R, int K,
+                                                              int kper, const bf16* __restrict__ bias, int gelu,
+                                                              const bf16* __restrict__ res, int ldr,
+                                                              bf16* __restrict__ out, int ldo, f32x4* __restrict__ ws) {
+  __shared__ __attribute__((aligned(16))) char xs[16 * NT * G2_PITCH];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int n = blockIdx.x * G3_ROWS + wave * 16 + l16;
+  const int z = blockIdx.y, splits = gridDim.y;
+  const int k_begin = z * kper, k_end = min(K, k_begin + kper);
+  const bf16* wrow = W + (long)n * ldw;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = k_begin; kc < k_end; kc += G2_KC) {
+    const int nsteps = min(G2_KC, k_end - kc) >> 5;
+    for (int r = wave; r < 16 * NT; r += G3_WAVES) {
+      const int rr = r < R ? r : R - 1;
+      const int col = min(kc + 8 * lane, K - 8);
+      __builtin_amdgcn_global_load_lds(X + (long)rr * ldx + col, (LDS_AS void*)(xs + r * G2_PITCH), 16, 0, 0);
+    }
+    asm volatile("" ::: "memory");
+    bf16x8 wv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = kc + 32 * min(s, nsteps - 1) + 8 * g;
+      wv[s] = *reinterpret_cast<const bf16x8*>(wrow + k);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this wave's x DMA (issued first) has landed
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < nsteps) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          bf16x8 xf = *reinterpret_cast<const bf16x8*>(xs + (16 * j + l16) * G2_PITCH + (32 * s + 8 * g) * 2);
+          if (16 * j + l16 >= R) xf = bf16x8{};
+          acc[j] = MFMA(xf, wv[s], acc[j]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int nb = n >> 4, NB = gridDim.x * G3_WAVES;
+  if (splits > 1) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) ws[((long)(z * NB + nb) * NT + j) * 64 + lane] = acc[j];
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * j + 4 * g + q;
+      if (r < R) gemv_store(acc[j][q], r, n, bias, gelu, res, ldr, out, ldo);
+    }
 }
 
 // ------------------------------------------------------- KV cache write
@@ -463,12 +535,26 @@ int gemv_splits(int nblocks, int K) {
   while (nblocks * s < 1024 && (K >> 5) / (2 * s) >= 8 * SK_WAVES) s *= 2;
   return s;
 }
-int g_gemv_variant = 2;  // 1 = skinny-loop GEMV, 2 = LDS-shared x (default); A/B knob
+int g_gemv_splits = 0;   // A/B knob: > 0 forces the v2 / v3 split count (clamped to K / 512 and 16)
+int g_gemv_variant = 3;  // 1 = skinny-loop GEMV, 2 = LDS-shared x, 3 = v2 with 128 rows per workgroup (default)
 // v2 K split: ~1024 workgroups, at least one 512-k chunk each; returns k per split (multiple of 32)
 int gemv2_kper(int N, int K) {
   const int groups = N / G2_ROWS;
   int splits = (1024 + groups - 1) / groups;
-  splits = std::max(1, std::min(splits, K / G2_KC));
+  splits = std::max(1, std::min(std::min(splits, K / G2_KC), G2_MAX_SPLITS));
+  if (g_gemv_splits > 0) splits = std::max(1, std::min(std::min(g_gemv_splits, K / G2_KC), G2_MAX_SPLITS));
+  int kper = (K + splits - 1) / splits;
+  return (kper + 31) / 32 * 32;
+}
+
+// v3 K split: the largest power of two <= min(8, K / 512) that keeps the grid within 1024
+// workgroups (4 per CU).  Power-of-two splits of K = 4096 give whole 512-k chunks; splits of 3 or
+// 6 leave a short tail chunk per workgroup and measured up to 30 % slower (tools/gemv_sweep.py).
+int gemv3_kper(int N, int K) {
+  const int groups = N / G3_ROWS;
+  int splits = 1;
+  while (splits * 2 <= std::min(8, K / G2_KC) && groups * splits * 2 <= 1024) splits *= 2;
+  if (g_gemv_splits > 0) splits = std::max(1, std::min(std::min(g_gemv_splits, K / G2_KC), G2_MAX_SPLITS));
   int kper = (K + splits - 1) / splits;
   return (kper + 31) / 32 * 32;
 }
@@ -482,11 +568,22 @@ extern "C" size_t ospo_decode_gemv_ws_bytes(int R, int N, int K) {
   if (N % G2_ROWS || K % 32) return v1;
   const int kper = gemv2_kper(N, K);
   const size_t v2 = (size_t)((K + kper - 1) / kper) * nb * nt * 64 * sizeof(f32x4);
-  return std::max(v1, v2);
+  size_t v3 = 0;
+  if (N % G3_ROWS == 0) {
+    const int kp = gemv3_kper(N, K);
+    v3 = (size_t)((K + kp - 1) / kp) * nb * nt * 64 * sizeof(f32x4);
+  }
+  return std::max(std::max(v1, v2), v3);
+}
+
+extern "C" int ospo_set_gemv_splits(int s) {
+  if (s < 0 || s > G2_MAX_SPLITS) return OSPO_ERR_ARG;
+  g_gemv_splits = s;
+  return OSPO_OK;
 }
 
 extern "C" int ospo_set_gemv_variant(int v) {
-  if (v != 1 && v != 2) return OSPO_ERR_ARG;
+  if (v < 1 || v > 3) return OSPO_ERR_ARG;
   g_gemv_variant = v;
   return OSPO_OK;
 }
@@ -502,7 +599,27 @@ extern "C" int ospo_decode_gemv(const void* W, int ldw, const void* X, int ldx, 
   const bf16 *w = (const bf16*)W, *x = (const bf16*)X, *bs = (const bf16*)bias, *rs = (const bf16*)residual;
   bf16* o = (bf16*)out;
   f32x4* wsp = (f32x4*)ws;
-  if (g_gemv_variant == 2 && R <= 32 && N % G2_ROWS == 0 && K >= 8) {
+  if (g_gemv_variant == 3 && R <= 32 && N % G3_ROWS == 0 && K >= 8) {
+    const int kper = gemv3_kper(N, K);
+    const int splits = (K + kper - 1) / kper;
+    if (splits > 1 && (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws))) return OSPO_ERR_ARG;
+    const dim3 grid(N / G3_ROWS, splits);
+#define GEMV3(NT_)                                                                                                \
+  hipLaunchKernelGGL((gemv3_kernel<NT_>), grid, dim3(64 * G3_WAVES), 0, stream, w, ldw, x, ldx, R, K, kper, bs, gelu, \
+                     rs, ldr, o, ldo, wsp);                                                                         \
+  if (splits > 1)                                                                                                 \
+    hipLaunchKernelGGL((gemv2_reduce_kernel<NT_>), dim3((nb + 3) / 4), dim3(256), 0, stream, wsp, splits, nb, R, bs,    \
+                       gelu, rs, ldr, o, ldo);
+    if (nt == 1) {
+      GEMV3(1)
+    } else {
+      GEMV3(2)
+    }
+#undef GEMV3
+    OSPO_CHECK_LAUNCH();
+    return OSPO_OK;
+  }
+  if (g_gemv_variant >= 2 && R <= 32 && N % G2_ROWS == 0 && K >= 8) {
     const int kper = gemv2_kper(N, K);
     const int splits = (K + kper - 1) / kper;
     if (splits > 1 && (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws))) return OSPO_ERR_ARG;

@@ -104,7 +104,7 @@ class T2IGenerator:
         self.tokens = torch.zeros(max_batch, n_img_tokens, dtype=torch.int32, device=dev)
         self.u = torch.zeros(n_img_tokens * max_batch, dtype=torch.float32, device=dev)  # [n, B] of this batch
         shapes = [(3 * D, D), (D, D), (2 * Fd, D), (D, Fd), (Dg, D), (V, Dg), (D, D)]
-        self.gws = torch.empty(max(ops.query("ospo_decode_gemv_ws_bytes", R, n, k) for n, k in shapes) // 4 + 4,
+        self.gws = torch.zeros(max(ops.query("ospo_decode_gemv_ws_bytes", R, n, k) for n, k in shapes) // 4 + 4,
                                dtype=torch.float32, device=dev)
         self.cos, self.sin = ops.rope_tables(self.Tmax, 128, dims.rope_theta, dev)
         self._graph = None

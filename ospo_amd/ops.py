@@ -390,7 +390,7 @@ def adamw_clip(p, g, m, v, lr, beta1, beta2, eps, wd, step, sumsq_buf, max_norm)
 # ------------------------------------------------------ step-3 T2I decode (config 4)
 def decode_gemv_ws(R: int, N: int, K: int, device) -> torch.Tensor:
     nbytes = query("ospo_decode_gemv_ws_bytes", R, N, K)
-    return torch.empty(max(nbytes // 4, 4), dtype=torch.float32, device=device)
+    return torch.zeros(max(nbytes // 4, 4), dtype=torch.float32, device=device)
 
 
 def decode_gemv(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu: bool = False, residual=None,
