@@ -407,6 +407,109 @@ __global__ __launch_bounds__(256) void attn_cache_kernel(const bf16* __restrict_
   }
 }
 
+// v2 of the cached attention: 16-B loads.  Lane (key group kg = 4 w + (lane >> 4), chunk
+// c = lane & 15) holds 8 head dims; a wave reads 4 whole K (V) rows per load instruction (1 KiB),
+// 4 instructions in flight.  The q.k dot is 8 FMAs + a 16-lane DPP reduction (no LDS round
+// trip); P.V accumulates 8 dims per lane over keys kg, kg + 16, ..., then the 16 key groups are
+// summed in a fixed order.  Rounding points as attn_cache_kernel.
+__device__ __forceinline__ float dpp_sum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xf, 0xf, false));  // row_ror:8
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xf, 0xf, false));  // row_ror:4
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4e, 0xf, 0xf, false));   // quad xor 2
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xb1, 0xf, 0xf, false));   // quad xor 1
+  return x;
+}
+
+__global__ __launch_bounds__(256) void attn_cache2_kernel(const bf16* __restrict__ q, int ldq,
+                                                          const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+                                                          int H, int Tmax, const int* __restrict__ start,
+                                                          const int* __restrict__ pos_dev, int nq, float scale,
+                                                          bf16* __restrict__ out, int ldo) {
+  __shared__ float sc[ATT_MAXT];
+  __shared__ float red[8];
+  __shared__ f32x4 part[16][16][2];
+  const int ri = blockIdx.x, h = blockIdx.y;
+  const int r = ri / nq, i = ri % nq;
+  const int p = (pos_dev ? *pos_dev : 0) + i;
+  const int s0 = start[r];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, kg = wave * 4 + (lane >> 4);
+  bf16* orow = out + (long)ri * ldo + h * HD;
+  if (p < s0 || p >= Tmax) {  // a padded query position: never consumed
+    if (threadIdx.x < 16) *reinterpret_cast<u32x4*>(orow + 8 * threadIdx.x) = u32x4{0u, 0u, 0u, 0u};
+    return;
+  }
+  const int L = p - s0 + 1;
+  float qf[8];
+  unpack8(*reinterpret_cast<const u32x4*>(q + (long)ri * ldq + h * HD + 8 * c), qf);
+  const long hb = ((long)r * H + h) * Tmax;
+  const bf16* kb = kc + (hb + s0) * HD + 8 * c;
+  for (int k0 = kg; k0 < L; k0 += 64) {
+    u32x4 kv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) kv[u] = *reinterpret_cast<const u32x4*>(kb + (long)min(k0 + 16 * u, L - 1) * HD);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float kf[8];
+      unpack8(kv[u], kf);
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(qf[e], kf[e], d);
+      d = dpp_sum16(d);
+      if (c == 0 && k0 + 16 * u < L) sc[k0 + 16 * u] = round_bf(round_bf(d) * scale);
+    }
+  }
+  __syncthreads();
+  float m = -INFINITY;
+  for (int k = threadIdx.x; k < L; k += 256) m = fmaxf(m, sc[k]);
+  m = wave_max(m);
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+  for (int k = threadIdx.x; k < L; k += 256) {
+    const float e = __expf(sc[k] - m);
+    sc[k] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  if (lane == 0) red[4 + wave] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  const bf16* vb = vc + (hb + s0) * HD + 8 * c;
+  float a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  for (int k0 = kg; k0 < L; k0 += 64) {
+    u32x4 vv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) vv[u] = *reinterpret_cast<const u32x4*>(vb + (long)min(k0 + 16 * u, L - 1) * HD);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float pk = (k0 + 16 * u < L) ? round_bf(sc[min(k0 + 16 * u, L - 1)] * inv) : 0.f;
+      float vf[8];
+      unpack8(vv[u], vf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = fmaf(pk, vf[e], a[e]);
+    }
+  }
+  part[kg][c][0] = f32x4{a[0], a[1], a[2], a[3]};
+  part[kg][c][1] = f32x4{a[4], a[5], a[6], a[7]};
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int cc = threadIdx.x;
+    f32x4 o0 = part[0][cc][0], o1 = part[0][cc][1];
+#pragma unroll
+    for (int g2 = 1; g2 < 16; ++g2) {
+      o0 += part[g2][cc][0];
+      o1 += part[g2][cc][1];
+    }
+    const float o[8] = {o0[0], o0[1], o0[2], o0[3], o1[0], o1[1], o1[2], o1[3]};
+    *reinterpret_cast<u32x4*>(orow + 8 * cc) = pack8(o);
+  }
+}
+
 // --------------------------------------------------------- CFG + sampling
 // one workgroup per image b: logits rows 2b (cond) and 2b+1 (uncond) [V] bf16 (train.py-style
 // interleaving of image_generation.py:132-141, 156-157).  l = bf16(lu + bf16(w * bf16(lc - lu))),
@@ -684,9 +787,12 @@ extern "C" int ospo_attn_cache(const void* q, int ldq, const void* k_cache, cons
   if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
   if (R <= 0 || nq <= 0 || n_heads <= 0 || Tmax <= 0 || Tmax > ATT_MAXT) return OSPO_ERR_SHAPE;
   if (ldq < n_heads * HD || ldo < n_heads * HD || ldq % 2 || ldo % 2) return OSPO_ERR_SHAPE;
-  hipLaunchKernelGGL(attn_cache_kernel, dim3(R * nq, n_heads), dim3(256), 0, stream, (const bf16*)q, ldq,
-                     (const bf16*)k_cache, (const bf16*)v_cache, n_heads, Tmax, start, pos_dev, nq, scale, (bf16*)out,
-                     ldo);
+  // v2 (16-B loads) needs 16-B aligned q / out rows and caches; else the 4-B form
+  const bool v2 = ldq % 8 == 0 && ldo % 8 == 0 && aligned16(q) && aligned16(out) && aligned16(k_cache) &&
+                  aligned16(v_cache);
+  hipLaunchKernelGGL(v2 ? attn_cache2_kernel : attn_cache_kernel, dim3(R * nq, n_heads), dim3(256), 0, stream,
+                     (const bf16*)q, ldq, (const bf16*)k_cache, (const bf16*)v_cache, n_heads, Tmax, start, pos_dev, nq,
+                     scale, (bf16*)out, ldo);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
