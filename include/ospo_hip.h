@@ -292,7 +292,7 @@ int ospo_decode_advance(int* pos_dev, int* step_dev, hipStream_t stream);
 /* Test / A-B knob of the 256x256 GEMMs: 0 = cost-model split of the tail round (default), 2..8 = force
  * that split-K factor on the tail tiles (bounded by K / 4 K-tiles per piece). */
 int ospo_gemm_force_split(int s);
-/* A/B knob of the LoRA skinny products: 1 = 16-row loop, 2 = 64-row LDS-shared (default). */
+/* A/B knob of the LoRA skinny products: 1 = 16-row loop, 2 = 64-row LDS-shared, 3 = 2 with K splits of whole chunks (default). */
 int ospo_set_skinny_variant(int v);
 /* A/B knob of the decode GEMV schedule: 1 = skinny loop, 2 = LDS-shared activations,
  * 3 = the same with 128 weight rows per workgroup and power-of-two K splits (default). */

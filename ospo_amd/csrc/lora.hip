@@ -257,7 +257,17 @@ __global__ void skinny2_reduce_kernel(const float* __restrict__ ws, int splits, 
   const int m = (int)(tid / cq), c = (int)(tid % cq) * 4;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   if (m < M && c < ctot) {
-    for (int z = 0; z < splits; ++z) v += *reinterpret_cast<const f32x4*>(ws + ((long)z * M_pad + m) * ctot + c);
+    // 8 splits' partials in flight at a time (a serial load chain was latency-bound), summed in
+    // split order as before
+    for (int z0 = 0; z0 < splits; z0 += 8) {
+      f32x4 p[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (z0 + u < splits) p[u] = *reinterpret_cast<const f32x4*>(ws + ((long)(z0 + u) * M_pad + m) * ctot + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (z0 + u < splits) v += p[u];
+    }
   }
   uint2 pk;
   pk.x = pack2(v[0] * scale, v[1] * scale);
@@ -283,15 +293,22 @@ struct SkDropArgs {
   int ldxd = 0;
 };
 
-static int g_skinny_variant = 2;  // 1 = 16-row skinny loop, 2 = 64-row LDS-shared (default); A/B knob
+static int g_skinny_variant = 3;  // 1 = 16-row skinny loop, 2 = 64-row LDS-shared, 3 = 2 with whole-chunk splits (default)
 
-// v2 K split: ~1024 workgroups over (64-row blocks x modules), each split >= one chunk
-static int skinny2_kper(int M_out, int K, int nz, int KC) {
+// v2 K split: ~1024 workgroups over (64-row blocks x modules), each split >= one chunk.
+// Variant 3: splits own whole KC chunks (kper = a multiple of KC), so no workgroup runs a short
+// remainder chunk of its own; only the last split can be shorter.
+static int skinny2_kper(int M_out, int K, int nz, int KC, bool whole_chunks) {
   const int blocks = (M_out + 63) / 64 * nz;
   int splits = (1024 + blocks - 1) / blocks;
   splits = splits < 1 ? 1 : splits;
   const int maxs = K / KC > 0 ? K / KC : 1;
   splits = splits > maxs ? maxs : splits;
+  if (whole_chunks) {
+    const int chunks = (K + KC - 1) / KC;
+    const int cpk = (chunks + splits - 1) / splits;
+    return cpk * KC;
+  }
   const int kper = (K + splits - 1) / splits;
   return (kper + 31) / 32 * 32;
 }
@@ -304,7 +321,7 @@ extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
   size_t v2 = 0;
   for (int nz = 1; nz <= n_tiles; nz = nz * 2 > n_tiles && nz < n_tiles ? n_tiles : nz * 2) {
     for (int KC = 128; KC <= 512; KC *= 2) {
-      const int kper = skinny2_kper(M_out, K, nz, KC);
+      const int kper = skinny2_kper(M_out, K, nz, KC, false);  // the larger split count of the two rules
       const size_t sp2 = (K + kper - 1) / kper;
       const size_t b = sp2 > 1 ? sp2 * (size_t)((M_out + 63) / 64 * 64) * 16 * n_tiles * 4 : 0;
       v2 = b > v2 ? b : v2;
@@ -315,7 +332,7 @@ extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
 }
 
 extern "C" int ospo_set_skinny_variant(int v) {
-  if (v != 1 && v != 2) return OSPO_ERR_ARG;
+  if (v < 1 || v > 3) return OSPO_ERR_ARG;
   g_skinny_variant = v;
   return OSPO_OK;
 }
@@ -324,7 +341,7 @@ template <int NT>
 static int launch_skinny2(const bf16* a, int lda, const bf16* b, int ldb, int b_rows, int M, int M_out, int K,
                           int a_koff, int nz, int tiles_total, float scale, bf16* o, int ldo, int out_cols, float* part,
                           size_t ws_bytes, hipStream_t stream, const SkDropArgs& dr) {
-  const int kper = skinny2_kper(M_out, K, nz, Sk2Cfg<NT>::KC);
+  const int kper = skinny2_kper(M_out, K, nz, Sk2Cfg<NT>::KC, g_skinny_variant == 3);
   const int splits = (K + kper - 1) / kper;
   const int M_pad = (M_out + 63) / 64 * 64;
   if (splits > 1 && ws_bytes < (size_t)splits * M_pad * 16 * tiles_total * 4) return OSPO_ERR_SHAPE;
@@ -406,7 +423,7 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
   const bf16* b = (const bf16*)Bt;
   bf16* o = (bf16*)out;
   f32x4* part = (f32x4*)ws;
-  if (g_skinny_variant == 2 && out_cols % 4 == 0 && K >= 128) {
+  if (g_skinny_variant >= 2 && out_cols % 4 == 0 && K >= 128) {
     // dense: one workgroup column over all n-tiles; block-diagonal: grid z = module
     const int nz = a_koff > 0 ? nmods : 1;
     const int nt = a_koff > 0 ? module_tiles : n_tiles;

@@ -12,6 +12,7 @@ from ospo_amd._lib import call  # noqa: E402
 
 M = 4800
 r = int(os.environ.get("SK_R", "16"))
+VA, VB = (int(v) for v in os.environ.get("SK_VARIANTS", "1,2").split(","))
 CASES = [  # name, K (contraction per module), nmods, dense(u)?, dropout
     ("u_qkv", 4096, 3, True, 0.05), ("u_o", 4096, 1, True, 0.05), ("u_gu", 4096, 2, True, 0.05),
     ("u_down", 11008, 1, True, 0.05), ("g_qkv", 4096, 3, False, 0), ("g_o", 4096, 1, False, 0),
@@ -54,12 +55,12 @@ for name, K, nm, dense, p in CASES:
 
     def run():
         ops.lora_skinny(A, Bt, out, M, M, Ktot, nt, koff, 2.0, **kw)
-    res, outs = {1: [], 2: []}, {}
+    res, outs = {VA: [], VB: []}, {}
     for _ in range(5):
-        for v in (1, 2):
+        for v in (VA, VB):
             call("ospo_set_skinny_variant", v)
             res[v].append(timeit(run))
-    for v in (1, 2):
+    for v in (VA, VB):
         call("ospo_set_skinny_variant", v)
         out.fill_(7)
         run()
@@ -67,9 +68,9 @@ for name, K, nm, dense, p in CASES:
     call("ospo_set_skinny_variant", 2)
     nbytes = A.numel() * 2 * (2 if xd is not None else 1)
     line = {"case": name, "K": K, "nmods": nm, "r": r,
-            "v1_vs_v2_relerr": float((outs[1][0].float() - outs[2][0].float()).norm() / outs[1][0].float().norm()),
-            "xd_equal": bool(torch.equal(outs[1][1], outs[2][1])) if xd is not None else None}
-    for v in (1, 2):
+            "a_vs_b_relerr": float((outs[VA][0].float() - outs[VB][0].float()).norm() / outs[VA][0].float().norm()),
+            "xd_equal": bool(torch.equal(outs[VA][1], outs[VB][1])) if xd is not None else None}
+    for v in (VA, VB):
         t = sorted(res[v])[2]
         line[f"v{v}"] = {"us": round(t * 1e3, 1), "GBps": round(nbytes / t / 1e6, 1)}
     print(json.dumps(line), flush=True)
