@@ -326,7 +326,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
 // owns 16 keys (K, V fragments in registers, dK^T dV^T accumulators) and
 // sweeps the query tiles at/after its block.  Q / dO tiles (+ lse, delta) are
 // double-buffered in LDS through global_load_lds; no atomics.
-template <int NW>
+// DBG (A/B decomposition only, results invalid): 1 = no softmax VALU (P = S, dS = dP),
+// 2 = no dV/dK products, 3 = no S/dP products, 4 = no Q/dO loads after the first tile
+template <int NW, int DBG = 0>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
                                                             int vc, const bf16* __restrict__ dout, int ldd,
                                                             const float* __restrict__ lse,
@@ -385,7 +387,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
   auto tile = [&](const int qt, auto diag_c) {
     constexpr bool DIAG = decltype(diag_c)::value;
     const int b = (qt - qt0) & 1;
-    if (qt + 1 < nq) stage(qt + 1, b ^ 1);
+    if (qt + 1 < nq && DBG != 4) stage(qt + 1, b ^ 1);
     const char* Qs = smem + b * 2 * TILE_BYTES;
     const char* Os = Qs + TILE_BYTES;
     const float* Ls = Lsb + b * 64;
@@ -399,14 +401,22 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
       dp[a] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        sv[a] = MFMA(frag_row(Qs, 16 * a, d, lane), kf[d], sv[a]);
-        dp[a] = MFMA(frag_row(Os, 16 * a, d, lane), vf[d], dp[a]);
+        if constexpr (DBG == 3) {
+          asm volatile("" ::"v"(frag_row(Qs, 16 * a, d, lane)), "v"(frag_row(Os, 16 * a, d, lane)));
+        } else {
+          sv[a] = MFMA(frag_row(Qs, 16 * a, d, lane), kf[d], sv[a]);
+          dp[a] = MFMA(frag_row(Os, 16 * a, d, lane), vf[d], dp[a]);
+        }
       }
     }
     // element (a, j) is query qt*QB + 4g + 16a + j: masked below the key (causal) or at / past T
     const int lo = key_l - (qt * QB + 4 * g), hi = T - (qt * QB + 4 * g);
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 4; ++a) {
+      if constexpr (DBG == 1) break;
+      // this lane's 4 queries of sub-tile a are consecutive: one 16-B LDS read each for lse, delta
+      const f32x4 lq = *reinterpret_cast<const f32x4*>(Ls + 16 * a + 4 * g);
+      const f32x4 dq4 = *reinterpret_cast<const f32x4*>(Dl + 16 * a + 4 * g);
 #pragma unroll
       for (int j = 0; j < 4; j += 2) {
         float x = sv[a][j], y = sv[a][j + 1];
@@ -416,14 +426,14 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
           x = (e < lo || e >= hi) ? -INFINITY : x;
           y = (e + 1 < lo || e + 1 >= hi) ? -INFINITY : y;
         }
-        const int ql = 16 * a + 4 * g + j;
-        const float px = __builtin_amdgcn_exp2f((x - Ls[ql]) * L2E);
-        const float py = __builtin_amdgcn_exp2f((y - Ls[ql + 1]) * L2E);
+        const float px = __builtin_amdgcn_exp2f((x - lq[j]) * L2E);
+        const float py = __builtin_amdgcn_exp2f((y - lq[j + 1]) * L2E);
         sv[a][j] = px;
         sv[a][j + 1] = py;
-        dp[a][j] = px * (dp[a][j] - Dl[ql]) * scale;
-        dp[a][j + 1] = py * (dp[a][j + 1] - Dl[ql + 1]) * scale;
+        dp[a][j] = px * (dp[a][j] - dq4[j]) * scale;
+        dp[a][j + 1] = py * (dp[a][j + 1] - dq4[j + 1]) * scale;
       }
+    }
     // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . (scale dS)[q][key]
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -439,10 +449,14 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
         trp_issue(Qs, 32 * u, 16 * d0, lane, lo[2], hi[2]);
         trp_issue(Qs, 32 * u, 16 * (d0 + 1), lane, lo[3], hi[3]);
         trp_wait4(lo, hi);
-        dv[d0] = MFMA(trp_join(lo[0], hi[0]), pb, dv[d0]);
-        dv[d0 + 1] = MFMA(trp_join(lo[1], hi[1]), pb, dv[d0 + 1]);
-        dk[d0] = MFMA(trp_join(lo[2], hi[2]), sb, dk[d0]);
-        dk[d0 + 1] = MFMA(trp_join(lo[3], hi[3]), sb, dk[d0 + 1]);
+        if constexpr (DBG != 2) {
+          dv[d0] = MFMA(trp_join(lo[0], hi[0]), pb, dv[d0]);
+          dv[d0 + 1] = MFMA(trp_join(lo[1], hi[1]), pb, dv[d0 + 1]);
+          dk[d0] = MFMA(trp_join(lo[2], hi[2]), sb, dk[d0]);
+          dk[d0 + 1] = MFMA(trp_join(lo[3], hi[3]), sb, dk[d0 + 1]);
+        } else {
+          asm volatile("" ::"v"(pb), "v"(sb));
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -656,7 +670,16 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
                      scale, rc, rs);
   OSPO_CHECK_LAUNCH();
   dim3 grid(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
-  hipLaunchKernelGGL(nw == 8 ? attn_bwd_dkdv_kernel<8> : attn_bwd_dkdv_kernel<4>, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+  static const int dkdv_dbg = [] {  // ablation only (results invalid): tools/attn_bench.py
+    const char* e = getenv("OSPO_ATTN_DKDV_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  auto dkdv = nw == 4 ? attn_bwd_dkdv_kernel<4> : attn_bwd_dkdv_kernel<8>;
+  if (nw == 8 && dkdv_dbg == 1) dkdv = attn_bwd_dkdv_kernel<8, 1>;
+  if (nw == 8 && dkdv_dbg == 2) dkdv = attn_bwd_dkdv_kernel<8, 2>;
+  if (nw == 8 && dkdv_dbg == 3) dkdv = attn_bwd_dkdv_kernel<8, 3>;
+  if (nw == 8 && dkdv_dbg == 4) dkdv = attn_bwd_dkdv_kernel<8, 4>;
+  hipLaunchKernelGGL(dkdv, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
                      v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
