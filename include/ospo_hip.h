@@ -294,6 +294,17 @@ int ospo_decode_advance(int* pos_dev, int* step_dev, hipStream_t stream);
 int ospo_gemm_force_split(int s);
 /* A/B knob of the LoRA skinny products: 1 = 16-row loop, 2 = 64-row LDS-shared, 3 = 2 with K splits of whole chunks (default). */
 int ospo_set_skinny_variant(int v);
+/* Decode-step fusions of the GEMV split sum with its consumer (bit-identical to the unfused
+ * ospo_decode_gemv + consumer; need ospo_decode_gemv_fusable(R, N, K), else OSPO_ERR_UNSUPPORTED):
+ * ospo_decode_gemv_kv: q|k|v = X . W^T (W [3 H 128, K]) then RoPE + KV-cache store as ospo_kv_store
+ *   (one query per row at *pos_dev; q to q_out);
+ * ospo_decode_gemv_swiglu: gate|up = X . W^T (W [2F, K]) then h = SwiGLU as ospo_swiglu_fwd. */
+int ospo_decode_gemv_fusable(int R, int N, int K);
+int ospo_decode_gemv_kv(const void* W, int ldw, const void* X, int ldx, int R, int n_heads, int head_dim, int K,
+                        void* ws, size_t ws_bytes, const int* pos_dev, const void* rope_cos, const void* rope_sin,
+                        void* k_cache, void* v_cache, int Tmax, void* q_out, int ldq, hipStream_t stream);
+int ospo_decode_gemv_swiglu(const void* W, int ldw, const void* X, int ldx, int R, int F, int K, void* ws,
+                            size_t ws_bytes, void* h, int ldh, hipStream_t stream);
 /* A/B knob of the decode GEMV schedule: 1 = skinny loop, 2 = LDS-shared activations,
  * 3 = the same with 128 weight rows per workgroup and power-of-two K splits (default). */
 int ospo_set_gemv_variant(int v);

@@ -53,6 +53,9 @@ SIGNATURES = {
     "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, U, F, P, I, P],
     "ospo_lora_skinny_ws_bytes": [I, I, I],
     "ospo_decode_gemv_ws_bytes": [I, I, I],
+    "ospo_decode_gemv_fusable": [I, I, I],
+    "ospo_decode_gemv_kv": [P, I, P, I, I, I, I, I, P, Z, P, P, P, P, P, I, P, I, P],
+    "ospo_decode_gemv_swiglu": [P, I, P, I, I, I, I, P, Z, P, I, P],
     "ospo_decode_gemv": [P, I, P, I, I, I, I, P, I, P, I, P, I, P, Z, P],
     "ospo_kv_store": [P, I, I, I, P, I, P, P, P, P, I, I, I, P, I, P],
     "ospo_attn_cache": [P, I, P, P, I, I, I, I, I, P, P, F, P, I, P],

@@ -260,6 +260,88 @@ __global__ __launch_bounds__(64 * G3_WAVES) void gemv3_kernel(const bf16* __rest
     }
 }
 
+// Split-sum + consumer fusions of the decode step (v3 partial layout [split][N/16][NT][64] f32x4,
+// lane (g, l16) = rows 16 j + 4 g + q, column 16 nb + l16).  Each sums the splits in split order and
+// rounds exactly as gemv_store (bf16 product), then applies its consumer with that consumer's own
+// rounding, so the outputs are bit-identical to gemv + ospo_kv_store / ospo_swiglu_fwd.
+template <int NT>
+__device__ __forceinline__ f32x4 split_sum(const f32x4* __restrict__ ws, int splits, int NB, int nb, int j, int lane) {
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int z0 = 0; z0 < splits; z0 += 8) {
+    f32x4 p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (z0 + u < splits) p[u] = ws[((long)((z0 + u) * NB + nb) * NT + j) * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (z0 + u < splits) v += p[u];
+  }
+  return v;
+}
+
+// q|k|v = x . W_qkv^T: grid (3H head slices, NT), 256 threads; thread (pr = t >> 6, lane) owns columns
+// d = 16 pr + l16 and d + 64 of its head (the RoPE pair) for 4 rows.
+template <int NT>
+__global__ __launch_bounds__(256) void gemv_reduce_kv_kernel(const f32x4* __restrict__ ws, int splits, int R,
+                                                             const int* __restrict__ pos_dev,
+                                                             const bf16* __restrict__ cs, const bf16* __restrict__ sn,
+                                                             bf16* __restrict__ kc, bf16* __restrict__ vc, int H,
+                                                             int Tmax, bf16* __restrict__ q_out, int ldq) {
+  const int lane = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int hs = blockIdx.x, j = blockIdx.y;
+  const int which = hs / H, h = hs % H;
+  const int NB = 3 * H * 8;
+  const int nb = hs * 8 + pr;
+  const int g = lane >> 4, d = pr * 16 + (lane & 15);
+  const int p = *pos_dev;
+  if (p >= Tmax) return;
+  const f32x4 v1 = split_sum<NT>(ws, splits, NB, nb, j, lane);
+  const f32x4 v2 = split_sum<NT>(ws, splits, NB, nb + 4, j, lane);
+  const float c = which < 2 ? bf2f(cs[(long)p * 64 + d]) : 0.f;
+  const float sv = which < 2 ? bf2f(sn[(long)p * 64 + d]) : 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 16 * j + 4 * g + q;
+    if (r >= R) continue;
+    const float x1 = round_bf(v1[q]), x2 = round_bf(v2[q]);
+    float o1 = x1, o2 = x2;
+    if (which < 2) {  // rotate-half RoPE, rounded per op as kv_store_kernel
+      o1 = round_bf(x1 * c) + round_bf(-x2 * sv);
+      o2 = round_bf(x2 * c) + round_bf(x1 * sv);
+    }
+    if (which == 0) {
+      bf16* qo = q_out + (long)r * ldq + h * HD;
+      qo[d] = f2bf(o1);
+      qo[d + 64] = f2bf(o2);
+    } else {
+      bf16* cache = (which == 1 ? kc : vc) + (((long)r * H + h) * Tmax + p) * HD;
+      cache[d] = f2bf(o1);
+      cache[d + 64] = f2bf(o2);
+    }
+  }
+}
+
+// gate|up = x . W_gu^T, h = bf16(bf16(silu(gate)) * up): grid (F / 64, NT), 256 threads; thread
+// (pr, lane) owns gate column 16 (4 bx + pr) + l16 and its up column F + that.
+template <int NT>
+__global__ __launch_bounds__(256) void gemv_reduce_swiglu_kernel(const f32x4* __restrict__ ws, int splits, int R, int F,
+                                                                 bf16* __restrict__ hout, int ldh) {
+  const int lane = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int j = blockIdx.y;
+  const int NB = 2 * F / 16;
+  const int nb = blockIdx.x * 4 + pr;
+  const int g = lane >> 4, col = nb * 16 + (lane & 15);
+  const f32x4 vg = split_sum<NT>(ws, splits, NB, nb, j, lane);
+  const f32x4 vu = split_sum<NT>(ws, splits, NB, nb + F / 16, j, lane);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 16 * j + 4 * g + q;
+    if (r >= R) continue;
+    const float gt = round_bf(vg[q]), up = round_bf(vu[q]);
+    hout[(long)r * ldh + col] = f2bf(round_bf(silu(gt)) * up);
+  }
+}
+
 // ------------------------------------------------------- KV cache write
 // rows [R][nq] of qkv (q|k|v, H heads of 128 each): position p = pos0 + i (pos0 = *pos_dev, or 0).
 // rope: HF rotate-half on q and k at position p, rounded per op like the eager bf16 path
@@ -688,6 +770,75 @@ extern "C" int ospo_set_gemv_splits(int s) {
 extern "C" int ospo_set_gemv_variant(int v) {
   if (v < 1 || v > 3) return OSPO_ERR_ARG;
   g_gemv_variant = v;
+  return OSPO_OK;
+}
+
+// the fused split-sum consumers need the v3 schedule with a K split (else: gemv + the consumer)
+extern "C" int ospo_decode_gemv_fusable(int R, int N, int K) {
+  if (g_gemv_variant != 3 || R <= 0 || R > 32 || N % G3_ROWS || K < 8 || K % 32) return 0;
+  const int kper = gemv3_kper(N, K);
+  return (K + kper - 1) / kper > 1 ? 1 : 0;
+}
+
+static int gemv3_partials(const bf16* w, int ldw, const bf16* x, int ldx, int R, int N, int K, f32x4* ws,
+                          size_t ws_bytes, hipStream_t stream, int& splits) {
+  const int kper = gemv3_kper(N, K);
+  splits = (K + kper - 1) / kper;
+  if (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws)) return OSPO_ERR_ARG;
+  const dim3 grid(N / G3_ROWS, splits);
+  if (R <= 16)
+    hipLaunchKernelGGL((gemv3_kernel<1>), grid, dim3(64 * G3_WAVES), 0, stream, w, ldw, x, ldx, R, K, kper, nullptr,
+                       0, nullptr, 0, nullptr, 0, ws);
+  else
+    hipLaunchKernelGGL((gemv3_kernel<2>), grid, dim3(64 * G3_WAVES), 0, stream, w, ldw, x, ldx, R, K, kper, nullptr,
+                       0, nullptr, 0, nullptr, 0, ws);
+  return OSPO_OK;
+}
+
+extern "C" int ospo_decode_gemv_kv(const void* W, int ldw, const void* X, int ldx, int R, int n_heads, int head_dim,
+                                   int K, void* ws, size_t ws_bytes, const int* pos_dev, const void* rope_cos,
+                                   const void* rope_sin, void* k_cache, void* v_cache, int Tmax, void* q_out, int ldq,
+                                   hipStream_t stream) {
+  if (!W || !X || !pos_dev || !rope_cos || !rope_sin || !k_cache || !v_cache || !q_out) return OSPO_ERR_ARG;
+  if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
+  const int N = 3 * n_heads * HD;
+  if (!ospo_decode_gemv_fusable(R, N, K)) return OSPO_ERR_UNSUPPORTED;
+  if (ldw < K || ldx < K || ldw % 8 || ldx % 8 || ldq < n_heads * HD || Tmax <= 0) return OSPO_ERR_SHAPE;
+  if (!aligned16(W) || !aligned16(X)) return OSPO_ERR_ALIGN;
+  int splits = 0;
+  const int rc = gemv3_partials((const bf16*)W, ldw, (const bf16*)X, ldx, R, N, K, (f32x4*)ws, ws_bytes, stream, splits);
+  if (rc != OSPO_OK) return rc;
+  const dim3 grid(3 * n_heads, (R + 15) / 16);
+  if (R <= 16)
+    hipLaunchKernelGGL((gemv_reduce_kv_kernel<1>), grid, dim3(256), 0, stream, (const f32x4*)ws, splits, R, pos_dev,
+                       (const bf16*)rope_cos, (const bf16*)rope_sin, (bf16*)k_cache, (bf16*)v_cache, n_heads, Tmax,
+                       (bf16*)q_out, ldq);
+  else
+    hipLaunchKernelGGL((gemv_reduce_kv_kernel<2>), grid, dim3(256), 0, stream, (const f32x4*)ws, splits, R, pos_dev,
+                       (const bf16*)rope_cos, (const bf16*)rope_sin, (bf16*)k_cache, (bf16*)v_cache, n_heads, Tmax,
+                       (bf16*)q_out, ldq);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_decode_gemv_swiglu(const void* W, int ldw, const void* X, int ldx, int R, int F, int K, void* ws,
+                                       size_t ws_bytes, void* h, int ldh, hipStream_t stream) {
+  if (!W || !X || !h) return OSPO_ERR_ARG;
+  const int N = 2 * F;
+  if (F % 64 || !ospo_decode_gemv_fusable(R, N, K)) return OSPO_ERR_UNSUPPORTED;
+  if (ldw < K || ldx < K || ldw % 8 || ldx % 8 || ldh < F) return OSPO_ERR_SHAPE;
+  if (!aligned16(W) || !aligned16(X)) return OSPO_ERR_ALIGN;
+  int splits = 0;
+  const int rc = gemv3_partials((const bf16*)W, ldw, (const bf16*)X, ldx, R, N, K, (f32x4*)ws, ws_bytes, stream, splits);
+  if (rc != OSPO_OK) return rc;
+  const dim3 grid(F / 64, (R + 15) / 16);
+  if (R <= 16)
+    hipLaunchKernelGGL((gemv_reduce_swiglu_kernel<1>), grid, dim3(256), 0, stream, (const f32x4*)ws, splits, R, F,
+                       (bf16*)h, ldh);
+  else
+    hipLaunchKernelGGL((gemv_reduce_swiglu_kernel<2>), grid, dim3(256), 0, stream, (const f32x4*)ws, splits, R, F,
+                       (bf16*)h, ldh);
+  OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
 

@@ -181,17 +181,27 @@ class T2IGenerator:
         scale = 1.0 / math.sqrt(128)
         g = self.gws
         x, xo = self.x[:R], self.xo[:R]
+        D, Fd = dims.d_model, dims.d_ff
+        fuse_qkv = ops.decode_gemv_fusable(R, 3 * D, D)  # split sum + RoPE/KV store in one kernel
+        fuse_gu = ops.decode_gemv_fusable(R, 2 * Fd, D)  # split sum + SwiGLU in one kernel
         for i, lw in enumerate(self.layers):
             ops.rmsnorm_fwd(x, lw["ln_in"], self.xn[:R], self.rstd[:R], dims.rms_eps)
-            ops.decode_gemv(self.xn[:R], lw["qkv"], self.qkv[:R], ws=g)
-            ops.kv_store(self.qkv[:R], R, 1, self.pos, self.kc[i], self.vc[i], H, self.Tmax, rope=(self.cos, self.sin),
-                         q_out=self.q[:R])
+            if fuse_qkv:
+                ops.decode_gemv_kv(self.xn[:R], lw["qkv"], g, self.pos, (self.cos, self.sin), self.kc[i], self.vc[i],
+                                   H, self.Tmax, self.q[:R])
+            else:
+                ops.decode_gemv(self.xn[:R], lw["qkv"], self.qkv[:R], ws=g)
+                ops.kv_store(self.qkv[:R], R, 1, self.pos, self.kc[i], self.vc[i], H, self.Tmax,
+                             rope=(self.cos, self.sin), q_out=self.q[:R])
             ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos, scale,
                            self.attn[:R])
             ops.decode_gemv(self.attn[:R], lw["o"], self.xmid[:R], residual=x, ws=g)
             ops.rmsnorm_fwd(self.xmid[:R], lw["ln_post"], self.xn2[:R], self.rstd[:R], dims.rms_eps)
-            ops.decode_gemv(self.xn2[:R], lw["gu"], self.gu[:R], ws=g)
-            ops.swiglu_fwd(self.gu[:R], self.h[:R])
+            if fuse_gu:
+                ops.decode_gemv_swiglu(self.xn2[:R], lw["gu"], g, self.h[:R])
+            else:
+                ops.decode_gemv(self.xn2[:R], lw["gu"], self.gu[:R], ws=g)
+                ops.swiglu_fwd(self.gu[:R], self.h[:R])
             ops.decode_gemv(self.h[:R], lw["down"], xo, residual=self.xmid[:R], ws=g)
             x, xo = xo, x
         self._head_and_sample(x, R)

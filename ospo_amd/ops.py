@@ -408,6 +408,34 @@ def decode_gemv(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=Non
     return out
 
 
+def decode_gemv_fusable(R: int, N: int, K: int) -> bool:
+    return bool(query("ospo_decode_gemv_fusable", R, N, K))
+
+
+def decode_gemv_kv(x, w, ws, pos_dev, rope, k_cache, v_cache, n_heads, Tmax, q_out):
+    """q|k|v = x . w^T then RoPE + KV store (ospo_decode_gemv_kv; == decode_gemv + kv_store)."""
+    _chk(x, BF16, "x")
+    _chk(w, BF16, "w")
+    R, K = x.shape
+    cos, sin = rope
+    call("ospo_decode_gemv_kv", _p(w), _ld(w), _p(x), _ld(x), R, n_heads, 128, K, _p(ws), ws.numel() * 4,
+         _p(pos_dev), _p(cos), _p(sin), _p(k_cache), _p(v_cache), Tmax, _p(q_out), _ld(q_out), _s())
+
+
+def decode_gemv_swiglu(x, w, ws, h):
+    """h = swiglu(x . w^T), w = [gate; up] (ospo_decode_gemv_swiglu; == decode_gemv + swiglu_fwd)."""
+    _chk(x, BF16, "x")
+    _chk(w, BF16, "w")
+    _chk(h, BF16, "h")
+    R, K = x.shape
+    F = w.shape[0] // 2
+    if h.shape[0] < R or h.shape[1] != F:
+        raise ValueError(f"decode_gemv_swiglu: h{tuple(h.shape)} for R={R}, F={F}")
+    call("ospo_decode_gemv_swiglu", _p(w), _ld(w), _p(x), _ld(x), R, F, K, _p(ws), ws.numel() * 4, _p(h), _ld(h),
+         _s())
+    return h
+
+
 def kv_store(qkv, R, nq, pos_dev, k_cache, v_cache, n_heads, Tmax, *, rope=None, q_out=None):
     cos, sin = rope if rope is not None else (None, None)
     call("ospo_kv_store", _p(qkv), _ld(qkv), R, nq, _p(pos_dev), int(rope is not None), _p(cos), _p(sin), _p(k_cache),

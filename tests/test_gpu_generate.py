@@ -200,3 +200,32 @@ def test_generate_7b_shapes_two_layers():
     assert float(l1.mean()) <= max(1.5 * float(floor.mean()), 2e-2)
     assert float(l1.max()) <= max(1.5 * float(floor.max()), 2e-2)
     assert torch.equal(gen.generate(prompts, seed=1, use_graph=True).cpu(), tok)
+
+
+@pytest.mark.parametrize("R", [32, 12])
+def test_decode_gemv_fused_consumers_equal_unfused(R):
+    """The decode step's fused split-sum consumers -- q|k|v GEMV + RoPE/KV store and gate|up GEMV +
+    SwiGLU -- write exactly what decode_gemv followed by kv_store / swiglu_fwd write."""
+    H, D, F, Tmax, p = 32, 4096, 11008, 96, 57
+    assert ops().decode_gemv_fusable(R, 3 * D, D) and ops().decode_gemv_fusable(R, 2 * F, D)
+    x = (torch.randn(R, D, device=DEV)).bfloat16()
+    wq = (torch.randn(3 * D, D, device=DEV) * 0.02).bfloat16()
+    wg = (torch.randn(2 * F, D, device=DEV) * 0.02).bfloat16()
+    ws = ops().decode_gemv_ws(R, 2 * F, D, DEV)
+    ws = torch.zeros(max(ws.numel(), ops().decode_gemv_ws(R, 3 * D, D, DEV).numel()), device=DEV)
+    pos = torch.tensor([p], dtype=torch.int32, device=DEV)
+    cos, sin = ops().rope_tables(Tmax, 128, 1e4, DEV)
+    z = lambda *sh: torch.zeros(*sh, dtype=torch.bfloat16, device=DEV)  # noqa: E731
+    kc1, vc1, q1 = z(R, H, Tmax, 128), z(R, H, Tmax, 128), z(R, D)
+    kc2, vc2, q2 = z(R, H, Tmax, 128), z(R, H, Tmax, 128), z(R, D)
+    qkv = z(R, 3 * D)
+    ops().decode_gemv(x, wq, qkv, ws=ws)
+    ops().kv_store(qkv, R, 1, pos, kc1, vc1, H, Tmax, rope=(cos, sin), q_out=q1)
+    ops().decode_gemv_kv(x, wq, ws, pos, (cos, sin), kc2, vc2, H, Tmax, q2)
+    assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    assert float(kc2[:, :, p].abs().sum()) > 0 and float(kc2[:, :, p + 1].abs().sum()) == 0
+    gu, h1, h2 = z(R, 2 * F), z(R, F), z(R, F)
+    ops().decode_gemv(x, wg, gu, ws=ws)
+    ops().swiglu_fwd(gu, h1)
+    ops().decode_gemv_swiglu(x, wg, ws, h2)
+    assert torch.equal(h1, h2)
