@@ -457,16 +457,21 @@ class SimPOEngine:
 
     def _lora_grads(self, gs, x_in, dy, u, g, gbase):
         """dA = g_s^T . x_in  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal).
-        Only the nmods*r used columns of g enter dA (no atomics of padding rows); 8 K splits."""
+        Only the nmods*r used columns of g enter dA (no atomics of padding rows)."""
         r = self.layout.r
         Mk = self.Mk
         used = g.nmods * r
         a_off = gbase + g.a_off
         dA = self.grads[a_off: a_off + used * g.Kin].view(used, g.Kin)
-        ops.gemm_f32acc(gs[:Mk, :used], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True, k_splits=8)
+        # K splits measured per product on the 7B layer shapes (tools/lora_grads_sweep.py,
+        # profiles/r01/lora_grads_sweep.jsonl): dA 8 (4 for the 11008-wide down input); dB 4 for the
+        # multi-module groups, 8 for the single-module ones
+        ops.gemm_f32acc(gs[:Mk, :used], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True,
+                        k_splits=4 if g.Kin > 8192 else 8)
         b_off = gbase + g.b_off
         dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
-        ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=8, diag=(g.Nmod, r))
+        ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=4 if g.nmods > 1 else 8,
+                        diag=(g.Nmod, r))
 
     # ------------------------------------------------------------ optimizer
     def grad_norm_sq(self) -> torch.Tensor:
