@@ -185,6 +185,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
   const u32x4* dr = reinterpret_cast<const u32x4*>(dy + row * D);
   const u32x4* wr = reinterpret_cast<const u32x4*>(w);
   const u32x4* rr = dres ? reinterpret_cast<const u32x4*>(dres + row * D) : nullptr;
+  // x and dy (the dot's operands) first; the residual grad is loaded after the dot, so it does not
+  // hold IT more registers across it (160 -> ~110 VGPRs: 4 waves per SIMD instead of 3)
   u32x4 xv[IT], dv[IT], rv[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -192,7 +194,6 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
     if (FULL || c < nch) {
       xv[it] = xr[c];
       dv[it] = dr[c];
-      if (rr) rv[it] = rr[c];
     }
   }
   float dot = 0.f;
@@ -209,6 +210,14 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
     }
   }
   const float mdot = wave_sum(dot) / (float)D;
+  asm volatile("" ::: "memory");  // the residual loads stay below the dot
+  if (rr) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int c = it * 64 + lane;
+      if (FULL || c < nch) rv[it] = rr[c];
+    }
+  }
 #pragma unroll
   for (int it = 0; it < IT; ++it) asm volatile("" : "+v"(xv[it]), "+v"(dv[it]));
   asm volatile("" ::: "memory");
