@@ -135,6 +135,18 @@ int ospo_rope_bwd(void* dqkv, int ld, int q_col, int k_col, int S, int T, int n_
 /* --------------------------------------------------------------- SwiGLU ---
  * HF LlamaMLP: h = bf16(bf16(silu(g)) * u) with gu = [g | u] (cols [0,F), [F,2F)). */
 int ospo_swiglu_fwd(const void* gu, int ld_gu, void* h, int ld_h, int M, int F, hipStream_t stream);
+/* The fp8 variant's producers: as ospo_rmsnorm_fwd / _bwd, ospo_swiglu_fwd / _bwd, plus the MXFP8
+ * copy of the bf16 output (q [M, ldq] e4m3, s = scales in ospo_quant_mx8's tile layout; K = D,
+ * D, F, 2F; K % 128 == 0) -- byte-identical to ospo_quant_mx8 of the bf16 output, one HBM pass
+ * less per GEMM operand. */
+int ospo_rmsnorm_fwd_mx8(const void* x, const void* w, void* y, float* rstd, int M, int D, float eps, void* q,
+                         int ldq, void* s, hipStream_t stream);
+int ospo_rmsnorm_bwd_mx8(const void* dy, const void* x, const void* w, const float* rstd, const void* dres, void* dx,
+                         int M, int D, void* q, int ldq, void* s, hipStream_t stream);
+int ospo_swiglu_fwd_mx8(const void* gu, int ld_gu, void* h, int ld_h, int M, int F, void* q, int ldq, void* s,
+                        hipStream_t stream);
+int ospo_swiglu_bwd_mx8(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu, int M, int F,
+                        void* q, int ldq, void* s, hipStream_t stream);
 int ospo_swiglu_bwd(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu,
                     int M, int F, hipStream_t stream);
 

@@ -36,6 +36,10 @@ SIGNATURES = {
     "ospo_rope_fwd": [P, I, I, I, I, I, I, I, P, P, P],
     "ospo_rope_bwd": [P, I, I, I, I, I, I, I, P, P, P],
     "ospo_swiglu_fwd": [P, I, P, I, I, I, P],
+    "ospo_rmsnorm_fwd_mx8": [P, P, P, P, I, I, F, P, I, P, P],
+    "ospo_rmsnorm_bwd_mx8": [P, P, P, P, P, P, I, I, P, I, P, P],
+    "ospo_swiglu_fwd_mx8": [P, I, P, I, I, I, P, I, P, P],
+    "ospo_swiglu_bwd_mx8": [P, I, P, I, P, I, I, I, P, I, P, P],
     "ospo_swiglu_bwd": [P, I, P, I, P, I, I, I, P],
     "ospo_flash_attn_fwd": [P, I, I, I, I, P, I, P, I, I, I, I, F, P],
     "ospo_flash_attn_bwd": [P, I, I, I, I, P, I, P, I, P, P, P, P, I, I, I, I, I, F, P, P, P],

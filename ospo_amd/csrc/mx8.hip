@@ -15,7 +15,7 @@
 // so lane l of a 16-row MFMA fragment finds the scale of (row l & 15, k-block l >> 4) in one
 // dword, with OPSEL picking the fragment's 16-row group.  Rows are padded to a multiple of 256
 // (the GEMM tile); the padding's scales are written as 0.
-#include "common.h"
+#include "mx8.h"
 
 namespace {
 
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void quant_mx8_kernel(const bf16* __restrict__
   if (idx >= (long)Mp * nb) return;
   const int row = (int)(idx / nb), b = (int)(idx % nb);
   const int KT = K >> 7;
-  const long sidx = (((long)(row >> 6) * KT + (b >> 2)) * 64 + (b & 3) * 16 + (row & 15)) * 4 + ((row & 63) >> 4);
+  const long sidx = mx8_scale_index(row, b, KT);
   if (row >= M) {
     S[sidx] = 0;
     return;
@@ -45,20 +45,11 @@ __global__ __launch_bounds__(256) void quant_mx8_kernel(const bf16* __restrict__
       v[8 * i + 2 * q + 1] = __uint_as_float(w[i][q] & 0xffff0000u);
       amax = fmaxf(amax, fmaxf(fabsf(v[8 * i + 2 * q]), fabsf(v[8 * i + 2 * q + 1])));
     }
-  const uint32_t abits = __float_as_uint(amax);
-  const int ebits = (int)((abits >> 23) & 0xff);
-  const int sbyte = min(max(ebits - 8 + ((abits & 0x7fffffu) > 0x600000u ? 1 : 0), 0), 254);
-  const float inv = __uint_as_float((uint32_t)(254 - sbyte) << 23);  // 2^(127 - sbyte) = 1 / X
+  const int sbyte = mx8_scale_byte(amax);
+  const float inv = mx8_inv_scale(sbyte);
   uint32_t o[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    float f[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) f[q] = fminf(fmaxf(v[4 * i + q] * inv, -448.f), 448.f);
-    int r = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], r, true);
-    o[i] = (uint32_t)r;
-  }
+  for (int i = 0; i < 8; ++i) o[i] = mx8_pack4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3], inv);
   uint8_t* dst = Q + (long)row * ldq + b * 32;
   *reinterpret_cast<u32x4*>(dst) = u32x4{o[0], o[1], o[2], o[3]};
   *reinterpret_cast<u32x4*>(dst + 16) = u32x4{o[4], o[5], o[6], o[7]};

@@ -3,6 +3,7 @@
 // loss, LoRA operand packing and the fused clip + AdamW.  All bf16 traffic is
 // 16 B per lane (8 bf16); reductions are wave shuffles (64 lanes) + LDS.
 #include "common.h"
+#include "mx8.h"
 
 #include <math.h>
 
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16* __restrict
 template <int IT, bool FULL>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_w_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                             bf16* __restrict__ y, float* __restrict__ rstd, long M,
-                                                            int D, float eps) {
+                                                            int D, float eps, const Mx8Out mo) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -165,7 +166,12 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_w_kernel(const bf16* __restri
       unpack8(wr[c], g);
 #pragma unroll
       for (int q = 0; q < 8; ++q) f[q] = g[q] * round_bf(f[q] * r);
-      yr[c] = pack8(f);
+      const u32x4 pk = pack8(f);
+      yr[c] = pk;
+      if (mo.q) {  // the fp8 variant's GEMM operand, from the bf16 values just stored
+        unpack8(pk, f);
+        mx8_store8(mo, row, c, f);
+      }
     }
   }
   if (lane == 0) rstd[row] = r;
@@ -175,7 +181,7 @@ template <int IT, bool FULL>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                             const bf16* __restrict__ w, const float* __restrict__ rstd,
                                                             const bf16* __restrict__ dres, bf16* __restrict__ dx,
-                                                            long M, int D) {
+                                                            long M, int D, const Mx8Out mo) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -234,7 +240,12 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
       if (rr) unpack8(rv[it], res);
 #pragma unroll
       for (int q = 0; q < 8; ++q) o[q] = res[q] + r * (d[q] * ww[q] - f[q] * r * mdot);
-      outr[c] = pack8(o);
+      const u32x4 pk = pack8(o);
+      outr[c] = pk;
+      if (mo.q) {
+        unpack8(pk, o);
+        mx8_store8(mo, row, c, o);
+      }
     }
   }
 }
@@ -280,7 +291,8 @@ __global__ void rope_kernel(bf16* __restrict__ x, int ld, int q_col, int k_col, 
 }
 
 // ------------------------------------------------------------------- SwiGLU
-__global__ void swiglu_fwd_kernel(const bf16* __restrict__ gu, int ldg, bf16* __restrict__ h, int ldh, long M, int F) {
+__global__ void swiglu_fwd_kernel(const bf16* __restrict__ gu, int ldg, bf16* __restrict__ h, int ldh, long M, int F,
+                                  const Mx8Out mo) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cpr = F / 8;
   if (tid >= M * cpr) return;
@@ -291,11 +303,16 @@ __global__ void swiglu_fwd_kernel(const bf16* __restrict__ gu, int ldg, bf16* __
   unpack8(*reinterpret_cast<const u32x4*>(gu + m * ldg + F + c * 8), u);
 #pragma unroll
   for (int q = 0; q < 8; ++q) o[q] = round_bf(silu(g[q])) * u[q];
-  *reinterpret_cast<u32x4*>(h + m * ldh + c * 8) = pack8(o);
+  const u32x4 pk = pack8(o);
+  *reinterpret_cast<u32x4*>(h + m * ldh + c * 8) = pk;
+  if (mo.q) {  // 4 consecutive threads = one 32-block of the row (F % 32 == 0)
+    unpack8(pk, o);
+    mx8_store8(mo, m, c, o);
+  }
 }
 
 __global__ void swiglu_bwd_kernel(const bf16* __restrict__ dh, int lddh, const bf16* __restrict__ gu, int ldg,
-                                  bf16* __restrict__ dgu, int lddg, long M, int F) {
+                                  bf16* __restrict__ dgu, int lddg, long M, int F, const Mx8Out mo) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cpr = F / 8;
   if (tid >= M * cpr) return;
@@ -313,8 +330,15 @@ __global__ void swiglu_bwd_kernel(const bf16* __restrict__ dh, int lddh, const b
     const float da = round_bf(d[q] * u[q]);
     dg[q] = da * sg * (1.f + g[q] * (1.f - sg));
   }
-  *reinterpret_cast<u32x4*>(dgu + m * lddg + c * 8) = pack8(dg);
-  *reinterpret_cast<u32x4*>(dgu + m * lddg + F + c * 8) = pack8(du);
+  const u32x4 pg = pack8(dg), pu = pack8(du);
+  *reinterpret_cast<u32x4*>(dgu + m * lddg + c * 8) = pg;
+  *reinterpret_cast<u32x4*>(dgu + m * lddg + F + c * 8) = pu;
+  if (mo.q) {  // [dgate | dup] as one row of 2F columns (F % 32 == 0: blocks never straddle the halves)
+    unpack8(pg, dg);
+    unpack8(pu, du);
+    mx8_store8(mo, m, c, dg);
+    mx8_store8(mo, m, F / 8 + c, du);
+  }
 }
 
 // --------------------------------------------------------------------- GELU
@@ -609,8 +633,8 @@ extern "C" int ospo_abi_version(void) { return 1; }
 // host restatement of the device dropout hash (tests pin ospo_amd/dropout.py against it)
 extern "C" unsigned ospo_dropout_hash(unsigned idx, unsigned seed) { return drop_hash(idx, seed); }
 
-extern "C" int ospo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int M, int D, float eps,
-                                hipStream_t st) {
+static int rmsnorm_fwd_impl(const void* x, const void* w, void* y, float* rstd, int M, int D, float eps,
+                            const Mx8Out& mo, hipStream_t st) {
   if (!x || !w || !y || !rstd) return OSPO_ERR_ARG;
   if (M <= 0 || D % 8 || D > 256 * 8 * RMS_MAXIT) return OSPO_ERR_SHAPE;
   if (!aligned16(x) || !aligned16(w) || !aligned16(y)) return OSPO_ERR_ALIGN;
@@ -618,19 +642,20 @@ extern "C" int ospo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rs
   const dim3 gw((M + 3) / 4);
   const bf16 *xb = (const bf16*)x, *wb = (const bf16*)w;
   const long Ml = M;
-  if (D == 4096) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<8, true>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
-  else if (D == 2048) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<4, true>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
-  else if (it <= 1) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<1, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
-  else if (it <= 2) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<2, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
-  else if (it <= 4) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<4, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
-  else if (it <= 8) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<8, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps);
+  if (D == 4096) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<8, true>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps, mo);
+  else if (D == 2048) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<4, true>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps, mo);
+  else if (it <= 1) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<1, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps, mo);
+  else if (it <= 2) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<2, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps, mo);
+  else if (it <= 4) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<4, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps, mo);
+  else if (it <= 8) hipLaunchKernelGGL((rmsnorm_fwd_w_kernel<8, false>), gw, dim3(256), 0, st, xb, wb, (bf16*)y, rstd, Ml, D, eps, mo);
+  else if (mo.q) return OSPO_ERR_UNSUPPORTED;
   else hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3(M), dim3(256), 0, st, xb, wb, (bf16*)y, rstd, D, eps);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
 
-extern "C" int ospo_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, const void* dres,
-                                void* dx, int M, int D, hipStream_t st) {
+static int rmsnorm_bwd_impl(const void* dy, const void* x, const void* w, const float* rstd, const void* dres,
+                            void* dx, int M, int D, const Mx8Out& mo, hipStream_t st) {
   if (!dy || !x || !w || !rstd || !dx) return OSPO_ERR_ARG;
   if (M <= 0 || D % 8 || D > 256 * 8 * RMS_MAXIT) return OSPO_ERR_SHAPE;
   if (!aligned16(dy) || !aligned16(x) || !aligned16(w) || !aligned16(dx) || (dres && !aligned16(dres)))
@@ -639,15 +664,39 @@ extern "C" int ospo_rmsnorm_bwd(const void* dy, const void* x, const void* w, co
   const dim3 gw((M + 3) / 4);
   const bf16 *dyb = (const bf16*)dy, *xb = (const bf16*)x, *wb = (const bf16*)w, *rb = (const bf16*)dres;
   const long Ml = M;
-  if (D == 4096) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<8, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
-  else if (D == 2048) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<4, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
-  else if (it <= 1) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<1, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
-  else if (it <= 2) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<2, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
-  else if (it <= 4) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<4, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
-  else if (it <= 8) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<8, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D);
+  if (D == 4096) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<8, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
+  else if (D == 2048) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<4, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
+  else if (it <= 1) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<1, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
+  else if (it <= 2) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<2, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
+  else if (it <= 4) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<4, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
+  else if (it <= 8) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<8, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
+  else if (mo.q) return OSPO_ERR_UNSUPPORTED;
   else hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(M), dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, D);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
+}
+
+static bool mx8_out_ok(const void* q, int ldq, const void* s, int M, int K) {
+  return q && s && K % 128 == 0 && ldq >= K && ldq % 16 == 0 && M > 0 && aligned16(q) && aligned16(s);
+}
+
+extern "C" int ospo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int M, int D, float eps,
+                                hipStream_t st) {
+  return rmsnorm_fwd_impl(x, w, y, rstd, M, D, eps, Mx8Out{nullptr, 0, nullptr, 0}, st);
+}
+extern "C" int ospo_rmsnorm_fwd_mx8(const void* x, const void* w, void* y, float* rstd, int M, int D, float eps,
+                                    void* q, int ldq, void* s, hipStream_t st) {
+  if (!mx8_out_ok(q, ldq, s, M, D)) return OSPO_ERR_ARG;
+  return rmsnorm_fwd_impl(x, w, y, rstd, M, D, eps, Mx8Out{(uint8_t*)q, ldq, (uint8_t*)s, D}, st);
+}
+extern "C" int ospo_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, const void* dres,
+                                void* dx, int M, int D, hipStream_t st) {
+  return rmsnorm_bwd_impl(dy, x, w, rstd, dres, dx, M, D, Mx8Out{nullptr, 0, nullptr, 0}, st);
+}
+extern "C" int ospo_rmsnorm_bwd_mx8(const void* dy, const void* x, const void* w, const float* rstd, const void* dres,
+                                    void* dx, int M, int D, void* q, int ldq, void* s, hipStream_t st) {
+  if (!mx8_out_ok(q, ldq, s, M, D)) return OSPO_ERR_ARG;
+  return rmsnorm_bwd_impl(dy, x, w, rstd, dres, dx, M, D, Mx8Out{(uint8_t*)q, ldq, (uint8_t*)s, D}, st);
 }
 
 static int rope_common(bool bwd, void* x, int ld, int q_col, int k_col, int S, int T, int H, int hd, const void* c,
@@ -675,27 +724,45 @@ extern "C" int ospo_rope_bwd(void* dqkv, int ld, int q_col, int k_col, int S, in
   return rope_common(true, dqkv, ld, q_col, k_col, S, T, n_heads, head_dim, cos_tab, sin_tab, st);
 }
 
-extern "C" int ospo_swiglu_fwd(const void* gu, int ld_gu, void* h, int ld_h, int M, int F, hipStream_t st) {
+static int swiglu_fwd_impl(const void* gu, int ld_gu, void* h, int ld_h, int M, int F, const Mx8Out& mo,
+                           hipStream_t st) {
   if (!gu || !h) return OSPO_ERR_ARG;
   if (M <= 0 || F % 8 || ld_gu < 2 * F || ld_h < F || ld_gu % 8 || ld_h % 8) return OSPO_ERR_SHAPE;
   if (!aligned16(gu) || !aligned16(h)) return OSPO_ERR_ALIGN;
   const long n = (long)M * (F / 8);
   hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(blocks(n)), dim3(256), 0, st, (const bf16*)gu, ld_gu, (bf16*)h, ld_h,
-                     (long)M, F);
+                     (long)M, F, mo);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
-extern "C" int ospo_swiglu_bwd(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu, int M,
-                               int F, hipStream_t st) {
+static int swiglu_bwd_impl(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu, int M, int F,
+                           const Mx8Out& mo, hipStream_t st) {
   if (!dh || !gu || !dgu) return OSPO_ERR_ARG;
   if (M <= 0 || F % 8 || ld_gu < 2 * F || ld_dgu < 2 * F || ld_dh < F || ld_dh % 8 || ld_gu % 8 || ld_dgu % 8)
     return OSPO_ERR_SHAPE;
   if (!aligned16(dh) || !aligned16(gu) || !aligned16(dgu)) return OSPO_ERR_ALIGN;
   const long n = (long)M * (F / 8);
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(blocks(n)), dim3(256), 0, st, (const bf16*)dh, ld_dh, (const bf16*)gu,
-                     ld_gu, (bf16*)dgu, ld_dgu, (long)M, F);
+                     ld_gu, (bf16*)dgu, ld_dgu, (long)M, F, mo);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
+}
+extern "C" int ospo_swiglu_fwd(const void* gu, int ld_gu, void* h, int ld_h, int M, int F, hipStream_t st) {
+  return swiglu_fwd_impl(gu, ld_gu, h, ld_h, M, F, Mx8Out{nullptr, 0, nullptr, 0}, st);
+}
+extern "C" int ospo_swiglu_fwd_mx8(const void* gu, int ld_gu, void* h, int ld_h, int M, int F, void* q, int ldq,
+                                   void* s, hipStream_t st) {
+  if (!mx8_out_ok(q, ldq, s, M, F)) return OSPO_ERR_ARG;
+  return swiglu_fwd_impl(gu, ld_gu, h, ld_h, M, F, Mx8Out{(uint8_t*)q, ldq, (uint8_t*)s, F}, st);
+}
+extern "C" int ospo_swiglu_bwd(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu, int M,
+                               int F, hipStream_t st) {
+  return swiglu_bwd_impl(dh, ld_dh, gu, ld_gu, dgu, ld_dgu, M, F, Mx8Out{nullptr, 0, nullptr, 0}, st);
+}
+extern "C" int ospo_swiglu_bwd_mx8(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu, int M,
+                                   int F, void* q, int ldq, void* s, hipStream_t st) {
+  if (F % 64 || !mx8_out_ok(q, ldq, s, M, 2 * F)) return OSPO_ERR_ARG;
+  return swiglu_bwd_impl(dh, ld_dh, gu, ld_gu, dgu, ld_dgu, M, F, Mx8Out{(uint8_t*)q, ldq, (uint8_t*)s, 2 * F}, st);
 }
 
 extern "C" int ospo_gelu_fwd(const void* x, void* y, long n, hipStream_t st) {

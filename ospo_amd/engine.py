@@ -224,11 +224,21 @@ class SimPOEngine:
             ops.lora_pack(A, B, g.nmods, r, g.Kin, g.Nmod, g.Rp, Acat, AcatT, Bcat, BT, n_layers=L,
                           layer_stride=self.layout.per_layer)
 
-    def _lin(self, x: torch.Tensor, w, out: torch.Tensor, **kw) -> torch.Tensor:
+    def _mxo(self, K: int):
+        """mx8 mode: the MXFP8 operand a producer kernel (norm / SwiGLU) fills next to its bf16
+        output, so the following _lin(..., pre=True) skips its quantize pass; bf16 mode: None."""
+        return self._mx.get(K)
+
+    def _lin(self, x: torch.Tensor, w, out: torch.Tensor, pre: bool = False, **kw) -> torch.Tensor:
         """A frozen decoder Linear (+ LoRA K-extension / bias / residual / RoPE / dropout epilogues):
-        the bf16 MFMA GEMM, or in mx8 mode: quantize x (MXFP8, one pass) + the block-scaled fp8 GEMM."""
+        the bf16 MFMA GEMM, or in mx8 mode: quantize x (MXFP8, one pass) + the block-scaled fp8 GEMM.
+        pre=True: x's producer already wrote its MXFP8 copy into self._mxo(K) (no quantize pass)."""
         if self.linear_dtype == "mx8":
-            a = ops.quant_mx8(x, self._mx[x.shape[1]])
+            a = self._mx[x.shape[1]]
+            if not pre:
+                ops.quant_mx8(x, a)
+            elif a.m != x.shape[0]:
+                raise RuntimeError(f"pre-quantized operand holds {a.m} rows, the Linear needs {x.shape[0]}")
             return ops.gemm_nt_mx8(a, w, out, **kw)
         return ops.gemm_nt(x, w, out, **kw)
 
@@ -333,28 +343,29 @@ class SimPOEngine:
         for i in range(dims.n_layers):
             a, lw, pk = self.acts[i], self.layers[i], self.packed[i]
             x = a["x"]
-            ops.rmsnorm_fwd(x[:M], lw["ln_in"], a["xn1"][:M], a["rstd1"][:M], dims.rms_eps)
+            ops.rmsnorm_fwd(x[:M], lw["ln_in"], a["xn1"][:M], a["rstd1"][:M], dims.rms_eps, mx=self._mxo(D))
             Acat, _, Bcat, _ = pk["qkv"]
             self._lora_down(a["xn1"], Acat, a["u_qkv"], M, lay.groups["qkv"].nmods, self._drop(i, "qkv"), a.get("xd_qkv"))
             if (3 * D) % 256 == 0:  # q|k RoPE fused into the projection's epilogue
-                self._lin(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat,
+                self._lin(a["xn1"][:M], lw["qkv"], a["qkv"][:M], pre=True, a2=a["u_qkv"][:M], b2=Bcat,
                           rope=(self.cos, self.sin, T, 2 * D))
             else:
-                self._lin(a["xn1"][:M], lw["qkv"], a["qkv"][:M], a2=a["u_qkv"][:M], b2=Bcat)
+                self._lin(a["xn1"][:M], lw["qkv"], a["qkv"][:M], pre=True, a2=a["u_qkv"][:M], b2=Bcat)
                 ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
             ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn)
             Acat, _, Bcat, _ = pk["o"]
             self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods, self._drop(i, "o"), a.get("xd_o"))
             self._lin(a["attn"][:M], lw["o"], a["xmid"][:M], a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
-            ops.rmsnorm_fwd(a["xmid"][:M], lw["ln_post"], a["xn2"][:M], a["rstd2"][:M], dims.rms_eps)
+            ops.rmsnorm_fwd(a["xmid"][:M], lw["ln_post"], a["xn2"][:M], a["rstd2"][:M], dims.rms_eps,
+                            mx=self._mxo(D))
             Acat, _, Bcat, _ = pk["gu"]
             self._lora_down(a["xn2"], Acat, a["u_gu"], M, lay.groups["gu"].nmods, self._drop(i, "gu"), a.get("xd_gu"))
-            self._lin(a["xn2"][:M], lw["gu"], a["gu"][:M], a2=a["u_gu"][:M], b2=Bcat)
-            ops.swiglu_fwd(a["gu"][:M], a["h"][:M])
+            self._lin(a["xn2"][:M], lw["gu"], a["gu"][:M], pre=True, a2=a["u_gu"][:M], b2=Bcat)
+            ops.swiglu_fwd(a["gu"][:M], a["h"][:M], mx=self._mxo(Fd))
             Acat, _, Bcat, _ = pk["down"]
             self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods, self._drop(i, "down"), a.get("xd_d"))
             xn = self.acts[i + 1]["x"] if i + 1 < dims.n_layers else self.x_final
-            self._lin(a["h"][:M], lw["down"], xn[:M], a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
+            self._lin(a["h"][:M], lw["down"], xn[:M], pre=True, a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
         ops.rmsnorm_fwd(self.x_final[:M], self.norm, self.hf[:M], self.rstd_f[:M], dims.rms_eps)
         # gen_head on the N positions that predict image tokens: t = Lt-1 .. T-2 (train.py:385-391)
         ops.gather_rows(self.hf, S, T, Lt - 1, N, self.hsel[:R])
@@ -385,7 +396,7 @@ class SimPOEngine:
         ops.gelu_bwd(self.dz[:R], self.zpre[:R], self.dz[:R])
         ops.gemm_nt(self.dz[:R], self.gh_w1T, self.dhsel[:R])
         ops.scatter_rows(self.dhsel[:R], S, T, Lt - 1, N, self.dxn[:M])
-        ops.rmsnorm_bwd(self.dxn[:M], self.x_final[:M], self.norm, self.rstd_f[:M], self.dx[:M])
+        ops.rmsnorm_bwd(self.dxn[:M], self.x_final[:M], self.norm, self.rstd_f[:M], self.dx[:M], mx=self._mxo(D))
         scale_attn = 1.0 / math.sqrt(hd)
         lay = self.layout
         # LoRA weight grads (dA = g^T x, dB = dy^T u) of each group run on a side stream,
@@ -419,24 +430,24 @@ class SimPOEngine:
             guard("down")
             gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M)
             dr = self._drop(i, "down")
-            self._lin(dx[:M], lw["downT"], self.dh[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("down", gs, a["xd_d"] if dr else a["h"], dx, a["u_d"], gbase)
             guard("gu")  # dgu is rewritten here
-            ops.swiglu_bwd(self.dh[:M], a["gu"][:M], self.dgu[:M])
+            ops.swiglu_bwd(self.dh[:M], a["gu"][:M], self.dgu[:M], mx=self._mxo(2 * Fd))
             # ---- gate/up
             Acat, AcatT, Bcat, BT = pk["gu"]
             gs = self._lora_g(self.dgu, lay.groups["gu"], Bcat, BT, M)
             dr = self._drop(i, "gu")
-            self._lin(self.dgu[:M], lw["guT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(self.dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("gu", gs, a["xd_gu"] if dr else a["xn2"], self.dgu, a["u_gu"], gbase)
             guard("o")  # dxmid is rewritten here
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], self.dxmid[:M],
-                            dres=dx[:M])
+                            dres=dx[:M], mx=self._mxo(D))
             # ---- o_proj
             Acat, AcatT, Bcat, BT = pk["o"]
             gs = self._lora_g(self.dxmid, lay.groups["o"], Bcat, BT, M)
             dr = self._drop(i, "o")
-            self._lin(self.dxmid[:M], lw["oT"], self.dattn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(self.dxmid[:M], lw["oT"], self.dattn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("o", gs, a["xd_o"] if dr else a["attn"], self.dxmid, a["u_o"], gbase)
             # ---- attention + RoPE
             guard("qkv")  # dqkv is rewritten here
@@ -449,7 +460,8 @@ class SimPOEngine:
             self._lin(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("qkv", gs, a["xd_qkv"] if dr else a["xn1"], self.dqkv, a["u_qkv"], gbase)
             guard("down")  # dx (the down group's dy) is rewritten here
-            ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M])
+            ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M],
+                            mx=self._mxo(D))
             if on_layer_grads is not None:
                 with torch.cuda.stream(side):  # this layer's dA/dB are the last side-stream work so far
                     on_layer_grads(gbase, gbase + lay.per_layer)

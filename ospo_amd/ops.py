@@ -226,15 +226,34 @@ def f32_to_bf16(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0) -> tor
 
 
 # ---------------------------------------------------------------- RMSNorm
-def rmsnorm_fwd(x, w, y, rstd, eps: float):
+def _mx_target(mx, M: int, K: int, who: str):
+    if K != mx.K or M > mx.rows:
+        raise ValueError(f"{who}: output [{M}, {K}] does not fit MX8[{mx.rows}, {mx.K}]")
+
+
+def rmsnorm_fwd(x, w, y, rstd, eps: float, mx: "MX8 | None" = None):
+    """y = rmsnorm(x) * w; with mx, also mx <- MXFP8(y) in the same pass (== quant_mx8(y, mx))."""
     M, D = x.shape
-    call("ospo_rmsnorm_fwd", _p(x), _p(w), _p(y), _p(rstd), M, D, float(eps), _s())
+    if mx is None:
+        call("ospo_rmsnorm_fwd", _p(x), _p(w), _p(y), _p(rstd), M, D, float(eps), _s())
+        return y
+    _mx_target(mx, M, D, "rmsnorm_fwd")
+    call("ospo_rmsnorm_fwd_mx8", _p(x), _p(w), _p(y), _p(rstd), M, D, float(eps), _p(mx.q), mx.q.stride(0),
+         _p(mx.s), _s())
+    mx.m = M
     return y
 
 
-def rmsnorm_bwd(dy, x, w, rstd, dx, dres=None):
+def rmsnorm_bwd(dy, x, w, rstd, dx, dres=None, mx: "MX8 | None" = None):
+    """dx = rmsnorm_bwd(dy) [+ dres]; with mx, also mx <- MXFP8(dx) in the same pass."""
     M, D = x.shape
-    call("ospo_rmsnorm_bwd", _p(dy), _p(x), _p(w), _p(rstd), _p(dres), _p(dx), M, D, _s())
+    if mx is None:
+        call("ospo_rmsnorm_bwd", _p(dy), _p(x), _p(w), _p(rstd), _p(dres), _p(dx), M, D, _s())
+        return dx
+    _mx_target(mx, M, D, "rmsnorm_bwd")
+    call("ospo_rmsnorm_bwd_mx8", _p(dy), _p(x), _p(w), _p(rstd), _p(dres), _p(dx), M, D, _p(mx.q),
+         mx.q.stride(0), _p(mx.s), _s())
+    mx.m = M
     return dx
 
 
@@ -253,15 +272,29 @@ def rope_tables(T: int, head_dim: int, theta: float, device) -> tuple:
 
 
 # ----------------------------------------------------------------- SwiGLU
-def swiglu_fwd(gu, h):
+def swiglu_fwd(gu, h, mx: "MX8 | None" = None):
+    """h = silu(g) * u; with mx, also mx <- MXFP8(h) in the same pass."""
     M, F2 = gu.shape
-    call("ospo_swiglu_fwd", _p(gu), _ld(gu), _p(h), _ld(h), M, F2 // 2, _s())
+    if mx is None:
+        call("ospo_swiglu_fwd", _p(gu), _ld(gu), _p(h), _ld(h), M, F2 // 2, _s())
+        return h
+    _mx_target(mx, M, F2 // 2, "swiglu_fwd")
+    call("ospo_swiglu_fwd_mx8", _p(gu), _ld(gu), _p(h), _ld(h), M, F2 // 2, _p(mx.q), mx.q.stride(0), _p(mx.s),
+         _s())
+    mx.m = M
     return h
 
 
-def swiglu_bwd(dh, gu, dgu):
+def swiglu_bwd(dh, gu, dgu, mx: "MX8 | None" = None):
+    """dgu = d(g|u); with mx, also mx <- MXFP8(dgu) (K = 2F) in the same pass."""
     M, F2 = gu.shape
-    call("ospo_swiglu_bwd", _p(dh), _ld(dh), _p(gu), _ld(gu), _p(dgu), _ld(dgu), M, F2 // 2, _s())
+    if mx is None:
+        call("ospo_swiglu_bwd", _p(dh), _ld(dh), _p(gu), _ld(gu), _p(dgu), _ld(dgu), M, F2 // 2, _s())
+        return dgu
+    _mx_target(mx, M, F2, "swiglu_bwd")
+    call("ospo_swiglu_bwd_mx8", _p(dh), _ld(dh), _p(gu), _ld(gu), _p(dgu), _ld(dgu), M, F2 // 2, _p(mx.q),
+         mx.q.stride(0), _p(mx.s), _s())
+    mx.m = M
     return dgu
 
 

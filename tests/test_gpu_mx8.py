@@ -45,6 +45,13 @@ def wild(M, K):
     return x.to(torch.bfloat16)
 
 
+def spread(M, K):
+    """finite bf16 data over many binades (rows scaled 2^-20..2^6), one all-zero block."""
+    x = torch.randn(M, K, device=DEV) * torch.exp2(torch.randint(-20, 7, (M, 1), device=DEV).float())
+    x[0, :32] = 0.0
+    return x.to(torch.bfloat16)
+
+
 @pytest.mark.parametrize("M,K", [(1, 128), (300, 512), (4800, 4096), (257, 11008)])
 def test_quant_mx8_bit_exact(M, K):
     x = wild(M, K)
@@ -166,3 +173,60 @@ def test_gemm_mx8_split_tail_rope_equals_unsplit():
     finally:
         call("ospo_gemm_force_split", 0)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("M,D", [(1, 128), (300, 512), (4800, 4096)])
+@pytest.mark.parametrize("bwd", [False, True])
+def test_rmsnorm_mx8_output_equals_quantized_output(M, D, bwd):
+    """The fp8 step's fused producers: rmsnorm fwd/bwd with an MXFP8 copy of their bf16 output ==
+    the plain kernel's output, and the copy == quant_mx8 of it, byte for byte (elements + scales)."""
+    x, w = spread(M, D), rnd(D)
+    rstd = torch.empty(M, device=DEV)
+    y = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    ops().rmsnorm_fwd(x, w, y, rstd, 1e-6)
+    if bwd:
+        dy, dres = rnd(M, D), rnd(M, D, s=0.5)
+        ref = torch.empty_like(y)
+        ops().rmsnorm_bwd(dy, x, w, rstd, ref, dres=dres)
+        fused, mx = torch.empty_like(y), ops().MX8(M, D, DEV)
+        ops().rmsnorm_bwd(dy, x, w, rstd, fused, dres=dres, mx=mx)
+    else:
+        ref = y
+        fused, mx = torch.empty_like(y), ops().MX8(M, D, DEV)
+        ops().rmsnorm_fwd(x, w, fused, torch.empty_like(rstd), 1e-6, mx=mx)
+    assert torch.equal(fused, ref)
+    q = ops().quant_mx8(ref, ops().MX8(M, D, DEV))
+    assert mx.m == M
+    assert torch.equal(mx.q[:M], q.q[:M])
+    assert torch.equal(mx.s, q.s)
+
+
+@pytest.mark.parametrize("M,F", [(1, 128), (257, 11008), (4800, 1024)])
+@pytest.mark.parametrize("bwd", [False, True])
+def test_swiglu_mx8_output_equals_quantized_output(M, F, bwd):
+    gu = spread(M, 2 * F)
+    if bwd:
+        dh = rnd(M, F)
+        ref = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+        ops().swiglu_bwd(dh, gu, ref)
+        fused, mx = torch.empty_like(ref), ops().MX8(M, 2 * F, DEV)
+        ops().swiglu_bwd(dh, gu, fused, mx=mx)
+    else:
+        ref = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+        ops().swiglu_fwd(gu, ref)
+        fused, mx = torch.empty_like(ref), ops().MX8(M, F, DEV)
+        ops().swiglu_fwd(gu, fused, mx=mx)
+    assert torch.equal(fused, ref)
+    q = ops().quant_mx8(ref, ops().MX8(M, ref.shape[1], DEV))
+    assert torch.equal(mx.q[:M], q.q[:M])
+    assert torch.equal(mx.s, q.s)
+
+
+def test_mx8_producers_reject_bad_targets():
+    x, w = rnd(64, 256), rnd(256)
+    rstd = torch.empty(64, device=DEV)
+    y = torch.empty_like(x)
+    with pytest.raises(ValueError):  # K mismatch
+        ops().rmsnorm_fwd(x, w, y, rstd, 1e-6, mx=ops().MX8(64, 384, DEV))
+    with pytest.raises(ValueError):  # too few rows
+        ops().rmsnorm_fwd(x, w, y, rstd, 1e-6, mx=ops().MX8(32, 256, DEV))
