@@ -762,7 +762,7 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem,
   }
 }
 
-template <int DBG = 0, bool DROP = false, bool MX = false>
+template <int DBG = 0, bool DROP = false, bool MX = false, bool SP = false>
 __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
                                                          int split, float* __restrict__ ws, int GM) {
   constexpr int BM = 256, BN = 256, HALF = 16384, SLOT = 4 * HALF;  // half order in a slot: A0 A1 B0 B1
@@ -859,15 +859,19 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bfr[2][2];
+  bf16x8 bsp[2][2][2];  // SP: [B half][n][k-substep], the whole K-tile's B fragments
   i32x8 a8[4], b8[2];  // MX tiles: both k-halves of a fragment in one 8-register operand
 
-  // prologue: tile 0 complete, A0 of tile 1 in flight
+  // prologue: tile 0 complete, A0 of tile 1 in flight (SP: tile 0 only)
+  static_assert(!(SP && MX), "SP: bf16 tiles only");
   if (nt > 0) {
     stage_scales(0);
     stage_half(0, 2); stage_half(0, 3); stage_half(0, 1); stage_half(0, 0);
   }
-  if (nt > 1) stage_half(1, 0);
-  if (nt > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  if (!SP && nt > 1) stage_half(1, 0);
+  if (SP && nt > 1) { stage_half(1, 2); stage_half(1, 3); stage_half(1, 0); }
+  if (!SP && nt > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (SP && nt > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -880,7 +884,83 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   // one K-tile = 4 phases; a lambda so the dropout variant can peel its extension tiles
   // mxt: an MXFP8 main tile (compile-time, so each loop below keeps one MFMA form and its
   // accumulators in place; a per-phase runtime branch made the compiler copy them)
+  // SP ("super-phase") schedule: 2 phases per K-tile of 32 MFMAs per wave (2 C-quadrants), half the
+  // barriers of the 8-phase schedule and 24 fragment reads per K-tile instead of 32 (the B fragments
+  // of both halves stay in registers across the tile).  Global intervals I (one barrier apart), g1 one
+  // interval behind g0:  I 4t..4t+3  g0: R(t,0) M(t,0) R(t,1) M(t,1);  g1: M(t-1,1) R(t,0) M(t,0) R(t,1).
+  // A slot half is refilled as soon as both groups have read it, from each wave's R sections:
+  //   A1 of tile t+1 in R(t,0), B0 B1 A0 of tile t+2 in R(t,1),
+  // and each wave waits for its pieces (vmcnt: 8 newer pieces at steady state) before the barrier
+  // that opens g0's first read of them -- 5-6 intervals of load latency per piece.
+  auto wait_sp = [&](int n) __attribute__((always_inline)) { wait_vmcnt_exact(n); };
+  auto run_tile_sp = [&](int t) __attribute__((always_inline)) {
+    const char* slot = smem + (t & 1) * SLOT;
+    const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const char* la = slot + p * HALF;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
+      if (p == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              bsp[h][n][s] = *reinterpret_cast<const bf16x8*>(slot + (2 + h) * HALF +
+                                                               mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+      }
+      if (p == 0 && n1) stage_half(t + 1, 1);
+      if (p == 1 && n2) { stage_half(t + 2, 2); stage_half(t + 2, 3); stage_half(t + 2, 0); }
+      if (g1) {
+        if (p == 0) wait_sp(n1 ? 8 : 0);         // A1(t)
+        if (p == 1 && n1) wait_sp(n2 ? 8 : 2);   // B0 B1 A0 (t+1)
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DBG != 2) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          // p 0: quadrants j 0 (ia 0, ib 0), 1 (0, 1); p 1: j 2 (1, 1), 3 (1, 0)
+          const int j = 2 * p + q;
+          const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int s = 0; s < 2; ++s)
+                acc[j][i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bsp[ib][n][s], af[i][s], acc[j][i][n], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i][0]), "v"(af[i][1]));
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) asm volatile("" ::"v"(bsp[h][n][0]), "v"(bsp[h][n][1]));
+      }
+      if (!g1) {
+        if (p == 0) wait_sp(n1 ? 8 : 0);
+        if (p == 1 && n1) wait_sp(n2 ? 8 : 2);
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  };
   auto run_tile = [&](int t, auto mxt) __attribute__((always_inline)) {
+    if constexpr (SP) {
+      run_tile_sp(t);
+      return;
+    }
     const char* slot = smem + (t & 1) * SLOT;
     constexpr bool mx_tile = MX && decltype(mxt)::value;
     uint32_t scA[2] = {0u, 0u}, scB[2] = {0u, 0u};
@@ -1156,7 +1236,7 @@ int num_cus() {
   return g_num_cus;
 }
 
-template <int DBG = 0, bool DROP = false, bool MX = false>
+template <int DBG = 0, bool DROP = false, bool MX = false, bool SP = false>
 int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
   const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
@@ -1193,7 +1273,7 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
     }
   }
   const int grid = dp + tail * split;
-  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP, MX>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split,
+  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP, MX, SP>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split,
                      g_splitk_ws, g_v5_gm);
   OSPO_CHECK_LAUNCH();
   if (tail) {
@@ -1215,7 +1295,7 @@ int launch_v3(const GemmArgs& a, hipStream_t s) {
   return OSPO_OK;
 }
 
-int g_gemm_variant = 0;  // 0 = 8-phase + split-K tail (default); others: A/B schedules, see dispatch
+int g_gemm_variant = 0;  // 0 = SP schedule + split-K tail (default); 17 = the 8-phase schedule; others: A/B, see dispatch
 
 // NT tile: 256 x 256 (8-phase, split-K tail) whenever N % 256 == 0, else the 64 x 64 simple kernel.
 int pick_nt_tile(int M, int N) {
@@ -1254,7 +1334,12 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 11: return launch<2, 4, 8, 4, false, false, EPI_BF16, 2>(a, stream);
     case 12: return launch_v5<1>(a, stream, false);
     case 13: return launch_v5<2>(a, stream, false);
-    default: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
+    // SP schedule (2 phases of 32 MFMAs per K-tile): 14 + split tail, 15 no loads, 16 no MFMA
+    case 14: return launch_v5<0, false, false, true>(a, stream, true);
+    case 15: return launch_v5<1, false, false, true>(a, stream, false);
+    case 16: return launch_v5<2, false, false, true>(a, stream, false);
+    case 17: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
+    default: return launch_v5<0, false, false, true>(a, stream, true);               // SP + split-K tail
   }
 }
 
@@ -1283,7 +1368,8 @@ extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int
   a.rope_sn = (const bf16*)rope_sin;
   a.rope_T = T;
   a.rope_cols = rope_cols;
-  return launch_v5<0>(a, stream);  // split-K tail fixups apply the RoPE epilogue too
+  // split-K tail fixups apply the RoPE epilogue too
+  return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, true>(a, stream);
 }
 
 extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
@@ -1299,12 +1385,13 @@ extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, 
   if (!aligned16(A) || !aligned16(B) || !aligned16(C) || !aligned16(A2) || !aligned16(B2)) return OSPO_ERR_ALIGN;
   GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
              M, N, K, K2, 1.f, nullptr, nullptr, 0, C, ldc, 1, 0, 0};
-  if (drop_p == 0.f) return launch_v5<0>(a, stream);
+  if (drop_p == 0.f)
+    return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, true>(a, stream);
   a.drop_seed = drop_seed;
   a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = N;
-  return launch_v5<0, true>(a, stream);
+  return g_gemm_variant == 17 ? launch_v5<0, true>(a, stream) : launch_v5<0, true, false, true>(a, stream);
 }
 
 extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, int ldb, const void* Bsc,
@@ -1363,7 +1450,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || v > 13 || (v > 5 && v < 10)) return OSPO_ERR_ARG;
+  if (v < 0 || v > 17 || (v > 5 && v < 10)) return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;

@@ -62,16 +62,19 @@ def main():
                 res[f"split{sp}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
             call("ospo_gemm_force_split", 0)
         exp = a.float() @ b.float().t() + (a2.float() @ b2.float().t() if k2 else 0)
-        errs = {}
+        errs, same = {}, {}
+        call("ospo_set_gemm_variant", 0)
+        ops.gemm_nt(a, b, ref, a2=a2, b2=b2)
         for v in VARIANTS:
             call("ospo_set_gemm_variant", v)
             out.zero_()
             ops.gemm_nt(a, b, out, a2=a2, b2=b2)
             errs[f"v{v}"] = float((out.float() - exp).norm() / exp.norm())
+            same[f"v{v}"] = bool(torch.equal(out, ref))
         call("ospo_set_gemm_variant", 0)
         del exp
         fl = 2.0 * m * n * k
-        line = {"shape": name, "M": m, "N": n, "K": k, "K2": k2, "tile": ops.gemm_nt_tile(m, n), "relerr": errs}
+        line = {"shape": name, "M": m, "N": n, "K": k, "K2": k2, "tile": ops.gemm_nt_tile(m, n), "relerr": errs, "bit_equal_v0": same}
         for kk, ts in res.items():
             t = sorted(ts)[len(ts) // 2]
             line[kk] = {"ms": round(t, 4), "tflops": round(fl / t / 1e9, 1)}
