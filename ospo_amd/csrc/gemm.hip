@@ -861,17 +861,17 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   bf16x8 af[4][2], bfr[2][2];
   bf16x8 bsp[2][2][2];  // SP: [B half][n][k-substep], the whole K-tile's B fragments
   i32x8 a8[4], b8[2];  // MX tiles: both k-halves of a fragment in one 8-register operand
+  i32x8 b8sp[2][2];    // SP + MX: [B half][n]
 
   // prologue: tile 0 complete, A0 of tile 1 in flight (SP: tile 0 only)
-  static_assert(!(SP && MX), "SP: bf16 tiles only");
   if (nt > 0) {
     stage_scales(0);
     stage_half(0, 2); stage_half(0, 3); stage_half(0, 1); stage_half(0, 0);
   }
   if (!SP && nt > 1) stage_half(1, 0);
-  if (SP && nt > 1) { stage_half(1, 2); stage_half(1, 3); stage_half(1, 0); }
+  if (SP && nt > 1) { stage_scales(1); stage_half(1, 2); stage_half(1, 3); stage_half(1, 0); }
   if (!SP && nt > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if (SP && nt > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (SP && nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MX ? 7 : 6) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -892,39 +892,90 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   //   A1 of tile t+1 in R(t,0), B0 B1 A0 of tile t+2 in R(t,1),
   // and each wave waits for its pieces (vmcnt: 8 newer pieces at steady state) before the barrier
   // that opens g0's first read of them -- 5-6 intervals of load latency per piece.
+  // MX: the E8M0 scales of tile t+2 travel with its B0 B1 A0 (7 pieces in that group, 9 newer at steady state)
+  constexpr int KB = MX ? 7 : 6;
   auto wait_sp = [&](int n) __attribute__((always_inline)) { wait_vmcnt_exact(n); };
-  auto run_tile_sp = [&](int t) __attribute__((always_inline)) {
+  auto run_tile_sp = [&](int t, auto mxt) __attribute__((always_inline)) {
+    constexpr bool mx_tile = MX && decltype(mxt)::value;
     const char* slot = smem + (t & 1) * SLOT;
     const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
+    uint32_t scA[2] = {0u, 0u}, scB[2] = {0u, 0u};
+    if constexpr (mx_tile) {  // staged with tile t's B0 B1 A0: landed per the same waits
+      const char* sc = smem + SC_BASE + (t & 1) * SC_SLOT;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        scA[h] = *reinterpret_cast<const uint32_t*>(sc + (h * 2 + wm) * 256 + lane * 4);
+        scB[h] = *reinterpret_cast<const uint32_t*>(sc + 1024 + (h * 2 + (wn >> 1)) * 256 + lane * 4) >>
+                 (16 * (wn & 1));
+      }
+    }
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const char* la = slot + p * HALF;
+      if constexpr (mx_tile) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+          a8[i].lo = *reinterpret_cast<const i32x4*>(la + mmaj_off(wm * 64 + i * 16 + frow, fcol));
+          a8[i].hi = *reinterpret_cast<const i32x4*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 + fcol));
+        }
+        if (p == 0) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
-          af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
-      if (p == 0) {
+          for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+            for (int n = 0; n < 2; ++n) {
+              const char* lb = slot + (2 + h) * HALF;
+              b8sp[h][n].lo = *reinterpret_cast<const i32x4*>(lb + mmaj_off(wn * 32 + n * 16 + frow, fcol));
+              b8sp[h][n].hi = *reinterpret_cast<const i32x4*>(lb + mmaj_off(wn * 32 + n * 16 + frow, 4 + fcol));
+            }
+        }
+      } else {
 #pragma unroll
-          for (int n = 0; n < 2; ++n)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-              bsp[h][n][s] = *reinterpret_cast<const bf16x8*>(slot + (2 + h) * HALF +
-                                                               mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+          for (int s = 0; s < 2; ++s)
+            af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
+        if (p == 0) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int s = 0; s < 2; ++s)
+                bsp[h][n][s] = *reinterpret_cast<const bf16x8*>(slot + (2 + h) * HALF +
+                                                                 mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+        }
       }
       if (p == 0 && n1) stage_half(t + 1, 1);
-      if (p == 1 && n2) { stage_half(t + 2, 2); stage_half(t + 2, 3); stage_half(t + 2, 0); }
+      if (p == 1 && n2) { stage_scales(t + 2); stage_half(t + 2, 2); stage_half(t + 2, 3); stage_half(t + 2, 0); }
       if (g1) {
-        if (p == 0) wait_sp(n1 ? 8 : 0);         // A1(t)
-        if (p == 1 && n1) wait_sp(n2 ? 8 : 2);   // B0 B1 A0 (t+1)
+        if (p == 0) wait_sp(n1 ? KB + 2 : 0);         // A1(t)
+        if (p == 1 && n1) wait_sp(n2 ? KB + 2 : 2);   // B0 B1 A0 (+ scales) of t+1
       }
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DBG != 2) {
+      if constexpr (DBG != 2 && mx_tile) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int j = 2 * p + q;
+          const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+              acc[j][i][n] = mx_mfma(b8sp[ib][n], a8[i], acc[j][i][n], n, scB[ib], i, scA[p]);
+        }
+        // keep the scaled MFMAs inside their phase (see the 8-phase loop)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[2 * p + q][i][n]));
+        __builtin_amdgcn_s_setprio(0);
+      } else if constexpr (DBG != 2) {
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -949,8 +1000,8 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
           for (int n = 0; n < 2; ++n) asm volatile("" ::"v"(bsp[h][n][0]), "v"(bsp[h][n][1]));
       }
       if (!g1) {
-        if (p == 0) wait_sp(n1 ? 8 : 0);
-        if (p == 1 && n1) wait_sp(n2 ? 8 : 2);
+        if (p == 0) wait_sp(n1 ? KB + 2 : 0);
+        if (p == 1 && n1) wait_sp(n2 ? KB + 2 : 2);
       }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -958,7 +1009,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   };
   auto run_tile = [&](int t, auto mxt) __attribute__((always_inline)) {
     if constexpr (SP) {
-      run_tile_sp(t);
+      run_tile_sp(t, mxt);
       return;
     }
     const char* slot = smem + (t & 1) * SLOT;
@@ -1424,16 +1475,16 @@ extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const 
     a.rope_sn = (const bf16*)rope_sin;
     a.rope_T = rope_T;
     a.rope_cols = rope_cols;
-    return launch_v5<0, false, true>(a, stream);
+    return g_gemm_variant == 17 ? launch_v5<0, false, true>(a, stream) : launch_v5<0, false, true, true>(a, stream);
   }
   if (drop) {
     a.drop_seed = drop_seed;
     a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
     a.drop_scale = 1.f / (1.f - drop_p);
     a.drop_ld = N;
-    return launch_v5<0, true, true>(a, stream);
+    return g_gemm_variant == 17 ? launch_v5<0, true, true>(a, stream) : launch_v5<0, true, true, true>(a, stream);
   }
-  return launch_v5<0, false, true>(a, stream);
+  return g_gemm_variant == 17 ? launch_v5<0, false, true>(a, stream) : launch_v5<0, false, true, true>(a, stream);
 }
 
 extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {

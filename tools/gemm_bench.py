@@ -48,10 +48,14 @@ def main():
             res[f"split{sp}"] = []
         if MX8:
             a8, b8 = ops.MX8.of(a), ops.MX8.of(b)
-            res["mx8"], res["mx8_quantA"] = [], []
+            res["mx8_quantA"] = []
+            for v in VARIANTS:
+                res[f"mx8_v{v}"] = []
         for _ in range(ROUNDS):
             if MX8:
-                res["mx8"].append(timeit(lambda: ops.gemm_nt_mx8(a8, b8, out, a2=a2, b2=b2)))
+                for v in VARIANTS:
+                    call("ospo_set_gemm_variant", v)
+                    res[f"mx8_v{v}"].append(timeit(lambda: ops.gemm_nt_mx8(a8, b8, out, a2=a2, b2=b2)))
                 res["mx8_quantA"].append(timeit(lambda: ops.quant_mx8(a, a8)))
             for v in VARIANTS:
                 call("ospo_set_gemm_variant", v)
