@@ -307,7 +307,7 @@ def main():
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_note": "HBM+Infinity-Cache bytes per launch (2*FETCH_SIZE+WRITE_SIZE, profiles/gemm_pmc.json)",
                 "algorithmic_bytes_per_launch": round(d["bytes"] / d["count"]),
-                "kernel": f"{dom} (gemm_nt_v5_kernel 8-phase MFMA {'MXFP8 e4m3' if mx else 'bf16'} + split-K fixup)",
+                "kernel": f"{dom} (gemm_nt_v5_kernel SP-schedule MFMA {'MXFP8 e4m3' if mx else 'bf16'} + split-K fixup)",
                 "launches": d["count"],
                 "avg_launch_us": round(d["ms"] * 1e3 / d["count"], 2),
                 "step_mfma_frac": round(flops_pair * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)}

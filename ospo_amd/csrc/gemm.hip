@@ -762,7 +762,7 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem,
   }
 }
 
-template <int DBG = 0, bool DROP = false, bool MX = false, bool SP = false>
+template <int DBG = 0, bool DROP = false, bool MX = false, int SP = 0>
 __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
                                                          int split, float* __restrict__ ws, int GM) {
   constexpr int BM = 256, BN = 256, HALF = 16384, SLOT = 4 * HALF;  // half order in a slot: A0 A1 B0 B1
@@ -912,6 +912,8 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const char* la = slot + p * HALF;
+      if (SP == 3 && p == 0 && n1) stage_half(t + 1, 1);
+      if (SP == 3 && p == 1 && n2) { stage_scales(t + 2); stage_half(t + 2, 2); stage_half(t + 2, 3); stage_half(t + 2, 0); }
       if constexpr (mx_tile) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -945,8 +947,8 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
                                                                  mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
         }
       }
-      if (p == 0 && n1) stage_half(t + 1, 1);
-      if (p == 1 && n2) { stage_scales(t + 2); stage_half(t + 2, 2); stage_half(t + 2, 3); stage_half(t + 2, 0); }
+      if (SP != 3 && p == 0 && n1) stage_half(t + 1, 1);
+      if (SP != 3 && p == 1 && n2) { stage_scales(t + 2); stage_half(t + 2, 2); stage_half(t + 2, 3); stage_half(t + 2, 0); }
       if (g1) {
         if (p == 0) wait_sp(n1 ? KB + 2 : 0);         // A1(t)
         if (p == 1 && n1) wait_sp(n2 ? KB + 2 : 2);   // B0 B1 A0 (+ scales) of t+1
@@ -976,7 +978,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
             for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[2 * p + q][i][n]));
         __builtin_amdgcn_s_setprio(0);
       } else if constexpr (DBG != 2) {
-        __builtin_amdgcn_s_setprio(1);
+        if (SP != 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           // p 0: quadrants j 0 (ia 0, ib 0), 1 (0, 1); p 1: j 2 (1, 1), 3 (1, 0)
@@ -1287,7 +1289,7 @@ int num_cus() {
   return g_num_cus;
 }
 
-template <int DBG = 0, bool DROP = false, bool MX = false, bool SP = false>
+template <int DBG = 0, bool DROP = false, bool MX = false, int SP = 0>
 int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
   const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
@@ -1386,11 +1388,13 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 12: return launch_v5<1>(a, stream, false);
     case 13: return launch_v5<2>(a, stream, false);
     // SP schedule (2 phases of 32 MFMAs per K-tile): 14 + split tail, 15 no loads, 16 no MFMA
-    case 14: return launch_v5<0, false, false, true>(a, stream, true);
-    case 15: return launch_v5<1, false, false, true>(a, stream, false);
-    case 16: return launch_v5<2, false, false, true>(a, stream, false);
+    case 14: return launch_v5<0, false, false, 1>(a, stream, true);
+    case 15: return launch_v5<1, false, false, 1>(a, stream, false);
+    case 16: return launch_v5<2, false, false, 1>(a, stream, false);
+    case 18: return launch_v5<0, false, false, 2>(a, stream, true);  // SP without s_setprio
+    case 19: return launch_v5<0, false, false, 3>(a, stream, true);  // SP, refills ahead of the reads
     case 17: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
-    default: return launch_v5<0, false, false, true>(a, stream, true);               // SP + split-K tail
+    default: return launch_v5<0, false, false, 1>(a, stream, true);               // SP + split-K tail
   }
 }
 
@@ -1420,7 +1424,7 @@ extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int
   a.rope_T = T;
   a.rope_cols = rope_cols;
   // split-K tail fixups apply the RoPE epilogue too
-  return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, true>(a, stream);
+  return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, 1>(a, stream);
 }
 
 extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
@@ -1437,12 +1441,12 @@ extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, 
   GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
              M, N, K, K2, 1.f, nullptr, nullptr, 0, C, ldc, 1, 0, 0};
   if (drop_p == 0.f)
-    return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, true>(a, stream);
+    return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, 1>(a, stream);
   a.drop_seed = drop_seed;
   a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = N;
-  return g_gemm_variant == 17 ? launch_v5<0, true>(a, stream) : launch_v5<0, true, false, true>(a, stream);
+  return g_gemm_variant == 17 ? launch_v5<0, true>(a, stream) : launch_v5<0, true, false, 1>(a, stream);
 }
 
 extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, int ldb, const void* Bsc,
@@ -1475,16 +1479,16 @@ extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const 
     a.rope_sn = (const bf16*)rope_sin;
     a.rope_T = rope_T;
     a.rope_cols = rope_cols;
-    return g_gemm_variant == 17 ? launch_v5<0, false, true>(a, stream) : launch_v5<0, false, true, true>(a, stream);
+    return g_gemm_variant == 17 ? launch_v5<0, false, true>(a, stream) : launch_v5<0, false, true, 1>(a, stream);
   }
   if (drop) {
     a.drop_seed = drop_seed;
     a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
     a.drop_scale = 1.f / (1.f - drop_p);
     a.drop_ld = N;
-    return g_gemm_variant == 17 ? launch_v5<0, true, true>(a, stream) : launch_v5<0, true, true, true>(a, stream);
+    return g_gemm_variant == 17 ? launch_v5<0, true, true>(a, stream) : launch_v5<0, true, true, 1>(a, stream);
   }
-  return g_gemm_variant == 17 ? launch_v5<0, false, true>(a, stream) : launch_v5<0, false, true, true>(a, stream);
+  return g_gemm_variant == 17 ? launch_v5<0, false, true>(a, stream) : launch_v5<0, false, true, 1>(a, stream);
 }
 
 extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {
@@ -1501,7 +1505,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || v > 17 || (v > 5 && v < 10)) return OSPO_ERR_ARG;
+  if (v < 0 || v > 19 || (v > 5 && v < 10)) return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;
