@@ -267,9 +267,13 @@ def main():
     timer = None if args.no_kernel_timer else ops.KernelTimer()
     odist.barrier()
     torch.cuda.synchronize()
-    ops.set_kernel_timer(timer)
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if i == args.steps - 1:
+            # per-launch HIP events on the last timed step only: an event pair around every GEMM
+            # costs ~1 % of the step (128.8 vs 127.5 ms), so recording them on all K steps would
+            # depress `value`; one step holds ~245 GEMM launches, enough for the average
+            ops.set_kernel_timer(timer)
         out = train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
     odist.barrier()
     torch.cuda.synchronize()

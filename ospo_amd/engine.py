@@ -196,14 +196,16 @@ class SimPOEngine:
         self.seq_logps = z(S, dt=F32)
         # backward scratch (shared by all layers)
         self.u32_flat = z(Mc * Rmax, dt=F32)
-        # one g buffer per LoRA group: the side stream's dA/dB of a group may still read it
-        self.gsc = {name: z(Mc, g.Rp) for name, g in self.layout.groups.items()}
-        self.dx = z(Mc, D)
-        self.dxmid = z(Mc, D)
+        # Every buffer the side stream's dA/dB read (a group's g buffer and its dy) comes in two copies,
+        # used by layer parity: main rewrites a copy in layer i only after the side stream finished
+        # layer i+2's products, so the guards below practically never stall the main stream.
+        self.gsc2 = {name: [z(Mc, g.Rp), z(Mc, g.Rp)] for name, g in self.layout.groups.items()}
+        self.dx2 = [z(Mc, D), z(Mc, D)]
+        self.dxmid2 = [z(Mc, D), z(Mc, D)]
+        self.dqkv2 = [z(Mc, 3 * D), z(Mc, 3 * D)]
+        self.dgu2 = [z(Mc, 2 * Fd), z(Mc, 2 * Fd)]
         self.dxn = z(Mc, D)
         self.dattn = z(Mc, D)
-        self.dqkv = z(Mc, 3 * D)
-        self.dgu = z(Mc, 2 * Fd)
         self.dh = z(Mc, Fd)
         self.delta_ws = z(S * H * Tm, dt=F32)
         self.dz = z(R, Dg)
@@ -280,10 +282,10 @@ class SimPOEngine:
         ops.lora_skinny(x, Acat, out_bf16, M, self.Mk, K, nt, 0, self.scale, b_rows=used, ws=self._skinny_ws(K, nt),
                         dropout=drop, xd=xd if drop else None)
 
-    def _lora_g(self, dy, g, Bcat, BT, M):
-        """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows M..Mk-1 zero)."""
+    def _lora_g(self, dy, g, Bcat, BT, M, par=0):
+        """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows M..Mk-1 zero), into g buffer copy `par`."""
         r = self.layout.r
-        out = self.gsc[g.name]
+        out = self.gsc2[g.name][par]
         if g.nmods == 1:
             nt = (r + 15) // 16
             ops.lora_skinny(dy, BT, out, M, self.Mk, g.Nmod, nt, 0, self.scale, b_rows=r,
@@ -396,7 +398,9 @@ class SimPOEngine:
         ops.gelu_bwd(self.dz[:R], self.zpre[:R], self.dz[:R])
         ops.gemm_nt(self.dz[:R], self.gh_w1T, self.dhsel[:R])
         ops.scatter_rows(self.dhsel[:R], S, T, Lt - 1, N, self.dxn[:M])
-        ops.rmsnorm_bwd(self.dxn[:M], self.x_final[:M], self.norm, self.rstd_f[:M], self.dx[:M], mx=self._mxo(D))
+        L = dims.n_layers
+        ops.rmsnorm_bwd(self.dxn[:M], self.x_final[:M], self.norm, self.rstd_f[:M], self.dx2[(L - 1) % 2][:M],
+                        mx=self._mxo(D))
         scale_attn = 1.0 / math.sqrt(hd)
         lay = self.layout
         # LoRA weight grads (dA = g^T x, dB = dy^T u) of each group run on a side stream,
@@ -404,14 +408,14 @@ class SimPOEngine:
         # main stream rewrites it (g buffer per group, dy buffers, next layer).
         main, side = torch.cuda.current_stream(self.device), self._side
         side.wait_stream(main)
-        done = {}  # group -> event after its dA/dB were enqueued on the side stream
+        done = {}  # (group, layer parity) -> event after its dA/dB were enqueued on the side stream
 
-        def guard(name):  # main must not rewrite what group `name`'s pending dA/dB read
-            ev = done.pop(name, None)
+        def guard(name, par):  # main must not rewrite what group `name`'s pending dA/dB of parity `par` read
+            ev = done.pop((name, par), None)
             if ev is not None:
                 main.wait_event(ev)
 
-        def lora_grads_async(name, gs, x_in, dy, u, gbase):
+        def lora_grads_async(name, par, gs, x_in, dy, u, gbase):
             ev = torch.cuda.Event()
             ev.record(main)
             side.wait_event(ev)
@@ -419,49 +423,51 @@ class SimPOEngine:
                 self._lora_grads(gs, x_in, dy, u, lay.groups[name], gbase)
             ev2 = torch.cuda.Event()
             ev2.record(side)
-            done[name] = ev2
+            done[(name, par)] = ev2
 
         for i in reversed(range(dims.n_layers)):
             a, lw, pk = self.acts[i], self.layers[i], self.packed[i]
             gbase = lay.layer_off(i)
-            dx = self.dx  # gradient w.r.t. this layer's output (bf16)
+            q = i % 2  # copy of every side-stream operand this layer writes
+            dx = self.dx2[q]  # gradient w.r.t. this layer's output (bf16)
+            dgu, dxmid, dqkv = self.dgu2[q], self.dxmid2[q], self.dqkv2[q]
             # ---- down_proj: out = xmid + h W_d^T + s (h A_d^T) B_d^T
             Acat, AcatT, Bcat, BT = pk["down"]
-            guard("down")
-            gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M)
+            guard("down", q)  # g buffer copy q (layer i+2's down products read it)
+            gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M, q)
             dr = self._drop(i, "down")
             self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("down", gs, a["xd_d"] if dr else a["h"], dx, a["u_d"], gbase)
-            guard("gu")  # dgu is rewritten here
-            ops.swiglu_bwd(self.dh[:M], a["gu"][:M], self.dgu[:M], mx=self._mxo(2 * Fd))
+            lora_grads_async("down", q, gs, a["xd_d"] if dr else a["h"], dx, a["u_d"], gbase)
+            guard("gu", q)  # dgu / g copy q
+            ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
             # ---- gate/up
             Acat, AcatT, Bcat, BT = pk["gu"]
-            gs = self._lora_g(self.dgu, lay.groups["gu"], Bcat, BT, M)
+            gs = self._lora_g(dgu, lay.groups["gu"], Bcat, BT, M, q)
             dr = self._drop(i, "gu")
-            self._lin(self.dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("gu", gs, a["xd_gu"] if dr else a["xn2"], self.dgu, a["u_gu"], gbase)
-            guard("o")  # dxmid is rewritten here
-            ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], self.dxmid[:M],
+            self._lin(dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
+            lora_grads_async("gu", q, gs, a["xd_gu"] if dr else a["xn2"], dgu, a["u_gu"], gbase)
+            guard("o", q)  # dxmid / g copy q
+            ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], dxmid[:M],
                             dres=dx[:M], mx=self._mxo(D))
             # ---- o_proj
             Acat, AcatT, Bcat, BT = pk["o"]
-            gs = self._lora_g(self.dxmid, lay.groups["o"], Bcat, BT, M)
+            gs = self._lora_g(dxmid, lay.groups["o"], Bcat, BT, M, q)
             dr = self._drop(i, "o")
-            self._lin(self.dxmid[:M], lw["oT"], self.dattn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("o", gs, a["xd_o"] if dr else a["attn"], self.dxmid, a["u_o"], gbase)
+            self._lin(dxmid[:M], lw["oT"], self.dattn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
+            lora_grads_async("o", q, gs, a["xd_o"] if dr else a["attn"], dxmid, a["u_o"], gbase)
             # ---- attention + RoPE
-            guard("qkv")  # dqkv is rewritten here
+            guard("qkv", q)  # dqkv / g copy q
             ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, None,
-                               self.dqkv, S, T, H, hd, scale_attn, rope_cos=self.cos, rope_sin=self.sin)
+                               dqkv, S, T, H, hd, scale_attn, rope_cos=self.cos, rope_sin=self.sin)
             # ---- q/k/v
             Acat, AcatT, Bcat, BT = pk["qkv"]
-            gs = self._lora_g(self.dqkv, lay.groups["qkv"], Bcat, BT, M)
+            gs = self._lora_g(dqkv, lay.groups["qkv"], Bcat, BT, M, q)
             dr = self._drop(i, "qkv")
-            self._lin(self.dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("qkv", gs, a["xd_qkv"] if dr else a["xn1"], self.dqkv, a["u_qkv"], gbase)
-            guard("down")  # dx (the down group's dy) is rewritten here
-            ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx[:M], dres=self.dxmid[:M],
-                            mx=self._mxo(D))
+            self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            lora_grads_async("qkv", q, gs, a["xd_qkv"] if dr else a["xn1"], dqkv, a["u_qkv"], gbase)
+            guard("down", 1 - q)  # dx copy 1-q: layer i+1's down products read it
+            ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[1 - q][:M],
+                            dres=dxmid[:M], mx=self._mxo(D))
             if on_layer_grads is not None:
                 with torch.cuda.stream(side):  # this layer's dA/dB are the last side-stream work so far
                     on_layer_grads(gbase, gbase + lay.per_layer)
