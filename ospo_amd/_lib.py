@@ -30,6 +30,7 @@ SIGNATURES = {
     "ospo_gemm_nt_mx8": [P, I, P, P, I, P, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P, P, I, I, U, F, P],
     "ospo_gemm_set_workspace": [P, Z],
     "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],
+    "ospo_gemm_f32acc_bdrop": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, U, F, P],
     "ospo_f32_to_bf16": [P, P, L, F, P],
     "ospo_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "ospo_rmsnorm_bwd": [P, P, P, P, P, P, I, I, P],

@@ -186,10 +186,38 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) 
     }
   };
 
+  // LoRA dropout recomputed on a K-major B operand (the dA product's activations): the landed tile
+  // is masked in LDS, element (m = reduction row, n) kept iff drop_hash(m * drop_ld + n) >= thresh and
+  // scaled by 1/(1-p) with the bf16 rounding of the forward's masked copy -- the same bf16 values the
+  // forward's skinny product multiplied, without storing them.
+  auto mask_b = [&](int t, int buf) {
+    if constexpr (EPI == EPI_F32_ATOMIC && BKM) {
+      if (args.drop_scale > 0.f && t < nt1) {
+        char* lb = smem + buf * STAGE + A_BYTES;
+        constexpr int LPR = BN / 8, RPP = 64 / LPR, ROWB = BN * 2;
+        for (int c = threadIdx.x; c < B_BYTES / 16; c += NW * 64) {
+          const int p = c >> 6, ln = c & 63;
+          const int row = p * RPP + ln / LPR;
+          const int x = (ln % LPR) ^ kmaj_swz<ROWB>(row);
+          const uint32_t base = (uint32_t)(t * BK + row) * (uint32_t)args.drop_ld + (uint32_t)(n0 + x * 8);
+          bf16x8 v = *reinterpret_cast<const bf16x8*>(lb + c * 16);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const bool keep = drop_hash(base + e, args.drop_seed) >= args.drop_thresh;
+            v[e] = keep ? f2bf(bf2f(v[e]) * args.drop_scale) : f2bf(0.f);
+          }
+          *reinterpret_cast<bf16x8*>(lb + c * 16) = v;
+        }
+        __syncthreads();
+      }
+    }
+  };
+
   if (t_begin < t_end) {
     stage(t_begin, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    mask_b(t_begin, 0);
     for (int t = t_begin; t < t_end; ++t) {
       const int buf = (t - t_begin) & 1;
       if (DBG != 1 && t + 1 < t_end) stage(t + 1, buf ^ 1);
@@ -232,6 +260,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) 
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (t + 1 < t_end) mask_b(t + 1, buf ^ 1);
     }
   }
 
@@ -1513,9 +1542,28 @@ extern "C" int ospo_set_gemm_variant(int v) {
 
 extern "C" int ospo_gemm_nt_tile(int M, int N) { return pick_nt_tile(M, N); }
 
+static int gemm_f32acc_impl(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor, int M, int N,
+                            int K, int k_splits, float alpha, float* C, int ldc, int diag_nblk, int diag_r,
+                            uint32_t drop_seed, float drop_p, hipStream_t stream);
+
 extern "C" int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
                                 int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
                                 int diag_nblk, int diag_r, hipStream_t stream) {
+  return gemm_f32acc_impl(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, k_splits, alpha, C, ldc, diag_nblk, diag_r, 0u,
+                          0.f, stream);
+}
+
+extern "C" int ospo_gemm_f32acc_bdrop(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
+                                      int M, int N, int K, int k_splits, float alpha, float* C, int ldc, int diag_nblk,
+                                      int diag_r, uint32_t drop_seed, float drop_p, hipStream_t stream) {
+  if (!b_kmajor || !(drop_p > 0.f && drop_p < 1.f)) return OSPO_ERR_ARG;
+  return gemm_f32acc_impl(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, k_splits, alpha, C, ldc, diag_nblk, diag_r,
+                          drop_seed, drop_p, stream);
+}
+
+static int gemm_f32acc_impl(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor, int M, int N,
+                            int K, int k_splits, float alpha, float* C, int ldc, int diag_nblk, int diag_r,
+                            uint32_t drop_seed, float drop_p, hipStream_t stream) {
   if (!A || !B || !C) return OSPO_ERR_ARG;
   if (M <= 0 || N <= 0 || K <= 0 || K % BK || N % 64) return OSPO_ERR_SHAPE;
   if (k_splits < 1) k_splits = 1;
@@ -1528,6 +1576,12 @@ extern "C" int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void
   if (!aligned16(A) || !aligned16(B)) return OSPO_ERR_ALIGN;
   GemmArgs a{(const bf16*)A, (const bf16*)B, nullptr, nullptr, lda, ldb, 0, 0, M, N, K, 0, alpha,
              nullptr, nullptr, 0, C, ldc, k_splits, diag_nblk, diag_r};
+  if (drop_p > 0.f) {  // mask on B [K, N] (K-major), index m * N + n
+    a.drop_seed = drop_seed;
+    a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
+    a.drop_scale = 1.f / (1.f - drop_p);
+    a.drop_ld = N;
+  }
   const bool wideN = (N % 256 == 0);
   const bool tallM = a_kmajor ? (M % 256 == 0 && lda >= M) : (M >= 1024);
   if (!a_kmajor && !b_kmajor) return launch<2, 2, 2, 2, false, false, EPI_F32_ATOMIC>(a, stream);

@@ -176,8 +176,6 @@ class SimPOEngine:
                 "u_gu": z(Mc, self.layout.groups["gu"].Rp), "gu": z(Mc, 2 * Fd), "h": z(Mc, Fd),
                 "u_d": z(Mc, self.layout.groups["down"].Rp),
             })
-            if self.lora_dropout > 0:  # dropout(x) of each adapter input, the backward's dA operand
-                self.acts[-1].update({"xd_qkv": z(Mc, D), "xd_o": z(Mc, D), "xd_gu": z(Mc, D), "xd_d": z(Mc, Fd)})
         self.x_final = z(Mc, D)
         self.hf = z(Mc, D)
         self.rstd_f = z(Mc, dt=F32)
@@ -275,7 +273,8 @@ class SimPOEngine:
 
     def _lora_down(self, x, Acat, out_bf16, M, nmods, drop=None, xd=None):
         """out = bf16(scale * dropout(x) . Acat^T)  ([Mcap, Rp]; rows M..Mk-1 and unused columns zero).
-        With drop=(seed, p) the masked x is also written to xd (the backward's dA operand)."""
+        With drop=(seed, p) and xd given, the masked x is also written to xd (the engine passes none:
+        the backward's dA recomputes the mask, ops.gemm_f32acc(b_dropout=...))."""
         Rp, K = Acat.shape
         used = nmods * self.layout.r
         nt = (used + 15) // 16
@@ -347,7 +346,7 @@ class SimPOEngine:
             x = a["x"]
             ops.rmsnorm_fwd(x[:M], lw["ln_in"], a["xn1"][:M], a["rstd1"][:M], dims.rms_eps, mx=self._mxo(D))
             Acat, _, Bcat, _ = pk["qkv"]
-            self._lora_down(a["xn1"], Acat, a["u_qkv"], M, lay.groups["qkv"].nmods, self._drop(i, "qkv"), a.get("xd_qkv"))
+            self._lora_down(a["xn1"], Acat, a["u_qkv"], M, lay.groups["qkv"].nmods, self._drop(i, "qkv"))
             if (3 * D) % 256 == 0:  # q|k RoPE fused into the projection's epilogue
                 self._lin(a["xn1"][:M], lw["qkv"], a["qkv"][:M], pre=True, a2=a["u_qkv"][:M], b2=Bcat,
                           rope=(self.cos, self.sin, T, 2 * D))
@@ -356,16 +355,16 @@ class SimPOEngine:
                 ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
             ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn)
             Acat, _, Bcat, _ = pk["o"]
-            self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods, self._drop(i, "o"), a.get("xd_o"))
+            self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods, self._drop(i, "o"))
             self._lin(a["attn"][:M], lw["o"], a["xmid"][:M], a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
             ops.rmsnorm_fwd(a["xmid"][:M], lw["ln_post"], a["xn2"][:M], a["rstd2"][:M], dims.rms_eps,
                             mx=self._mxo(D))
             Acat, _, Bcat, _ = pk["gu"]
-            self._lora_down(a["xn2"], Acat, a["u_gu"], M, lay.groups["gu"].nmods, self._drop(i, "gu"), a.get("xd_gu"))
+            self._lora_down(a["xn2"], Acat, a["u_gu"], M, lay.groups["gu"].nmods, self._drop(i, "gu"))
             self._lin(a["xn2"][:M], lw["gu"], a["gu"][:M], pre=True, a2=a["u_gu"][:M], b2=Bcat)
             ops.swiglu_fwd(a["gu"][:M], a["h"][:M], mx=self._mxo(Fd))
             Acat, _, Bcat, _ = pk["down"]
-            self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods, self._drop(i, "down"), a.get("xd_d"))
+            self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods, self._drop(i, "down"))
             xn = self.acts[i + 1]["x"] if i + 1 < dims.n_layers else self.x_final
             self._lin(a["h"][:M], lw["down"], xn[:M], pre=True, a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
         ops.rmsnorm_fwd(self.x_final[:M], self.norm, self.hf[:M], self.rstd_f[:M], dims.rms_eps)
@@ -415,12 +414,12 @@ class SimPOEngine:
             if ev is not None:
                 main.wait_event(ev)
 
-        def lora_grads_async(name, par, gs, x_in, dy, u, gbase):
+        def lora_grads_async(name, par, gs, x_in, dy, u, gbase, drop):
             ev = torch.cuda.Event()
             ev.record(main)
             side.wait_event(ev)
             with torch.cuda.stream(side):
-                self._lora_grads(gs, x_in, dy, u, lay.groups[name], gbase)
+                self._lora_grads(gs, x_in, dy, u, lay.groups[name], gbase, drop)
             ev2 = torch.cuda.Event()
             ev2.record(side)
             done[(name, par)] = ev2
@@ -437,7 +436,7 @@ class SimPOEngine:
             gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M, q)
             dr = self._drop(i, "down")
             self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("down", q, gs, a["xd_d"] if dr else a["h"], dx, a["u_d"], gbase)
+            lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr)
             guard("gu", q)  # dgu / g copy q
             ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
             # ---- gate/up
@@ -445,7 +444,7 @@ class SimPOEngine:
             gs = self._lora_g(dgu, lay.groups["gu"], Bcat, BT, M, q)
             dr = self._drop(i, "gu")
             self._lin(dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("gu", q, gs, a["xd_gu"] if dr else a["xn2"], dgu, a["u_gu"], gbase)
+            lora_grads_async("gu", q, gs, a["xn2"], dgu, a["u_gu"], gbase, dr)
             guard("o", q)  # dxmid / g copy q
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], dxmid[:M],
                             dres=dx[:M], mx=self._mxo(D))
@@ -454,7 +453,7 @@ class SimPOEngine:
             gs = self._lora_g(dxmid, lay.groups["o"], Bcat, BT, M, q)
             dr = self._drop(i, "o")
             self._lin(dxmid[:M], lw["oT"], self.dattn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("o", q, gs, a["xd_o"] if dr else a["attn"], dxmid, a["u_o"], gbase)
+            lora_grads_async("o", q, gs, a["attn"], dxmid, a["u_o"], gbase, dr)
             # ---- attention + RoPE
             guard("qkv", q)  # dqkv / g copy q
             ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, None,
@@ -464,7 +463,7 @@ class SimPOEngine:
             gs = self._lora_g(dqkv, lay.groups["qkv"], Bcat, BT, M, q)
             dr = self._drop(i, "qkv")
             self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("qkv", q, gs, a["xd_qkv"] if dr else a["xn1"], dqkv, a["u_qkv"], gbase)
+            lora_grads_async("qkv", q, gs, a["xn1"], dqkv, a["u_qkv"], gbase, dr)
             guard("down", 1 - q)  # dx copy 1-q: layer i+1's down products read it
             ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[1 - q][:M],
                             dres=dxmid[:M], mx=self._mxo(D))
@@ -473,7 +472,7 @@ class SimPOEngine:
                     on_layer_grads(gbase, gbase + lay.per_layer)
         main.wait_stream(side)
 
-    def _lora_grads(self, gs, x_in, dy, u, g, gbase):
+    def _lora_grads(self, gs, x_in, dy, u, g, gbase, drop=None):
         """dA = g_s^T . x_in  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal).
         Only the nmods*r used columns of g enter dA (no atomics of padding rows)."""
         r = self.layout.r
@@ -484,8 +483,9 @@ class SimPOEngine:
         # K splits measured per product on the 7B layer shapes (tools/lora_grads_sweep.py,
         # profiles/r01/lora_grads_sweep.jsonl): dA 8 (4 for the 11008-wide down input); dB 4 for the
         # multi-module groups, 8 for the single-module ones
+        # with LoRA dropout the mask is recomputed on x_in as it is staged (the forward keeps no masked copy)
         ops.gemm_f32acc(gs[:Mk, :used], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True,
-                        k_splits=4 if g.Kin > 8192 else 8)
+                        k_splits=4 if g.Kin > 8192 else 8, b_dropout=drop)
         b_off = gbase + g.b_off
         dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
         ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=4 if g.nmods > 1 else 8,

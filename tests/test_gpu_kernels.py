@@ -118,6 +118,28 @@ def test_gemm_f32acc_dA_used_rows_of_padded_g():
     assert torch.all(out[used] == 7.0)
 
 
+@pytest.mark.parametrize("K,N,used,splits", [(4800, 4096, 48, 1), (4800, 4096, 48, 8), (4800, 11008, 16, 4),
+                                              (640, 256, 32, 1)])
+def test_gemm_f32acc_dropout_recompute_equals_stored_mask(K, N, used, splits):
+    """dA with the LoRA dropout mask recomputed on the staged activations == dA on the masked copy
+    the forward's skinny product writes (the same bf16 values, the same accumulation): bit-exact."""
+    p, seed = 0.05, 987654
+    x = rnd(K, N)
+    g = rnd(K, 64)
+    xd = torch.empty_like(x)
+    u = torch.empty(K, 64, device=DEV, dtype=torch.bfloat16)
+    A = torch.zeros(64, N, device=DEV, dtype=torch.bfloat16)
+    ops().lora_skinny(x, A, u, K, K, N, 1, 0, 1.0, b_rows=16, dropout=(seed, p), xd=xd)
+    ref = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().gemm_f32acc(g[:, :used], xd, ref, a_kmajor=True, b_kmajor=True, k_splits=splits)
+    out = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().gemm_f32acc(g[:, :used], x, out, a_kmajor=True, b_kmajor=True, k_splits=splits, b_dropout=(seed, p))
+    if splits == 1:
+        assert torch.equal(out, ref)
+    else:  # the K-split partials meet in fp32 atomics, in no fixed order
+        assert relerr(out, ref) < 1e-6
+
+
 def test_gemm_f32acc_blockdiag_scatter():
     """dB of a packed q|k|v LoRA: keep only the diagonal blocks, peft layout."""
     r, nblk, nm = 16, 256, 3
