@@ -73,6 +73,17 @@ int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, in
                               const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
                               unsigned drop_seed, float drop_p, hipStream_t stream);
 
+/* down_proj backward fused with the SwiGLU backward (replaces ospo_gemm_nt_dropout_bf16 into dh +
+ * ospo_swiglu_bwd; the autograd of `down_proj(act_fn(gate_proj(x)) * up_proj(x))` in HF
+ * LlamaMLP.forward, reached from ospo/wrapper/train.py:352-354).  dh = bf16(A.B^T + mask (.) A2.B2^T
+ * / (1 - p)) [M, F] is never stored: the epilogue reads gate | up from gu [M, 2F] and writes
+ * [dgate | dup] to dgu [M, 2F], bit-identical to the two-launch path.  drop_p = 0: no mask
+ * (K2 may be 0).  F % 256 == 0. */
+int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* B, int ldb, int M, int F, int K,
+                                 const void* A2, int lda2, const void* B2, int ldb2, int K2,
+                                 const void* gu, int ld_gu, void* dgu, int ld_dgu, unsigned drop_seed,
+                                 float drop_p, hipStream_t stream);
+
 /* The LoRA dropout mask hash (host copy of the device function): element idx of an
  * adapter input is kept iff ospo_dropout_hash(idx, seed) >= p * 2^32. */
 unsigned ospo_dropout_hash(unsigned idx, unsigned seed);

@@ -23,6 +23,7 @@ SIGNATURES = {
     "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P],
     "ospo_gemm_nt_tile": [I, I],
     "ospo_gemm_nt_dropout_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, U, F, P],
+    "ospo_gemm_nt_swiglu_bwd_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, I, U, F, P],
     "ospo_gemm_nt_rope_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, P, I, I, P],
     "ospo_set_gemm_variant": [I],
     "ospo_mx8_scale_bytes": [I, I],

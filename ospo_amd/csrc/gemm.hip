@@ -132,7 +132,25 @@ struct GemmArgs {
   // in BYTES; sa / sb the E8M0 block scales in ospo_quant_mx8's tile layout (mx8.hip).
   const uint32_t* sa = nullptr;
   const uint32_t* sb = nullptr;
+  // fused SwiGLU backward (ospo_gemm_nt_swiglu_bwd_bf16): the bf16 product is dh [M, N = F]; instead of
+  // storing it, the epilogue reads gate / up from swg_gu [M, 2F] and writes [dgate | dup] to swg_dgu
+  const bf16* swg_gu = nullptr;
+  bf16* swg_dgu = nullptr;
+  int ld_gu = 0, ld_dgu = 0;
 };
+
+// the SwiGLU-backward store of 8 product columns (row m, columns n..n+7 of F = args.N)
+__device__ __forceinline__ void swiglu_bwd_store8(const GemmArgs& args, long m, int n, const u32x4& v) {
+  float d[8], g[8], u[8], dg[8], du[8];
+  unpack8(v, d);
+  const bf16* gr = args.swg_gu + m * args.ld_gu + n;
+  unpack8(*reinterpret_cast<const u32x4*>(gr), g);
+  unpack8(*reinterpret_cast<const u32x4*>(gr + args.N), u);
+  swiglu_bwd8(d, g, u, dg, du);
+  bf16* o = args.swg_dgu + m * args.ld_dgu + n;
+  *reinterpret_cast<u32x4*>(o) = pack8(dg);
+  *reinterpret_cast<u32x4*>(o + args.N) = pack8(du);
+}
 
 // DBG (A/B decomposition only, results invalid): 1 = no global loads after the
 // prologue, 2 = no MFMA, 3 = global loads only (no LDS reads, no MFMA).
@@ -787,6 +805,10 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem,
         v[qq] = pack2(lo, hi);
       }
     }
+    if (args.swg_gu) {
+      swiglu_bwd_store8(args, m, n0 + cc * 8, v);
+      continue;
+    }
     *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8) = v;
   }
 }
@@ -1300,6 +1322,10 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
     for (int q = 0; q < 4; ++q)
       o[q] = pack2(bits2f(o[q] & 0xffff) + bits2f(rv[q] & 0xffff), bits2f(o[q] >> 16) + bits2f(rv[q] >> 16));
   }
+  if (args.swg_gu) {
+    swiglu_bwd_store8(args, m, n0 + c, o);
+    return;
+  }
   *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(args.C) + (long)m * args.ldc + n0 + c) = o;
 }
 
@@ -1475,6 +1501,36 @@ extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, 
   a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = N;
+  return g_gemm_variant == 17 ? launch_v5<0, true>(a, stream) : launch_v5<0, true, false, 1>(a, stream);
+}
+
+extern "C" int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* B, int ldb, int M, int F, int K,
+                                            const void* A2, int lda2, const void* B2, int ldb2, int K2,
+                                            const void* gu, int ld_gu, void* dgu, int ld_dgu, unsigned drop_seed,
+                                            float drop_p, hipStream_t stream) {
+  if (!A || !B || !gu || !dgu || (K2 > 0 && (!A2 || !B2))) return OSPO_ERR_ARG;
+  if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && K2 <= 0)) return OSPO_ERR_ARG;
+  if (M <= 0 || F <= 0 || K <= 0 || K % BK || K2 < 0 || K2 % BK) return OSPO_ERR_SHAPE;
+  if (F % 256) return OSPO_ERR_UNSUPPORTED;
+  if ((long)M * F > 0xFFFFFFFFL) return OSPO_ERR_SHAPE;  // 32-bit mask index
+  if (lda < K || ldb < K || (lda % 8) || (ldb % 8) || ld_gu < 2 * F || ld_dgu < 2 * F || ld_gu % 8 || ld_dgu % 8)
+    return OSPO_ERR_SHAPE;
+  if (K2 > 0 && (lda2 < K2 || ldb2 < K2 || lda2 % 8 || ldb2 % 8)) return OSPO_ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(B) || !aligned16(gu) || !aligned16(dgu) ||
+      (K2 > 0 && (!aligned16(A2) || !aligned16(B2))))
+    return OSPO_ERR_ALIGN;
+  GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
+             M, F, K, K2, 1.f, nullptr, nullptr, 0, nullptr, 0, 1, 0, 0};
+  a.swg_gu = (const bf16*)gu;
+  a.swg_dgu = (bf16*)dgu;
+  a.ld_gu = ld_gu;
+  a.ld_dgu = ld_dgu;
+  if (drop_p == 0.f)
+    return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, 1>(a, stream);
+  a.drop_seed = drop_seed;
+  a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
+  a.drop_scale = 1.f / (1.f - drop_p);
+  a.drop_ld = F;
   return g_gemm_variant == 17 ? launch_v5<0, true>(a, stream) : launch_v5<0, true, false, 1>(a, stream);
 }
 

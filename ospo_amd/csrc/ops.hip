@@ -322,14 +322,7 @@ __global__ void swiglu_bwd_kernel(const bf16* __restrict__ dh, int lddh, const b
   unpack8(*reinterpret_cast<const u32x4*>(dh + m * lddh + c * 8), d);
   unpack8(*reinterpret_cast<const u32x4*>(gu + m * ldg + c * 8), g);
   unpack8(*reinterpret_cast<const u32x4*>(gu + m * ldg + F + c * 8), u);
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const float sg = 1.f / (1.f + __expf(-g[q]));
-    const float a = round_bf(g[q] * sg);
-    du[q] = d[q] * a;
-    const float da = round_bf(d[q] * u[q]);
-    dg[q] = da * sg * (1.f + g[q] * (1.f - sg));
-  }
+  swiglu_bwd8(d, g, u, dg, du);
   const u32x4 pg = pack8(dg), pu = pack8(du);
   *reinterpret_cast<u32x4*>(dgu + m * lddg + c * 8) = pg;
   *reinterpret_cast<u32x4*>(dgu + m * lddg + F + c * 8) = pu;

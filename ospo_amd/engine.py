@@ -24,6 +24,7 @@ MI355X-first memory plan (288 GB HBM3E per GPU):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -84,6 +85,10 @@ class SimPOEngine:
         # "mx8": the frozen decoder Linears (q|k|v, o, gate|up, down; forward and dX) run as MXFP8
         # block-scaled fp8 MFMA GEMMs (BASELINE config 5; oracle/mx8_ref.py defines the arithmetic)
         self.linear_dtype = linear_dtype
+        # OSPO_FUSE_SWIGLU_BWD=1 (bf16): the down_proj dX GEMM writes the SwiGLU backward (dgate | dup) from
+        # its epilogue and dh is never stored (ospo_gemm_nt_swiglu_bwd_bf16, bit-identical).  Off by default:
+        # the step time is the same (the epilogue's gu/dgu traffic is not overlapped with MFMA)
+        self.fuse_swiglu_bwd = linear_dtype == "bf16" and os.environ.get("OSPO_FUSE_SWIGLU_BWD", "0") == "1"
         # peft lora_dropout on the adapter inputs (ospo_amd/dropout.py: counter-based masks, one per input)
         self.lora_dropout = float(lora_dropout)
         self.training = True
@@ -204,7 +209,7 @@ class SimPOEngine:
         self.dgu2 = [z(Mc, 2 * Fd), z(Mc, 2 * Fd)]
         self.dxn = z(Mc, D)
         self.dattn = z(Mc, D)
-        self.dh = z(Mc, Fd)
+        self.dh = None if self.fuse_swiglu_bwd else z(Mc, Fd)
         self.delta_ws = z(S * H * Tm, dt=F32)
         self.dz = z(R, Dg)
         self.dhsel = z(R, D)
@@ -435,10 +440,15 @@ class SimPOEngine:
             guard("down", q)  # g buffer copy q (layer i+2's down products read it)
             gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M, q)
             dr = self._drop(i, "down")
-            self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr)
-            guard("gu", q)  # dgu / g copy q
-            ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
+            if self.fuse_swiglu_bwd:
+                guard("gu", q)  # dgu / g copy q
+                ops.gemm_nt_swiglu_bwd(dx[:M], lw["downT"], a["gu"][:M], dgu[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+                lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr)
+            else:
+                self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
+                lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr)
+                guard("gu", q)  # dgu / g copy q
+                ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
             # ---- gate/up
             Acat, AcatT, Bcat, BT = pk["gu"]
             gs = self._lora_g(dgu, lay.groups["gu"], Bcat, BT, M, q)

@@ -134,6 +134,40 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
     return out
 
 
+def gemm_nt_swiglu_bwd(a: torch.Tensor, b: torch.Tensor, gu: torch.Tensor, dgu: torch.Tensor, *, a2=None, b2=None,
+                       dropout=None) -> torch.Tensor:
+    """dgu[M, 2F] = SwiGLU backward of dh = bf16(a.b^T + a2.b2^T) (b = down_proj's W^T, [F, K]) at gu [M, 2F],
+    without storing dh (ospo_gemm_nt_swiglu_bwd_bf16; bit-identical to gemm_nt(..., dropout) + swiglu_bwd).
+    dropout=(seed, p): the a2.b2^T term is masked as in gemm_nt."""
+    for t, n in ((a, "a"), (b, "b"), (gu, "gu"), (dgu, "dgu")):
+        _chk(t, BF16, n)
+    M, K = a.shape
+    F = b.shape[0]
+    if b.shape[1] != K or gu.shape != (M, 2 * F) or dgu.shape != (M, 2 * F):
+        raise ValueError(f"gemm_nt_swiglu_bwd shape mismatch a{tuple(a.shape)} b{tuple(b.shape)} "
+                         f"gu{tuple(gu.shape)} dgu{tuple(dgu.shape)}")
+    K2 = 0
+    if a2 is not None:
+        K2 = a2.shape[1]
+        if a2.shape[0] != M or b2.shape != (F, K2):
+            raise ValueError("gemm_nt_swiglu_bwd K-extension shape mismatch")
+    seed, p = (0, 0.0) if dropout is None else (int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]))
+    if p > 0 and a2 is None:
+        raise ValueError("gemm_nt_swiglu_bwd: dropout needs a2/b2")
+    if not _GEMM_WS:
+        gemm_workspace(a.device)
+    st = torch.cuda.current_stream()
+    e0 = _TIMER.start(st) if _TIMER is not None else None
+    call("ospo_gemm_nt_swiglu_bwd_bf16", _p(a), _ld(a), _p(b), _ld(b), M, F, K,
+         _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2,
+         _p(gu), _ld(gu), _p(dgu), _ld(dgu), seed, p, st.cuda_stream)
+    if e0 is not None:
+        # algorithmic: the frozen product's flops; bytes A, B once, gu read and dgu written (2F columns each)
+        nbytes = 2.0 * (M * K + F * K + 4 * M * F)
+        _TIMER.add(f"gemm_nt_{gemm_nt_tile(M, F)}x{F if F < 256 else 256}", 2.0 * M * F * K, e0, st, nbytes)
+    return dgu
+
+
 # ------------------------------------------------------------ MXFP8 (config 5)
 class MX8:
     """An MXFP8 operand on the device: e4m3 bytes q [rows, K] + E8M0 scales in the GEMM's tile

@@ -565,3 +565,34 @@ def test_gemm_split_tail_equals_unsplit(split):
     assert torch.equal(outs[split][0], ref)
     assert torch.equal(outs[split][0], outs[1][0])
     assert torch.equal(outs[split][1], outs[1][1])
+
+
+@pytest.mark.parametrize("M,F,K,K2,p,split", [(4800, 11008, 4096, 64, 0.05, 0), (600, 1024, 512, 64, 0.05, 2),
+                                              (300, 512, 256, 0, 0.0, 0), (1000, 2048, 512, 128, 0.05, 3),
+                                              (1000, 2048, 512, 64, 0.0, 2)])
+def test_gemm_swiglu_bwd_fused_equals_two_launches(M, F, K, K2, p, split):
+    """down_proj dX GEMM with the SwiGLU backward in its epilogue (dh never stored) is bit-identical to
+    the dh GEMM (+ masked LoRA extension) followed by swiglu_bwd, on the same split-K decisions."""
+    from ospo_amd._lib import call
+    seed = 4242
+    dy, w = rnd(M, K), rnd(F, K, s=0.05)
+    a2 = rnd(M, K2) if K2 else None
+    b2 = rnd(F, K2, s=0.05) if K2 else None
+    gu = rnd(M, 2 * F, s=2.0)
+    dr = (seed, p) if p > 0 else None
+    try:
+        call("ospo_gemm_force_split", split)
+        dh = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+        ops().gemm_nt(dy, w, dh, a2=a2, b2=b2, dropout=dr)
+        ref = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+        ops().swiglu_bwd(dh, gu, ref)
+        out = torch.full((M, 2 * F), float("nan"), device=DEV, dtype=torch.bfloat16)
+        ops().gemm_nt_swiglu_bwd(dy, w, gu, out, a2=a2, b2=b2, dropout=dr)
+    finally:
+        call("ospo_gemm_force_split", 0)
+    assert torch.equal(out, ref)
+    # and against an fp32 statement of the op (HF LlamaMLP: h = bf16(silu(g)) * u)
+    g, u, d = gu[:, :F].float(), gu[:, F:].float(), dh.float()
+    sg = torch.sigmoid(g)
+    ref32 = torch.cat([bf(d * u).float() * sg * (1 + g * (1 - sg)), d * bf(g * sg).float()], 1)
+    assert relerr(out.float(), ref32) < 1e-2
