@@ -12,6 +12,7 @@ rank 0.  See DESIGN.md "Measurement".
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -262,6 +263,14 @@ def main():
     batches = [synthetic_batch(B, Lt, N, dims.vocab, dims.img_vocab, seed=1000 * rank + i, device=dev)
                for i in range(4)]
 
+    # OSPO_MAIN_PRIO < 0 (A/B knob): the step's main stream is a high-priority HIP stream, so its GEMMs
+    # are dispatched ahead of the side stream's LoRA dA/dB products
+    prio = int(os.environ.get("OSPO_MAIN_PRIO", "0"))
+    hp = torch.cuda.Stream(device=dev, priority=prio) if prio else None
+    if hp is not None:
+        hp.wait_stream(torch.cuda.current_stream(dev))
+    stream_ctx = torch.cuda.stream(hp) if hp is not None else contextlib.nullcontext()
+    stream_ctx.__enter__()
     for i in range(args.warmup):
         train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
     timer = None if args.no_kernel_timer else ops.KernelTimer()
@@ -278,6 +287,7 @@ def main():
     odist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    stream_ctx.__exit__(None, None, None)
     ops.set_kernel_timer(None)
     loss = float(out["loss"].item())
     if not math.isfinite(loss):
