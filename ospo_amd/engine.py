@@ -158,6 +158,11 @@ class SimPOEngine:
         # launches are dispatched ahead of the main stream's GEMM workgroups and get out of their way
         # (+0.3 %, profiles/r01/stream_priority_ab.log; main-stream high priority instead: -0.2 %).
         # OSPO_SIDE_PRIO=0 restores the default priority (A/B knob).
+        # K splits of the LoRA dA / dB products: dA (Kin <= 8192, > 8192), dB (multi-module, single-module);
+        # OSPO_DADB_SPLITS="8,4,4,8" overrides them (A/B knob)
+        self._dadb_splits = tuple(int(v) for v in os.environ.get("OSPO_DADB_SPLITS", "8,4,4,8").split(","))
+        if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
+            raise ValueError("OSPO_DADB_SPLITS must be four positive split counts")
         self._side = torch.cuda.Stream(device=self.device, priority=int(os.environ.get("OSPO_SIDE_PRIO", "-1")))
 
     def ensure_capacity(self, pairs: int, text_len: int):
@@ -498,11 +503,12 @@ class SimPOEngine:
         # profiles/r01/lora_grads_sweep.jsonl): dA 8 (4 for the 11008-wide down input); dB 4 for the
         # multi-module groups, 8 for the single-module ones
         # with LoRA dropout the mask is recomputed on x_in as it is staged (the forward keeps no masked copy)
+        sa_small, sa_big, sb_multi, sb_single = self._dadb_splits
         ops.gemm_f32acc(gs[:Mk, :used], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True,
-                        k_splits=4 if g.Kin > 8192 else 8, b_dropout=drop)
+                        k_splits=sa_big if g.Kin > 8192 else sa_small, b_dropout=drop)
         b_off = gbase + g.b_off
         dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
-        ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=4 if g.nmods > 1 else 8,
+        ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=sb_multi if g.nmods > 1 else sb_single,
                         diag=(g.Nmod, r))
 
     # ------------------------------------------------------------ optimizer
