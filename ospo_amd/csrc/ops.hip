@@ -392,6 +392,32 @@ __global__ void gen_aligner_in_kernel(const int* __restrict__ ids, int R, const 
   out[tid] = f2bf(gelu_erf(pre));
 }
 
+// E == 8, D % 8 == 0: a thread owns 8 consecutive outputs of a row -- one 16-B load of the embedding row,
+// 8 x 16 B of w1 rows, one 16-B store (the scalar kernel above did 2-B accesses per output).  Same
+// per-output arithmetic as gen_aligner_in_kernel (sequential fp32 dot over j, bf16 pre-activation).
+__global__ void gen_aligner_in8_kernel(const int* __restrict__ ids, int R, const bf16* __restrict__ emb, int V,
+                                       const bf16* __restrict__ w1, const bf16* __restrict__ b1, int D,
+                                       bf16* __restrict__ out) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cpr = D / 8;
+  if (tid >= (long)R * cpr) return;
+  const long r = tid / cpr;
+  const int d0 = (int)(tid % cpr) * 8;
+  float e[8], bb[8], o[8];
+  unpack8(*reinterpret_cast<const u32x4*>(emb + (long)min(max(ids[r], 0), V - 1) * 8), e);
+  unpack8(*reinterpret_cast<const u32x4*>(b1 + d0), bb);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float w[8];
+    unpack8(*reinterpret_cast<const u32x4*>(w1 + (long)(d0 + q) * 8), w);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += e[j] * w[j];
+    o[q] = gelu_erf(round_bf(acc + bb[q]));
+  }
+  *reinterpret_cast<u32x4*>(out + r * D + d0) = pack8(o);
+}
+
 __global__ void gather_rows_kernel(const bf16* __restrict__ src, int lds, int T, int t0, int N, int D,
                                    bf16* __restrict__ dst, long rows_out) {
   const int cpr = D / 8;
@@ -793,6 +819,13 @@ extern "C" int ospo_gen_aligner_in(const int* ids, int R, const void* gen_embed,
                                    const void* w1, const void* b1, int D, void* out, hipStream_t st) {
   if (!ids || !gen_embed || !w1 || !b1 || !out) return OSPO_ERR_ARG;
   if (R <= 0 || E <= 0 || D <= 0 || img_vocab <= 0) return OSPO_ERR_SHAPE;
+  if (E == 8 && D % 8 == 0 && aligned16(gen_embed) && aligned16(w1) && aligned16(b1) && aligned16(out)) {
+    const long n8 = (long)R * (D / 8);
+    hipLaunchKernelGGL(gen_aligner_in8_kernel, dim3(blocks(n8)), dim3(256), 0, st, ids, R, (const bf16*)gen_embed,
+                       img_vocab, (const bf16*)w1, (const bf16*)b1, D, (bf16*)out);
+    OSPO_CHECK_LAUNCH();
+    return OSPO_OK;
+  }
   const long n = (long)R * D;
   hipLaunchKernelGGL(gen_aligner_in_kernel, dim3(blocks(n)), dim3(256), 0, st, ids, R, (const bf16*)gen_embed,
                      img_vocab, E,
