@@ -12,7 +12,6 @@ rank 0.  See DESIGN.md "Measurement".
 from __future__ import annotations
 
 import argparse
-import contextlib
 import json
 import math
 import os
@@ -53,32 +52,62 @@ def synthetic_batch(B, Lt, N, vocab, img_vocab, seed, device):
     return text.to(device), chosen.to(device), rejected.to(device)
 
 
-def cpu_baseline(Lt=24, N=576):
-    """The CPU oracle (oracle/simpo_ref.py, bf16 CPU path) on a bounded sample:
-    one pair, full 7B shapes, fwd+bwd with 1 and with 2 decoder layers;
-    t_layer = t2 - t1, t_head = t1 - t_layer, per-pair = t_head + 30 * t_layer."""
+def host_cpu_info():
+    """(usable CPUs, host CPU count, CPU model).  Usable = the affinity mask, capped by the cgroup
+    CPU quota when one is set (a GPU box shows the whole machine in os.cpu_count() but grants a
+    share of it)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            usable = max(1, min(usable, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, os.cpu_count() or 1, model
+
+
+def cpu_baseline(Lt=24, N=576, L=30, reps=2):
+    """The CPU oracle (oracle/simpo_ref.py, bf16 CPU path) timed on the host cores: one pair at
+    full Janus-Pro-7B shapes, fwd + bwd through ALL L decoder layers, gen_head, log-probs and the
+    SimPO loss.  The L layers share one layer's frozen weights (aliased dict entries): the
+    arithmetic per layer is identical and the 7B-sized weight init on CPU would take longer than
+    the measurement.  Median of ``reps`` timed passes after one untimed warm-up pass."""
     from oracle import simpo_ref as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    threads, host_cpus, model = host_cpu_info()
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     text = [torch.randint(0, 4096, (1, Lt), generator=g, dtype=torch.int32)]
     ch = torch.randint(0, 16384, (1, N), generator=g)
     rj = torch.randint(0, 16384, (1, N), generator=g)
-    times = {}
-    for L in (1, 2):
-        dims = O.JanusDims(n_layers=L, vocab=4096)
-        w = O.init_weights(dims, seed=1, dtype=torch.bfloat16)
+    dims = O.JanusDims(n_layers=L, vocab=4096)
+    w = O.init_weights(O.JanusDims(n_layers=1, vocab=4096), seed=1, dtype=torch.bfloat16)
+    for k in list(w):
+        if k.startswith("layers.0."):
+            for i in range(1, L):
+                w[f"layers.{i}." + k[len("layers.0."):]] = w[k]
+    O.simpo_step(text, ch[:, :64], rj[:, :64], w, dims, dtype=torch.bfloat16)  # warm-up (short sequence)
+    times = []
+    for _ in range(reps):
         t0 = time.perf_counter()
         O.simpo_step(text, ch, rj, w, dims, dtype=torch.bfloat16)
-        times[L] = time.perf_counter() - t0
-        del w
-    t_layer = max(times[2] - times[1], 1e-6)
-    t_head = max(times[1] - t_layer, 0.0)
-    t_pair = t_head + 30 * t_layer
+        times.append(time.perf_counter() - t0)
+    t_pair = sorted(times)[len(times) // 2]
     return {"value": round(1.0 / t_pair, 5), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"1 pair (T={Lt + N}), oracle bf16 fwd+bwd with 1 and 2 full-size 7B decoder layers "
-                      f"({times[1]:.1f}s, {times[2]:.1f}s): t_layer {t_layer:.2f}s, head+loss {t_head:.2f}s, "
-                      f"scaled to 30 layers = {t_pair:.1f}s/pair"}
+            "host_cpus": host_cpus, "cpu_model": model,
+            "sample": f"1 pair (T={Lt + N}), oracle bf16 fwd+bwd through all {L} full-size 7B decoder layers "
+                      f"(layer weights shared), gen_head, logps, SimPO loss; {reps} passes "
+                      f"{', '.join(f'{t:.2f}' for t in times)} s, median {t_pair:.2f} s/pair, {threads} threads"}
 
 
 def t2i_bytes_per_step(dims, R, T_keys):
@@ -207,21 +236,111 @@ def bench_vq(args):
     }
     if not args.no_cpu_baseline:
         from oracle import vq_ref as V
-        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
+        threads, _, model = host_cpu_info()
+        torch.set_num_threads(threads)
         t0 = time.perf_counter()
         V.encode_ref(x[:1].cpu(), w)
         tc = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": round(1.0 / tc, 4), "unit": "images/s", "cores": torch.get_num_threads(),
+        line["cpu_baseline"] = {"value": round(1.0 / tc, 4), "unit": "images/s", "cores": threads, "cpu_model": model,
                                 "kind": "port", "sample": f"1 image, oracle/vq_ref.py encode_ref fp32 ({tc:.2f} s)"}
     print(json.dumps(line), flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args) -> bool:
+    """``python bench.py --gpus N`` with no torch.distributed env: start N ranks with
+    torch.distributed.run as a CHILD process (this parent never touches the GPU, so nothing is
+    exec'd from a process that initialised HIP) and return True; the caller exits with the
+    child's return code.  Under a launcher (WORLD_SIZE set), --gpus must agree with it."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if args.gpus is not None and int(env_world) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+        return False
+    if (args.gpus or 1) <= 1:
+        return False
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={args.master_port or _free_port()}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    args.child_rc = subprocess.call(cmd)
+    return True
+
+
+def default_pairs_per_gpu(world: int) -> int:
+    """BASELINE configs: 4 pairs on one GPU (config 2), 8 pairs per GPU with DP (config 3: global
+    batch 64 on 8 GPUs).  Per-GPU work is fixed for every N > 1 (weak scaling)."""
+    return 4 if world == 1 else 8
+
+
+def timed_region(step, warmup, steps, barrier, sync, world, device, on_last=None):
+    """W untimed steps; barrier + sync; K timed steps; barrier + sync; MAX over ranks."""
+    for i in range(warmup):
+        step(i)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    out = None
+    for i in range(steps):
+        if on_last is not None and i == steps - 1:
+            on_last()
+        out = step(i)
+    barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=device, dtype=torch.float64)
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item()), out
+
+
+def bench_stub(args):
+    """CPU rehearsal of the multi-rank bench (gloo): the same launcher, rank env, timed region,
+    max-over-ranks and JSON line, around a toy step (a small fp32 matmul per pair whose flat
+    gradient buffer goes through GradAllReduce's overlapped form).  For tests only: no GPU."""
+    from ospo_amd import dist as odist
+    world, rank, _ = odist.init(backend="gloo")
+    B = args.pairs_per_gpu or default_pairs_per_gpu(world)
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(B, 64, 64, generator=g)
+    w = torch.randn(64, 64, generator=torch.Generator().manual_seed(0))
+    grads = torch.zeros(4 * 64 * 64)
+    ar = odist.GradAllReduce(world, bucket_elems=64 * 64)
+
+    def step(_):
+        y = torch.tanh(x @ w)
+        ar.begin(grads)
+        for q in range(3, -1, -1):  # four "layers", last first, as the engine pushes them
+            grads[q * 4096:(q + 1) * 4096] = (x.transpose(1, 2) @ (1 - y * y)).sum(0).flatten() * (q + 1)
+            ar.push(q * 4096, (q + 1) * 4096)
+        ar.finish()
+        return y
+
+    dt, _ = timed_region(step, args.warmup, args.steps, odist.barrier, lambda: None, world, "cpu")
+    if rank == 0:
+        print(json.dumps({"metric": "stub pairs/sec (CPU launcher rehearsal)", "value": round(B * world * args.steps / dt, 3),
+                          "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (CPU stub)",
+                          "config": {"workload": "stub", "pairs_per_gpu": B, "global_batch": B * world,
+                                     "parallelism": f"dp{world}", "backend": "gloo",
+                                     "grad_checksum": round(float(grads.sum()), 3)}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None)  # default: WORLD_SIZE under a launcher, else 1
+    ap.add_argument("--master-port", type=int, default=0)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pairs-per-gpu", type=int, default=4)
+    ap.add_argument("--pairs-per-gpu", type=int, default=None)  # default: 4 at N=1, 8 at N>1
     ap.add_argument("--text-len", type=int, default=24)
     ap.add_argument("--img-tokens", type=int, default=576)
     ap.add_argument("--layers", type=int, default=30)
@@ -230,17 +349,22 @@ def main():
     ap.add_argument("--lora-dropout", type=float, default=0.05)
     # BASELINE config 5: the frozen decoder Linears on MXFP8 block-scaled fp8 MFMA (use with --lora-r 32)
     ap.add_argument("--linear-dtype", choices=("bf16", "mx8"), default="bf16")
-    ap.add_argument("--workload", choices=("simpo", "t2i", "vq"), default="simpo")  # t2i: config 4; vq: §8f-3
+    # t2i: config 4; vq: §8f-3; stub: CPU rehearsal of the multi-rank launcher (tests)
+    ap.add_argument("--workload", choices=("simpo", "t2i", "vq", "stub"), default="simpo")
     ap.add_argument("--vq-batch", type=int, default=16)
     ap.add_argument("--t2i-batch", type=int, default=16)       # parallel_size: prompts (x2 rows with CFG)
     ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
     args = ap.parse_args()
-    if args.workload == "t2i":
-        return bench_t2i(args)
-    if args.workload == "vq":
-        return bench_vq(args)
+    if launch_ranks(args):
+        sys.exit(args.child_rc)
+    if args.workload == "stub":
+        return bench_stub(args)
+    if args.workload in ("t2i", "vq"):
+        if (args.gpus or 1) != 1:
+            raise SystemExit(f"bench.py --workload {args.workload} is a single-GPU workload")
+        return bench_t2i(args) if args.workload == "t2i" else bench_vq(args)
 
     from ospo_amd import dist as odist
     from ospo_amd import ops
@@ -249,9 +373,13 @@ def main():
 
     world, rank, local = odist.init()
     dev = torch.device("cuda", local)
+    backend = "none"
+    if world > 1:
+        import torch.distributed as tdist
+        backend = tdist.get_backend()
     dims = JANUS_PRO_7B.__class__(**{**JANUS_PRO_7B.__dict__, "n_layers": args.layers, "lora_r": args.lora_r,
                                      "lora_alpha": 2 * args.lora_r})
-    B, Lt, N = args.pairs_per_gpu, args.text_len, args.img_tokens
+    B, Lt, N = args.pairs_per_gpu or default_pairs_per_gpu(world), args.text_len, args.img_tokens
     weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)  # identical on every rank (same seeds)
     eng = SimPOEngine(dims, weights, device=dev, max_pairs=B, max_text_len=Lt, n_img_tokens=N,
                       lora_dropout=args.lora_dropout, dropout_seed=42, linear_dtype=args.linear_dtype)
@@ -260,43 +388,24 @@ def main():
     cfg = SimPOConfig()
     buf = SimPOLossBuffers(B, dev)
     allreduce = odist.GradAllReduce(world) if world > 1 else None
+    # each rank draws its own pairs (the DistributedSampler shard of the global batch)
     batches = [synthetic_batch(B, Lt, N, dims.vocab, dims.img_vocab, seed=1000 * rank + i, device=dev)
                for i in range(4)]
 
-    # OSPO_MAIN_PRIO < 0 (A/B knob): the step's main stream is a high-priority HIP stream, so its GEMMs
-    # are dispatched ahead of the side stream's LoRA dA/dB products
-    prio = int(os.environ.get("OSPO_MAIN_PRIO", "0"))
-    hp = torch.cuda.Stream(device=dev, priority=prio) if prio else None
-    if hp is not None:
-        hp.wait_stream(torch.cuda.current_stream(dev))
-    stream_ctx = torch.cuda.stream(hp) if hp is not None else contextlib.nullcontext()
-    stream_ctx.__enter__()
-    for i in range(args.warmup):
-        train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
     timer = None if args.no_kernel_timer else ops.KernelTimer()
-    odist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        if i == args.steps - 1:
-            # per-launch HIP events on the last timed step only: an event pair around every GEMM
-            # costs ~1 % of the step (128.8 vs 127.5 ms), so recording them on all K steps would
-            # depress `value`; one step holds ~245 GEMM launches, enough for the average
-            ops.set_kernel_timer(timer)
-        out = train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
-    odist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    stream_ctx.__exit__(None, None, None)
+
+    def step(i):
+        return train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
+
+    # per-launch HIP events on the last timed step only: an event pair around every GEMM costs ~1 %
+    # of the step (128.8 vs 127.5 ms), so recording them on all K steps would depress `value`; one
+    # step holds ~245 GEMM launches, enough for the average
+    dt, out = timed_region(step, args.warmup, args.steps, odist.barrier, torch.cuda.synchronize, world, dev,
+                           on_last=(lambda: ops.set_kernel_timer(timer)) if timer is not None else None)
     ops.set_kernel_timer(None)
     loss = float(out["loss"].item())
     if not math.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
-    t = torch.tensor([dt], device=dev)
-    if world > 1:
-        import torch.distributed as tdist
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-    dt = float(t.item())
     if rank != 0:
         return
     global_batch = B * world
@@ -334,8 +443,8 @@ def main():
                                f"train step, LoRA r={dims.lora_r} dropout {args.lora_dropout}, {N} image tokens, "
                                f"{B} pairs/GPU" + (", MXFP8 decoder Linears (config 5)" if args.linear_dtype == "mx8" else ""),
                    "lora_dropout": args.lora_dropout, "linear_dtype": args.linear_dtype,
-                   "global_batch": global_batch, "seq_len": T, "parallelism": f"dp{world}",
-                   "algorithmic_tflop_per_pair": round(flops_pair / 1e12, 3)},
+                   "pairs_per_gpu": B, "global_batch": global_batch, "seq_len": T, "parallelism": f"dp{world}",
+                   "backend": backend, "algorithmic_tflop_per_pair": round(flops_pair / 1e12, 3)},
         "roofline": roof,
         "loss": round(loss, 5),
         "gemm_kernels": {k: {"count": v["count"], "ms": round(v["ms"], 2),

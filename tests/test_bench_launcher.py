@@ -1,0 +1,45 @@
+"""bench.py's multi-rank launcher on CPU (gloo): ``python bench.py --gpus 2`` must start two
+ranks by itself (torch.distributed.run as a child process), time the region with barrier + max
+over ranks, and print ONE JSON line from rank 0 reporting n_gpus = 2.  The
+stub workload exercises the same launcher / env / timing / all-reduce code as the GPU bench."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=240, env=env, cwd=ROOT)
+
+
+def _json_lines(out):
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+def test_bench_gpus2_launches_two_ranks():
+    p = _run(["--gpus", "2", "--workload", "stub", "--steps", "3", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["steps"] == 3 and ln["warmup"] == 1
+    assert ln["config"]["parallelism"] == "dp2" and ln["config"]["backend"] == "gloo"
+    assert ln["config"]["pairs_per_gpu"] == 8 and ln["config"]["global_batch"] == 16  # config 3's per-GPU load
+    assert ln["value"] > 0
+
+
+def test_bench_single_process_default():
+    p = _run(["--workload", "stub", "--steps", "2", "--warmup", "0", "--pairs-per-gpu", "3"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    (ln,) = _json_lines(p.stdout)
+    assert ln["n_gpus"] == 1 and ln["config"]["global_batch"] == 3
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    p = _run(["--gpus", "4", "--workload", "stub"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stderr + p.stdout)
