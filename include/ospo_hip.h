@@ -89,18 +89,12 @@ int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* B, int ldb,
 unsigned ospo_dropout_hash(unsigned idx, unsigned seed);
 
 /* Split-K workspace for the GEMM's tail round (tiles % CUs leftover tiles are split
- * along K into fp32 partial tiles, then summed + epilogued by a fixup launch).
- * bytes >= 256 KiB x CU count uses the split everywhere it pays; NULL disables it.
- * The library keeps the pointer: it must outlive every later GEMM call, and GEMMs
- * sharing it must be stream-ordered. */
+ * along K into fp32 partial tiles, then summed + epilogued by a fixup launch), registered
+ * for the CURRENT device (hipGetDevice): each device has its own, and a GEMM uses the one of
+ * the device it runs on.  bytes >= 256 KiB x CU count uses the split everywhere it pays; NULL
+ * disables it.  The library keeps the pointer: it must outlive every later GEMM call on that
+ * device, and GEMMs sharing it must be stream-ordered. */
 int ospo_gemm_set_workspace(void* ws, size_t bytes);
-
-/* Tuning knob (process-global) selecting the NT GEMM schedule for N % 256 == 0:
- * 0 = 256x256 8-phase ping-pong with counted vmcnt + split-K tail (default);
- * 1 = simple double-buffered 256x256; 2 = simple 160x256; 3 = register-prefetch
- * (v3); 4 = BK=32 LDS ring (v4); 5 = 8-phase without the split tail;
- * 10-13 = ablations for profiling (results INVALID: no loads / no MFMA). */
-int ospo_set_gemm_variant(int variant);
 
 /* Row count of the tile ospo_gemm_nt_bf16 uses for an M x N output (256 or 64). */
 int ospo_gemm_nt_tile(int M, int N);
@@ -322,8 +316,6 @@ int ospo_decode_advance(int* pos_dev, int* step_dev, hipStream_t stream);
 /* Test / A-B knob of the 256x256 GEMMs: 0 = cost-model split of the tail round (default), 2..8 = force
  * that split-K factor on the tail tiles (bounded by K / 4 K-tiles per piece). */
 int ospo_gemm_force_split(int s);
-/* A/B knob of the LoRA skinny products: 1 = 16-row loop, 2 = 64-row LDS-shared, 3 = 2 with K splits of whole chunks (default). */
-int ospo_set_skinny_variant(int v);
 /* Decode-step fusions of the GEMV split sum with its consumer (bit-identical to the unfused
  * ospo_decode_gemv + consumer; need ospo_decode_gemv_fusable(R, N, K), else OSPO_ERR_UNSUPPORTED):
  * ospo_decode_gemv_kv: q|k|v = X . W^T (W [3 H 128, K]) then RoPE + KV-cache store as ospo_kv_store
@@ -335,11 +327,6 @@ int ospo_decode_gemv_kv(const void* W, int ldw, const void* X, int ldx, int R, i
                         void* k_cache, void* v_cache, int Tmax, void* q_out, int ldq, hipStream_t stream);
 int ospo_decode_gemv_swiglu(const void* W, int ldw, const void* X, int ldx, int R, int F, int K, void* ws,
                             size_t ws_bytes, void* h, int ldh, hipStream_t stream);
-/* A/B knob of the decode GEMV schedule: 1 = skinny loop, 2 = LDS-shared activations,
- * 3 = the same with 128 weight rows per workgroup and power-of-two K splits (default). */
-int ospo_set_gemv_variant(int v);
-/* A/B knob: force the K-split count of GEMV schedules 2 / 3 (0 = automatic). */
-int ospo_set_gemv_splits(int s);
 
 /* ------------------------------------------------------- VQ image tokenizer ---
  * janus/models/vq_model.py Encoder (:46-124) + quant_conv + VectorQuantizer

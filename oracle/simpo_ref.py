@@ -334,9 +334,11 @@ class StepOut:
 
 def simpo_step(text_tokens, chosen_ids, rejected_ids, w, dims: JanusDims, dtype=torch.bfloat16,
                beta=10.0, gamma_beta_ratio=0.5, label_smoothing=0.0, loss_type="sigmoid",
-               backward: bool = True, training: bool = True, dropout_masks=None, mx8: bool = False) -> StepOut:
+               backward: bool = True, training: bool = True, dropout_masks=None, mx8: bool = False,
+               sft_weight: float = 0.0) -> StepOut:
     """One SimPO step: preprocess -> concatenated forward -> logps -> loss
-    (train.py:399-445) -> backward to the LoRA tensors (autograd)."""
+    (train.py:399-445, + sft_weight * CE on the chosen logits, :421-430) -> backward to the
+    LoRA tensors (autograd)."""
     w = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in w.items()}
     lnames = [k for k in w if ".lora_" in k]
     if backward:
@@ -354,6 +356,13 @@ def simpo_step(text_tokens, chosen_ids, rejected_ids, w, dims: JanusDims, dtype=
         c, r = logps[:B], logps[B:]
         losses, cr, rr = simpo_loss(c, r, beta, gamma_beta_ratio, label_smoothing, loss_type)
         loss = losses.mean()
+        sft_loss = None
+        if sft_weight > 0.0:  # train.py:421-428: CrossEntropyLoss (ignore -100) on logits[:, :-1] vs labels[:, 1:]
+            cl = logits[:B, :-1, :].float()
+            lab = cb["concatenated_labels"][:B, 1:]
+            sft_loss = torch.nn.functional.cross_entropy(cl.reshape(-1, cl.shape[-1]), lab.reshape(-1),
+                                                         ignore_index=LABEL_PAD)
+            loss = sft_weight * sft_loss + loss
     metrics = {
         "rewards/chosen": cr.mean().item(), "rewards/rejected": rr.mean().item(),
         "rewards/accuracies": (cr > rr).float().mean().item(),
@@ -362,6 +371,10 @@ def simpo_step(text_tokens, chosen_ids, rejected_ids, w, dims: JanusDims, dtype=
         "logits/chosen": logits[:B].detach().float().mean().item(),
         "logits/rejected": logits[B:].detach().float().mean().item(),
     }
+    if sft_loss is not None:
+        metrics["sft_loss"] = sft_loss.item()
+        # train.py:422 rebinds policy_chosen_logits to [..., :-1, :] before the logging at :442
+        metrics["logits/chosen"] = logits[:B, :-1].detach().float().mean().item()
     grads = None
     if backward:
         loss.backward()

@@ -25,7 +25,6 @@ SIGNATURES = {
     "ospo_gemm_nt_dropout_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, U, F, P],
     "ospo_gemm_nt_swiglu_bwd_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, I, U, F, P],
     "ospo_gemm_nt_rope_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, P, I, I, P],
-    "ospo_set_gemm_variant": [I],
     "ospo_mx8_scale_bytes": [I, I],
     "ospo_quant_mx8": [P, I, I, I, P, I, P, P],
     "ospo_gemm_nt_mx8": [P, I, P, P, I, P, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P, P, I, I, U, F, P],
@@ -68,9 +67,6 @@ SIGNATURES = {
     "ospo_cfg_sample": [P, I, I, I, F, F, P, P, I, P, P, P, P],
     "ospo_embed_rows": [P, L, P, I, I, P, P],
     "ospo_decode_advance": [P, P, P],
-    "ospo_set_gemv_variant": [I],
-    "ospo_set_gemv_splits": [I],
-    "ospo_set_skinny_variant": [I],
     "ospo_gemm_force_split": [I],
     "ospo_vq_conv2d": [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, P, P, P],
     "ospo_vq_bmm_nt": [P, P, I, I, I, I, P, P],
@@ -83,6 +79,10 @@ SIGNATURES = {
     "ospo_sumsq": [P, L, P, P],
     "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],
 }
+
+# include/ospo_hip_ablation.h: only in libospo_hip_ablation.so (tools/ A/B runs, OSPO_HIP_LIB=...)
+ABLATION_SIGNATURES = {"ospo_set_gemm_variant": [I], "ospo_set_gemv_variant": [I], "ospo_set_gemv_splits": [I],
+                       "ospo_set_skinny_variant": [I]}
 
 RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
@@ -105,6 +105,11 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = argt
             fn.restype = RESTYPES.get(name, c_int)
+        for name, argt in ABLATION_SIGNATURES.items():
+            if hasattr(h, name):
+                fn = getattr(h, name)
+                fn.argtypes = argt
+                fn.restype = c_int
         h.ospo_strerror.argtypes = [c_int]
         h.ospo_strerror.restype = ctypes.c_char_p
         _lib = h

@@ -618,13 +618,17 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
 }
 
 // waves per workgroup (16 query rows / keys each): 8 shares every staged K/V (Q/dO)
-// tile between twice the rows; OSPO_ATTN_WAVES=4 selects the 64-row form (A/B)
+// tile between twice the rows; the ablation build's OSPO_ATTN_WAVES=4 selects the 64-row form (A/B)
 int attn_waves() {
+#ifdef OSPO_ABLATION
   static const int nw = [] {
     const char* e = getenv("OSPO_ATTN_WAVES");
     return (e && atoi(e) == 4) ? 4 : 8;
   }();
   return nw;
+#else
+  return 8;
+#endif
 }
 
 }  // namespace
@@ -639,8 +643,12 @@ extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k
   if (!aligned16(qkv) || !aligned16(o)) return OSPO_ERR_ALIGN;
   const int nw = attn_waves();
   dim3 grid(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
-  static const bool dbg = getenv("OSPO_ATTN_DBG") != nullptr;  // ablation only
+#ifdef OSPO_ABLATION
+  static const bool dbg = getenv("OSPO_ATTN_DBG") != nullptr;  // ablation only (results invalid)
   auto kfn = dbg ? attn_fwd_kernel<8, 1> : (nw == 8 ? attn_fwd_kernel<8, 0> : attn_fwd_kernel<4, 0>);
+#else
+  auto kfn = attn_fwd_kernel<8, 0>;
+#endif
   hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                      (bf16*)o, ld_o, lse, T, n_heads, scale);
   OSPO_CHECK_LAUNCH();
@@ -670,6 +678,7 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
                      scale, rc, rs);
   OSPO_CHECK_LAUNCH();
   dim3 grid(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
+#ifdef OSPO_ABLATION
   static const int dkdv_dbg = [] {  // ablation only (results invalid): tools/attn_bench.py
     const char* e = getenv("OSPO_ATTN_DKDV_DBG");
     return e ? atoi(e) : 0;
@@ -679,6 +688,9 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
   if (nw == 8 && dkdv_dbg == 2) dkdv = attn_bwd_dkdv_kernel<8, 2>;
   if (nw == 8 && dkdv_dbg == 3) dkdv = attn_bwd_dkdv_kernel<8, 3>;
   if (nw == 8 && dkdv_dbg == 4) dkdv = attn_bwd_dkdv_kernel<8, 4>;
+#else
+  auto dkdv = attn_bwd_dkdv_kernel<8>;
+#endif
   hipLaunchKernelGGL(dkdv, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
                      v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
   OSPO_CHECK_LAUNCH();

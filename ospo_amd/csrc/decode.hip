@@ -720,8 +720,13 @@ int gemv_splits(int nblocks, int K) {
   while (nblocks * s < 1024 && (K >> 5) / (2 * s) >= 8 * SK_WAVES) s *= 2;
   return s;
 }
+#ifdef OSPO_ABLATION
 int g_gemv_splits = 0;   // A/B knob: > 0 forces the v2 / v3 split count (clamped to K / 512 and 16)
 int g_gemv_variant = 3;  // 1 = skinny-loop GEMV, 2 = LDS-shared x, 3 = v2 with 128 rows per workgroup (default)
+#else
+constexpr int g_gemv_splits = 0;
+constexpr int g_gemv_variant = 3;  // the product library runs the v3 GEMV
+#endif
 // v2 K split: ~1024 workgroups, at least one 512-k chunk each; returns k per split (multiple of 32)
 int gemv2_kper(int N, int K) {
   const int groups = N / G2_ROWS;
@@ -761,6 +766,7 @@ extern "C" size_t ospo_decode_gemv_ws_bytes(int R, int N, int K) {
   return std::max(std::max(v1, v2), v3);
 }
 
+#ifdef OSPO_ABLATION
 extern "C" int ospo_set_gemv_splits(int s) {
   if (s < 0 || s > G2_MAX_SPLITS) return OSPO_ERR_ARG;
   g_gemv_splits = s;
@@ -772,6 +778,7 @@ extern "C" int ospo_set_gemv_variant(int v) {
   g_gemv_variant = v;
   return OSPO_OK;
 }
+#endif
 
 // the fused split-sum consumers need the v3 schedule with a K split (else: gemv + the consumer)
 extern "C" int ospo_decode_gemv_fusable(int R, int N, int K) {

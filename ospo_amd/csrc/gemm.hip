@@ -735,7 +735,11 @@ int launch_v4(const GemmArgs& a, hipStream_t s) {
 //    wave waits for its own DMA of it (vmcnt(2+2) before q0, vmcnt(6) before q2),
 //    placed just before the barrier that precedes the first reader.
 // Tile order: XCD-contiguous chunks of the data-parallel workgroups, GM = 4 row-tile groups.
+#ifdef OSPO_ABLATION
 int g_v5_gm = 4;  // row tiles per L2 group (A/B knob, variants 20-23)
+#else
+constexpr int g_v5_gm = 4;  // row tiles per L2 group
+#endif
 
 __device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0, int& n0, int GM = 4) {
   const int gsize = GM * tiles_n;
@@ -1329,19 +1333,27 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
   *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(args.C) + (long)m * args.ldc + n0 + c) = o;
 }
 
-float* g_splitk_ws = nullptr;
-size_t g_splitk_ws_bytes = 0;
-int g_num_cus = 0;
-int g_force_split = 0;  // test / A-B knob: > 0 forces that split of the tail round (still bounded below)
+// Per-device state: the caller-owned split-K workspace registered for each device (ospo_gemm_set_workspace
+// registers it for the current device) and the device's CU count.  A launch uses the current device's.
+constexpr int kMaxDevices = 64;
+struct DeviceState {
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  int cus = 0;
+};
+DeviceState g_dev[kMaxDevices];
+int g_force_split = 0;  // test knob: > 0 forces that split of the tail round (still bounded below)
 
-int num_cus() {
-  if (!g_num_cus) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    g_num_cus = n;
+DeviceState& dev_state() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+  DeviceState& d = g_dev[dev];
+  if (!d.cus) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    d.cus = n;
   }
-  return g_num_cus;
+  return d;
 }
 
 template <int DBG = 0, bool DROP = false, bool MX = false, int SP = 0>
@@ -1349,7 +1361,8 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
   const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
   const int ntot = (MX ? a.K / 128 : a.K / BK) + a.K2 / BK;
-  const int cus = num_cus();
+  DeviceState& ds = dev_state();
+  const int cus = ds.cus;
   int dp = tiles, split = 1, tail = 0;
   if (allow_split && tiles > cus) {
     tail = tiles % cus;
@@ -1360,7 +1373,7 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
     if (tail) {
       const double T = ntot * (MX ? 2.3 : 1.9);
       double best = T;
-      const int sp_max = std::min(std::min(8, ntot / 4), (int)(g_splitk_ws_bytes / (65536 * sizeof(float)) / tail));
+      const int sp_max = std::min(std::min(8, ntot / 4), (int)(ds.ws_bytes / (65536 * sizeof(float)) / tail));
       for (int sp = 2; sp <= sp_max; ++sp) {
         const double cost = (double)((tail * sp + cus - 1) / cus) / sp * T + 0.13 * tail * sp;
         if (cost < best - 1e-9) {
@@ -1373,7 +1386,7 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
     const size_t need = (size_t)tail * split * 65536 * sizeof(float);
     // (with dropout every extension tile must sit in K-range 0, which applies the mask)
     const bool drop_ok = !DROP || (long)(a.K2 / BK) * split <= ntot;
-    if (tail && split >= 2 && ntot >= 16 && drop_ok && g_splitk_ws && need <= g_splitk_ws_bytes) {
+    if (tail && split >= 2 && ntot >= 16 && drop_ok && ds.ws && need <= ds.ws_bytes) {
       dp = tiles - tail;
     } else {
       split = 1;
@@ -1382,11 +1395,11 @@ int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   }
   const int grid = dp + tail * split;
   hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP, MX, SP>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split,
-                     g_splitk_ws, g_v5_gm);
+                     ds.ws, g_v5_gm);
   OSPO_CHECK_LAUNCH();
   if (tail) {
     hipLaunchKernelGGL(splitk_fixup_kernel, dim3(tail * 32), dim3(256), 0, s, a, tm, tn, dp, split,
-                       (const float*)g_splitk_ws, g_v5_gm);
+                       (const float*)ds.ws, g_v5_gm);
     OSPO_CHECK_LAUNCH();
   }
   return OSPO_OK;
@@ -1403,7 +1416,11 @@ int launch_v3(const GemmArgs& a, hipStream_t s) {
   return OSPO_OK;
 }
 
+#ifdef OSPO_ABLATION
 int g_gemm_variant = 0;  // 0 = SP schedule + split-K tail (default); 17 = the 8-phase schedule; others: A/B, see dispatch
+#else
+constexpr int g_gemm_variant = 0;  // the product library runs the default schedule only
+#endif
 
 // NT tile: 256 x 256 (8-phase, split-K tail) whenever N % 256 == 0, else the 64 x 64 simple kernel.
 int pick_nt_tile(int M, int N) {
@@ -1430,6 +1447,9 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
              M, N, K, K2, alpha, (const bf16*)bias, (const bf16*)residual, ldr, C, ldc, 1, 0, 0};
   const int tile = pick_nt_tile(M, N);
   if (tile == 64) return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
+#ifndef OSPO_ABLATION
+  return launch_v5<0, false, false, 1>(a, stream, true);  // SP + split-K tail
+#else
   switch (g_gemm_variant) {
     // A/B alternatives (tools/gemm_bench.py); results identical, schedules differ
     case 1: return launch<2, 4, 8, 4, false, false, EPI_BF16>(a, stream);            // simple double-buffered
@@ -1451,6 +1471,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 17: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
     default: return launch_v5<0, false, false, 1>(a, stream, true);               // SP + split-K tail
   }
+#endif
 }
 
 extern "C" int ospo_gemm_force_split(int s) {
@@ -1578,11 +1599,13 @@ extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const 
 
 extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {
   if (bytes && (!ws || !aligned16(ws))) return OSPO_ERR_ARG;
-  g_splitk_ws = (float*)ws;
-  g_splitk_ws_bytes = ws ? bytes : 0;
+  DeviceState& d = dev_state();
+  d.ws = (float*)ws;
+  d.ws_bytes = ws ? bytes : 0;
   return OSPO_OK;
 }
 
+#ifdef OSPO_ABLATION
 extern "C" int ospo_set_gemm_variant(int v) {
   if (v >= 20 && v <= 23) {  // L2 row-group size of the default schedule: 2, 8, 16, 4
     const int gms[4] = {2, 8, 16, 4};
@@ -1595,6 +1618,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
   g_gemm_variant = v;
   return OSPO_OK;
 }
+#endif
 
 extern "C" int ospo_gemm_nt_tile(int M, int N) { return pick_nt_tile(M, N); }
 
@@ -1646,7 +1670,11 @@ static int gemm_f32acc_impl(const void* A, int lda, int a_kmajor, const void* B,
   // both K-major (LoRA weight gradients): big tiles only when they alone fill the chip,
   // otherwise 64 x 64 tiles (parallelism from tiles, not from more fp32-atomic K splits)
   const long ks = a.k_splits > 1 ? a.k_splits : 1;
+#ifdef OSPO_ABLATION
   static const bool legacy = getenv("OSPO_F32ACC_LEGACY") != nullptr;  // A/B of the tile rule only
+#else
+  constexpr bool legacy = false;
+#endif
   if (legacy) {
     if (wideN && !tallM) return launch<2, 4, 2, 4, true, true, EPI_F32_ATOMIC>(a, stream);
     if (tallM && !wideN) return launch<4, 2, 4, 2, true, true, EPI_F32_ATOMIC>(a, stream);

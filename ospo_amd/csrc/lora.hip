@@ -293,7 +293,11 @@ struct SkDropArgs {
   int ldxd = 0;
 };
 
+#ifdef OSPO_ABLATION
 static int g_skinny_variant = 3;  // 1 = 16-row skinny loop, 2 = 64-row LDS-shared, 3 = 2 with whole-chunk splits (default)
+#else
+constexpr int g_skinny_variant = 3;  // the product library runs the whole-chunk-split v2 kernels
+#endif
 
 // v2 K split: ~1024 workgroups over (64-row blocks x modules), each split >= one chunk.
 // Variant 3: splits own whole KC chunks (kper = a multiple of KC), so no workgroup runs a short
@@ -331,11 +335,13 @@ extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
   return (v1 > v2 ? v1 : v2) + 16;
 }
 
+#ifdef OSPO_ABLATION
 extern "C" int ospo_set_skinny_variant(int v) {
   if (v < 1 || v > 3) return OSPO_ERR_ARG;
   g_skinny_variant = v;
   return OSPO_OK;
 }
+#endif
 
 template <int NT>
 static int launch_skinny2(const bf16* a, int lda, const bf16* b, int ldb, int b_rows, int M, int M_out, int K,

@@ -24,7 +24,6 @@ MI355X-first memory plan (288 GB HBM3E per GPU):
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -77,7 +76,8 @@ class SimPOEngine:
 
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_pairs: int = 4,
                  max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
-                 dropout_seed: int = 42, linear_dtype: str = "bf16"):
+                 dropout_seed: int = 42, linear_dtype: str = "bf16", fuse_swiglu_bwd: bool = False,
+                 dadb_splits=(8, 4, 4, 8), side_priority: int = -1):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
         if linear_dtype not in ("bf16", "mx8"):
@@ -85,10 +85,10 @@ class SimPOEngine:
         # "mx8": the frozen decoder Linears (q|k|v, o, gate|up, down; forward and dX) run as MXFP8
         # block-scaled fp8 MFMA GEMMs (BASELINE config 5; oracle/mx8_ref.py defines the arithmetic)
         self.linear_dtype = linear_dtype
-        # OSPO_FUSE_SWIGLU_BWD=1 (bf16): the down_proj dX GEMM writes the SwiGLU backward (dgate | dup) from
-        # its epilogue and dh is never stored (ospo_gemm_nt_swiglu_bwd_bf16, bit-identical).  Off by default:
-        # the step time is the same (the epilogue's gu/dgu traffic is not overlapped with MFMA)
-        self.fuse_swiglu_bwd = linear_dtype == "bf16" and os.environ.get("OSPO_FUSE_SWIGLU_BWD", "0") == "1"
+        # fuse_swiglu_bwd (bf16): the down_proj dX GEMM writes the SwiGLU backward (dgate | dup) from its
+        # epilogue and dh is never stored (ospo_gemm_nt_swiglu_bwd_bf16, bit-identical).  Off by default: the
+        # step time is the same (the epilogue's gu/dgu traffic is not overlapped with MFMA)
+        self.fuse_swiglu_bwd = linear_dtype == "bf16" and bool(fuse_swiglu_bwd)
         # peft lora_dropout on the adapter inputs (ospo_amd/dropout.py: counter-based masks, one per input)
         self.lora_dropout = float(lora_dropout)
         self.training = True
@@ -157,13 +157,12 @@ class SimPOEngine:
         # The LoRA weight-gradient side stream runs at high HIP priority (-1): its short memory-bound dA/dB
         # launches are dispatched ahead of the main stream's GEMM workgroups and get out of their way
         # (+0.3 %, profiles/r01/stream_priority_ab.log; main-stream high priority instead: -0.2 %).
-        # OSPO_SIDE_PRIO=0 restores the default priority (A/B knob).
-        # K splits of the LoRA dA / dB products: dA (Kin <= 8192, > 8192), dB (multi-module, single-module);
-        # OSPO_DADB_SPLITS="8,4,4,8" overrides them (A/B knob)
-        self._dadb_splits = tuple(int(v) for v in os.environ.get("OSPO_DADB_SPLITS", "8,4,4,8").split(","))
+        # K splits of the LoRA dA / dB products: dA (Kin <= 8192, > 8192), dB (multi-module, single-module)
+        # (8, 4, 4, 8 measured best, profiles/r01/dadb_splits_ab_highprio.log)
+        self._dadb_splits = tuple(int(v) for v in dadb_splits)
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
-            raise ValueError("OSPO_DADB_SPLITS must be four positive split counts")
-        self._side = torch.cuda.Stream(device=self.device, priority=int(os.environ.get("OSPO_SIDE_PRIO", "-1")))
+            raise ValueError("dadb_splits must be four positive split counts")
+        self._side = torch.cuda.Stream(device=self.device, priority=int(side_priority))
 
     def ensure_capacity(self, pairs: int, text_len: int):
         """Grow the activation buffers when a batch exceeds them (ragged prompts)."""
@@ -390,6 +389,31 @@ class SimPOEngine:
         ops.logprob_fwd(self.logits[:R], self.img_ids[:R], N, self.lse_tok[:R], self.tok_logp[:R],
                         self.seq_logps[:S])
         return self.seq_logps[:S]
+
+    def logit_sums(self, skip_last: bool = False) -> torch.Tensor:
+        """fp32 [S]: per sequence, the sum of the gen_head logits over every position and code --
+        what the reference's ``all_logits[:B].mean()`` logging reduces (train.py:441-442) -- without
+        the [S, T, V] tensor: sum_v (z W2^T + b2)_v = z . colsum(W2) + sum(b2), z = GELU(h W1^T + b1).
+        The N predicting positions reuse the forward's z; the Lt other positions (text, and the
+        last, whose logits no loss term reads) run gen_head's first Linear here.  skip_last: leave
+        position T-1 out (train.py:422 rebinds the logits to [..., :-1, :] when sft_weight > 0).
+        Call after forward() and before backward()."""
+        S, T, Lt, N, D = self.S, self.T, self.Lt, self.N, self.dims.d_model
+        if not hasattr(self, "_w2sum"):
+            self._w2sum = self.gh_w2.float().sum(0)
+            self._b2sum = self.gh_b2.float().sum()
+        seq = torch.mv(self.zact[: S * N].float(), self._w2sum).view(S, N).sum(1)
+        pos = list(range(Lt - 1)) + ([] if skip_last else [T - 1])
+        if pos:
+            rows = (torch.arange(S, device=self.device)[:, None] * T +
+                    torch.tensor(pos, device=self.device)[None, :]).reshape(-1)
+            hx = self.hf.index_select(0, rows)
+            zp = torch.empty(hx.shape[0], self.dims.gen_head_dim, dtype=BF16, device=self.device)
+            ops.gemm_nt(hx, self.gh_w1, zp, bias=self.gh_b1)
+            za = torch.empty_like(zp)
+            ops.gelu_fwd(zp, za)
+            seq = seq + torch.mv(za.float(), self._w2sum).view(S, len(pos)).sum(1)
+        return seq + (N + len(pos)) * self._b2sum
 
     # ------------------------------------------------------------ backward
     def zero_grad(self):

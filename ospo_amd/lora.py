@@ -90,6 +90,16 @@ class LoraLayout:
         return {name: flat[off:off + s[0] * s[1]].view(*s) for name, off, s in self.slices()}
 
 
+PEFT_MODULE_ORDER = ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj")
+
+
+def peft_param_order(n_layers: int) -> List[str]:
+    """The adapter tensors in ``model.parameters()`` order of the peft-wrapped Llama (layer by
+    layer; self_attn q, k, v, o then mlp gate, up, down; lora_A before lora_B) -- the order of
+    the trainable entries of the reference's ``AdamW(self.parameters())`` (train.py:108-115)."""
+    return [f"layers.{i}.{m}.lora_{ab}" for i in range(n_layers) for m in PEFT_MODULE_ORDER for ab in "AB"]
+
+
 def peft_key(name: str) -> str:
     """layers.{i}.{proj}.lora_{A,B} -> the key PL/peft write into the .ckpt state_dict
     (model.language_model.base_model.model.model.layers.{i}.{self_attn|mlp}.{proj}.lora_A.default.weight)."""

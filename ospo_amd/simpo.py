@@ -31,8 +31,8 @@ class SimPOConfig:
 
     def __post_init__(self):
         ops.loss_type_id(self.loss_type)  # ValueError on unknown type, like train.py:335-337
-        if self.sft_weight:
-            raise NotImplementedError("sft_weight > 0 (train.py:421-430) is not on the built path")
+        if self.sft_weight < 0:
+            raise ValueError("sft_weight must be >= 0")
 
 
 class SimPOLossBuffers:
@@ -63,6 +63,13 @@ def train_step(engine, text_ids, chosen_ids, rejected_ids, cfg: SimPOConfig, buf
     logps = engine.forward(text_ids, chosen_ids, rejected_ids)
     losses, mean, rewards = simpo_forward(logps, B, cfg, buf)
     glogps = simpo_backward(logps, B, cfg, buf)
+    sft = None
+    if cfg.sft_weight > 0.0:
+        # train.py:421-428: CE over the chosen logits' valid (image-token) positions; every chosen row
+        # has exactly N of them, so CE = -mean(chosen per-token-mean logps) and d/d logps = -1/B
+        sft = -logps[:B].mean()
+        mean = mean + cfg.sft_weight * sft
+        glogps[:B] -= cfg.sft_weight / B
     engine.zero_grad()
     if allreduce is not None and hasattr(allreduce, "begin"):
         allreduce.begin(engine.grads)  # layer buckets all-reduced while the backward runs on
@@ -74,7 +81,10 @@ def train_step(engine, text_ids, chosen_ids, rejected_ids, cfg: SimPOConfig, buf
             allreduce(engine.grads)
     if optimizer:
         engine.optimizer_step(cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay, cfg.max_norm)
-    return {"loss": mean, "losses": losses, "logps": logps, "rewards": rewards}
+    out = {"loss": mean, "losses": losses, "logps": logps, "rewards": rewards}
+    if sft is not None:
+        out["sft_loss"] = sft
+    return out
 
 
 # --------------------------------------------------------------------------- autograd
@@ -106,11 +116,9 @@ class SimPOLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_losses):
         (logps,) = ctx.saved_tensors
-        # d/dlogps of sum_i g_i * loss_i: the kernel gives d(mean)/dlogps for g = 1,
-        # so feed B * g_i via a per-call scale (losses.mean() gives g_i = 1/B).
-        g = g_losses.contiguous()
-        if not torch.all(g == g[0]):
-            raise NotImplementedError("non-uniform loss weights")
-        scale = (g[:1] * ctx.B).float()
-        glogps = simpo_backward(logps.contiguous(), ctx.B, ctx.cfg, ctx.buf, scale)
-        return glogps.clone(), None, None, None
+        # d/dlogps of sum_i g_i * loss_i: loss_i depends on (c_i, r_i) only and the kernel gives
+        # d(mean)/dlogps = (1/B) dloss_i/d(c_i, r_i) for a unit upstream grad, so scale by B * g_i
+        # (no host sync; losses.mean() gives g_i = 1/B)
+        g = g_losses.contiguous().float()
+        glogps = simpo_backward(logps.contiguous(), ctx.B, ctx.cfg, ctx.buf)
+        return glogps * (ctx.B * torch.cat([g, g])), None, None, None

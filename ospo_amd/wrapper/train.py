@@ -13,13 +13,18 @@ defaults (:30-43), same method names and return shapes, same errors:
   configure_optimizers() -> ([opt], [{"scheduler", "interval"}])  (:108-132)
   compute_total_grad_norm() -> float                              (:459-469)
 
+Batches come in the reference's collate format (train_dataset.py:53-55): images as f32
+pixel tensors [1, 3, 384, 384], VQ-encoded on the GPU inside ``preprocess_batch`` (all 2B
+images of the step in one encode, train.py:246-261), or as VQ token ids [1, N] (a token cache).
+
 Differences by construction (documented in DESIGN.md):
-  * images arrive as VQ token ids (int [1, N]); VQ encode is the step before the
-    hot path.  Float pixel tensors raise NotImplementedError.
+  * the VQ encode runs in fp32 (exact ids; the reference's bf16 autocast moves ~10 % of them).
   * the embeddings are assembled inside the fused engine, so preprocess_batch
     returns ids/labels instead of [B, T, D] inputs_embeds.
-  * logits are materialised for the N image-token positions only (the positions
-    whose log-probs the loss uses); ``logits/*`` logging averages over those.
+  * concatenated_forward returns the logits of the N image-token positions (a copy,
+    [B, N, V]; the other positions carry label -100); ``logits/*`` logging still averages
+    over all [B, T, V] logits as the reference does (engine.logit_sums).
+  * logged scalars stay on the device until read (``logged``), so a step has no host sync.
 """
 from __future__ import annotations
 
@@ -30,6 +35,7 @@ import torch
 from .. import dist as odist
 from .. import ops
 from ..config import save_config
+from ..lora import peft_param_order
 from ..simpo import PolicyLogps, SimPOConfig, SimPOLossBuffers, SimPOLossFn
 
 
@@ -52,16 +58,54 @@ class FusedLoraAdamW:
         self.engine.zero_grad()
 
     def state_dict(self):
+        """torch.optim.AdamW's format: ``state`` {i: {step, exp_avg, exp_avg_sq}} and ``param_groups``
+        [{..., params: [0..n-1]}] over the adapter tensors in peft ``parameters()`` order
+        (``ospo_param_names`` names them)."""
         e = self.engine
-        return {"step": e.opt_step, "exp_avg": e.exp_avg.cpu(), "exp_avg_sq": e.exp_avg_sq.cpu(),
-                "param_groups": [dict(g) for g in self.param_groups]}
+        names = peft_param_order(e.dims.n_layers)
+        m, v = e.layout.from_flat(e.exp_avg), e.layout.from_flat(e.exp_avg_sq)
+        step = torch.tensor(float(e.opt_step))
+        state = {i: {"step": step.clone(), "exp_avg": m[n].detach().cpu().clone(),
+                     "exp_avg_sq": v[n].detach().cpu().clone()} for i, n in enumerate(names)} if e.opt_step else {}
+        g = dict(self.param_groups[0], amsgrad=False, maximize=False, foreach=None, capturable=False,
+                 differentiable=False, fused=None, params=list(range(len(names))))
+        g["betas"] = tuple(g["betas"])
+        return {"state": state, "param_groups": [g], "ospo_param_names": names}
 
     def load_state_dict(self, sd):
+        """Our state_dict, or a torch AdamW state_dict over the whole reference module tree
+        (``AdamW(self.parameters())``): only the adapters train, so its entries WITH state are the
+        adapter tensors in peft order, which is how they are mapped."""
         e = self.engine
-        e.opt_step = int(sd["step"])
-        e.exp_avg.copy_(sd["exp_avg"])
-        e.exp_avg_sq.copy_(sd["exp_avg_sq"])
-        self.param_groups = [dict(g) for g in sd["param_groups"]]
+        names = peft_param_order(e.dims.n_layers)
+        if "state" not in sd or "param_groups" not in sd:
+            raise ValueError("optimizer state: expected a torch.optim.AdamW state_dict (state, param_groups)")
+        keys = sorted(sd["state"])
+        if keys and len(keys) != len(names):
+            raise ValueError(f"optimizer state holds {len(keys)} tensors with state, the adapters are {len(names)}")
+        shapes = {n: s for n, _, s in e.layout.slices()}
+        m, v = {}, {}
+        steps = set()
+        for k, n in zip(keys, names):
+            st = sd["state"][k]
+            if tuple(st["exp_avg"].shape) != shapes[n]:
+                raise ValueError(f"optimizer state {k}: shape {tuple(st['exp_avg'].shape)} != {n} {shapes[n]}")
+            m[n], v[n] = st["exp_avg"], st["exp_avg_sq"]
+            steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"optimizer state: adapters at different step counts {sorted(steps)}")
+        if keys:
+            e.layout.to_flat({n: t.to(e.exp_avg.dtype) for n, t in m.items()}, fm := torch.zeros_like(e.exp_avg, device="cpu"))
+            e.layout.to_flat({n: t.to(e.exp_avg_sq.dtype) for n, t in v.items()}, fv := torch.zeros_like(e.exp_avg_sq, device="cpu"))
+            e.exp_avg.copy_(fm)
+            e.exp_avg_sq.copy_(fv)
+        else:
+            e.exp_avg.zero_()
+            e.exp_avg_sq.zero_()
+        e.opt_step = steps.pop() if steps else 0
+        g = sd["param_groups"][0]
+        self.param_groups = [{k: g[k] for k in ("lr", "initial_lr", "betas", "eps", "weight_decay") if k in g}]
+        self.param_groups[0].setdefault("initial_lr", self.param_groups[0]["lr"])
 
 
 class ConstantLR:
@@ -138,7 +182,8 @@ class JanusProTrainWrapper:
         self.device = self.engine.device
         self._buf = SimPOLossBuffers(max(1, self.engine.cap_pairs), self.device)
         self.global_step = 0
-        self.logged: Dict[str, float] = {}
+        self._logged: Dict[str, float] = {}
+        self._pending: List[Tuple[List[str], torch.Tensor]] = []
         self.trainer = None
         self.log_dir = None
 
@@ -162,21 +207,26 @@ class JanusProTrainWrapper:
             print(f"{name}: {tuple(t.shape)}, dtype={t.dtype}")
 
     # ------------------------------------------------------------ logging (PL log / log_dict)
+    @property
+    def logged(self) -> Dict[str, float]:
+        """The logged scalars as floats (reading them is the only host sync of the logging)."""
+        if self._pending:
+            for names, vals in self._pending:
+                for n, v in zip(names, vals.tolist()):
+                    self._logged[n] = v
+            self._pending = []
+        return self._logged
+
     def log(self, name, value, sync_dist: bool = True, **kw):
-        t = value.detach().float().reshape(1).to(self.device) if torch.is_tensor(value) else \
-            torch.tensor([float(value)], device=self.device)
-        if sync_dist:
-            odist.all_reduce_mean_(t)
-        self.logged[name] = float(t.item())
+        self.log_dict({name: value}, sync_dist=sync_dist)
 
     def log_dict(self, d: Dict[str, Any], sync_dist: bool = True, **kw):
         names = list(d)
-        vals = torch.stack([(v.detach().float().reshape(()) if torch.is_tensor(v) else torch.tensor(float(v)))
-                            .to(self.device) for v in d.values()])
+        vals = torch.stack([(v.detach().float().reshape(()).to(self.device) if torch.is_tensor(v)
+                             else torch.tensor(float(v), device=self.device)) for v in d.values()])
         if sync_dist:
             odist.all_reduce_mean_(vals)  # one fused all-reduce for all scalars
-        for n, v in zip(names, vals.tolist()):
-            self.logged[n] = v
+        self._pending.append((names, vals))
 
     # ------------------------------------------------------------ the step
     def training_step(self, batch, batch_idx):
@@ -187,7 +237,7 @@ class JanusProTrainWrapper:
         return loss
 
     def on_before_optimizer_step(self, *args, **kwargs):
-        self.log("train/grad_norm", self.compute_total_grad_norm(), sync_dist=False)
+        self.log("train/grad_norm", self.engine.grad_norm_sq().sqrt(), sync_dist=False)  # stays on device
 
     def configure_optimizers(self):
         c = self.config
@@ -206,33 +256,40 @@ class JanusProTrainWrapper:
 
     # ------------------------------------------------------------ data -> ids
     def preprocess_batch(self, batch: Tuple) -> Dict[str, Any]:
+        """train.py:219-279: text ids right-padded to the batch max (the engine zero-embeds the
+        padding), image ids from the VQ encoder (pixels) or as given (token ids), labels
+        [-100 x Lt | image ids]."""
         item_ids, text_tokens, chosen_t, rejected_t = batch
         B = len(item_ids)
         Lt = max(int(t.shape[-1]) for t in text_tokens)
         text_ids = torch.full((B, Lt), -1, dtype=torch.int32)
         for i, t in enumerate(text_tokens):
             text_ids[i, : t.shape[-1]] = t.reshape(-1).to(torch.int32)
-        ch = torch.stack([self._image_ids(x) for x in chosen_t])
-        rj = torch.stack([self._image_ids(x) for x in rejected_t])
         d = self.engine.dims
         if int(text_ids.max()) >= d.vocab:
             raise ValueError(f"text token id >= vocab ({d.vocab})")
-        if int(torch.cat([ch, rj]).max()) >= d.img_vocab or int(torch.cat([ch, rj]).min()) < 0:
-            raise ValueError(f"VQ token id outside [0, {d.img_vocab})")
-        lab_txt = torch.full((B, Lt), self.label_pad_token_id, dtype=torch.long)
+        images = list(chosen_t) + list(rejected_t)
+        pixels = [x.is_floating_point() for x in images]
+        if all(pixels):
+            # gen_vision_model.encode of all 2B images at once (the reference loops per sample)
+            ids = self.model.vq_encode(torch.cat([x.reshape(-1, *x.shape[-3:]) for x in images]))
+            if ids.shape != (2 * B, self.engine.N):
+                raise ValueError(f"{ids.shape[1]} VQ tokens per image, the engine expects {self.engine.N}")
+            ch, rj = ids[:B], ids[B:]
+        elif not any(pixels):
+            ids = torch.stack([x.reshape(-1).long() for x in images])
+            if int(ids.max()) >= d.img_vocab or int(ids.min()) < 0:
+                raise ValueError(f"VQ token id outside [0, {d.img_vocab})")
+            ch, rj = ids[:B].to(self.device, torch.int32), ids[B:].to(self.device, torch.int32)
+        else:
+            raise ValueError("a batch mixes pixel tensors and VQ token ids")
+        lab_txt = torch.full((B, Lt), self.label_pad_token_id, dtype=torch.long, device=ch.device)
         return {
             "item_ids": list(item_ids),
             "text_ids": text_ids.to(self.device, non_blocking=True),
-            "chosen_ids": ch.to(self.device, torch.int32), "rejected_ids": rj.to(self.device, torch.int32),
+            "chosen_ids": ch, "rejected_ids": rj,
             "chosen_labels": torch.cat([lab_txt, ch.long()], 1), "rejected_labels": torch.cat([lab_txt, rj.long()], 1),
         }
-
-    @staticmethod
-    def _image_ids(x: torch.Tensor) -> torch.Tensor:
-        if x.is_floating_point():
-            raise NotImplementedError("pixel tensors need VQ encode, which is not on the built path "
-                                      "(SURVEY §8f rank 3): feed VQ token ids (dataset token_cache)")
-        return x.reshape(-1).long()
 
     def concatenated_inputs(self, batch: Dict[str, Any]) -> Dict[str, torch.Tensor]:
         """cat chosen | rejected along dim 0 (train.py:282-314; pad_to_length is a no-op here)."""
@@ -247,7 +304,8 @@ class JanusProTrainWrapper:
         all_logps = PolicyLogps.apply(self.model.lora_anchor, self.engine, batch["text_ids"], batch["chosen_ids"],
                                       batch["rejected_ids"])
         e = self.engine
-        logits = e.logits[: e.S * e.N].view(e.S, e.N, -1)
+        # a copy: the engine's logits buffer becomes d(loss)/d(logits) in backward()
+        logits = e.logits[: e.S * e.N].view(e.S, e.N, -1).clone()
         return (all_logps[:len_chosen], all_logps[len_chosen:], logits[:len_chosen], logits[len_chosen:],
                 batch["chosen_labels"])
 
@@ -281,16 +339,27 @@ class JanusProTrainWrapper:
 
     def get_batch_loss_metrics(self, batch, train_eval: Literal["train", "val"] = "train"):
         prefix = "val" if train_eval == "val" else "train"
-        c, r, cl, rl, _ = self.concatenated_forward(batch)
+        c, r, _, _, _ = self.concatenated_forward(batch)
         losses, cr, rr = self.simpo_loss(c, r)
         loss = losses.mean()
-        if self.sft_weight > 0.0:
-            raise NotImplementedError("sft_weight > 0 is not on the built path")
+        e = self.engine
+        sft = self.sft_weight > 0.0
+        if sft:
+            # train.py:421-428: CrossEntropyLoss(ignore -100) over logits[:, :-1] vs labels[:, 1:] of the chosen
+            # rows.  Each chosen row has exactly N valid labels, so CE = -mean(chosen per-token-mean logps):
+            # the same value and gradient without the [B, T-1, V] tensor
+            sft_loss = -c.mean()
+            loss = self.sft_weight * sft_loss + loss
+            self.log(f"{prefix}/sft_loss", sft_loss.detach(), sync_dist=True)
+        # logits/*: mean over all [B, T, V] (over [B, T-1, V] for chosen with sft, train.py:422, 441-442)
+        B, T, V = e.B, e.T, e.dims.img_vocab
+        sums = e.logit_sums()
+        lc = (e.logit_sums(skip_last=True)[:B].sum() / (B * (T - 1) * V)) if sft else sums[:B].sum() / (B * T * V)
         self.log_dict({f"{prefix}/rewards/chosen": cr.mean(), f"{prefix}/rewards/rejected": rr.mean(),
                        f"{prefix}/rewards/accuracies": (cr > rr).float().mean(),
                        f"{prefix}/rewards/margins": (cr - rr).mean(),
                        f"{prefix}/logps/rejected": r.detach().mean(), f"{prefix}/logps/chosen": c.detach().mean(),
-                       f"{prefix}/logits/rejected": rl.float().mean(), f"{prefix}/logits/chosen": cl.float().mean()})
+                       f"{prefix}/logits/rejected": sums[B:].sum() / (B * T * V), f"{prefix}/logits/chosen": lc})
         return loss
 
     def compute_loss(self, inputs):

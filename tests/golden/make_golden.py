@@ -22,6 +22,8 @@ Outputs (``tests/golden/*.npz``, data only -- never reference source):
   step_tiny_weights.npz  D=256 L=2 model weights (bf16 bits), shared by:
   step_tiny_fp32.npz   2 ragged pairs, N=64, reference run in fp32
   step_tiny_bf16.npz   same inputs, bf16 model (reference CPU bf16 path)
+  step_tiny_sft_fp32.npz  the tiny fp32 step with algo.sft_weight = 0.5 (CE on the
+                       chosen logits, train.py:421-430)
   step_1b2l_bf16.npz   Janus-Pro-1B dims, 2 layers, 4 pairs from train.json
                        (synthetic prompt ids), N=64; weights regenerated from a
                        seed by ``oracle.simpo_ref.init_weights`` (checksum kept)
@@ -380,6 +382,22 @@ def make_tiny():
                   store_weights=False, seed=0)
 
 
+def make_tiny_sft():
+    """The make_tiny inputs and weights, fp32, with sft_weight = 0.5."""
+    g = torch.Generator().manual_seed(7)
+    text = [torch.randint(0, TINY.vocab, (1, 5), generator=g, dtype=torch.int32),
+            torch.randint(0, TINY.vocab, (1, 8), generator=g, dtype=torch.int32)]
+    N = 64
+    chosen = torch.randint(0, TINY.img_vocab, (2, N), generator=g)
+    rejected = torch.randint(0, TINY.img_vocab, (2, N), generator=g)
+    w = O.init_weights(TINY, seed=0, dtype=torch.bfloat16, lora_b_std=2e-2)
+    wd = {k: v.to(torch.float32) for k, v in w.items()}
+    algo = dict(ALGO, sft_weight=0.5)
+    out = run_reference_step(TINY, wd, torch.float32, text, chosen, rejected, algo)
+    save_step(os.path.join(HERE, "step_tiny_sft_fp32.npz"), TINY, wd, text, chosen, rejected, out, algo,
+              store_weights=False, seed=0)
+
+
 ONEB_2L = O.JanusDims(n_layers=2, d_model=2048, d_ff=5632, n_heads=16, head_dim=128, vocab=102400,
                       img_vocab=16384, img_embed=8, gen_head_dim=2048, lora_r=16, lora_alpha=32)
 
@@ -400,6 +418,7 @@ def make_1b():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    make_logps_kat()
-    make_tiny()
-    make_1b()
+    which = sys.argv[1:] or ["kat", "tiny", "sft", "1b"]
+    for name, fn in (("kat", make_logps_kat), ("tiny", make_tiny), ("sft", make_tiny_sft), ("1b", make_1b)):
+        if name in which:
+            fn()

@@ -5,6 +5,7 @@ FLOP model) behaves like the reference's."""
 import ctypes
 import json
 import os
+import types
 import re
 import subprocess
 import sys
@@ -137,7 +138,7 @@ def test_preference_dataset_prompt_and_collate():
     from ospo_amd.data import PreferenceDataset, SyntheticTokenizer, sft_prompt
     assert sft_prompt("A black umbrella") == "User: A black umbrella\n\nAssistant:<begin_of_image>"
     ds = PreferenceDataset(seed=42, data_path=os.path.join(ROOT, "tests", "golden", "train_step4.json"),
-                           tokenizer=SyntheticTokenizer(), num_samples=4)
+                           tokenizer=SyntheticTokenizer(), num_samples=4, synthetic_tokens=True)
     assert len(ds) == 4
     items = [ds[i] for i in range(4)]
     ids, text, ch, rj = ds.collate_fn(items)
@@ -147,6 +148,62 @@ def test_preference_dataset_prompt_and_collate():
     assert torch.equal(again[2], items[0][2])  # deterministic tokens
     with pytest.raises(ValueError):
         ds.decode({"item_id": "x", "prompt": "p"})
+
+
+def test_chat_processor_deepseek_template():
+    """apply_sft_template_for_multi_turn_prompts (processing_vlm.py:137-177, conversation.py:80-91)."""
+    from ospo_amd.data import ChatProcessor, sft_prompt
+    cp = ChatProcessor()
+    conv = [{"role": "User", "content": "  A red cube  "}, {"role": "Assistant", "content": ""}]
+    assert cp.apply_sft_template_for_multi_turn_prompts(conv, "deepseek", "") + cp.image_start_tag == \
+        sft_prompt("A red cube")
+    assert cp.apply_sft_template_for_multi_turn_prompts(conv, "deepseek", "sys") == "sys\n\nUser: A red cube\n\nAssistant:"
+
+
+def test_preference_dataset_pixels_reference_format():
+    """Default image source = the reference's collate format: PIL -> VLMImageProcessor (384, mean = std
+    = 0.5) -> f32 [1, 3, 384, 384]; the example train.json's absolute paths remapped to the fixtures.
+    The 384-px example PNG gives exactly the pixels the VQ goldens were made from (make_golden_vq.py)."""
+    import numpy as np
+    from ospo_amd.data import PreferenceDataset, SyntheticTokenizer, VLMImageProcessor
+    golden = os.path.join(ROOT, "tests", "golden")
+    ds = PreferenceDataset(seed=42, data_path=os.path.join(golden, "train_pixels.json"), tokenizer=SyntheticTokenizer(),
+                           path_map={"/home/elicer/OSPO/example": golden})
+    item_id, text, ch, rj = ds[0]
+    assert ch.dtype == torch.float32 and ch.shape == (1, 3, 384, 384) and rj.shape == (1, 3, 384, 384)
+    assert float(ch.min()) >= -1.0 and float(ch.max()) <= 1.0
+    u8 = np.load(os.path.join(golden, "vq_golden.npz"))["img2_u8"]
+    px = ds.get_image_tensor("/home/elicer/OSPO/example/step3/negative/layout/1000001/02.png")
+    want = ((u8.astype(np.float64) / 255.0).astype(np.float32) - 0.5) / 0.5
+    assert np.array_equal(px[0].numpy(), want.transpose(2, 0, 1))
+    # non-square input: long side resized to 384 (bicubic), padded with the mean colour
+    from PIL import Image
+    im = Image.fromarray(u8[:, :192])
+    x = VLMImageProcessor()([im])["pixel_values"]
+    assert x.shape == (1, 3, 384, 384)
+    assert float(x[0, :, :, :96].abs().max()) == pytest.approx(abs(127 / 255 - 0.5) / 0.5)
+
+
+def test_dataset_batch_equals_reference_dataset_with_our_processors():
+    """The reference's own PreferenceDataset + collate_fn fed the processor objects get_model returns
+    (tests/golden/make_golden_dataset.py) gives the batch our PreferenceDataset gives: same text ids,
+    bit-identical pixel tensors.  So the reference's unchanged dataloader (ospo/step5.py:17-23) feeds
+    the wrapper exactly what the GPU pixel-path tests feed it."""
+    import hashlib
+    import numpy as np
+    from ospo_amd.data import PreferenceDataset, SyntheticTokenizer
+    golden = os.path.join(ROOT, "tests", "golden")
+    z = np.load(os.path.join(golden, "dataset_batch.npz"))
+    ds = PreferenceDataset(seed=42, data_path=os.path.join(golden, "train_pixels.json"), tokenizer=SyntheticTokenizer(),
+                           path_map={"/home/elicer/OSPO/example": golden})
+    ids, text, ch, rj = ds.collate_fn([ds[i] for i in range(len(ds))])
+    assert list(ids) == list(z["item_ids"])
+    for i, t in enumerate(text):
+        assert np.array_equal(t.numpy(), z[f"text{i}"])
+    for side, ts in (("chosen", ch), ("rejected", rj)):
+        for i, t in enumerate(ts):
+            a = t.numpy()
+            assert hashlib.sha256(a.tobytes()).hexdigest() == str(z[f"{side}{i}_sha256"]), (side, i)
 
 
 def test_algorithmic_flops_match_survey():
@@ -163,6 +220,7 @@ def test_checkpoint_roundtrip_cpu(tmp_path):
 
     class StubEngine:
         def __init__(self):
+            self.dims = types.SimpleNamespace(n_layers=2)
             self.layout = LoraLayout(2, 256, 512, 16)
             self.lora = torch.randn(self.layout.numel).to(torch.bfloat16)
             self.exp_avg = torch.randn(self.layout.numel).to(torch.bfloat16)
@@ -188,6 +246,49 @@ def test_checkpoint_roundtrip_cpu(tmp_path):
     opt2 = FusedLoraAdamW(e2, 4e-5, (0.9, 0.95), 1e-8, 0.0, 1.0)
     load_checkpoint(p, e2, opt2, ConstantLR(opt2))
     assert torch.equal(e2.lora, e.lora) and torch.equal(e2.exp_avg_sq, e.exp_avg_sq) and e2.opt_step == 7
+    assert torch.equal(e2.exp_avg, e.exp_avg)
+    sd = ck["optimizer_states"][0]
+    assert set(sd) >= {"state", "param_groups"} and len(sd["state"]) == 2 * 7 * 2
+
+
+def test_optimizer_state_from_torch_adamw_over_the_reference_tree():
+    """A torch.optim.AdamW state_dict as the reference's PL run writes it (AdamW(self.parameters()):
+    frozen tensors interleaved, state only for the adapters) loads into the fused optimizer."""
+    from ospo_amd.lora import LoraLayout, peft_param_order
+    from ospo_amd.wrapper.train import FusedLoraAdamW
+    layout = LoraLayout(2, 256, 512, 16)
+    shapes = {n: s for n, _, s in layout.slices()}
+    params = []
+    for n in peft_param_order(2):
+        if n.endswith("lora_A"):
+            params.append(torch.zeros(4, 4, requires_grad=False))  # a frozen base weight before each module
+        params.append(torch.randn(*shapes[n], requires_grad=True))
+    opt = torch.optim.AdamW(params, lr=4e-5, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0)
+    for _ in range(3):
+        for q in params:
+            if q.requires_grad:
+                q.grad = torch.randn_like(q)
+        opt.step()
+    sd = opt.state_dict()
+
+    class StubEngine:
+        dims = types.SimpleNamespace(n_layers=2)
+
+        def __init__(self):
+            self.layout = layout
+            self.exp_avg = torch.zeros(layout.numel, dtype=torch.bfloat16)
+            self.exp_avg_sq = torch.zeros(layout.numel, dtype=torch.bfloat16)
+            self.opt_step = 0
+    e = StubEngine()
+    f = FusedLoraAdamW(e, 1e-3, (0.9, 0.99), 1e-6, 0.0, 1.0)
+    f.load_state_dict(sd)
+    assert e.opt_step == 3 and f.param_groups[0]["lr"] == 4e-5
+    m = layout.from_flat(e.exp_avg)
+    trained = [q for q in params if q.requires_grad]
+    for n, q in zip(peft_param_order(2), trained):
+        assert torch.equal(m[n], opt.state[q]["exp_avg"].to(torch.bfloat16)), n
+    with pytest.raises(ValueError):
+        f.load_state_dict({"step": 1, "exp_avg": None})  # not a torch AdamW state_dict
 
 
 def test_dropout_hash_host_c_and_numpy_agree(lib):

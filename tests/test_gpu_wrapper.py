@@ -12,22 +12,33 @@ from tests import fixtures as FX
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-TINY = ["model.arch=janus-pro-1b",
+TINY = ["model.synthetic=true", "dataset.train.synthetic_tokens=true",
+        f"dataset.train.data_path={ROOT}/tests/golden/train_step4.json", "model.arch=janus-pro-1b",
         "model.override={'n_layers': 2, 'd_model': 256, 'd_ff': 512, 'n_heads': 2, 'vocab': 512, "
         "'img_vocab': 2048, 'gen_head_dim': 256}",
         "lora.lora_rank=16", "lora.lora_alpha=32", "dataset.train.batch_size=2", "experiment.max_training_steps=4",
         "experiment.save_steps=2"]
 
 
-def make(tmp_path, extra=()):
+# images as the reference feeds them: the 2 example pairs' PNGs (tests/golden/step3) -> f32 pixels;
+# the VQ codebook is 16384 x 8, so img_vocab stays 16384 and every image is 576 tokens
+PIXELS = ["model.synthetic=true", f"dataset.train.data_path={ROOT}/tests/golden/train_pixels.json",
+          "dataset.train.path_map={'/home/elicer/OSPO/example': '" + ROOT + "/tests/golden'}",
+          "model.arch=janus-pro-1b",
+          "model.override={'n_layers': 2, 'd_model': 256, 'd_ff': 512, 'n_heads': 2, 'vocab': 512, "
+          "'gen_head_dim': 256}",
+          "lora.lora_rank=16", "lora.lora_alpha=32", "dataset.train.batch_size=2"]
+
+
+def make(tmp_path, extra=(), base=TINY):
     from ospo_amd.config import build_config
     from ospo_amd.data import train_dataloader
     from ospo_amd.model import get_model
     from ospo_amd.wrapper.train import JanusProTrainWrapper
     cfg = build_config(os.path.join(ROOT, "configs", "step5.yaml"),
-                       argv=TINY + [f"base.save_path={tmp_path}"] + list(extra))
+                       argv=list(base) + [f"base.save_path={tmp_path}"] + list(extra))
     model, cp, ip, tok = get_model(mode="train", config=cfg, seed=0)
-    dl = train_dataloader(cfg, tok, img_vocab=model.engine.dims.img_vocab)
+    dl = train_dataloader(cfg, tok, img_vocab=model.engine.dims.img_vocab, chat_processor=cp, image_processor=ip)
     w = JanusProTrainWrapper(cfg, model, cp, ip, tok)
     return cfg, model, dl, w
 
@@ -84,3 +95,84 @@ def test_get_batch_logps_matches_reference_kat(tmp_path):
     torch.testing.assert_close(tot, torch.from_numpy(z["logps_sum"]), rtol=2e-5, atol=2e-4)
     with pytest.raises(ValueError):
         w.get_batch_logps(logits[:, :-1], labels)
+
+
+def _vq_golden_weights(model):
+    """Give the policy's VQ encoder the seeded weights the VQ goldens were made with (make_golden_vq.py)."""
+    from oracle import vq_ref as V
+    z = FX.load("vq_golden.npz")
+    model._vq, model._vq_weights = None, V.init_vq_weights(int(z["seed"]))
+
+
+def test_pixel_batches_vq_encoded_in_preprocess_match_token_cache(tmp_path):
+    """The reference's collate format (f32 pixels, train_dataset.py:79-84) goes through the GPU VQ encode
+    inside preprocess_batch (train.py:246-261): ids equal a token cache built by the same encoder, and
+    the step's logps / loss / grads are identical to the cache path's."""
+    import numpy as np
+    from ospo_amd.vq import build_token_cache
+    cfg, model, dl, w = make(tmp_path, base=PIXELS)
+    _vq_golden_weights(model)
+    batch = next(iter(torch.utils.data.DataLoader(dl.dataset, batch_size=2, shuffle=False,
+                                                  collate_fn=dl.dataset.collate_fn)))
+    assert batch[2][0].dtype == torch.float32 and batch[2][0].shape == (1, 3, 384, 384)
+    pre = w.preprocess_batch(batch)
+    assert pre["chosen_ids"].shape == (2, 576) and pre["chosen_ids"].is_cuda
+    # the same PNGs through the token-cache CLI path
+    golden = os.path.join(ROOT, "tests", "golden")
+    items = []
+    for ex in dl.dataset.dataset:
+        for side in ("chosen", "rejected"):
+            items.append((f"{ex['item_id']}/{side}", dl.dataset.remap(ex[side])))
+    cache = build_token_cache(model.gen_vision_model, items, str(tmp_path / "cache.npz"))
+    for i, ex in enumerate(dl.dataset.dataset):
+        assert np.array_equal(pre["chosen_ids"][i].cpu().numpy(), cache[f"{ex['item_id']}/chosen"])
+        assert np.array_equal(pre["rejected_ids"][i].cpu().numpy(), cache[f"{ex['item_id']}/rejected"])
+    eng = w.engine
+    eng.zero_grad()
+    loss = w.training_step(batch, 0)
+    loss.backward()
+    g_pix = eng.grads.clone()
+    id_batch = (batch[0], batch[1], [torch.from_numpy(cache[f"{i}/chosen"]).view(1, -1) for i in batch[0]],
+                [torch.from_numpy(cache[f"{i}/rejected"]).view(1, -1) for i in batch[0]])
+    eng.zero_grad()
+    loss2 = w.training_step(id_batch, 0)
+    loss2.backward()
+    torch.cuda.synchronize()
+    assert float(loss) == float(loss2)
+    assert torch.equal(g_pix, eng.grads)
+    # the 384-px example PNG the VQ goldens hold: ids identical to the reference vq_model.py's
+    z = FX.load("vq_golden.npz")
+    px = dl.dataset.get_image_tensor("/home/elicer/OSPO/example/step3/negative/layout/1000001/02.png")
+    ids = model.vq_encode(px)
+    assert np.array_equal(ids[0].cpu().numpy(), z["img2_ids"])
+
+
+def test_wrapper_sft_weight_and_logits_metrics_vs_oracle(tmp_path):
+    """algo.sft_weight > 0 (train.py:421-430) and the reference's logits/* logging (mean over all
+    [B, T, V] logits, [B, T-1, V] for chosen with sft) through the wrapper, against the oracle."""
+    from oracle import simpo_ref as O
+    cfg, model, dl, w = make(tmp_path, extra=["algo.sft_weight=0.5"])
+    batch = next(iter(dl))
+    eng = w.engine
+    eng.zero_grad()
+    loss = w.training_step(batch, 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    pre = w.preprocess_batch(batch)
+    d = eng.dims
+    dims = O.JanusDims(n_layers=d.n_layers, d_model=d.d_model, d_ff=d.d_ff, n_heads=d.n_heads, head_dim=d.head_dim,
+                       vocab=d.vocab, img_vocab=d.img_vocab, img_embed=d.img_embed, gen_head_dim=d.gen_head_dim,
+                       lora_r=d.lora_r, lora_alpha=d.lora_alpha)
+    from ospo_amd.engine import synthetic_weights
+    wts = {k: v.cpu() for k, v in synthetic_weights(d, "cuda", seed=0, lora_seed=1).items()}  # get_model's seeds
+    text = [t.to(torch.int32) for t in batch[1]]
+    ref = O.simpo_step(text, pre["chosen_ids"].cpu().long(), pre["rejected_ids"].cpu().long(), wts, dims,
+                       dtype=torch.float32, sft_weight=0.5)
+    lg = w.logged
+    assert abs(float(loss) - float(ref.loss)) / abs(float(ref.loss)) < 2e-3
+    assert lg["train/sft_loss"] == pytest.approx(ref.metrics["sft_loss"], rel=1e-3)
+    for k in ("logits/chosen", "logits/rejected"):
+        assert lg["train/" + k] == pytest.approx(ref.metrics[k], rel=2e-2, abs=2e-4), k
+    g = eng.grad_tensors()
+    errs = [FX.rel_err(g[k].cpu(), v) for k, v in ref.lora_grads.items()]
+    assert max(errs) < 5e-2

@@ -50,7 +50,7 @@ def _run(name, dtype):
     w = FX.step_weights(z, name, dims)
     out = O.simpo_step(text, chosen, rejected, w, dims, dtype=dtype, beta=algo["beta"],
                        gamma_beta_ratio=algo["gamma_beta_ratio"], label_smoothing=algo["label_smoothing"],
-                       loss_type=algo["loss_type"])
+                       loss_type=algo["loss_type"], sft_weight=algo.get("sft_weight", 0.0))
     return out, FX.step_outputs(z)
 
 
@@ -66,6 +66,17 @@ def test_oracle_tiny_fp32_matches_reference():
         key = k.split("/", 1)[1]
         if key in out.metrics:
             assert out.metrics[key] == pytest.approx(v, rel=1e-4, abs=1e-5), k
+
+
+def test_oracle_tiny_sft_fp32_matches_reference():
+    """algo.sft_weight = 0.5: loss = SimPO + 0.5 * CE(chosen logits) (train.py:421-430), the
+    grads through both terms and the logged sft_loss / logits metrics."""
+    out, ref = _run("step_tiny_sft_fp32.npz", torch.float32)
+    torch.testing.assert_close(out.loss, ref["loss"], rtol=1e-5, atol=1e-5)
+    for k, g in ref["grads"].items():
+        assert FX.rel_err(out.lora_grads[k].float(), g) < 1e-4, k
+    for k, v in ref["logged"].items():
+        assert out.metrics[k.split("/", 1)[1]] == pytest.approx(v, rel=1e-4, abs=1e-6), k
 
 
 def test_oracle_tiny_bf16_matches_reference():

@@ -1,6 +1,7 @@
 """Time the attention kernels on the step's shape (S = 8 sequences, T = 600, 32 heads,
 head_dim 128): forward, and backward (dQ + dK/dV, RoPE-fused).  OSPO_ATTN_WAVES=4|8
 selects the workgroup size (read once per process)."""
+import os as _os; _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "ospo_amd", "libospo_hip_ablation.so"))  # A/B knobs: the ablation build
 import json
 import math
 import os

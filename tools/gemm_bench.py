@@ -1,6 +1,7 @@
 """A/B the NT GEMM variants on the SimPO step's exact shapes (M = 2B*T = 4800 rows at 4
 pairs, LoRA K-extension of 64) against torch.matmul (hipBLASLt), interleaved rounds in
 one process (cdna_hip_programming.md rule 24).  Prints one JSON line per shape."""
+import os as _os; _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "ospo_amd", "libospo_hip_ablation.so"))  # A/B knobs: the ablation build
 import json
 import sys
 import os

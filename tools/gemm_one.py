@@ -1,4 +1,5 @@
 """Run one GEMM shape/variant ITERS times (for rocprofv3 PMC collection)."""
+import os as _os; _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "ospo_amd", "libospo_hip_ablation.so"))  # A/B knobs: the ablation build
 import os
 import sys
 

@@ -1,5 +1,6 @@
 """A/B of the decode GEMV schedules (ospo_set_gemv_variant 1 / 2 / 3, GV_VARIANTS) on the 7B decode shapes, R = 32
 rows, interleaved rounds in one process.  Prints GB/s of weight streaming per shape."""
+import os as _os; _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "ospo_amd", "libospo_hip_ablation.so"))  # A/B knobs: the ablation build
 import json
 import os
 import sys

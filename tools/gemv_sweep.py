@@ -1,5 +1,6 @@
 """Sweep the decode GEMV's schedule (v2: 64 rows / v3: 128 rows per workgroup) x K-split count on
 the 7B decode shapes (R = 32), one process, interleaved rounds.  Prints the best per shape."""
+import os as _os; _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "ospo_amd", "libospo_hip_ablation.so"))  # A/B knobs: the ablation build
 import json
 import os
 import sys

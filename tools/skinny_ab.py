@@ -1,5 +1,6 @@
 """A/B of the LoRA skinny products (ospo_set_skinny_variant 1 / 2) on the step's shapes (M = 4800),
 interleaved rounds, both checked against each other and against fp32 torch."""
+import os as _os; _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "ospo_amd", "libospo_hip_ablation.so"))  # A/B knobs: the ablation build
 import json
 import os
 import sys
