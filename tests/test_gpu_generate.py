@@ -14,6 +14,7 @@ import torch
 
 from oracle import generate_ref as G
 from oracle import simpo_ref as O
+from tests.conftest import record_parity
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -94,6 +95,51 @@ def test_attn_cache_matches_masked_eager():
         pr = torch.softmax(torch.matmul(qq, kk.transpose(-1, -2)) * scale, -1, dtype=torch.float32).to(torch.bfloat16)
         rr = torch.matmul(pr, vv).reshape(-1)
         assert relerr(o1[r].cpu().float(), rr.float()) < 8e-3
+
+
+def test_attn_cache_config4_long_cache():
+    """Config 4's decode attention: 16 prompts x (cond, uncond) = 32 rows, 32 heads, a cache of
+    Tmax = 640 keys, left padding up to 30 keys; a 48-query prefill and single decode queries at
+    positions 100, 347 and 623 (the cache length of the last image token is 48 + 575) against
+    masked eager attention (fp32 softmax, bf16 P, as HF 4.38 eager)."""
+    torch.manual_seed(4)
+    R, H, Lp, Tmax = 32, 32, 48, 640
+    start = torch.randint(0, 31, (R,), dtype=torch.int32)
+    start[0] = 0
+    kc = torch.randn(R, H, Tmax, 128, device=DEV).to(torch.bfloat16)
+    vc = torch.randn(R, H, Tmax, 128, device=DEV).to(torch.bfloat16)
+    scale = 1.0 / math.sqrt(128)
+    st = start.to(DEV)
+    q = torch.randn(R * Lp, H * 128, device=DEV).to(torch.bfloat16)
+    out = torch.empty_like(q)
+    ops().attn_cache(q, kc, vc, R, Lp, H, Tmax, st, None, scale, out)
+    qh = q.view(R, Lp, H, 128).transpose(1, 2).float()
+    k, v = kc[:, :, :Lp].float(), vc[:, :, :Lp].float()
+    ok = (torch.ones(Lp, Lp, dtype=torch.bool, device=DEV).tril()[None] &
+          (torch.arange(Lp, device=DEV)[None] >= st[:, None])[:, None, :])
+    s_ = (torch.matmul(qh, k.transpose(-1, -2))).to(torch.bfloat16).float() * scale
+    s_ = s_.masked_fill(~ok[:, None], float("-inf"))
+    p = torch.softmax(s_, -1).to(torch.bfloat16).float()
+    ref = torch.matmul(p, v).transpose(1, 2).reshape(R * Lp, H * 128)
+    valid = (torch.arange(Lp, device=DEV)[None] >= st[:, None]).reshape(-1)
+    e_pre = relerr(out[valid].float(), ref[valid])
+    errs = []
+    for P in (100, 347, Tmax - 17):
+        pos = torch.tensor([P], dtype=torch.int32, device=DEV)
+        q1 = torch.randn(R, H * 128, device=DEV).to(torch.bfloat16)
+        o1 = torch.empty_like(q1)
+        ops().attn_cache(q1, kc, vc, R, 1, H, Tmax, st, pos, scale, o1)
+        keys = torch.arange(P + 1, device=DEV)
+        m = keys[None] >= st[:, None]                                  # [R, P+1]
+        qq = q1.view(R, H, 1, 128).float()
+        sc = torch.matmul(qq, kc[:, :, :P + 1].float().transpose(-1, -2)).to(torch.bfloat16).float() * scale
+        sc = sc.masked_fill(~m[:, None, None], float("-inf"))
+        pr = torch.softmax(sc, -1).to(torch.bfloat16).float()
+        rr = torch.matmul(pr, vc[:, :, :P + 1].float()).reshape(R, H * 128)
+        errs.append(relerr(o1.float(), rr))
+    record_parity("attn_cache_config4", prefill=e_pre, decode=max(errs))
+    print(f"\nattn_cache R32 H32 Tmax640: prefill {e_pre:.2e}, decode {errs}")
+    assert e_pre < 8e-3 and max(errs) < 8e-3
 
 
 def test_kv_store_rope_matches_rope_kernel():
@@ -200,6 +246,40 @@ def test_generate_7b_shapes_two_layers():
     assert float(l1.mean()) <= max(1.5 * float(floor.mean()), 2e-2)
     assert float(l1.max()) <= max(1.5 * float(floor.max()), 2e-2)
     assert torch.equal(gen.generate(prompts, seed=1, use_graph=True).cpu(), tok)
+
+
+def test_generate_config4_576_tokens_16_prompts_small_width():
+    """Config 4's loop at full length: 16 prompts (32 cond/uncond rows), prompts of 20..48 tokens
+    (left padding), 576 image tokens over the 16384-code head, cfg 5, hipGraph decode -- at small
+    width (D 256, 2 layers) so the CPU oracle can follow all 576 steps.  The oracle, teacher-forced
+    on the HIP tokens, reproduces every step's probabilities; every HIP token is the inverse-CDF draw
+    of its probabilities; the graph replay equals the eager loop."""
+    from ospo_amd.engine import ModelDims
+    from ospo_amd.generate import T2IGenerator
+    dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=16384, gen_head_dim=256,
+                       lora_r=16, lora_alpha=32)
+    w = O.init_weights(dims, seed=19, dtype=torch.bfloat16, lora_b_std=1e-2)
+    g = torch.Generator().manual_seed(19)
+    B, n = 16, 576
+    prompts = [torch.randint(8, dims.vocab, (int(torch.randint(20, 49, (1,), generator=g)),), generator=g).tolist()
+               for _ in range(B)]
+    gen = T2IGenerator(ModelDims.from_any(dims), w, device=DEV, max_batch=B, max_prompt_len=48, n_img_tokens=n,
+                       cfg_weight=5.0, temperature=1.0, pad_id=7)
+    tok = gen.generate(prompts, seed=3, use_graph=False, record_probs=True).cpu().clone()
+    probs = gen.probs.cpu().clone()
+    gen.probs = None
+    u = gen.uniforms(3, B)
+    assert torch.equal(gen.generate(prompts, seed=3, use_graph=True).cpu(), tok)
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    _, ref_p = G.generate_ref(prompts, w, dims, n, u, 5.0, 1.0, pad_id=7, forced=tok)
+    l1 = (probs - ref_p).abs().sum(-1)  # [n, B]
+    record_parity("generate_config4_576x16", l1_max=float(l1.max()), l1_mean=float(l1.mean()),
+                  l1_last_step_max=float(l1[-1].max()))
+    print(f"\nT2I 576 tokens x 16 prompts: per-step L1(probs) max {float(l1.max()):.3e} mean {float(l1.mean()):.3e}")
+    assert float(l1.max()) < 2e-2
+    for s in range(0, n, 5):
+        for b in range(B):
+            assert int(tok[b, s]) == G.sample_inverse_cdf(probs[s, b].numpy(), float(u[s, b])), (s, b)
 
 
 @pytest.mark.parametrize("R", [32, 12])
