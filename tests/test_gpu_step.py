@@ -22,10 +22,14 @@ from tests.conftest import record_parity
 pytestmark = pytest.mark.gpu
 
 
-# LoRA-grad relative L2 error vs the fp32 oracle, ~2x what was measured (tests log the measured
-# values to $OSPO_PARITY_LOG; profiles/r02/parity_*.jsonl)
-GRAD_FP32_TOL = {"step_tiny_bf16.npz": 5e-2, "step_1b2l_bf16.npz": 5e-2, "tiny_fp32_ref": 5e-2, "7b_2l": 5e-2,
-                 "r32": 5e-2, "r8": 5e-2}
+# LoRA-grad relative L2 error vs the fp32 oracle: ~2x what was measured on MI355X (the tests log the
+# measured values to $OSPO_PARITY_LOG; profiles/r02/parity_*.jsonl): tiny 1.10e-2, 1B 2-layer 1.92e-2,
+# 7B-shape 2-layer 3.14e-2, r = 32 1.01e-2, r = 8 1.13e-2.  Each test also holds the HIP error to 1.25x
+# the oracle's own bf16-autograd error against fp32 (GRAD_FLOOR_RATIO; measured ratios 0.87-0.97): the
+# fp32-accumulated HIP backward is at least as close to the fp32 gradients as a bf16 autograd is.
+GRAD_FP32_TOL = {"step_tiny_bf16.npz": 2.5e-2, "step_1b2l_bf16.npz": 4e-2, "tiny_fp32_ref": 2.5e-2, "7b_2l": 6.5e-2,
+                 "r32": 2.5e-2, "r8": 2.5e-2}
+GRAD_FLOOR_RATIO = 1.25
 
 
 def pad_text(text):
@@ -97,6 +101,7 @@ def test_step_matches_oracle_and_golden(name):
                   grad_vs_fp32=g32, oracle_bf16_vs_fp32_grad=floor)
     assert max(ge.values()) < 5e-2, sorted(ge.items(), key=lambda kv: -kv[1])[:3]
     assert g32 < GRAD_FP32_TOL[name], (g32, floor)
+    assert g32 < GRAD_FLOOR_RATIO * floor, (g32, floor)
 
 
 def test_step_tiny_matches_fp32_reference():
@@ -159,6 +164,7 @@ def test_step_full_size_7b_shapes_two_layers():
     assert abs(loss - float(ora.loss)) / float(ora.loss) < 2e-3
     assert ge < 5e-2
     assert g32 < GRAD_FP32_TOL["7b_2l"], (g32, floor)
+    assert g32 < GRAD_FLOOR_RATIO * floor, (g32, floor)
 
 
 def test_step_full_depth_7b_30_layers_forward():
@@ -236,10 +242,11 @@ def test_step_lora_rank_variants_vs_oracle(r):
     assert abs(loss - float(ora.loss)) / float(ora.loss) < 2e-3
     ge = max(rel(grads[k], ora.lora_grads[k]) for k in ora.lora_grads)
     g32 = max(rel(grads[k], o32.lora_grads[k]) for k in o32.lora_grads)
-    record_parity(f"step_lora_r{r}", grad_vs_bf16=ge, grad_vs_fp32=g32,
-                  oracle_bf16_vs_fp32_grad=max(rel(ora.lora_grads[k], o32.lora_grads[k]) for k in o32.lora_grads))
+    floor = max(rel(ora.lora_grads[k], o32.lora_grads[k]) for k in o32.lora_grads)
+    record_parity(f"step_lora_r{r}", grad_vs_bf16=ge, grad_vs_fp32=g32, oracle_bf16_vs_fp32_grad=floor)
     assert ge < 5e-2
     assert g32 < GRAD_FP32_TOL[f"r{r}"]
+    assert g32 < GRAD_FLOOR_RATIO * floor, (g32, floor)
 
 
 def test_step_lora_dropout_vs_oracle_with_replayed_masks():
@@ -299,6 +306,8 @@ def _mx8_case(dims, seed, B, Lt, N):
     # because bf16-level differences in a quantizer's input flip ~1/16 of the fp8 roundings they touch
     o32 = O.simpo_step(text, chosen, rejected, w, dims, dtype=torch.float32, mx8=True)
     floor = {k: rel(o32.lora_grads[k], ora.lora_grads[k]) for k in ora.lora_grads}
+    _mx8_case.loss_floor = abs(float(o32.loss) - float(ora.loss)) / float(ora.loss)
+    _mx8_case.el32 = abs(loss - float(o32.loss)) / float(o32.loss)
     ratio = {k: ge[k] / max(floor[k], 5e-2) for k in ge}
     print(f"\nmx8 D{dims.d_model}: logp rel err vs mx8 oracle {e:.2e} (vs bf16 oracle {e_bf:.2e}); "
           f"loss {loss:.6f} vs {float(ora.loss):.6f} ({el:.2e}); max grad rel err {max(ge.values()):.2e}, "
@@ -333,10 +342,17 @@ def test_step_mx8_full_size_7b_shapes_two_layers():
 
 def test_step_mx8_full_size_7b_shapes_lora_r32():
     """Config 5 exactly: MXFP8 frozen Linears with LoRA r = 32 (alpha 64, configs/peft/lora.yaml) at
-    Janus-Pro-7B shapes, 2 layers, 2 pairs."""
+    Janus-Pro-7B shapes, 2 layers, 2 pairs.  Log-probs within 1e-3 (north star; measured 4.0e-4).  The
+    loss: beta = 10 turns a 4e-4 relative log-prob difference (4e-3 absolute at logp ~ -10) into ~4e-2
+    of the margin; measured 8.4e-3 relative against the bf16 fp8 oracle, so held to 1.5e-2 and to
+    the side of the fp32 fp8 oracle no further than twice the oracle's own bf16-vs-fp32 spread
+    (or 1e-2)."""
     dims = O.JanusDims(n_layers=2, lora_r=32, lora_alpha=64)
     logps, loss, e, el, ratio, ora, B = _mx8_case(dims, 43, 2, 24, 576)
-    record_parity("step_mx8_7b_r32", logp=e, loss=el, grad_ratio=max(ratio.values()))
+    record_parity("step_mx8_7b_r32", logp=e, loss=el, loss_vs_fp32=_mx8_case.el32, loss_floor=_mx8_case.loss_floor,
+                  grad_ratio=max(ratio.values()))
     assert e < 1e-3
-    assert el < 3e-3
+    assert abs(float(O.simpo_loss(logps[:B], logps[B:])[0].mean()) - loss) < 1e-5
+    assert el < 1.5e-2
+    assert _mx8_case.el32 < max(1e-2, 2 * _mx8_case.loss_floor)
     assert max(ratio.values()) < 1.5, sorted(ratio.items(), key=lambda kv: -kv[1])[:3]

@@ -139,7 +139,9 @@ def test_pixel_batches_vq_encoded_in_preprocess_match_token_cache(tmp_path):
     loss2.backward()
     torch.cuda.synchronize()
     assert float(loss) == float(loss2)
-    assert torch.equal(g_pix, eng.grads)
+    # same ids -> same step; the LoRA weight gradients sum K-split partials with fp32 atomics, so
+    # only their summation order may differ between the two runs
+    assert float((g_pix - eng.grads).norm() / eng.grads.norm()) < 1e-5
     # the 384-px example PNG the VQ goldens hold: ids identical to the reference vq_model.py's
     z = FX.load("vq_golden.npz")
     px = dl.dataset.get_image_tensor("/home/elicer/OSPO/example/step3/negative/layout/1000001/02.png")
