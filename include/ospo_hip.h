@@ -167,17 +167,19 @@ int ospo_swiglu_bwd(const void* dh, int ld_dh, const void* gu, int ld_gu, void* 
  * (scores * scale, causal mask, fp32 softmax), flash-style on MFMA.
  * q/k/v/o rows s*T+t, head h at column offset h*head_dim.  lse: fp32
  * [S, H, T] (natural-log sum-exp of the scaled scores).  head_dim == 128.
- * bwd needs the workspace delta fp32 [S*H*T]; dq_acc_ws is reserved (ignored,
- * may be NULL -- dQ is accumulated in registers, no atomics).  dq/dk/dv are
- * written (bf16) into dqkv.  With rope_cos/rope_sin (bf16 [T][head_dim/2], the
+ * bwd needs the workspace delta fp32 [S*H*T] and, for the 5-product form, ds_ws
+ * (ospo_flash_attn_bwd_ws_bytes: bf16 dS^T per (sequence, head), written by the dK/dV
+ * kernel and read by dQ = dS.K; NULL = the 7-product form that recomputes S and dP for
+ * dQ).  No atomics.  dq/dk/dv are written (bf16) into dqkv.  With rope_cos/rope_sin (bf16 [T][head_dim/2], the
  * ospo_rope_* tables) the RoPE backward is applied to dq and dk before the store
  * (q/k in qkv are then the post-RoPE values); NULL for plain attention. */
 int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
                         int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
                         hipStream_t stream);
+size_t ospo_flash_attn_bwd_ws_bytes(int S, int T, int n_heads);
 int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col,
                         const void* o, int ld_o, const void* dout, int ld_do, const float* lse,
-                        float* delta_ws, float* dq_acc_ws, void* dqkv, int ld_dqkv, int S, int T,
+                        float* delta_ws, void* ds_ws, void* dqkv, int ld_dqkv, int S, int T,
                         int n_heads, int head_dim, float scale, const void* rope_cos,
                         const void* rope_sin, hipStream_t stream);
 

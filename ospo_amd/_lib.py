@@ -44,6 +44,7 @@ SIGNATURES = {
     "ospo_swiglu_bwd": [P, I, P, I, P, I, I, I, P],
     "ospo_flash_attn_fwd": [P, I, I, I, I, P, I, P, I, I, I, I, F, P],
     "ospo_flash_attn_bwd": [P, I, I, I, I, P, I, P, I, P, P, P, P, I, I, I, I, I, F, P, P, P],
+    "ospo_flash_attn_bwd_ws_bytes": [I, I, I],
     "ospo_assemble_inputs": [P, I, I, P, I, P, I, I, P, P],
     "ospo_gen_aligner_in": [P, I, P, I, I, P, P, I, P, P],
     "ospo_gather_rows": [P, I, I, I, I, I, I, P, P],
@@ -84,7 +85,7 @@ SIGNATURES = {
 ABLATION_SIGNATURES = {"ospo_set_gemm_variant": [I], "ospo_set_gemv_variant": [I], "ospo_set_gemv_splits": [I],
                        "ospo_set_skinny_variant": [I]}
 
-RESTYPES = {"ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
+RESTYPES = {"ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 

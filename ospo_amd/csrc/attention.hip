@@ -334,7 +334,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                             int ldg, int T, int H, float scale,
-                                                            const bf16* __restrict__ rcs, const bf16* __restrict__ rsn) {
+                                                            const bf16* __restrict__ rcs, const bf16* __restrict__ rsn,
+                                                            bf16* __restrict__ dsT, int ds_ld) {
   // LDS: [Q | dO] x 2 buffers, then lse[2][64], delta[2][64]
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES + 4 * 64 * 4];
   float* Lsb = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
@@ -366,6 +367,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
   const bf16* obase = dout + rowbase * ldd + h * HD;
   const float* lse_sh = lse + ((long)s * H + h) * T;
   const float* del_sh = delta + ((long)s * H + h) * T;
+  // dS^T of this (sequence, head): [keys][queries], ds_ld columns per key row (dsT == nullptr: not kept)
+  bf16* dsrow = dsT ? dsT + ((long)s * H + h) * ds_ld * (long)ds_ld + (long)key_l * ds_ld : nullptr;
 
   auto stage = [&](int qt, int b) {
     char* Qs = smem + b * 2 * TILE_BYTES;
@@ -432,6 +435,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
         sv[a][j + 1] = py;
         dp[a][j] = px * (dp[a][j] - dq4[j]) * scale;
         dp[a][j + 1] = py * (dp[a][j + 1] - dq4[j + 1]) * scale;
+      }
+      if (dsrow) {  // dS^T[key][q .. q+3] in bf16, the values the dK product below rounds to (8 B per lane)
+        uint2 pk;
+        pk.x = pack2(dp[a][0], dp[a][1]);
+        pk.y = pack2(dp[a][2], dp[a][3]);
+        *reinterpret_cast<uint2*>(dsrow + qt * QB + 16 * a + 4 * g) = pk;
       }
     }
     // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . (scale dS)[q][key]
@@ -617,6 +626,135 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
   }
 }
 
+
+// delta[s, h, t] = rowsum(dO * O) over the head's 128 columns (fp32): the softmax-backward term the
+// dK/dV kernel reads.  One workgroup per row s*T + t; 16 lanes per head, 8 columns (16 B) per lane.
+__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16* __restrict__ dout, int ldd,
+                                                             const bf16* __restrict__ o, int ldo,
+                                                             float* __restrict__ delta, int T, int H) {
+  const long row = blockIdx.x;
+  const int s = (int)(row / T), t = (int)(row % T);
+  for (int c = threadIdx.x; c < H * 16; c += 256) {
+    const int h = c >> 4;
+    const u32x4 a = *reinterpret_cast<const u32x4*>(dout + row * ldd + c * 8);
+    const u32x4 b = *reinterpret_cast<const u32x4*>(o + row * ldo + c * 8);
+    float fa[8], fb[8];
+    unpack8(a, fa);
+    unpack8(b, fb);
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += fa[i] * fb[i];
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 16);
+    if ((c & 15) == 0) delta[((long)s * H + h) * T + t] = v;
+  }
+}
+
+// wait for 2 transposed fragments (4 reads): registers tied to the wait
+__device__ __forceinline__ void trp_wait2(i16x4 (&lo)[2], i16x4 (&hi)[2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[0]), "+v"(lo[1]), "+v"(hi[0]), "+v"(hi[1])::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// transposed fragment, natural k order (element j <- row kbase + 8g + j), asm form (see trp_issue)
+__device__ __forceinline__ void trn_issue(const char* lds, int kbase, int c0, int lane, i16x4& lo, i16x4& hi) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int r1 = kbase + 8 * g + q;
+  const int r2 = r1 + 4;
+  const int x = (c0 >> 3) + (p >> 1);
+  const int hh = (p & 1) << 3;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(lds_u32(lds + r1 * ROWB + ((x ^ aswz(r1)) << 4) + hh)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(lds_u32(lds + r2 * ROWB + ((x ^ aswz(r2)) << 4) + hh)));
+}
+
+// dQ = dS . K from the dS^T the dK/dV kernel stored: workgroup = NW waves x 32 query rows of one
+// (sequence, head); per 64-key tile the K tile [key][d] and the dS^T tile [key][128 queries] are
+// staged in LDS (LDS-DMA, double-buffered) and both MFMA operands come from transposed reads:
+// dQ^T[d][q] += K^T[d][key] . dS^T[key][q], each K^T fragment feeding the wave's two query
+// sub-tiles.  One product instead of the three (S, dP, dQ) of attn_bwd_dq_kernel.  Causal masking
+// is already in dS (zeros).  RoPE backward fused into the store.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ds_kernel(const bf16* __restrict__ qkv, int ldq, int qc,
+                                                             int kc, const bf16* __restrict__ dsT, int ds_ld,
+                                                             bf16* __restrict__ dqkv, int ldg, int T, int H,
+                                                             const bf16* __restrict__ rcs,
+                                                             const bf16* __restrict__ rsn) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // [K | dS^T] x 2 buffers
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int RB = 32 * NW;  // query rows per workgroup
+  const int qb = gridDim.z - 1 - blockIdx.z;  // longest sweeps first, chip-wide
+  const int h = blockIdx.x, s = blockIdx.y;
+  const int g = lane >> 4, l16 = lane & 15;
+  const long rowbase = (long)s * T;
+  const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
+  const bf16* dbase = dsT + ((long)s * H + h) * ds_ld * (long)ds_ld;
+
+  f32x4 dq[2][8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dq[a][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int last = (qb * RB + RB - 1 < T ? qb * RB + RB - 1 : T - 1);
+  const int n_kv = last / KB + 1;
+  auto stage = [&](int kt, int b) {
+    char* Ks = smem + b * 2 * TILE_BYTES;
+    stage64<NW>(kbase, ldq, kt * KB, T, 0, Ks, wave, lane);
+    stage64<NW>(dbase, ds_ld, kt * KB, ds_ld, qb * RB, Ks + TILE_BYTES, wave, lane);
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < n_kv; ++kt) {
+    const int b = kt & 1;
+    if (kt + 1 < n_kv) stage(kt + 1, b ^ 1);
+    const char* Ks = smem + b * 2 * TILE_BYTES;
+    const char* Ds = Ks + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      i16x4 blo[2], bhi[2];
+      trn_issue(Ds, 32 * ks, wave * 32, lane, blo[0], bhi[0]);
+      trn_issue(Ds, 32 * ks, wave * 32 + 16, lane, blo[1], bhi[1]);
+      trp_wait2(blo, bhi);
+      const bf16x8 b0 = trp_join(blo[0], bhi[0]), b1 = trp_join(blo[1], bhi[1]);
+#pragma unroll
+      for (int d0 = 0; d0 < 8; d0 += 4) {
+        i16x4 lo[4], hi[4];
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) trn_issue(Ks, 32 * ks, 16 * (d0 + dd), lane, lo[dd], hi[dd]);
+        trp_wait4(lo, hi);
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+          const bf16x8 a = trp_join(lo[dd], hi[dd]);
+          dq[0][d0 + dd] = MFMA(a, b0, dq[0][d0 + dd]);
+          dq[1][d0 + dd] = MFMA(a, b1, dq[1][d0 + dd]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // lane holds [d = 16dt + 4g + j][q = l16] of query sub-tile a
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int qrow = qb * RB + wave * 32 + 16 * a + l16;
+    if (qrow < T) {
+      if (rcs) rope_bwd_acc(dq[a], rcs, rsn, qrow, g);
+      bf16* dp = dqkv + (rowbase + qrow) * ldg + qc + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        uint2 pk;
+        pk.x = pack2(dq[a][dt][0], dq[a][dt][1]);
+        pk.y = pack2(dq[a][dt][2], dq[a][dt][3]);
+        *reinterpret_cast<uint2*>(dp + 16 * dt + 4 * g) = pk;
+      }
+    }
+  }
+}
+
+// dS^T rows / columns per (sequence, head): T rounded up to the dQ kernel's 128-query blocks
+int ds_pitch(int T) { return (T + 127) / 128 * 128; }
+
 // waves per workgroup (16 query rows / keys each): 8 shares every staged K/V (Q/dO)
 // tile between twice the rows; the ablation build's OSPO_ATTN_WAVES=4 selects the 64-row form (A/B)
 int attn_waves() {
@@ -655,28 +793,28 @@ extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k
   return OSPO_OK;
 }
 
+extern "C" size_t ospo_flash_attn_bwd_ws_bytes(int S, int T, int n_heads) {
+  if (S <= 0 || T <= 0 || n_heads <= 0) return 0;
+  const long p = ds_pitch(T);
+  return (size_t)S * n_heads * p * p * sizeof(bf16);
+}
+
 extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, const void* o,
                                    int ld_o, const void* dout, int ld_do, const float* lse, float* delta_ws,
-                                   float* dq_acc_ws, void* dqkv, int ld_dqkv, int S, int T, int n_heads,
+                                   void* ds_ws, void* dqkv, int ld_dqkv, int S, int T, int n_heads,
                                    int head_dim, float scale, const void* rope_cos, const void* rope_sin,
                                    hipStream_t stream) {
-  (void)dq_acc_ws;  // reserved (ABI v1 atomic-dQ workspace); may be NULL
   if (!qkv || !o || !dout || !lse || !delta_ws || !dqkv) return OSPO_ERR_ARG;
   if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
   if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || ld_do % 8 || ld_dqkv % 8) return OSPO_ERR_SHAPE;
   if (q_col % 8 || k_col % 8 || v_col % 8) return OSPO_ERR_SHAPE;
   if (!aligned16(qkv) || !aligned16(o) || !aligned16(dout) || !aligned16(dqkv)) return OSPO_ERR_ALIGN;
+  if (ds_ws && !aligned16(ds_ws)) return OSPO_ERR_ALIGN;
   if ((rope_cos == nullptr) != (rope_sin == nullptr)) return OSPO_ERR_ARG;
   if (rope_cos && (((uintptr_t)rope_cos & 7) || ((uintptr_t)rope_sin & 7))) return OSPO_ERR_ALIGN;
   const bf16* rc = (const bf16*)rope_cos;
   const bf16* rs = (const bf16*)rope_sin;
-  // dQ first: it also produces delta = rowsum(dO * O) for the dK/dV kernel
   const int nw = attn_waves();
-  dim3 gq(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
-  hipLaunchKernelGGL(nw == 8 ? attn_bwd_dq_kernel<8> : attn_bwd_dq_kernel<4>, gq, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
-                     (const bf16*)dout, ld_do, (const bf16*)o, ld_o, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads,
-                     scale, rc, rs);
-  OSPO_CHECK_LAUNCH();
   dim3 grid(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
 #ifdef OSPO_ABLATION
   static const int dkdv_dbg = [] {  // ablation only (results invalid): tools/attn_bench.py
@@ -691,8 +829,31 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
 #else
   auto dkdv = attn_bwd_dkdv_kernel<8>;
 #endif
+  if (ds_ws && nw == 8) {
+    // delta, then dK/dV (which also stores dS^T), then dQ = dS . K: 5 MFMA products instead of 7
+    const int p = ds_pitch(T);
+    hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(S * T), dim3(256), 0, stream, (const bf16*)dout, ld_do,
+                       (const bf16*)o, ld_o, delta_ws, T, n_heads);
+    OSPO_CHECK_LAUNCH();
+    hipLaunchKernelGGL(dkdv, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+                       (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
+                       (bf16*)ds_ws, p);
+    OSPO_CHECK_LAUNCH();
+    dim3 gq(n_heads, S, (T + 127) / 128);
+    hipLaunchKernelGGL(attn_bwd_dq_ds_kernel<4>, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+                       (const bf16*)ds_ws, p, (bf16*)dqkv, ld_dqkv, T, n_heads, rc, rs);
+    OSPO_CHECK_LAUNCH();
+    return OSPO_OK;
+  }
+  // no dS workspace: dQ first (it also produces delta = rowsum(dO * O)), recomputing S and dP
+  dim3 gq(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
+  hipLaunchKernelGGL(nw == 8 ? attn_bwd_dq_kernel<8> : attn_bwd_dq_kernel<4>, gq, dim3(64 * nw), 0, stream,
+                     (const bf16*)qkv, ld_qkv, q_col, k_col, v_col, (const bf16*)dout, ld_do, (const bf16*)o, ld_o,
+                     lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
+  OSPO_CHECK_LAUNCH();
   hipLaunchKernelGGL(dkdv, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
-                     v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs);
+                     v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
+                     (bf16*)nullptr, 0);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

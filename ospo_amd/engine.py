@@ -219,6 +219,9 @@ class SimPOEngine:
         self.dattn = z(Mc, D)
         self.dh = None if self.fuse_swiglu_bwd else z(Mc, Fd)
         self.delta_ws = z(S * H * Tm, dt=F32)
+        # dS^T of one layer's attention backward (bf16, ~210 MB at 8 sequences x T = 600): the dK/dV kernel
+        # writes it, dQ = dS.K reads it, so S and dP are not recomputed for dQ (5 MFMA products, not 7)
+        self.ds_ws = ops.flash_attn_bwd_ws(S, Tm, H, dev)
         self.dz = z(R, Dg)
         self.dhsel = z(R, D)
         # MXFP8 activation operands, one per contraction size (main-stream GEMMs only, reused in order)
@@ -499,7 +502,7 @@ class SimPOEngine:
             lora_grads_async("o", q, gs, a["attn"], dxmid, a["u_o"], gbase, dr)
             # ---- attention + RoPE
             guard("qkv", q)  # dqkv / g copy q
-            ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, None,
+            ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, self.ds_ws,
                                dqkv, S, T, H, hd, scale_attn, rope_cos=self.cos, rope_sin=self.sin)
             # ---- q/k/v
             Acat, AcatT, Bcat, BT = pk["qkv"]

@@ -346,11 +346,24 @@ def flash_attn_fwd(qkv, q_col, k_col, v_col, o, lse, S, T, n_heads, head_dim, sc
     return o, lse
 
 
-def flash_attn_bwd(qkv, q_col, k_col, v_col, o, dout, lse, delta_ws, dq_ws, dqkv, S, T, n_heads, head_dim, scale,
+def flash_attn_bwd_ws_bytes(S: int, T: int, n_heads: int) -> int:
+    return int(query("ospo_flash_attn_bwd_ws_bytes", S, T, n_heads))
+
+
+def flash_attn_bwd_ws(S: int, T: int, n_heads: int, device) -> torch.Tensor:
+    """The bf16 dS^T workspace of the 5-product backward (zeroed once; see ospo_flash_attn_bwd)."""
+    return torch.zeros(flash_attn_bwd_ws_bytes(S, T, n_heads) // 2, dtype=BF16, device=device)
+
+
+def flash_attn_bwd(qkv, q_col, k_col, v_col, o, dout, lse, delta_ws, ds_ws, dqkv, S, T, n_heads, head_dim, scale,
                    rope_cos=None, rope_sin=None):
-    """Attention backward; with rope_cos/rope_sin the RoPE backward is fused into the dq/dk stores."""
+    """Attention backward; with rope_cos/rope_sin the RoPE backward is fused into the dq/dk stores.
+    ds_ws (flash_attn_bwd_ws): dK/dV store dS^T and dQ = dS.K reads it (5 MFMA products); None: the
+    dQ kernel recomputes S and dP (7 products)."""
+    if ds_ws is not None and ds_ws.numel() * 2 < flash_attn_bwd_ws_bytes(S, T, n_heads):
+        raise ValueError("flash_attn_bwd: dS workspace too small")
     call("ospo_flash_attn_bwd", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(dout), _ld(dout),
-         _p(lse), _p(delta_ws), _p(dq_ws), _p(dqkv), _ld(dqkv), S, T, n_heads, head_dim, float(scale),
+         _p(lse), _p(delta_ws), _p(ds_ws), _p(dqkv), _ld(dqkv), S, T, n_heads, head_dim, float(scale),
          _p(rope_cos), _p(rope_sin), _s())
     return dqkv
 

@@ -246,8 +246,9 @@ def attn_ref(q, k, v, scale):
     return torch.softmax(s, -1) @ v
 
 
-@pytest.mark.parametrize("S,T,H", [(2, 72, 2), (1, 64, 1), (2, 600, 2), (1, 130, 3)])
-def test_flash_attention(S, T, H):
+@pytest.mark.parametrize("ws", [True, False], ids=["ds5", "recompute7"])
+@pytest.mark.parametrize("S,T,H", [(2, 72, 2), (1, 64, 1), (2, 600, 2), (1, 130, 3), (1, 520, 2)])
+def test_flash_attention(S, T, H, ws):
     hd = 128
     D = H * hd
     rows = S * T + 7
@@ -268,15 +269,19 @@ def test_flash_attention(S, T, H):
     ref.backward(do[: S * T].float().view(S, T, H, hd).transpose(1, 2))
     dqkv = torch.zeros(rows, 3 * D, device=DEV, dtype=torch.bfloat16)
     delta = torch.empty(S * H * T, device=DEV)
-    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, dqkv, S, T, H, hd, scale)
+    dsw = ops().flash_attn_bwd_ws(S, T, H, DEV) if ws else None
+    if dsw is not None:
+        dsw.fill_(float("nan"))  # dQ must not read any dS^T entry the dK/dV kernel did not write
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, dsw, dqkv, S, T, H, hd, scale)
     g = qf.grad.permute(1, 3, 0, 2, 4).reshape(S * T, 3 * D)
     for i, nm in enumerate("qkv"):
         e = relerr(dqkv[: S * T, i * D:(i + 1) * D].float(), g[:, i * D:(i + 1) * D])
         assert e < 2e-2, (nm, e)
 
 
+@pytest.mark.parametrize("ws", [True, False], ids=["ds5", "recompute7"])
 @pytest.mark.parametrize("S,T,H", [(2, 130, 2), (1, 600, 1)])
-def test_flash_attention_bwd_fused_rope(S, T, H):
+def test_flash_attention_bwd_fused_rope(S, T, H, ws):
     """dq/dk with the RoPE backward fused into the stores == the unfused chain
     (attention bwd, then ospo_rope_bwd), and both track fp32 autograd through
     rope -> attention w.r.t. the PRE-RoPE q, k."""
@@ -294,10 +299,11 @@ def test_flash_attention_bwd_fused_rope(S, T, H):
     do = rnd(rows, D)
     delta = torch.empty(S * H * T, device=DEV)
     fused = torch.zeros(rows, 3 * D, device=DEV, dtype=torch.bfloat16)
-    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, fused, S, T, H, hd, scale,
+    dsw = ops().flash_attn_bwd_ws(S, T, H, DEV) if ws else None
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, dsw, fused, S, T, H, hd, scale,
                          rope_cos=cos, rope_sin=sin)
     plain = torch.zeros(rows, 3 * D, device=DEV, dtype=torch.bfloat16)
-    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, plain, S, T, H, hd, scale)
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, dsw, plain, S, T, H, hd, scale)
     ops().rope(plain, 0, D, S, T, H, hd, cos, sin, backward=True)
     assert relerr(fused[: S * T].float(), plain[: S * T].float()) < 8e-3
     assert torch.equal(fused[: S * T, 2 * D:], plain[: S * T, 2 * D:])  # dv untouched by RoPE
@@ -602,3 +608,28 @@ def test_gemm_swiglu_bwd_fused_equals_two_launches(M, F, K, K2, p, split):
     sg = torch.sigmoid(g)
     ref32 = torch.cat([bf(d * u).float() * sg * (1 + g * (1 - sg)), d * bf(g * sg).float()], 1)
     assert relerr(out.float(), ref32) < 1e-2
+
+
+@pytest.mark.parametrize("S,T,H", [(2, 600, 4), (1, 200, 2)])
+def test_flash_attention_bwd_5_product_form_equals_7(S, T, H):
+    """The 5-product backward (dK/dV store dS^T, dQ = dS.K) against the 7-product one (dQ recomputes S
+    and dP): dV is bit-identical (same kernel, same operands); dK and dQ differ only by the fp32
+    summation order of delta and of the S / dP recompute."""
+    hd = 128
+    D = H * hd
+    rows = S * T
+    qkv = rnd(rows, 3 * D)
+    o = torch.zeros(rows, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(S * H * T, device=DEV)
+    scale = 1 / math.sqrt(hd)
+    ops().flash_attn_fwd(qkv, 0, D, 2 * D, o, lse, S, T, H, hd, scale)
+    do = rnd(rows, D)
+    delta = torch.empty(S * H * T, device=DEV)
+    a = torch.zeros(rows, 3 * D, device=DEV, dtype=torch.bfloat16)
+    b = torch.zeros_like(a)
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, ops().flash_attn_bwd_ws(S, T, H, DEV), a, S, T, H, hd,
+                         scale)
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, b, S, T, H, hd, scale)
+    assert torch.equal(a[:, 2 * D:], b[:, 2 * D:])
+    for i in range(2):
+        assert relerr(a[:, i * D:(i + 1) * D].float(), b[:, i * D:(i + 1) * D].float()) < 4e-3

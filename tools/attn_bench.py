@@ -40,9 +40,14 @@ def main():
     f = timeit(lambda: ops.flash_attn_fwd(qkv, 0, D, 2 * D, o, lse, S, T, H, hd, sc))
     b = timeit(lambda: ops.flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, dqkv, S, T, H, hd, sc,
                                           rope_cos=cos, rope_sin=sin))
-    fl = 4 * S * H * hd * T * (T + 1) / 2
-    print(json.dumps({"waves": os.environ.get("OSPO_ATTN_WAVES", "8"), "fwd_us": round(f, 1), "bwd_us": round(b, 1),
-                      "fwd_tflops": round(fl / f / 1e6, 1), "bwd_tflops(7 products)": round(3.5 * fl / b / 1e6, 1)}))
+    ws = ops.flash_attn_bwd_ws(S, T, H, "cuda")
+    b5 = timeit(lambda: ops.flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, ws, dqkv, S, T, H, hd, sc,
+                                           rope_cos=cos, rope_sin=sin))
+    fl = 4 * S * H * hd * T * (T + 1) / 2  # QK^T + PV, causal: the algorithmic forward
+    print(json.dumps({"waves": os.environ.get("OSPO_ATTN_WAVES", "8"), "fwd_us": round(f, 1),
+                      "bwd7_us": round(b, 1), "bwd5_us": round(b5, 1), "fwd_tflops": round(fl / f / 1e6, 1),
+                      "bwd7_alg_tflops": round(2 * fl / b / 1e6, 1), "bwd5_alg_tflops": round(2 * fl / b5 / 1e6, 1),
+                      "bwd5_frac_of_2500": round(2 * fl / b5 / 1e6 / 2500, 4)}))
 
 
 if __name__ == "__main__":
