@@ -125,25 +125,36 @@ def bench_t2i(args):
     (32 cond/uncond rows), hipGraph-captured decode.  One 'step' = one generate() call."""
     from ospo_amd.engine import JANUS_PRO_7B, synthetic_weights
     from ospo_amd.generate import T2IGenerator
+    from ospo_amd.vq import synthetic_vq_decoder_weights, synthetic_vq_weights
     dev = torch.device("cuda", 0)
     dims = JANUS_PRO_7B.__class__(**{**JANUS_PRO_7B.__dict__, "n_layers": args.layers})
     B, N, Lp = args.t2i_batch, args.img_tokens, args.t2i_prompt_len
     w = synthetic_weights(dims, dev, seed=0, lora_seed=1)
+    vw = {**synthetic_vq_weights(0), **synthetic_vq_decoder_weights(1)}  # gen_vision_model (pixel decoder)
     gen = T2IGenerator(dims, w, device=dev, max_batch=B, max_prompt_len=Lp, n_img_tokens=N, cfg_weight=5.0,
-                       temperature=1.0)
+                       temperature=1.0, vq_weights=vw)
     del w
     torch.cuda.empty_cache()
     g = torch.Generator().manual_seed(0)
     prompts = [torch.randint(0, dims.vocab, (int(torch.randint(Lp // 2, Lp + 1, (1,), generator=g)),),
                              generator=g).tolist() for _ in range(B)]
+    # a step = generate_image (image_generation.py:109-181) up to the saved pixels: 576 sampled tokens per
+    # image, decode_code, the uint8 conversion
     for i in range(args.warmup):
-        gen.generate(prompts, seed=i)
+        gen.generate_images(prompts, seed=i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        tok = gen.generate(prompts, seed=100 + i)
+        imgs = gen.generate_images(prompts, seed=100 + i)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    tok = gen.tokens[:B]
+    d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    d0.record()
+    gen.vq_decoder.to_images(gen.vq_decoder.decode_code(tok, 24, 24))
+    d1.record()
+    torch.cuda.synchronize()
+    decode_ms = d0.elapsed_time(d1)
     # decode-step roofline: graph replays of one step timed with HIP events on the replay stream
     R = 2 * B
     gen.pos.fill_(Lp + N // 2)
@@ -161,18 +172,21 @@ def bench_t2i(args):
     achieved = nbytes / (step_ms * 1e-3) / 1e9
     value = B * args.steps / dt
     line = {
-        "metric": "images/sec, Janus-Pro-7B step-3 T2I sampling (576 tokens, cfg 5, parallel_size 16)",
+        "metric": "images/sec, Janus-Pro-7B step-3 T2I generation (576 tokens, cfg 5, parallel_size 16, VQ decode)",
         "value": round(value, 3), "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init Janus-Pro-7B weights, random prompt ids)",
-        "config": {"workload": f"Janus-Pro-{'7B' if dims.n_layers == 30 else str(dims.n_layers) + 'L'} T2I sampling, "
-                               f"{B} prompts x (cond, uncond), {N} image tokens, hipGraph decode step",
-                   "prompt_len_max": Lp, "decode_steps": N - 1, "tokens_per_s": round(value * N, 1)},
+        "config": {"workload": f"Janus-Pro-{'7B' if dims.n_layers == 30 else str(dims.n_layers) + 'L'} T2I generation, "
+                               f"{B} prompts x (cond, uncond), {N} image tokens, hipGraph decode step, "
+                               "VQ-16 pixel decode to uint8 384x384",
+                   "prompt_len_max": Lp, "decode_steps": N - 1, "tokens_per_s": round(value * N, 1),
+                   "vq_decode_ms_per_batch": round(decode_ms, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                      "frac": round(achieved / 8000.0, 4), "traffic": None,
                      "kernel": "decode step (hipGraph: 30 x (4 decode_gemv + attn_cache + norms) + gen_head + sampler)",
                      "algorithmic_bytes_per_step": round(nbytes), "avg_step_us": round(step_ms * 1e3, 1)},
         "tokens_checksum": int(tok.long().sum().item()),
+        "pixels_checksum": int(imgs.long().sum().item()),
     }
     print(json.dumps(line), flush=True)
 

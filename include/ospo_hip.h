@@ -356,6 +356,16 @@ int ospo_vq_transpose(const float* x, int B, int R, int C, float* out, hipStream
 int ospo_vq_l2norm_rows(const float* x, long n, int d, float* out, hipStream_t stream);
 int ospo_vq_quantize(const float* z, long n, int e_dim, const float* codebook_l2, int n_codes, int* ids,
                      float* dmin, hipStream_t stream);
+/* Pixel decoder of step-3 sampling (image_generation.py:174-181: decode_code, vq_model.py:505-508):
+ * ospo_vq_embed_codes: out[v][0..e) = codebook_l2[ids[v]] (get_codebook_entry :284-298, NHWC);
+ * ospo_vq_conv2d_up2: ospo_vq_conv2d (stride 1, symmetric pad) of the nearest-neighbour 2x
+ *   upsampling of x (Upsample :411-427), read on the fly: output [B][2H+2pad-KH+1][2W+2pad-KW+1][Cout];
+ * ospo_vq_to_uint8: out[i] = (uint8) clip((x[i] + 1) / 2 * 255, 0, 255) (fp32, truncation). */
+int ospo_vq_embed_codes(const int* ids, long n, const float* codebook_l2, int n_codes, int e_dim, float* out,
+                        hipStream_t stream);
+int ospo_vq_conv2d_up2(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int KH, int KW,
+                       int pad, const float* bias, const float* residual, float* out, hipStream_t stream);
+int ospo_vq_to_uint8(const float* x, long n, unsigned char* out, hipStream_t stream);
 
 /* ------------------------------------------------------------ optimizer ---
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip

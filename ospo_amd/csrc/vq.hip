@@ -1,6 +1,8 @@
 // VQ image tokenizer (encoder + quantizer) of Janus-Pro's gen_vision_model on gfx950 (SURVEY §8f
 // rank 3): janus/models/vq_model.py Encoder (:46-124) -> quant_conv -> VectorQuantizer (:236-282),
-// the step before the SimPO path (ospo/wrapper/train.py:246-264 encodes every image of a batch).
+// the step before the SimPO path (ospo/wrapper/train.py:246-264 encodes every image of a batch);
+// and its pixel decoder (decode_code :505-508: codebook rows -> post_quant_conv -> Decoder :127-214,
+// the Upsample's nearest 2x read on the fly by the convolution) for step-3 sampling.
 //
 // fp32 end to end: the ids must be bit-exact, and bf16 moves ~10 % of them.
 //  * Convolutions are implicit GEMMs on v_mfma_f32_32x32x2_f32 (f32 in / f32 accumulate, exact
@@ -30,6 +32,7 @@ struct ConvArgs {
   float* out;        // [B][Ho][Wo][Cout]
   int B, H, W, Cin, Cout, KH, KW, stride, pad_t, pad_l, Ho, Wo;
   long x_bstride, w_bstride, o_bstride;  // per-image strides of x / w / out when w is per image (attention)
+  int up;  // 1: the input is read as its nearest-neighbour 2x upsampling (2H x 2W), Decoder's Upsample
 };
 
 // grid: (ceil(npix / 128), ceil(Cout / 64), nz); 256 threads; wave w: pixels 32w..32w+31 x 64 channels.
@@ -69,8 +72,9 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a, int per
     const int ky = kk / a.KW, kx = kk % a.KW;
     const int ci0 = cc * CV_BK;
     const int iy = oy * a.stride - a.pad_t + ky, ix = ox * a.stride - a.pad_l + kx;
-    const bool in = pvalid && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-    const float* src = xbase + (((long)ib * a.H + (in ? iy : 0)) * a.W + (in ? ix : 0)) * a.Cin + ci0 + lc;
+    const bool in = pvalid && iy >= 0 && iy < (a.H << a.up) && ix >= 0 && ix < (a.W << a.up);
+    const float* src = xbase + (((long)ib * a.H + (in ? iy >> a.up : 0)) * a.W + (in ? ix >> a.up : 0)) * a.Cin +
+                       ci0 + lc;
     if (in && vec && ci0 + lc + 16 <= a.Cin) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -354,6 +358,24 @@ __global__ void l2norm_rows_kernel(const float* __restrict__ x, long n, int d, f
   for (int q = 0; q < d; ++q) y[i * d + q] = x[i * d + q] * inv;
 }
 
+// decode_code's get_codebook_entry (vq_model.py:284-298): rows of the l2-normalised codebook, NHWC
+__global__ void vq_embed_codes_kernel(const int* __restrict__ ids, long n, const float* __restrict__ cb,
+                                      int n_codes, int e, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * e) return;
+  int id = ids[i / e];
+  id = id < 0 ? 0 : (id >= n_codes ? n_codes - 1 : id);
+  out[i] = cb[(long)id * e + i % e];
+}
+
+// image_generation.py:175-181: clip((x + 1) / 2 * 255, 0, 255) in fp32, stored as uint8 (truncation)
+__global__ void vq_to_uint8_kernel(const float* __restrict__ x, long n, unsigned char* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = fminf(fmaxf((x[i] + 1.f) / 2.f * 255.f, 0.f), 255.f);
+  out[i] = (unsigned char)v;
+}
+
 }  // namespace
 
 extern "C" int ospo_vq_conv2d(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int KH, int KW,
@@ -375,6 +397,40 @@ extern "C" int ospo_vq_conv2d(const float* x, int B, int H, int W, int Cin, cons
 
 // out[b][i][j] = sum_c x[b][i][c] * w[b][j][c] (+ residual): a per-image "1x1 convolution" whose weight is
 // another activation (AttnBlock's q.k^T and p.v^T); grid z = image.
+extern "C" int ospo_vq_conv2d_up2(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int KH,
+                                  int KW, int pad, const float* bias, const float* residual, float* out,
+                                  hipStream_t stream) {
+  if (!x || !w || !out) return OSPO_ERR_ARG;
+  if (B <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || KH <= 0 || KW <= 0 || pad < 0) return OSPO_ERR_SHAPE;
+  const int Ho = 2 * H + 2 * pad - KH + 1, Wo = 2 * W + 2 * pad - KW + 1;
+  if (Ho <= 0 || Wo <= 0) return OSPO_ERR_SHAPE;
+  ConvArgs a{x, w, bias, residual, out, B, H, W, Cin, Cout, KH, KW, 1, pad, pad, Ho, Wo, 0, 0, 0, 1};
+  const long npix = (long)B * Ho * Wo;
+  hipLaunchKernelGGL(conv_f32_kernel, dim3((unsigned)((npix + CV_BM - 1) / CV_BM), (Cout + CV_BN - 1) / CV_BN),
+                     dim3(256), 0, stream, a, 0);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_vq_embed_codes(const int* ids, long n, const float* codebook_l2, int n_codes, int e_dim,
+                                   float* out, hipStream_t stream) {
+  if (!ids || !codebook_l2 || !out) return OSPO_ERR_ARG;
+  if (n <= 0 || n_codes <= 0 || e_dim <= 0) return OSPO_ERR_SHAPE;
+  const long tot = n * e_dim;
+  hipLaunchKernelGGL(vq_embed_codes_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, ids, n,
+                     codebook_l2, n_codes, e_dim, out);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_vq_to_uint8(const float* x, long n, unsigned char* out, hipStream_t stream) {
+  if (!x || !out) return OSPO_ERR_ARG;
+  if (n <= 0) return OSPO_ERR_SHAPE;
+  hipLaunchKernelGGL(vq_to_uint8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, n, out);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
 extern "C" int ospo_vq_bmm_nt(const float* x, const float* w, int B, int n_rows, int n_cols, int K, float* out,
                               hipStream_t stream) {
   if (!x || !w || !out) return OSPO_ERR_ARG;

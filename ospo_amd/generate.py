@@ -18,8 +18,9 @@ attention (``ospo_attn_cache``); every step-dependent value is a device counter,
 captured as a hipGraph (``torch.cuda.CUDAGraph`` over the HIP launches) and replayed n-1 times.
 Sampling: inverse CDF on the bf16 probabilities with a seeded uniform per image and step
 (``ospo_cfg_sample``) -- the distribution ``torch.multinomial`` draws from, with a generator whose
-draws the oracle can replay.  The VQ pixel decoder (``decode_code``) is the VQ row of §8f (rank 3);
-``generate`` returns the image-token ids.
+draws the oracle can replay.  ``generate`` returns the image-token ids; ``generate_images`` adds the
+VQ pixel decoder (``decode_code``, image_generation.py:174) and the uint8 conversion of :175-181, so a
+batch of prompts becomes the [B, 384, 384, 3] images step 3 saves.
 """
 from __future__ import annotations
 
@@ -46,7 +47,7 @@ class T2IGenerator:
 
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_batch: int = 16,
                  max_prompt_len: int = 64, n_img_tokens: int = 576, cfg_weight: float = 5.0,
-                 temperature: float = 1.0, pad_id: int = PAD_ID):
+                 temperature: float = 1.0, pad_id: int = PAD_ID, vq_weights: Optional[Dict[str, torch.Tensor]] = None):
         if dims.head_dim != 128:
             raise ValueError("head_dim must be 128 (Janus-Pro)")
         if 2 * max_batch > 64:
@@ -110,6 +111,11 @@ class T2IGenerator:
         self._graph = None
         self._graph_B = None
         self.probs = None  # [n, B, V] fp32 when record_probs
+        # gen_vision_model's pixel decoder (VQ-16 weights: post_quant_conv.*, decoder.*, quantize.*)
+        self.vq_decoder = None
+        if vq_weights is not None:
+            from .vq import VQDecoder
+            self.vq_decoder = VQDecoder(vq_weights, device=dev)
 
     # ------------------------------------------------------------------ prefill
     def _prompt_rows(self, prompts: Sequence[Sequence[int]]):
@@ -207,6 +213,21 @@ class T2IGenerator:
         self._head_and_sample(x, R)
 
     # ----------------------------------------------------------------- generate
+    @torch.inference_mode()
+    def generate_images(self, prompts: Sequence[Sequence[int]], seed: int = 0, use_graph: bool = True,
+                        img_size: int = 384, patch_size: int = 16) -> torch.Tensor:
+        """generate_image (image_generation.py:109-181) up to the saved pixels: the image tokens, then
+        ``decode_code`` with shape [B, 8, img_size / patch_size, img_size / patch_size] and the uint8
+        conversion.  Returns uint8 [B, img_size, img_size, 3] on the device."""
+        if self.vq_decoder is None:
+            raise RuntimeError("T2IGenerator was built without vq_weights: no pixel decoder")
+        hw = img_size // patch_size
+        if hw * hw != self.n_img:
+            raise ValueError(f"{self.n_img} image tokens do not tile a {hw} x {hw} grid")
+        tok = self.generate(prompts, seed=seed, use_graph=use_graph)
+        dec = self.vq_decoder.decode_code(tok, hw, hw)
+        return self.vq_decoder.to_images(dec)
+
     def uniforms(self, seed: int, B: int) -> torch.Tensor:
         """The sampler's uniforms [n_img_tokens, B] for a seed (set_seed(seed) in the reference
         seeds torch.multinomial; here a CPU generator seeds the inverse-CDF draws)."""

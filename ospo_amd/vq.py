@@ -1,4 +1,5 @@
 """VQ image tokenizer on the MI355X: Janus-Pro's ``gen_vision_model.encode``
+and, for step-3 sampling, its pixel decoder ``decode_code`` (``VQDecoder``).  Encode:
 (``janus/models/vq_model.py``: Encoder :46-124, quant_conv, VectorQuantizer :236-282) -- pixels to the
 VQ ids the SimPO step consumes (``ospo/wrapper/train.py:246-264`` encodes each chosen / rejected
 image; here once, into a token cache, see ``build_token_cache``).
@@ -129,6 +130,130 @@ class VQEncoder:
              _s())
         ids = ids.view(B, -1)
         return (ids, z, dmin.view(B, -1)) if return_z else ids
+
+
+class VQDecoder:
+    """Device-resident VQ-16 pixel decoder: ``gen_vision_model.decode_code`` (vq_model.py:505-508) as the
+    step-3 sampler calls it (``image_generation.py:174``) and the uint8 images it saves (:175-181).
+    ``weights``: the reference's state_dict names (``post_quant_conv.*``, ``decoder.*``,
+    ``quantize.embedding.weight``).  fp32 on the same convolution / GroupNorm / attention kernels as
+    the encoder; the Upsample's nearest 2x is read on the fly by the next convolution."""
+
+    def __init__(self, weights: Dict[str, torch.Tensor], device="cuda", cfg=VQ16):
+        self.cfg, self.device = cfg, torch.device(device)
+        self.w = {}
+        for k, v in weights.items():
+            if not (k.startswith("decoder.") or k.startswith("post_quant_conv.") or k == "quantize.embedding.weight"):
+                continue
+            t = v.detach().to(device=self.device, dtype=F32)
+            if t.dim() == 4:
+                t = t.permute(0, 2, 3, 1)
+            self.w[k] = t.contiguous()
+        cb = self.w["quantize.embedding.weight"]
+        self.codebook = torch.empty_like(cb)
+        call("ospo_vq_l2norm_rows", _p(cb), cb.shape[0], cb.shape[1], _p(self.codebook), _s())
+        self.gn_ws = torch.empty(query("ospo_vq_groupnorm_ws_bytes", 64, 32) // 4 + 4, dtype=F32, device=self.device)
+
+    _conv = VQEncoder._conv
+    _gn = VQEncoder._gn
+    _res = VQEncoder._res
+    _attn = VQEncoder._attn
+
+    def _upconv(self, x, name):
+        B, H, W, Cin = x.shape
+        wt, b = self.w[name + ".weight"], self.w.get(name + ".bias")
+        Cout = wt.shape[0]
+        out = torch.empty(B, 2 * H, 2 * W, Cout, dtype=F32, device=self.device)
+        call("ospo_vq_conv2d_up2", _p(x), B, H, W, Cin, _p(wt), Cout, 3, 3, 1, _p(b), None, _p(out), _s())
+        return out
+
+    @torch.inference_mode()
+    def decode_code(self, ids: torch.Tensor, h: int = 24, w: int = 24) -> torch.Tensor:
+        """ids int [B, h*w] (device or host) -> fp32 NHWC [B, 16h, 16w, 3] in the decoder's output range."""
+        cfg = self.cfg
+        ids = ids.to(device=self.device, dtype=torch.int32).contiguous()
+        B = ids.shape[0]
+        if ids.shape[1] != h * w:
+            raise ValueError(f"{ids.shape[1]} ids per image, expected {h} x {w}")
+        if B > 64:
+            raise ValueError("at most 64 images per decode call")
+        e = cfg["e_dim"]
+        z = torch.empty(B, h, w, e, dtype=F32, device=self.device)
+        call("ospo_vq_embed_codes", _p(ids), B * h * w, _p(self.codebook), self.codebook.shape[0], e, _p(z), _s())
+        x = self._conv(z, "post_quant_conv", pad=0)
+        ch, mult, nrb = cfg["ch"], cfg["ch_mult"], cfg["num_res_blocks"]
+        nl = len(mult)
+        block_in = ch * mult[nl - 1]
+        x = self._conv(x, "decoder.conv_in")
+        x = self._res(x, "decoder.mid.0", block_in, block_in)
+        x = self._attn(x, "decoder.mid.1")
+        x = self._res(x, "decoder.mid.2", block_in, block_in)
+        for li, i_level in enumerate(reversed(range(nl))):  # Decoder.forward :199-207
+            block_out = ch * mult[i_level]
+            for j in range(nrb + 1):
+                x = self._res(x, f"decoder.conv_blocks.{li}.res.{j}", block_in, block_out)
+                block_in = block_out
+                if i_level == nl - 1:
+                    x = self._attn(x, f"decoder.conv_blocks.{li}.attn.{j}")
+            if i_level != 0:
+                x = self._upconv(x, f"decoder.conv_blocks.{li}.upsample.conv")
+        x = self._gn(x, "decoder.norm_out", True)
+        return self._conv(x, "decoder.conv_out")
+
+    @torch.inference_mode()
+    def to_images(self, dec: torch.Tensor) -> torch.Tensor:
+        """image_generation.py:175-181: uint8 [B, H, W, 3] = clip((dec + 1) / 2 * 255, 0, 255), truncated."""
+        out = torch.empty(dec.shape, dtype=torch.uint8, device=self.device)
+        call("ospo_vq_to_uint8", _p(dec), dec.numel(), _p(out), _s())
+        return out
+
+
+def synthetic_vq_decoder_weights(seed: int = 1, cfg=VQ16) -> Dict[str, torch.Tensor]:
+    """Random VQ-16 decoder weights (post_quant_conv + decoder.*), fan-in scaled convs."""
+    g = torch.Generator().manual_seed(int(seed))
+    w: Dict[str, torch.Tensor] = {}
+    ch, mult, nrb = cfg["ch"], cfg["ch_mult"], cfg["num_res_blocks"]
+
+    def conv(name, cin, cout, k):
+        w[name + ".weight"] = torch.randn(cout, cin, k, k, generator=g) / math.sqrt(cin * k * k)
+        w[name + ".bias"] = torch.randn(cout, generator=g) * 0.02
+
+    def norm(name, c):
+        w[name + ".weight"] = 1.0 + torch.randn(c, generator=g) * 0.05
+        w[name + ".bias"] = torch.randn(c, generator=g) * 0.05
+
+    def res(p, cin, cout):
+        norm(p + ".norm1", cin)
+        conv(p + ".conv1", cin, cout, 3)
+        norm(p + ".norm2", cout)
+        conv(p + ".conv2", cout, cout, 3)
+        if cin != cout:
+            conv(p + ".nin_shortcut", cin, cout, 1)
+
+    def attn(p, c):
+        norm(p + ".norm", c)
+        for n in ("q", "k", "v", "proj_out"):
+            conv(p + "." + n, c, c, 1)
+
+    nl = len(mult)
+    block_in = ch * mult[nl - 1]
+    conv("post_quant_conv", cfg["e_dim"], cfg["z_channels"], 1)
+    conv("decoder.conv_in", cfg["z_channels"], block_in, 3)
+    res("decoder.mid.0", block_in, block_in)
+    attn("decoder.mid.1", block_in)
+    res("decoder.mid.2", block_in, block_in)
+    for li, i_level in enumerate(reversed(range(nl))):
+        block_out = ch * mult[i_level]
+        for j in range(nrb + 1):
+            res(f"decoder.conv_blocks.{li}.res.{j}", block_in, block_out)
+            block_in = block_out
+            if i_level == nl - 1:
+                attn(f"decoder.conv_blocks.{li}.attn.{j}", block_in)
+        if i_level != 0:
+            conv(f"decoder.conv_blocks.{li}.upsample.conv", block_in, block_in, 3)
+    norm("decoder.norm_out", block_in)
+    conv("decoder.conv_out", block_in, cfg["in_channels"], 3)
+    return w
 
 
 def build_token_cache(encoder: VQEncoder, items: Iterable, out_path: str, size: int = 384, batch: int = 16):

@@ -11,6 +11,11 @@ init and is not used) and runs ``encode`` in fp32, eval mode, on example PNGs of
 Output ``tests/golden/vq_golden.npz`` (data only): the uint8 pixels actually fed (after resize), the
 weight seed, the reference's indices (``encode(x)[2][2]``, what train.py:257-258 keeps), its
 quant_conv output z and the top-2 distance margin per token.
+
+Decoder (step 3, ``image_generation.py:174-181``): with ``oracle.vq_ref.init_vq_decoder_weights(DEC_SEED)``
+loaded as well, the reference's ``decode_code`` of image 0's ids (128 px, decoded in full, fp32) and of
+image 2's ids (384 px: the uint8 image of image_generation.py:175-181 plus a strided fp32 sample),
+into ``tests/golden/vq_decode_golden.npz``.
 """
 from __future__ import annotations
 
@@ -31,6 +36,7 @@ IMAGES = [("examples/step3/negative/layout/1000003/01.png", 128),
           ("examples/step3/negative/layout/1000005/00.png", 128),
           ("examples/step3/negative/layout/1000001/02.png", 384)]
 SEED = 7
+DEC_SEED = 11
 
 
 def main():
@@ -40,9 +46,10 @@ def main():
     torch.manual_seed(0)
     model = mod.VQModel(mod.ModelArgs()).eval()
     w = V.init_vq_weights(SEED)
+    w.update(V.init_vq_decoder_weights(DEC_SEED))
     missing, unexpected = model.load_state_dict(w, strict=False)
     assert not unexpected, unexpected
-    assert all(k.startswith(("decoder.", "post_quant_conv.", "quantize.codebook_used")) for k in missing), missing
+    assert all(k.startswith("quantize.codebook_used") for k in missing), missing
     out = {"seed": np.int64(SEED)}
     torch.set_num_threads(8)
     for i, (rel, size) in enumerate(IMAGES):
@@ -63,6 +70,20 @@ def main():
         out[f"img{i}_margin"] = margin.reshape(-1).numpy().astype(np.float32)
         print(rel, size, "tokens", ids.numel(), "min margin", float(margin.min()))
     np.savez_compressed(os.path.join(HERE, "vq_golden.npz"), **out)
+    dec = {"seed": np.int64(SEED), "dec_seed": np.int64(DEC_SEED)}
+    with torch.no_grad():
+        d0 = model.decode_code(torch.from_numpy(out["img0_ids"]).view(1, -1).int(), shape=[1, 8, 8, 8])
+        d2 = model.decode_code(torch.from_numpy(out["img2_ids"]).view(1, -1).int(), shape=[1, 8, 24, 24])
+    dec["img0_dec"] = d0.numpy().astype(np.float32)
+    a2 = d2.numpy().astype(np.float32)
+    dec["img2_dec_sample"] = a2.reshape(-1)[::101].copy()
+    # image_generation.py:175-181
+    img = np.clip((a2.transpose(0, 2, 3, 1) + 1) / 2 * 255, 0, 255)
+    u8 = np.zeros(img.shape, dtype=np.uint8)
+    u8[:] = img
+    dec["img2_u8"] = u8
+    np.savez_compressed(os.path.join(HERE, "vq_decode_golden.npz"), **dec)
+    print("decode: 128 px", d0.shape, "384 px", d2.shape)
 
 
 if __name__ == "__main__":

@@ -144,3 +144,67 @@ def test_token_cache_cli_reads_step5_json(tmp_path):
     assert sorted(cache.files) == ["0000042/chosen", "0000042/rejected"]
     for k in cache.files:
         assert np.array_equal(cache[k].astype(np.int64), z["img2_ids"])
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 12, 12, 128, 128), (1, 24, 24, 512, 512), (1, 7, 5, 40, 70)])
+def test_conv2d_up2_equals_upsample_then_conv(B, H, W, Cin, Cout):
+    """The Upsample (nearest 2x, vq_model.py:411-427) read on the fly by the convolution: bit-identical to
+    the convolution of the explicitly upsampled tensor (same gathers, same order)."""
+    x = torch.randn(B, H, W, Cin, device=DEV)
+    w = (torch.randn(Cout, 3, 3, Cin) / (9 * Cin) ** 0.5).to(DEV)
+    b = torch.randn(Cout, device=DEV)
+    up = x.repeat_interleave(2, 1).repeat_interleave(2, 2).contiguous()
+    a = torch.empty(B, 2 * H, 2 * W, Cout, device=DEV)
+    c = torch.empty_like(a)
+    call("ospo_vq_conv2d", up.data_ptr(), B, 2 * H, 2 * W, Cin, w.data_ptr(), Cout, 3, 3, 1, 1, 1, 2 * H, 2 * W,
+         b.data_ptr(), None, a.data_ptr(), s())
+    call("ospo_vq_conv2d_up2", x.data_ptr(), B, H, W, Cin, w.data_ptr(), Cout, 3, 3, 1, b.data_ptr(), None,
+         c.data_ptr(), s())
+    torch.cuda.synchronize()
+    assert torch.equal(a, c)
+
+
+def test_decoder_matches_reference_golden():
+    """decode_code (image_generation.py:174) on the GPU against the reference's own vq_model.py decode of
+    the golden ids (tests/golden/vq_decode_golden.npz): fp32 decode to fp32 noise; the uint8 images of
+    image_generation.py:175-181 equal but for values within fp32 noise of an integer (+-1)."""
+    from ospo_amd.vq import VQDecoder
+    z = np.load(GOLD)
+    d = np.load(GOLD.replace("vq_golden", "vq_decode_golden"))
+    w = V.init_vq_weights(int(d["seed"]))
+    w.update(V.init_vq_decoder_weights(int(d["dec_seed"])))
+    dec = VQDecoder(w, device=DEV)
+    o0 = dec.decode_code(torch.from_numpy(z["img0_ids"]).view(1, -1), 8, 8)
+    ref0 = torch.from_numpy(d["img0_dec"]).permute(0, 2, 3, 1)
+    e0 = float((o0.cpu() - ref0).abs().max() / ref0.abs().max())
+    o2 = dec.decode_code(torch.from_numpy(z["img2_ids"]).view(1, -1), 24, 24)
+    smp = o2.permute(0, 3, 1, 2).reshape(-1)[::101].cpu().numpy()
+    e2 = float(np.abs(smp - d["img2_dec_sample"]).max() / np.abs(d["img2_dec_sample"]).max())
+    u8 = dec.to_images(o2).cpu().numpy()
+    diff = np.abs(u8.astype(np.int16) - d["img2_u8"].astype(np.int16))
+    print(f"\nVQ decode: 128 px max rel err {e0:.2e}, 384 px sample {e2:.2e}, uint8 pixels off by 1: "
+          f"{int((diff > 0).sum())} of {diff.size}")
+    assert e0 < 1e-4 and e2 < 1e-4
+    assert diff.max() <= 1 and (diff > 0).mean() < 1e-3
+
+
+def test_generate_images_decodes_the_sampled_tokens():
+    """T2IGenerator.generate_images = generate + decode_code + uint8 (image_generation.py:109-181) at
+    small LLM width: the images are the decoder's images of the tokens generate() returns."""
+    from ospo_amd.engine import ModelDims
+    from ospo_amd.generate import T2IGenerator
+    from ospo_amd.vq import VQDecoder
+    from oracle import simpo_ref as O
+    dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=16384, gen_head_dim=256)
+    w = O.init_weights(dims, seed=23, dtype=torch.bfloat16, lora_b_std=1e-2)
+    vw = V.init_vq_weights(1)
+    vw.update(V.init_vq_decoder_weights(2))
+    gen = T2IGenerator(ModelDims.from_any(dims), w, device=DEV, max_batch=2, max_prompt_len=16, n_img_tokens=64,
+                       vq_weights=vw)
+    prompts = [[5, 9, 200, 31], [7, 8, 9]]
+    imgs = gen.generate_images(prompts, seed=4, img_size=128)
+    tok = gen.generate(prompts, seed=4)
+    dec = VQDecoder(vw, device=DEV)
+    ref = dec.to_images(dec.decode_code(tok, 8, 8))
+    assert imgs.shape == (2, 128, 128, 3) and imgs.dtype == torch.uint8
+    assert torch.equal(imgs, ref)
