@@ -208,3 +208,18 @@ def test_generate_images_decodes_the_sampled_tokens():
     ref = dec.to_images(dec.decode_code(tok, 8, 8))
     assert imgs.shape == (2, 128, 128, 3) and imgs.dtype == torch.uint8
     assert torch.equal(imgs, ref)
+
+
+def test_decoder_reproduces_reference_generate_image_pngs():
+    """The HIP decoder on the tokens the reference's generate_image sampled (tests/golden/
+    generate_golden.npz, make_golden_generate.py) writes the PNG pixels the reference saved (+-1 where
+    a value sits within fp32 noise of an integer)."""
+    from ospo_amd.vq import VQDecoder
+    z = np.load(GOLD.replace("vq_golden", "generate_golden"))
+    _, vq_seed, vq_dec_seed, _ = z["seeds"].tolist()
+    w = V.init_vq_weights(int(vq_seed))
+    w.update(V.init_vq_decoder_weights(int(vq_dec_seed)))
+    dec = VQDecoder(w, device=DEV)
+    u8 = dec.to_images(dec.decode_code(torch.from_numpy(z["tokens"]), 8, 8)).cpu().numpy()
+    diff = np.abs(u8.astype(np.int16) - z["images_u8"].astype(np.int16))
+    assert diff.max() <= 1 and (diff > 0).mean() < 1e-3
