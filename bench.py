@@ -260,6 +260,69 @@ def bench_vq(args):
     print(json.dumps(line), flush=True)
 
 
+def bench_wrapper(args):
+    """The drop-in path timed end to end: JanusProTrainWrapper.training_step -> loss.backward()
+    -> Trainer all-reduce -> on_before_optimizer_step (grad-norm log) -> FusedLoraAdamW.step -> scheduler ->
+    the logged metrics read on the host, as ospo_amd.trainer.Trainer runs a step, on batches in the
+    reference's collate format: VQ token ids (a token cache), or with --inline-vq f32 pixel tensors
+    [1, 3, 384, 384] that preprocess_batch VQ-encodes on the GPU (train.py:246-261).  Inputs resident in
+    HBM; synthetic weights and pixels."""
+    from ospo_amd import dist as odist
+    from ospo_amd.config import build_config
+    from ospo_amd.model import get_model
+    from ospo_amd.wrapper.train import JanusProTrainWrapper
+    world, rank, local = odist.init()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B, Lt, N, r = args.pairs_per_gpu or default_pairs_per_gpu(world), args.text_len, args.img_tokens, args.lora_r
+    cfg = build_config(os.path.join(ROOT, "configs", "step5.yaml"), argv=[
+        "model.synthetic=true", f"model.override={{'n_layers': {args.layers}}}", f"lora.lora_rank={r}",
+        f"lora.lora_alpha={2 * r}", f"lora.lora_dropout={args.lora_dropout}", f"dataset.train.batch_size={B}",
+        f"model.linear_dtype={args.linear_dtype}"])
+    model, cp, ip, tok = get_model(mode="train", config=cfg, device=dev, max_text_len=Lt, n_img_tokens=N)
+    w = JanusProTrainWrapper(cfg, model, cp, ip, tok)
+    (opt,), (sch,) = w.configure_optimizers()
+    sched = sch["scheduler"]
+    allreduce = odist.GradAllReduce(world)
+    dims = model.engine.dims
+    g = torch.Generator().manual_seed(1000 * rank)
+    batches = []
+    for i in range(2):
+        text = [torch.randint(0, dims.vocab, (1, Lt - (j % 3)), generator=g, dtype=torch.int32) for j in range(B)]
+        if args.inline_vq:
+            imgs = [(torch.rand(1, 3, 384, 384, generator=g) * 2 - 1).to(dev) for _ in range(2 * B)]
+        else:
+            imgs = [torch.randint(0, dims.img_vocab, (1, N), generator=g) for _ in range(2 * B)]
+        batches.append(([f"{i}{j:06d}" for j in range(B)], text, imgs[:B], imgs[B:]))
+
+    def step(i):
+        loss = w.training_step(batches[i % 2], i)
+        loss.backward()
+        allreduce(model.engine.grads)
+        w.on_before_optimizer_step()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        return w.logged  # the Trainer writes the metrics every log step (host read)
+
+    dt, logged = timed_region(step, args.warmup, args.steps, odist.barrier, torch.cuda.synchronize, world, dev)
+    if rank != 0:
+        return
+    value = B * world * args.steps / dt
+    print(json.dumps({
+        "metric": METRIC, "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.linear_dtype == "bf16" else "mxfp8 linears",
+        "data": "synthetic (random-init Janus-Pro-7B-shaped weights, random prompts, "
+                + ("random pixels, VQ-encoded in the step)" if args.inline_vq else "random VQ ids)"),
+        "config": {"workload": "drop-in path: JanusProTrainWrapper.training_step + loss.backward + Trainer step "
+                               f"({'f32 pixels, VQ encode inside preprocess_batch' if args.inline_vq else 'VQ token ids'}), "
+                               f"LoRA r={r} dropout {args.lora_dropout}, {B} pairs/GPU",
+                   "pairs_per_gpu": B, "global_batch": B * world, "seq_len": Lt + N, "parallelism": f"dp{world}",
+                   "inline_vq": bool(args.inline_vq)},
+        "loss": round(logged.get("train/loss", float("nan")), 5)}), flush=True)
+
+
 def _free_port():
     import socket
     with socket.socket() as sk:
@@ -364,7 +427,9 @@ def main():
     # BASELINE config 5: the frozen decoder Linears on MXFP8 block-scaled fp8 MFMA (use with --lora-r 32)
     ap.add_argument("--linear-dtype", choices=("bf16", "mx8"), default="bf16")
     # t2i: config 4; vq: §8f-3; stub: CPU rehearsal of the multi-rank launcher (tests)
-    ap.add_argument("--workload", choices=("simpo", "t2i", "vq", "stub"), default="simpo")
+    ap.add_argument("--workload", choices=("simpo", "wrapper", "t2i", "vq", "stub"), default="simpo")
+    # wrapper workload: pixels in the batch, VQ-encoded inside preprocess_batch (the reference's data path)
+    ap.add_argument("--inline-vq", action="store_true")
     ap.add_argument("--vq-batch", type=int, default=16)
     ap.add_argument("--t2i-batch", type=int, default=16)       # parallel_size: prompts (x2 rows with CFG)
     ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
@@ -375,6 +440,8 @@ def main():
         sys.exit(args.child_rc)
     if args.workload == "stub":
         return bench_stub(args)
+    if args.workload == "wrapper":
+        return bench_wrapper(args)
     if args.workload in ("t2i", "vq"):
         if (args.gpus or 1) != 1:
             raise SystemExit(f"bench.py --workload {args.workload} is a single-GPU workload")

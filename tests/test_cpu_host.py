@@ -305,3 +305,54 @@ def test_dropout_hash_host_c_and_numpy_agree(lib):
     m2 = D.keep_mask(512, 4096, D.layer_seed(42, 1, 0, "o"), 0.05)
     assert 0.90 < (m == m2).mean() < 0.91  # independent masks agree where both keep or both drop
     assert D.layer_seed(42, 1, 3, "gu") != D.layer_seed(42, 2, 3, "gu")
+
+
+def test_checkpoint_keys_resolve_in_the_reference_module_tree(tmp_path):
+    """What ospo/inference.py:268-281 consumes: config.yaml read with yaml.safe_load as get_lora_config
+    (ospo/utils/model.py:74-89) reads it, and every adapter key of the .ckpt naming a Linear of the
+    transformers Llama tree under peft's prefixes (model. = the LightningModule's self.model,
+    language_model.base_model.model. = PeftModel -> LoraModel -> LlamaForCausalLM), with lora_A [r, in]
+    and lora_B [out, r] shapes of that Linear."""
+    import yaml
+    from transformers import LlamaConfig, LlamaForCausalLM
+    from ospo_amd.ckpt import save_checkpoint
+    from ospo_amd.config import build_config, save_config
+    from ospo_amd.lora import LoraLayout
+    from ospo_amd.wrapper.train import ConstantLR, FusedLoraAdamW
+    L, D, Fd, r = 2, 256, 512, 16
+    llama = LlamaForCausalLM(LlamaConfig(vocab_size=512, hidden_size=D, intermediate_size=Fd, num_hidden_layers=L,
+                                         num_attention_heads=2, num_key_value_heads=2))
+    mods = dict(llama.named_modules())
+
+    class StubEngine:
+        dims = types.SimpleNamespace(n_layers=L)
+
+        def __init__(self):
+            self.layout = LoraLayout(L, D, Fd, r)
+            self.lora = torch.randn(self.layout.numel).to(torch.bfloat16)
+            self.exp_avg = torch.zeros(self.layout.numel, dtype=torch.bfloat16)
+            self.exp_avg_sq = torch.zeros(self.layout.numel, dtype=torch.bfloat16)
+            self.opt_step = 0
+
+        def lora_tensors(self):
+            return self.layout.from_flat(self.lora)
+    e = StubEngine()
+    opt = FusedLoraAdamW(e, 4e-5, (0.9, 0.95), 1e-8, 0.0, 1.0)
+    p = save_checkpoint(str(tmp_path / "step=000001.ckpt"), e, opt, ConstantLR(opt), 0, 1)
+    cfg = build_config(os.path.join(ROOT, "configs", "step5.yaml"), argv=["lora.lora_rank=16", "lora.lora_alpha=32"])
+    save_config(str(tmp_path), cfg)
+    ck_cfg = yaml.safe_load(open(tmp_path / "config.yaml"))  # get_lora_config's reads
+    lc = ck_cfg["lora"]
+    assert lc.get("lora_rank") == r and lc["lora_alpha"] == 32 and lc["lora_dropout"] is not None
+    assert sorted(lc["target_modules"]) == sorted(["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj",
+                                                   "down_proj"])
+    sd = torch.load(p, weights_only=True)["state_dict"]
+    assert len(sd) == L * 7 * 2
+    pre = "model.language_model.base_model.model."
+    for k, t in sd.items():
+        assert k.startswith(pre) and k.endswith((".lora_A.default.weight", ".lora_B.default.weight")), k
+        name, ab = k[len(pre):].rsplit(".lora_", 1)
+        m = mods[name]
+        assert isinstance(m, torch.nn.Linear), name
+        assert tuple(t.shape) == ((r, m.in_features) if ab.startswith("A") else (m.out_features, r)), k
+        assert name.split(".")[-1] in lc["target_modules"]
