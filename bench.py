@@ -435,6 +435,7 @@ def main():
     ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--wgrad-wgs", type=int, default=0)  # A/B: LoRA weight grads as ospo_lora_wgrad streams
     args = ap.parse_args()
     if launch_ranks(args):
         sys.exit(args.child_rc)
@@ -463,7 +464,8 @@ def main():
     B, Lt, N = args.pairs_per_gpu or default_pairs_per_gpu(world), args.text_len, args.img_tokens
     weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)  # identical on every rank (same seeds)
     eng = SimPOEngine(dims, weights, device=dev, max_pairs=B, max_text_len=Lt, n_img_tokens=N,
-                      lora_dropout=args.lora_dropout, dropout_seed=42, linear_dtype=args.linear_dtype)
+                      lora_dropout=args.lora_dropout, dropout_seed=42, linear_dtype=args.linear_dtype,
+                      wgrad_wgs=args.wgrad_wgs)
     del weights
     torch.cuda.empty_cache()
     cfg = SimPOConfig()

@@ -110,6 +110,15 @@ int ospo_gemm_nt_tile(int M, int N);
  * C + n*diag_r + (j % diag_r)  (ldc ignored) -- peft B_q|B_k|B_v contiguous.
  * Requires K % 64 == 0; N % 64 == 0; M arbitrary (stores predicated on m < M; a
  * K-major A must have lda >= roundup(M, 64) readable columns). */
+/* LoRA weight gradients (autograd of peft lora.Linear: dA = g^T . dropout(x), dB = dy^T . u) as one
+ * stream over the big operand X [K][N] (row-major, ldx), contracting over its K rows (tokens) against the
+ * small S [K][lds] (lds = the padded rank width, 64 or 128), fp32 atomics into C:
+ *   mode 0 (dA): C[j * ldc + n] += sum_k S[k][j] X[k][n]           j < s_cols, N % 256 == 0
+ *   mode 1 (dB): C[n * r + jr]  += sum_k X[k][n] S[k][(n / nmod) * r + jr]   (block diagonal; r 16 or 32)
+ * K % 64 == 0 (rows past the real tokens must hold zeros in S); splits = K-range splits (<= K / 64).
+ * drop_p > 0 (mode 0): X is masked as ospo_lora_skinny masked it in the forward (index k * N + n). */
+int ospo_lora_wgrad(const void* X, int ldx, int N, const void* S, int lds, int s_cols, int K, int mode, int nmod,
+                    int r, float* C, int ldc, int splits, uint32_t drop_seed, float drop_p, hipStream_t stream);
 int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
                      int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
                      int diag_nblk, int diag_r, hipStream_t stream);

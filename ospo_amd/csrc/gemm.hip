@@ -383,6 +383,162 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 //   read(t,1)->SB | MFMA(SA) | vmcnt(0) lgkmcnt(0) s_barrier | stage(t+2) | read(t+1,0)->SA | MFMA(SB)
 // Two LDS buffers; tile t+2 streams into tile t's buffer right after the barrier that
 // certifies every wave finished reading it.  Loads get one K-tile of slack.
+
+// LoRA weight gradients as one stream over the big operand (round 2; replaces the 64 x 64 f32-atomic
+// tiles of gemm_kernel for dA / dB):
+//   mode 0 (dA):  C[j][n]      += sum_m S[m][j] X[m][n]             j < s_cols (the used rank rows)
+//   mode 1 (dB):  C[n][jr]     += sum_m X[m][n] S[m][mod * r + jr]  mod = n / nmod, jr < r (block diagonal)
+// X [Mk][N] is the big activation (x_in for dA, dy for dB), S [Mk][>= s_cols] the small LoRA operand
+// (g for dA, u for dB).  A workgroup owns a TN-column stripe of X and a range of 64-row K-tiles; the
+// stripe and the S rows of a K-tile stream through an NS-deep LDS ring by LDS-DMA (one barrier per
+// K-tile, NS - 1 tiles in flight), both MFMA operands are transposed reads (the contraction runs over
+// rows), each X fragment feeds every rank tile.  Split partials meet in fp32 atomics.  With dropout
+// (dA of a dropped-out adapter input) the X fragments are masked in registers with the forward's hash
+// and bf16 rounding.
+template <int TN, int TS, int NS, int MODE, bool DROP>
+__global__ __launch_bounds__(256) void lora_wgrad_kernel(const bf16* __restrict__ X, int ldx, int N,
+                                                         const bf16* __restrict__ S, int lds, int s_cols, int K,
+                                                         int nmod, int r, float* __restrict__ C, int ldc,
+                                                         uint32_t dseed, uint32_t dthresh, float dscale, int drop_ld) {
+  constexpr int XB = TN * BK * 2, SB = TS * BK * 2, STG = XB + SB;
+  constexpr int NF = TN / 64;                       // 16-column X fragments per wave
+  constexpr int RT = MODE == 0 ? TS / 16 : 2;       // rank tiles of the product (dB: r <= 32)
+  __shared__ __attribute__((aligned(16))) char smem[NS * STG];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n0 = blockIdx.x * TN;
+  const int nt = K / BK;
+  const int t0 = (int)((long)nt * blockIdx.y / gridDim.y), t1 = (int)((long)nt * (blockIdx.y + 1) / gridDim.y);
+  // S columns this stripe needs: all s_cols (dA), or the module's r columns (dB); the S tile holds the
+  // whole padded row (TS = its leading dimension), the fragments start at rbase
+  const int rbase = MODE == 0 ? 0 : (n0 / nmod) * r;
+  const int rt_used = MODE == 0 ? (s_cols + 15) / 16 : r / 16;
+  f32x4 acc[RT][NF];
+#pragma unroll
+  for (int j = 0; j < RT; ++j)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[j][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto stage = [&](int t, int slot) {
+    char* xs = smem + slot * STG;
+    stage_tile<TN, true, 4>(X, ldx, n0, N, t * BK, xs, wave, lane);
+    stage_tile<TS, true, 4>(S, lds, 0, TS, t * BK, xs + XB, wave, lane);
+  };
+  constexpr int PIECES = STG / 1024 / 4;  // LDS-DMA pieces per wave per stage
+  const int n_my = t1 - t0;
+  // prologue: NS - 1 stages in flight
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < n_my) stage(t0 + i, i);
+  const int g = lane >> 4, l16 = lane & 15;
+  for (int i = 0; i < n_my; ++i) {
+    // this wave's pieces of stage i have landed (NS - 2 newer stages may still be in flight)
+    const int newer = min(NS - 2, n_my - 1 - i);
+    if (newer >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
+    else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's pieces of stage i visible; every wave done with stage i - 1
+    if (i + NS - 1 < n_my) stage(t0 + i + NS - 1, (i + NS - 1) % NS);
+    const char* xs = smem + (i % NS) * STG;
+    const char* ss = xs + XB;
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      bf16x8 bx[NF], as[RT];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) bx[f] = read_frag<TN, true>(xs, wave * (TN / 4) + 16 * f, sk, lane);
+#pragma unroll
+      for (int j = 0; j < RT; ++j) as[j] = read_frag<TS, true>(ss, rbase + 16 * (j < rt_used ? j : 0), sk, lane);
+      if constexpr (DROP) {  // element e: row m = 64 t + 32 sk + 8 g + e, column n
+        const uint32_t mrow = (uint32_t)((t0 + i) * BK + 32 * sk + 8 * g);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          const uint32_t n = (uint32_t)(n0 + wave * (TN / 4) + 16 * f + l16);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const bool keep = drop_hash((mrow + e) * (uint32_t)drop_ld + n, dseed) >= dthresh;
+            bx[f][e] = keep ? f2bf(bf2f(bx[f][e]) * dscale) : f2bf(0.f);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RT; ++j)
+        if (j < rt_used)
+#pragma unroll
+          for (int f = 0; f < NF; ++f)
+            acc[j][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[j], bx[f], acc[j][f], 0, 0, 0);
+    }
+  }
+  // lane holds D[rank row 16 j + 4 g + q][column n0 + wave TN/4 + 16 f + l16]
+#pragma unroll
+  for (int j = 0; j < RT; ++j) {
+    if (j >= rt_used) continue;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int n = n0 + wave * (TN / 4) + 16 * f + l16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int jr = 16 * j + 4 * g + q;
+        if (MODE == 0) {
+          if (jr < s_cols) atomicAdd(C + (long)jr * ldc + n, acc[j][f][q]);
+        } else {
+          atomicAdd(C + (long)n * r + jr, acc[j][f][q]);
+        }
+      }
+    }
+  }
+}
+
+template <int TN, int TS, int MODE, bool DROP>
+int launch_wgrad(const bf16* X, int ldx, int N, const bf16* S, int lds, int s_cols, int K, int nmod, int r, float* C,
+                 int ldc, int splits, uint32_t seed, uint32_t thresh, float scale, int drop_ld, hipStream_t st) {
+  constexpr int NS = 3;
+  hipLaunchKernelGGL((lora_wgrad_kernel<TN, TS, NS, MODE, DROP>), dim3(N / TN, splits), dim3(256), 0, st, X, ldx, N, S,
+                     lds, s_cols, K, nmod, r, C, ldc, seed, thresh, scale, drop_ld);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+}  // namespace
+
+extern "C" int ospo_lora_wgrad(const void* X, int ldx, int N, const void* S, int lds, int s_cols, int K, int mode,
+                               int nmod, int r, float* C, int ldc, int splits, uint32_t drop_seed, float drop_p,
+                               hipStream_t stream) {
+  if (!X || !S || !C) return OSPO_ERR_ARG;
+  if (N <= 0 || K <= 0 || K % BK || s_cols <= 0 || splits < 1 || splits > K / BK) return OSPO_ERR_SHAPE;
+  if (ldx < N || ldx % 8 || lds % 8) return OSPO_ERR_SHAPE;
+  if (!aligned16(X) || !aligned16(S)) return OSPO_ERR_ALIGN;
+  if (drop_p < 0.f || drop_p >= 1.f) return OSPO_ERR_ARG;
+  const bool drop = drop_p > 0.f;
+  const uint32_t thresh = (uint32_t)((double)drop_p * 4294967296.0);
+  const float dscale = drop ? 1.f / (1.f - drop_p) : 0.f;
+  const bf16* x = (const bf16*)X;
+  const bf16* sp = (const bf16*)S;
+  // S rows are staged whole: lds = the padded rank width (64 or 128 columns)
+  if (lds != 64 && lds != 128) return OSPO_ERR_SHAPE;
+  if (mode == 0) {  // dA: C[s_cols][N], ldc >= N
+    if (ldc < N || N % 256 || s_cols > lds) return OSPO_ERR_SHAPE;
+    if (lds == 64)
+      return drop ? launch_wgrad<256, 64, 0, true>(x, ldx, N, sp, lds, s_cols, K, 0, 0, C, ldc, splits, drop_seed, thresh,
+                                                   dscale, N, stream)
+                  : launch_wgrad<256, 64, 0, false>(x, ldx, N, sp, lds, s_cols, K, 0, 0, C, ldc, splits, 0, 0, 0.f, N,
+                                                    stream);
+    return drop ? launch_wgrad<256, 128, 0, true>(x, ldx, N, sp, lds, s_cols, K, 0, 0, C, ldc, splits, drop_seed, thresh,
+                                                  dscale, N, stream)
+                : launch_wgrad<256, 128, 0, false>(x, ldx, N, sp, lds, s_cols, K, 0, 0, C, ldc, splits, 0, 0, 0.f, N,
+                                                   stream);
+  }
+  if (mode == 1) {  // dB: C[N][r] block-diagonal, module = n / nmod; S columns mod * r .. + r
+    if (drop || r <= 0 || r % 16 || r > 32 || nmod % 256 || N % nmod) return OSPO_ERR_UNSUPPORTED;
+    if ((N / nmod) * r > lds) return OSPO_ERR_SHAPE;
+    return lds == 64 ? launch_wgrad<256, 64, 1, false>(x, ldx, N, sp, lds, s_cols, K, nmod, r, C, 0, splits, 0, 0, 0.f, 0,
+                                                       stream)
+                     : launch_wgrad<256, 128, 1, false>(x, ldx, N, sp, lds, s_cols, K, nmod, r, C, 0, splits, 0, 0, 0.f,
+                                                        0, stream);
+  }
+  return OSPO_ERR_ARG;
+}
+
+namespace {
+
 template <int FM, int STAGES, bool REMAP, bool PRIO, int WM = 2, int WN = 4, int FN = 4, int DBG = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_nt_v3_kernel(const GemmArgs args, int tiles_m, int tiles_n) {
   constexpr int NW = WM * WN;

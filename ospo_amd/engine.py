@@ -77,7 +77,7 @@ class SimPOEngine:
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_pairs: int = 4,
                  max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
                  dropout_seed: int = 42, linear_dtype: str = "bf16", fuse_swiglu_bwd: bool = False,
-                 dadb_splits=(8, 4, 4, 8), side_priority: int = -1):
+                 dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
         if linear_dtype not in ("bf16", "mx8"):
@@ -160,6 +160,9 @@ class SimPOEngine:
         # K splits of the LoRA dA / dB products: dA (Kin <= 8192, > 8192), dB (multi-module, single-module)
         # (8, 4, 4, 8 measured best, profiles/r01/dadb_splits_ab_highprio.log)
         self._dadb_splits = tuple(int(v) for v in dadb_splits)
+        # > 0: the LoRA weight gradients as ospo_lora_wgrad streams of ~wgrad_wgs workgroups; 0: the 64 x 64
+        # f32-atomic tiles (faster in isolation, 180.8 vs 198.8 us per layer, tools/lora_grads_bench.py)
+        self.wgrad_wgs = int(wgrad_wgs)
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
             raise ValueError("dadb_splits must be four positive split counts")
         self._side = torch.cuda.Stream(device=self.device, priority=int(side_priority))
@@ -508,35 +511,49 @@ class SimPOEngine:
             Acat, AcatT, Bcat, BT = pk["qkv"]
             gs = self._lora_g(dqkv, lay.groups["qkv"], Bcat, BT, M, q)
             dr = self._drop(i, "qkv")
-            self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+            if i > 0:
+                self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("qkv", q, gs, a["xn1"], dqkv, a["u_qkv"], gbase, dr)
-            guard("down", 1 - q)  # dx copy 1-q: layer i+1's down products read it
-            ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[1 - q][:M],
-                            dres=dxmid[:M], mx=self._mxo(D))
+            if i > 0:
+                guard("down", 1 - q)  # dx copy 1-q: layer i+1's down products read it
+                ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[1 - q][:M],
+                                dres=dxmid[:M], mx=self._mxo(D))
+            # layer 0: the gradient w.r.t. its input (the text / image embeddings) feeds nothing that
+            # trains -- the embedding tables and gen_aligner are frozen (train.py:148-216) -- so its q|k|v dX
+            # GEMM and the input RMSNorm backward are not run
             if on_layer_grads is not None:
                 with torch.cuda.stream(side):  # this layer's dA/dB are the last side-stream work so far
                     on_layer_grads(gbase, gbase + lay.per_layer)
         main.wait_stream(side)
 
     def _lora_grads(self, gs, x_in, dy, u, g, gbase, drop=None):
-        """dA = g_s^T . x_in  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal).
-        Only the nmods*r used columns of g enter dA (no atomics of padding rows)."""
+        """dA = g_s^T . dropout(x_in)  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal), each one
+        stream over its big operand (ospo_lora_wgrad); with LoRA dropout the mask is recomputed on x_in
+        (the forward keeps no masked copy)."""
         r = self.layout.r
         Mk = self.Mk
         used = g.nmods * r
         a_off = gbase + g.a_off
         dA = self.grads[a_off: a_off + used * g.Kin].view(used, g.Kin)
-        # K splits measured per product on the 7B layer shapes (tools/lora_grads_sweep.py,
-        # profiles/r01/lora_grads_sweep.jsonl): dA 8 (4 for the 11008-wide down input); dB 4 for the
-        # multi-module groups, 8 for the single-module ones
-        # with LoRA dropout the mask is recomputed on x_in as it is staged (the forward keeps no masked copy)
+        b_off = gbase + g.b_off
+        dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
+        if self.wgrad_wgs > 0 and r % 16 == 0 and g.Rp in (64, 128):
+            sa, sb = self._wgrad_splits(g.Kin), self._wgrad_splits(g.nmods * g.Nmod)
+            ops.lora_wgrad(x_in[:Mk], gs[:Mk], dA, mode=0, s_cols=used, splits=sa, dropout=drop)
+            ops.lora_wgrad(dy[:Mk], u[:Mk], dB, mode=1, s_cols=used, splits=sb, nmod=g.Nmod, r=r)
+            return
+        # other ranks: the 64 x 64 f32-atomic tiles (K splits measured on the 7B shapes, profiles/r01/
+        # lora_grads_sweep.jsonl)
         sa_small, sa_big, sb_multi, sb_single = self._dadb_splits
         ops.gemm_f32acc(gs[:Mk, :used], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True,
                         k_splits=sa_big if g.Kin > 8192 else sa_small, b_dropout=drop)
-        b_off = gbase + g.b_off
-        dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
         ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=sb_multi if g.nmods > 1 else sb_single,
                         diag=(g.Nmod, r))
+
+    def _wgrad_splits(self, N: int) -> int:
+        """K-range splits of a LoRA weight-gradient stream: ~wgrad_wgs workgroups of 256-column stripes."""
+        stripes = max(1, N // 256)
+        return max(1, min(self.Mk // 64 // 4, round(self.wgrad_wgs / stripes)))
 
     # ------------------------------------------------------------ optimizer
     def grad_norm_sq(self) -> torch.Tensor:

@@ -257,6 +257,25 @@ def gemm_f32acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a_kmajor
     return out
 
 
+def lora_wgrad(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor, *, mode: int, s_cols: int, splits: int,
+               nmod: int = 0, r: int = 0, dropout: Optional[tuple] = None) -> torch.Tensor:
+    """LoRA weight gradients streamed over the big operand x [Mk, N] (ospo_lora_wgrad), fp32 atomics into out:
+    mode 0 (dA): out[j, n] += sum_m s[m, j] x[m, n], j < s_cols (s [Mk, Rp], Rp = 64 or 128);
+    mode 1 (dB): out[n, jr] += sum_m x[m, n] s[m, (n // nmod) * r + jr]  (block diagonal, out [N, r]).
+    dropout=(seed, p) (mode 0): x is masked with the adapter input's forward mask as it is read."""
+    _chk(x, BF16, "x")
+    _chk(s, BF16, "s")
+    _chk(out, torch.float32, "out")
+    K, N = x.shape
+    if s.shape[0] != K:
+        raise ValueError(f"lora_wgrad: {s.shape[0]} rows of s, {K} of x")
+    seed, p = dropout if dropout is not None else (0, 0.0)
+    ldc = _ld(out) if mode == 0 else 0
+    call("ospo_lora_wgrad", _p(x), _ld(x), N, _p(s), _ld(s), int(s_cols), K, int(mode), int(nmod), int(r), _p(out),
+         ldc, int(splits), int(seed) & 0xFFFFFFFF, float(p), _s())
+    return out
+
+
 def f32_to_bf16(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     _chk(src, torch.float32, "src")
     _chk(dst, BF16, "dst")

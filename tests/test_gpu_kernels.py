@@ -633,3 +633,48 @@ def test_flash_attention_bwd_5_product_form_equals_7(S, T, H):
     assert torch.equal(a[:, 2 * D:], b[:, 2 * D:])
     for i in range(2):
         assert relerr(a[:, i * D:(i + 1) * D].float(), b[:, i * D:(i + 1) * D].float()) < 4e-3
+
+
+@pytest.mark.parametrize("K,N,used,Rp,splits", [(4800, 4096, 48, 64, 8), (320, 11008, 16, 64, 2),
+                                                (640, 4096, 96, 128, 3), (192, 256, 32, 64, 1)])
+def test_lora_wgrad_da_exact_integers(K, N, used, Rp, splits):
+    """dA = g^T x streamed over x (ospo_lora_wgrad mode 0): exact on integer operands (every product and
+    partial sum is an integer below 2^24), all used rank rows, any split."""
+    x = ints(K, N)
+    g = ints(K, Rp)
+    out = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().lora_wgrad(x, g, out, mode=0, s_cols=used, splits=splits)
+    ref = g[:, :used].float().T @ x.float()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("nm,nmod,r,Rp,splits", [(3, 4096, 16, 64, 3), (2, 11008, 16, 64, 2), (1, 4096, 32, 64, 4),
+                                                 (3, 256, 32, 128, 1)])
+def test_lora_wgrad_db_blockdiag_exact_integers(nm, nmod, r, Rp, splits):
+    """dB = dy^T u (mode 1): each module's dy columns against its own r columns of u, peft layout [N, r]."""
+    K = 448
+    dy = ints(K, nm * nmod)
+    u = ints(K, Rp)
+    out = torch.zeros(nm * nmod, r, device=DEV, dtype=torch.float32)
+    ops().lora_wgrad(dy, u, out, mode=1, s_cols=nm * r, splits=splits, nmod=nmod, r=r)
+    full = dy.float().T @ u.float()
+    ref = torch.cat([full[i * nmod:(i + 1) * nmod, i * r:(i + 1) * r] for i in range(nm)], 0)
+    assert torch.equal(out, ref)
+
+
+def test_lora_wgrad_dropout_recompute_equals_stored_mask():
+    """mode 0 with dropout: x masked in registers with the forward skinny product's hash and bf16 rounding
+    == dA on the masked copy that product writes."""
+    p, seed, K, N = 0.05, 4242, 640, 4096
+    x = rnd(K, N)
+    g = rnd(K, 64)
+    xd = torch.empty_like(x)
+    u = torch.empty(K, 64, device=DEV, dtype=torch.bfloat16)
+    A = torch.zeros(64, N, device=DEV, dtype=torch.bfloat16)
+    ops().lora_skinny(x, A, u, K, K, N, 1, 0, 1.0, b_rows=16, dropout=(seed, p), xd=xd)
+    ref = torch.zeros(48, N, device=DEV, dtype=torch.float32)
+    ops().lora_wgrad(xd, g, ref, mode=0, s_cols=48, splits=1)
+    out = torch.zeros(48, N, device=DEV, dtype=torch.float32)
+    ops().lora_wgrad(x, g, out, mode=0, s_cols=48, splits=1, dropout=(seed, p))
+    assert torch.equal(out, ref)
+    assert relerr(out, (g[:, :48].float().T @ xd.float())) < 1e-5

@@ -10,9 +10,10 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ospo_amd import ops
 
-Mk, D, F, r, Rp = 4864, 4096, 11008, 16, 64
+Mk, D, F, r, Rp = 4800, 4096, 11008, 16, 64
 GROUPS = [("qkv", 3, D, D), ("o", 1, D, D), ("gu", 2, D, F), ("down", 1, F, D)]  # name, nmods, Kin, Nmod
 legacy = os.environ.get("OSPO_F32ACC_LEGACY") is not None
+STREAM = int(os.environ.get("OSPO_WGRAD_WGS", "0"))  # > 0: ospo_lora_wgrad with ~this many workgroups per product
 
 
 def main():
@@ -27,8 +28,14 @@ def main():
         dA = torch.zeros(Rp if legacy else used, kin, device="cuda")
         dB = torch.zeros(nm * nmod, r, device="cuda")
 
+        def splits(n):
+            return max(1, min(Mk // 64 // 4, round(STREAM / max(1, n // 256))))
+
         def run():
-            if legacy:
+            if STREAM:
+                ops.lora_wgrad(x, g, dA, mode=0, s_cols=used, splits=splits(kin))
+                ops.lora_wgrad(dy, u, dB, mode=1, s_cols=used, splits=splits(nm * nmod), nmod=nmod, r=r)
+            elif legacy:
                 ops.gemm_f32acc(g, x, dA, a_kmajor=True, b_kmajor=True, k_splits=min(Mk // 512, 16))
                 ops.gemm_f32acc(dy, u, dB, a_kmajor=True, b_kmajor=True, k_splits=min(Mk // 1024, 8), diag=(nmod, r))
             else:
@@ -44,8 +51,10 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 20 * 1e3
         tot += us
-        print(json.dumps({"group": name, "legacy": legacy, "dA+dB_us": round(us, 1)}), flush=True)
-    print(json.dumps({"legacy": legacy, "per_layer_us": round(tot, 1)}), flush=True)
+        gb = Mk * (kin + nm * nmod) * 2 / 1e9
+        print(json.dumps({"group": name, "legacy": legacy, "stream_wgs": STREAM, "dA+dB_us": round(us, 1),
+                          "GBps": round(gb / us * 1e6, 1)}), flush=True)
+    print(json.dumps({"legacy": legacy, "stream_wgs": STREAM, "per_layer_us": round(tot, 1)}), flush=True)
 
 
 if __name__ == "__main__":
