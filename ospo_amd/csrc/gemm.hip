@@ -1062,6 +1062,44 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
     }
   };
 
+  // SP >= 5 (bf16): the main (non-extension) tiles are staged by buffer_load_dwordx4 ... lds from per-lane
+  // byte offsets fixed for the whole launch, the K advance riding in the scalar soffset: no VALU address math
+  // and no per-piece operand selects in the loop (SP 6: the same schedule with the generic staging, for A/B).
+  static_assert(!(SP >= 5 && MX), "SP 5-7 are bf16 schedules");
+  constexpr bool FAST = (SP == 5 || SP == 7);  // buffer-offset staging of the main tiles
+  constexpr bool BAL = (SP == 5 || SP == 6);   // 4 + 4 refills per K-tile
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)args.A, 0, (int)((long)Mlast * args.lda * 2 + args.K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)args.B, 0, (int)((long)Nlast * args.ldb * 2 + args.K * 2), 0x00020000);
+  uint32_t voff[4][2] = {};
+  if constexpr (FAST) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool isA = h < 2;
+        const int row = (h & 1) * 128 + (wave * 2 + i) * 8 + rr8;
+        const int g = min((isA ? m0 : n0) + row, isA ? Mlast : Nlast);
+        voff[h][i] = (uint32_t)g * (uint32_t)(isA ? args.lda : args.ldb) * 2u + ((c8 ^ rr8) << 4);
+      }
+  }
+  auto is_ext = [&](int tl) { return abs_tile(tl) >= nt1; };
+  auto stage_fast = [&](int tl, int h) __attribute__((always_inline)) {
+    char* dst = smem + (tl & 1) * SLOT + h * HALF;
+    const int kb = abs_tile(tl) * (BK * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (LDS_AS void*)(dst + (wave * 2 + i) * 1024), 16,
+                                               voff[h][i], kb, 0, 0);
+  };
+  auto stage_any = [&](int tl, int h) __attribute__((always_inline)) {
+    if (FAST && !is_ext(tl))
+      stage_fast(tl, h);
+    else
+      stage_half(tl, h);
+  };
+
   f32x4 acc[4][4][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -1075,15 +1113,21 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   i32x8 b8sp[2][2];    // SP + MX: [B half][n]
 
   // prologue: tile 0 complete, A0 of tile 1 in flight (SP: tile 0 only)
+  if constexpr (BAL) {  // tile 0 complete; B0 B1 of tile 1 in flight (its A0 A1 are staged in R(0,0))
+    if (nt > 0) { stage_any(0, 2); stage_any(0, 3); stage_any(0, 0); stage_any(0, 1); }
+    if (nt > 1) { stage_any(1, 2); stage_any(1, 3); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
   if (nt > 0) {
     stage_scales(0);
-    stage_half(0, 2); stage_half(0, 3); stage_half(0, 1); stage_half(0, 0);
+    stage_any(0, 2); stage_any(0, 3); stage_any(0, 1); stage_any(0, 0);
   }
   if (!SP && nt > 1) stage_half(1, 0);
-  if (SP && nt > 1) { stage_scales(1); stage_half(1, 2); stage_half(1, 3); stage_half(1, 0); }
+  if (SP && nt > 1) { stage_scales(1); stage_any(1, 2); stage_any(1, 3); stage_any(1, 0); }
   if (!SP && nt > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if (SP && nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MX ? 7 : 6) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (g1) {  // the ping-pong offset
@@ -1123,8 +1167,8 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const char* la = slot + p * HALF;
-      if (SP == 3 && p == 0 && n1) stage_half(t + 1, 1);
-      if (SP == 3 && p == 1 && n2) { stage_scales(t + 2); stage_half(t + 2, 2); stage_half(t + 2, 3); stage_half(t + 2, 0); }
+      if (SP == 3 && p == 0 && n1) stage_any(t + 1, 1);
+      if (SP == 3 && p == 1 && n2) { stage_scales(t + 2); stage_any(t + 2, 2); stage_any(t + 2, 3); stage_any(t + 2, 0); }
       if constexpr (mx_tile) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1158,8 +1202,8 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
                                                                  mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
         }
       }
-      if (SP != 3 && p == 0 && n1) stage_half(t + 1, 1);
-      if (SP != 3 && p == 1 && n2) { stage_scales(t + 2); stage_half(t + 2, 2); stage_half(t + 2, 3); stage_half(t + 2, 0); }
+      if (SP != 3 && p == 0 && n1) stage_any(t + 1, 1);
+      if (SP != 3 && p == 1 && n2) { stage_scales(t + 2); stage_any(t + 2, 2); stage_any(t + 2, 3); stage_any(t + 2, 0); }
       if (g1) {
         if (p == 0) wait_sp(n1 ? KB + 2 : 0);         // A1(t)
         if (p == 1 && n1) wait_sp(n2 ? KB + 2 : 2);   // B0 B1 A0 (+ scales) of t+1
@@ -1220,7 +1264,81 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       asm volatile("" ::: "memory");
     }
   };
+  // SP 5/6: the SP intervals with the refills balanced 4 + 4 pieces per K-tile: A0 A1 of tile t+1 in R(t,0)
+  // (their slot halves were last read in R(t-1,.)), B0 B1 of tile t+2 in R(t,1).  Counted waits (before the
+  // barrier that opens g0's first read): A1(t) before R(t,1) -- 8 newer pieces (B(t+1), A(t+1)); A0 B of t+1
+  // before R(t+1,0) -- 6 newer (A1(t+1), B(t+2)).  STEADY: t+1 and t+2 exist and are main tiles, so the waits
+  // are constants and staging takes the fast path with no branch.
+  auto run_tile_sp5 = [&](int t, auto steady) __attribute__((always_inline)) {
+    constexpr bool ST = decltype(steady)::value;
+    const char* slot = smem + (t & 1) * SLOT;
+    const bool n1 = ST || t + 1 < nt, n2 = ST || t + 2 < nt;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const char* la = slot + p * HALF;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
+      if (p == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              bsp[h][n][s] = *reinterpret_cast<const bf16x8*>(slot + (2 + h) * HALF +
+                                                               mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+      }
+      if (ST && FAST) {
+        if (p == 0) { stage_fast(t + 1, 0); stage_fast(t + 1, 1); }
+        if (p == 1) { stage_fast(t + 2, 2); stage_fast(t + 2, 3); }
+      } else if (ST) {
+        if (p == 0) { stage_half(t + 1, 0); stage_half(t + 1, 1); }
+        if (p == 1) { stage_half(t + 2, 2); stage_half(t + 2, 3); }
+      } else {
+        if (p == 0 && n1) { stage_any(t + 1, 0); stage_any(t + 1, 1); }
+        if (p == 1 && n2) { stage_any(t + 2, 2); stage_any(t + 2, 3); }
+      }
+      auto waits = [&]() __attribute__((always_inline)) {
+        if (ST) {
+          if (p == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+          if (p == 0) wait_vmcnt_exact(n1 ? 8 : 0);
+          if (p == 1 && n1) wait_vmcnt_exact(n2 ? 6 : 2);
+        }
+      };
+      if (g1) waits();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = 2 * p + q;
+        const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              acc[j][i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bsp[ib][n][s], af[i][s], acc[j][i][n], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (!g1) waits();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  };
   auto run_tile = [&](int t, auto mxt) __attribute__((always_inline)) {
+    if constexpr (BAL) {
+      run_tile_sp5(t, std::integral_constant<bool, false>{});
+      return;
+    }
     if constexpr (SP) {
       run_tile_sp(t, mxt);
       return;
@@ -1367,6 +1485,12 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
     const int main_end = DROP ? nt : min(nt, max(pre, nt1 - tb));
     for (int t = pre; t < main_end; ++t) run_tile(t, MXT{});
     for (int t = main_end; t < nt; ++t) run_tile(t, BFT{});
+  } else if constexpr (BAL) {
+    // steady tiles: t+1 and t+2 exist and are main tiles (non-dropout: the extension tiles come last)
+    const int main_lim = DROP ? nt : min(nt, max(0, nt1 - tb));
+    int t = pre;
+    for (; t < main_lim - 2; ++t) run_tile_sp5(t, std::integral_constant<bool, true>{});
+    for (; t < nt; ++t) run_tile_sp5(t, std::integral_constant<bool, false>{});
   } else {
     for (int t = pre; t < nt; ++t) run_tile(t, BFT{});
   }
@@ -1515,6 +1639,10 @@ DeviceState& dev_state() {
 template <int DBG = 0, bool DROP = false, bool MX = false, int SP = 0>
 int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
+  if constexpr (SP == 5 || SP == 7) {  // 32-bit buffer offsets: operands beyond 2 GiB take the generic staging
+    if ((long)a.M * a.lda * 2 >= (1L << 31) || (long)a.N * a.ldb * 2 >= (1L << 31))
+      return launch_v5<DBG, DROP, MX, (SP == 5 ? 6 : 1)>(a, s, allow_split);
+  }
   const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
   const int ntot = (MX ? a.K / 128 : a.K / BK) + a.K2 / BK;
   DeviceState& ds = dev_state();
@@ -1578,6 +1706,19 @@ int g_gemm_variant = 0;  // 0 = SP schedule + split-K tail (default); 17 = the 8
 constexpr int g_gemm_variant = 0;  // the product library runs the default schedule only
 #endif
 
+// the bf16 256 x 256 schedule every entry point runs (the ablation build can switch it for A/B)
+template <bool DROP>
+int launch_default(const GemmArgs& a, hipStream_t s) {
+#ifdef OSPO_ABLATION
+  if (g_gemm_variant == 17) return launch_v5<0, DROP>(a, s);
+  if (g_gemm_variant == 14) return launch_v5<0, DROP, false, 1>(a, s);
+  if (g_gemm_variant == 24) return launch_v5<0, DROP, false, 5>(a, s);
+  if (g_gemm_variant == 25) return launch_v5<0, DROP, false, 6>(a, s);
+  if (g_gemm_variant == 26) return launch_v5<0, DROP, false, 7>(a, s);
+#endif
+  return launch_v5<0, DROP, false, 5>(a, s);
+}
+
 // NT tile: 256 x 256 (8-phase, split-K tail) whenever N % 256 == 0, else the 64 x 64 simple kernel.
 int pick_nt_tile(int M, int N) {
   (void)M;
@@ -1604,7 +1745,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   const int tile = pick_nt_tile(M, N);
   if (tile == 64) return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
 #ifndef OSPO_ABLATION
-  return launch_v5<0, false, false, 1>(a, stream, true);  // SP + split-K tail
+  return launch_v5<0, false, false, 5>(a, stream, true);  // SP (4 + 4 refills, buffer-offset staging) + split-K tail
 #else
   switch (g_gemm_variant) {
     // A/B alternatives (tools/gemm_bench.py); results identical, schedules differ
@@ -1619,13 +1760,16 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 12: return launch_v5<1>(a, stream, false);
     case 13: return launch_v5<2>(a, stream, false);
     // SP schedule (2 phases of 32 MFMAs per K-tile): 14 + split tail, 15 no loads, 16 no MFMA
-    case 14: return launch_v5<0, false, false, 1>(a, stream, true);
+    case 14: return launch_v5<0, false, false, 1>(a, stream, true);  // SP1 (2 + 6 refills, generic staging)
     case 15: return launch_v5<1, false, false, 1>(a, stream, false);
     case 16: return launch_v5<2, false, false, 1>(a, stream, false);
     case 18: return launch_v5<0, false, false, 2>(a, stream, true);  // SP without s_setprio
     case 19: return launch_v5<0, false, false, 3>(a, stream, true);  // SP, refills ahead of the reads
+    case 24: return launch_v5<0, false, false, 5>(a, stream, true);  // SP, 4 + 4 refills, buffer-offset staging
+    case 25: return launch_v5<0, false, false, 6>(a, stream, true);  // SP, 4 + 4 refills, generic staging
+    case 26: return launch_v5<0, false, false, 7>(a, stream, true);  // SP, 2 + 6 refills, buffer-offset staging
     case 17: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
-    default: return launch_v5<0, false, false, 1>(a, stream, true);               // SP + split-K tail
+    default: return launch_v5<0, false, false, 5>(a, stream, true);               // SP5 + split-K tail
   }
 #endif
 }
@@ -1656,7 +1800,7 @@ extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int
   a.rope_T = T;
   a.rope_cols = rope_cols;
   // split-K tail fixups apply the RoPE epilogue too
-  return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, 1>(a, stream);
+  return launch_default<false>(a, stream);
 }
 
 extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
@@ -1673,12 +1817,12 @@ extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, 
   GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
              M, N, K, K2, 1.f, nullptr, nullptr, 0, C, ldc, 1, 0, 0};
   if (drop_p == 0.f)
-    return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, 1>(a, stream);
+    return launch_default<false>(a, stream);
   a.drop_seed = drop_seed;
   a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = N;
-  return g_gemm_variant == 17 ? launch_v5<0, true>(a, stream) : launch_v5<0, true, false, 1>(a, stream);
+  return launch_default<true>(a, stream);
 }
 
 extern "C" int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* B, int ldb, int M, int F, int K,
@@ -1703,12 +1847,12 @@ extern "C" int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* 
   a.ld_gu = ld_gu;
   a.ld_dgu = ld_dgu;
   if (drop_p == 0.f)
-    return g_gemm_variant == 17 ? launch_v5<0>(a, stream) : launch_v5<0, false, false, 1>(a, stream);
+    return launch_default<false>(a, stream);
   a.drop_seed = drop_seed;
   a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = F;
-  return g_gemm_variant == 17 ? launch_v5<0, true>(a, stream) : launch_v5<0, true, false, 1>(a, stream);
+  return launch_default<true>(a, stream);
 }
 
 extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, int ldb, const void* Bsc,
@@ -1769,7 +1913,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || v > 19 || (v > 5 && v < 10)) return OSPO_ERR_ARG;
+  if (v < 0 || v > 26 || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23) return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;

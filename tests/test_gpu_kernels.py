@@ -55,6 +55,26 @@ def test_gemm_nt_exact_integers(M, N, K):
     assert torch.equal(out.float(), ref_bf), (out.float() - ref_bf).abs().max()
 
 
+@pytest.mark.parametrize("M,N,K,K2,split", [(4800, 4096, 4096, 64, 0), (4800, 4096, 4096, 64, 3),
+                                            (1000, 2048, 1024, 128, 2), (777, 1280, 320, 64, 0),
+                                            (4608, 4096, 2048, 0, 4)])
+def test_gemm_nt_schedule_exact_integers_long_k(M, N, K, K2, split):
+    """The default 256x256 schedule over many K-tiles (steady loop), the LoRA extension tiles after the main
+    ones, ragged M and split-K tails (workgroups whose K-range starts mid-way): exact on small integers."""
+    from ospo_amd._lib import call
+    a, b = ints(M, K, lo=-2, hi=3), ints(N, K, lo=-2, hi=3)
+    a2 = ints(M, K2) if K2 else None
+    b2 = ints(N, K2) if K2 else None
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    try:
+        call("ospo_gemm_force_split", split)
+        ops().gemm_nt(a, b, out, a2=a2, b2=b2)
+    finally:
+        call("ospo_gemm_force_split", 0)
+    ref = a.double() @ b.double().T + (a2.double() @ b2.double().T if K2 else 0)
+    assert torch.equal(out.float(), bf(ref.float()).float()), (out.float() - ref.float()).abs().max()
+
+
 def test_gemm_nt_asymmetric_identity():
     """A = I-like selector with an asymmetric B catches a transposed C write."""
     M = N = K = 256
