@@ -16,6 +16,8 @@ extern "C" {
  * 2 / 8 / 16 / 4 of the default; 10-13, 15, 16 = decompositions (results INVALID: no loads /
  * no MFMA). */
 int ospo_set_gemm_variant(int variant);
+/* variant 29 (s_memtime stamps of one steady K-tile): 16 uint32 per wave, [grid][8 waves][16] */
+int ospo_gemm_set_debug_buffer(void* buf);
 /* LoRA skinny products: 1 = 16-row loop, 2 = 64-row LDS-shared, 3 = 2 with K splits of whole chunks (default). */
 int ospo_set_skinny_variant(int v);
 /* Decode GEMV schedule: 1 = skinny loop, 2 = LDS-shared activations, 3 = the same with 128 weight

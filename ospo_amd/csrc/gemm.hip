@@ -137,6 +137,7 @@ struct GemmArgs {
   const bf16* swg_gu = nullptr;
   bf16* swg_dgu = nullptr;
   int ld_gu = 0, ld_dgu = 0;
+  uint32_t* dbg = nullptr;  // ablation build, DBG 4: per-wave s_memtime stamps of one K-tile
 };
 
 // the SwiGLU-backward store of 8 product columns (row m, columns n..n+7 of F = args.N)
@@ -1066,8 +1067,10 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   // byte offsets fixed for the whole launch, the K advance riding in the scalar soffset: no VALU address math
   // and no per-piece operand selects in the loop (SP 6: the same schedule with the generic staging, for A/B).
   static_assert(!(SP >= 5 && MX), "SP 5-7 are bf16 schedules");
-  constexpr bool FAST = (SP == 5 || SP == 7);  // buffer-offset staging of the main tiles
-  constexpr bool BAL = (SP == 5 || SP == 6);   // 4 + 4 refills per K-tile
+  constexpr bool FAST = (SP == 5 || SP == 7 || SP == 8 || SP == 9);  // buffer-offset staging of the main tiles
+  constexpr bool BAL = (SP == 5 || SP == 6 || SP == 8 || SP == 9);  // 4 + 4 refills per K-tile
+  constexpr bool UNR2 = (SP == 8 || SP == 9);             // steady loop unrolled by 2 (slot parity constant)
+  constexpr bool EARLYB = (SP == 9);                      // B0 of tile t+1 read in R(t,1): 12 + 12 fragment reads
   const __amdgpu_buffer_rsrc_t rsA =
       __builtin_amdgcn_make_buffer_rsrc((void*)args.A, 0, (int)((long)Mlast * args.lda * 2 + args.K * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
@@ -1085,8 +1088,8 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       }
   }
   auto is_ext = [&](int tl) { return abs_tile(tl) >= nt1; };
-  auto stage_fast = [&](int tl, int h) __attribute__((always_inline)) {
-    char* dst = smem + (tl & 1) * SLOT + h * HALF;
+  auto stage_fast = [&](int tl, int h, int par = -1) __attribute__((always_inline)) {
+    char* dst = smem + (par >= 0 ? par : (tl & 1)) * SLOT + h * HALF;
     const int kb = abs_tile(tl) * (BK * 2);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1100,6 +1103,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       stage_half(tl, h);
   };
 
+  uint32_t stp[2][5] = {};  // DBG 4
   f32x4 acc[4][4][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -1109,6 +1113,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       for (int j = 0; j < 2; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bfr[2][2];
   bf16x8 bsp[2][2][2];  // SP: [B half][n][k-substep], the whole K-tile's B fragments
+  bf16x8 b0n[2][2];     // SP 9: B0 fragments of the next K-tile
   i32x8 a8[4], b8[2];  // MX tiles: both k-halves of a fragment in one 8-register operand
   i32x8 b8sp[2][2];    // SP + MX: [B half][n]
 
@@ -1133,6 +1138,13 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   if (g1) {  // the ping-pong offset
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+  }
+  if constexpr (EARLYB) {  // B0 of tile 0 (landed per the prologue wait; retired by the first lgkmcnt(0))
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        b0n[n][s] = *reinterpret_cast<const bf16x8*>(smem + 2 * HALF + mmaj_off(wn * 32 + n * 16 + (lane & 15), 4 * s + (lane >> 4)));
   }
 
   const int frow = lane & 15, fcol = lane >> 4;
@@ -1269,19 +1281,47 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   // barrier that opens g0's first read): A1(t) before R(t,1) -- 8 newer pieces (B(t+1), A(t+1)); A0 B of t+1
   // before R(t+1,0) -- 6 newer (A1(t+1), B(t+2)).  STEADY: t+1 and t+2 exist and are main tiles, so the waits
   // are constants and staging takes the fast path with no branch.
-  auto run_tile_sp5 = [&](int t, auto steady) __attribute__((always_inline)) {
+  auto run_tile_sp5 = [&](int t, auto steady, auto parity) __attribute__((always_inline)) {
     constexpr bool ST = decltype(steady)::value;
-    const char* slot = smem + (t & 1) * SLOT;
+    constexpr int PAR = decltype(parity)::value;  // slot parity of tile t when known at compile time, else -1
+    const char* slot = smem + (PAR >= 0 ? PAR : (t & 1)) * SLOT;
     const bool n1 = ST || t + 1 < nt, n2 = ST || t + 2 < nt;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
+      uint32_t st_raw[5];
+#define STAMP(k)                                                       \
+  if constexpr (DBG == 4 && ST && PAR == 0) {                           \
+    __builtin_amdgcn_sched_barrier(0);                                  \
+    st_raw[k] = (uint32_t)__builtin_amdgcn_s_memtime();                 \
+    __builtin_amdgcn_sched_barrier(0);                                  \
+  }
+      STAMP(0);
       const char* la = slot + p * HALF;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s = 0; s < 2; ++s)
           af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
-      if (p == 0) {
+      if (EARLYB) {
+        if (p == 0) {  // B0(t) came with R(t-1,1); B1(t) now
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              bsp[0][n][s] = b0n[n][s];
+              bsp[1][n][s] = *reinterpret_cast<const bf16x8*>(slot + 3 * HALF +
+                                                               mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+            }
+        } else if (n1) {
+          const char* nslot = smem + (PAR >= 0 ? 1 - PAR : ((t + 1) & 1)) * SLOT;
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              b0n[n][s] = *reinterpret_cast<const bf16x8*>(nslot + 2 * HALF +
+                                                          mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+        }
+      } else if (p == 0) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1292,8 +1332,8 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
                                                                mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
       }
       if (ST && FAST) {
-        if (p == 0) { stage_fast(t + 1, 0); stage_fast(t + 1, 1); }
-        if (p == 1) { stage_fast(t + 2, 2); stage_fast(t + 2, 3); }
+        if (p == 0) { stage_fast(t + 1, 0, PAR >= 0 ? 1 - PAR : -1); stage_fast(t + 1, 1, PAR >= 0 ? 1 - PAR : -1); }
+        if (p == 1) { stage_fast(t + 2, 2, PAR); stage_fast(t + 2, 3, PAR); }
       } else if (ST) {
         if (p == 0) { stage_half(t + 1, 0); stage_half(t + 1, 1); }
         if (p == 1) { stage_half(t + 2, 2); stage_half(t + 2, 3); }
@@ -1303,18 +1343,20 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       }
       auto waits = [&]() __attribute__((always_inline)) {
         if (ST) {
-          if (p == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          if (p == 0 && !EARLYB) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // EARLYB p 0: A1(t) and B0(t+1)
         } else {
-          if (p == 0) wait_vmcnt_exact(n1 ? 8 : 0);
+          if (p == 0) wait_vmcnt_exact(n1 ? (EARLYB ? 6 : 8) : 0);
           if (p == 1 && n1) wait_vmcnt_exact(n2 ? 6 : 2);
         }
       };
       if (g1) waits();
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      STAMP(1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      STAMP(2);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -1329,14 +1371,21 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
               acc[j][i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bsp[ib][n][s], af[i][s], acc[j][i][n], 0, 0, 0);
       }
       __builtin_amdgcn_s_setprio(0);
+      STAMP(3);
       if (!g1) waits();
+      STAMP(4);
+      if constexpr (DBG == 4 && ST && PAR == 0) {  // commit (only memtimes are pending here)
+        const bool rec = (t == 8);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) stp[p][k] = rec ? st_raw[k] : stp[p][k];
+      }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
   };
   auto run_tile = [&](int t, auto mxt) __attribute__((always_inline)) {
     if constexpr (BAL) {
-      run_tile_sp5(t, std::integral_constant<bool, false>{});
+      run_tile_sp5(t, std::integral_constant<bool, false>{}, std::integral_constant<int, -1>{});
       return;
     }
     if constexpr (SP) {
@@ -1488,9 +1537,19 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   } else if constexpr (BAL) {
     // steady tiles: t+1 and t+2 exist and are main tiles (non-dropout: the extension tiles come last)
     const int main_lim = DROP ? nt : min(nt, max(0, nt1 - tb));
+    using STT = std::integral_constant<bool, true>;
+    using STF = std::integral_constant<bool, false>;
+    using PRT = std::integral_constant<int, -1>;
     int t = pre;
-    for (; t < main_lim - 2; ++t) run_tile_sp5(t, std::integral_constant<bool, true>{});
-    for (; t < nt; ++t) run_tile_sp5(t, std::integral_constant<bool, false>{});
+    if constexpr (UNR2) {
+      if ((t & 1) && t < main_lim - 2) run_tile_sp5(t++, STT{}, PRT{});
+      for (; t + 1 < main_lim - 2; t += 2) {
+        run_tile_sp5(t, STT{}, std::integral_constant<int, 0>{});
+        run_tile_sp5(t + 1, STT{}, std::integral_constant<int, 1>{});
+      }
+    }
+    for (; t < main_lim - 2; ++t) run_tile_sp5(t, STT{}, PRT{});
+    for (; t < nt; ++t) run_tile_sp5(t, STF{}, PRT{});
   } else {
     for (int t = pre; t < nt; ++t) run_tile(t, BFT{});
   }
@@ -1500,6 +1559,9 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (DBG == 4) {
+    if (args.dbg && lane < 10) args.dbg[((long)blockIdx.x * 8 + wave) * 16 + lane] = stp[lane / 5][lane % 5];
+  }
 
   // epilogue: quadrant j, frag (i, n): D[n][m] -> lane holds m = l16, n = 4g..4g+3
   const int g = lane >> 4, l16 = lane & 15;
@@ -1639,7 +1701,7 @@ DeviceState& dev_state() {
 template <int DBG = 0, bool DROP = false, bool MX = false, int SP = 0>
 int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
-  if constexpr (SP == 5 || SP == 7) {  // 32-bit buffer offsets: operands beyond 2 GiB take the generic staging
+  if constexpr (SP == 5 || SP >= 7) {  // 32-bit buffer offsets: operands beyond 2 GiB take the generic staging
     if ((long)a.M * a.lda * 2 >= (1L << 31) || (long)a.N * a.ldb * 2 >= (1L << 31))
       return launch_v5<DBG, DROP, MX, (SP == 5 ? 6 : 1)>(a, s, allow_split);
   }
@@ -1701,6 +1763,7 @@ int launch_v3(const GemmArgs& a, hipStream_t s) {
 }
 
 #ifdef OSPO_ABLATION
+uint32_t* g_dbg_buf = nullptr;  // variant 29: s_memtime stamps, 16 words per wave
 int g_gemm_variant = 0;  // 0 = SP schedule + split-K tail (default); 17 = the 8-phase schedule; others: A/B, see dispatch
 #else
 constexpr int g_gemm_variant = 0;  // the product library runs the default schedule only
@@ -1715,8 +1778,10 @@ int launch_default(const GemmArgs& a, hipStream_t s) {
   if (g_gemm_variant == 24) return launch_v5<0, DROP, false, 5>(a, s);
   if (g_gemm_variant == 25) return launch_v5<0, DROP, false, 6>(a, s);
   if (g_gemm_variant == 26) return launch_v5<0, DROP, false, 7>(a, s);
+  if (g_gemm_variant == 27) return launch_v5<0, DROP, false, 8>(a, s);
+  if (g_gemm_variant == 28) return launch_v5<0, DROP, false, 9>(a, s);
 #endif
-  return launch_v5<0, DROP, false, 5>(a, s);
+  return launch_v5<0, DROP, false, 8>(a, s);
 }
 
 // NT tile: 256 x 256 (8-phase, split-K tail) whenever N % 256 == 0, else the 64 x 64 simple kernel.
@@ -1745,7 +1810,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   const int tile = pick_nt_tile(M, N);
   if (tile == 64) return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
 #ifndef OSPO_ABLATION
-  return launch_v5<0, false, false, 5>(a, stream, true);  // SP (4 + 4 refills, buffer-offset staging) + split-K tail
+  return launch_v5<0, false, false, 8>(a, stream, true);  // SP8 (4 + 4 refills, buffer-offset staging, 2-tile unroll) + split-K tail
 #else
   switch (g_gemm_variant) {
     // A/B alternatives (tools/gemm_bench.py); results identical, schedules differ
@@ -1765,11 +1830,14 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 16: return launch_v5<2, false, false, 1>(a, stream, false);
     case 18: return launch_v5<0, false, false, 2>(a, stream, true);  // SP without s_setprio
     case 19: return launch_v5<0, false, false, 3>(a, stream, true);  // SP, refills ahead of the reads
-    case 24: return launch_v5<0, false, false, 5>(a, stream, true);  // SP, 4 + 4 refills, buffer-offset staging
+    case 24: return launch_v5<0, false, false, 5>(a, stream, true);  // SP5: 4 + 4 refills, buffer-offset staging
     case 25: return launch_v5<0, false, false, 6>(a, stream, true);  // SP, 4 + 4 refills, generic staging
     case 26: return launch_v5<0, false, false, 7>(a, stream, true);  // SP, 2 + 6 refills, buffer-offset staging
+    case 27: return launch_v5<0, false, false, 8>(a, stream, true);  // SP5 unrolled by 2
+    case 28: return launch_v5<0, false, false, 9>(a, stream, true);  // SP8 + B0 of the next tile read early
+    case 29: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<4, false, false, 8>(d, stream, false); }  // SP8 + stamps
     case 17: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
-    default: return launch_v5<0, false, false, 5>(a, stream, true);               // SP5 + split-K tail
+    default: return launch_v5<0, false, false, 8>(a, stream, true);               // SP8 + split-K tail
   }
 #endif
 }
@@ -1906,6 +1974,11 @@ extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {
 }
 
 #ifdef OSPO_ABLATION
+extern "C" int ospo_gemm_set_debug_buffer(void* p) {
+  g_dbg_buf = (uint32_t*)p;
+  return OSPO_OK;
+}
+
 extern "C" int ospo_set_gemm_variant(int v) {
   if (v >= 20 && v <= 23) {  // L2 row-group size of the default schedule: 2, 8, 16, 4
     const int gms[4] = {2, 8, 16, 4};
@@ -1913,7 +1986,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || v > 26 || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23) return OSPO_ERR_ARG;
+  if (v < 0 || v > 29 || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23) return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;
