@@ -275,6 +275,164 @@ __global__ void skinny2_reduce_kernel(const float* __restrict__ ws, int splits, 
   *reinterpret_cast<uint2*>(out + (long)m * ldo + c) = pk;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// v3: the activation streamed through LDS in whole 128-B lines.  v2 loaded each lane's 16 B straight
+// into its MFMA fragment, so a wave instruction touched 16 rows x 64 B (half lines): the texture path,
+// not HBM, set its rate.  Here a workgroup (4 waves, 64 rows) walks its K range in chunks of 64
+// (one 128-B line per row): each chunk is 8 LDS-DMA pieces of 8 rows x 128 B (buffer_load ... lds from
+// launch-constant per-lane offsets, the K advance in soffset), XOR-swizzled by row so the 16-row
+// fragment reads are conflict-free, in an NS-stage ring with NS - 1 chunks in flight.  The Bt rows
+// of the workgroup's tiles ride in the same stage (padded to 2 / 4 / 8 tiles so every wave issues the
+// same number of pieces and the counted waits are uniform).  Split-K partials as v2.
+template <int NT>
+struct Sk3Cfg {
+  static constexpr int NTP = NT <= 2 ? 2 : (NT <= 4 ? 4 : 8);  // staged Bt tiles
+  static constexpr int BPW = NTP / 2;                           // Bt pieces per wave per chunk
+  static constexpr int PW = 2 + BPW;                            // pieces per wave per chunk
+  static constexpr int NS = 4;                                  // ring stages
+  static constexpr int STAGE = 8192 + NTP * 2048;               // A 64 x 128 B + Bt 16 NTP x 128 B
+};
+
+// (a device function: hipcc's host pass drops the kernel's launch stub when this builtin sits in the
+// kernel body itself inside a loop)
+__device__ __forceinline__ void sk3_lds16(__amdgpu_buffer_rsrc_t rs, char* dst, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ void sk3_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+
+template <int NT, bool DROP>
+__global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A, int lda, int a_bytes,
+                                                      const bf16* __restrict__ Bt, int ldb, int b_rows, int b_bytes,
+                                                      int M, int M_out, int K, int kper, int a_koff, int tiles_total,
+                                                      float scale, bf16* __restrict__ out, int ldo, int out_cols,
+                                                      float* __restrict__ ws, int M_pad, uint32_t dseed,
+                                                      uint32_t dthresh, float dscale) {
+  using C = Sk3Cfg<NT>;
+  __shared__ __attribute__((aligned(16))) char smem[C::NS * C::STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4, r8 = lane >> 3, c8 = lane & 7;
+  const int m0 = blockIdx.x * 64;
+  const int z = blockIdx.y, splits = gridDim.y, mod = blockIdx.z;
+  const int tbase = mod * NT;
+  const int k_begin = z * kper, k_end = min(K, k_begin + kper);
+  const int nch = (k_end - k_begin + 63) >> 6;  // K % 64 == 0 (host check)
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, b_bytes, 0x00020000);
+  // per-lane byte offsets of this wave's pieces (rows clamped; the swizzled 16-B chunk of the row)
+  uint32_t va[2], vb[C::BPW];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + r8;
+    const int gr = min(m0 + row, M - 1);
+    va[i] = ((uint32_t)gr * (uint32_t)lda + (uint32_t)(mod * a_koff) + (uint32_t)k_begin) * 2u + ((c8 ^ r8) << 4);
+  }
+#pragma unroll
+  for (int i = 0; i < C::BPW; ++i) {
+    const int row = (wave * C::BPW + i) * 8 + r8;
+    const int br = min(16 * tbase + row, b_rows - 1);
+    vb[i] = ((uint32_t)br * (uint32_t)ldb + (uint32_t)k_begin) * 2u + ((c8 ^ r8) << 4);
+  }
+#define SK3_STAGE(cc)                                                                                            \
+  {                                                                                                              \
+    char* st_ = smem + ((cc) % C::NS) * C::STAGE;                                                               \
+    const int kb_ = (cc) * 128;                                                                                  \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                                \
+        sk3_lds16(rsA, st_ + (wave * 2 + i) * 1024, va[i], kb_);                                                 \
+    _Pragma("unroll") for (int i = 0; i < C::BPW; ++i)                                                           \
+        sk3_lds16(rsB, st_ + 8192 + (wave * C::BPW + i) * 1024, vb[i], kb_);                                     \
+  }
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow_l = wave * 16 + l16;  // this lane's fragment row in the 64-row block
+  const uint32_t drow = (uint32_t)min(m0 + arow_l, M - 1) * (uint32_t)K;
+  bool bok[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) bok[j] = 16 * (tbase + j) + l16 < b_rows;
+
+#pragma unroll
+  for (int j = 0; j < C::NS - 1; ++j)
+    if (j < nch) SK3_STAGE(j);
+  for (int c = 0; c < nch; ++c) {
+    sk3_wait(C::PW * min(C::NS - 2, nch - 1 - c));  // this wave's pieces of chunk c landed
+    __builtin_amdgcn_s_barrier();                    // everyone's; and chunk c-1's slot is free
+    asm volatile("" ::: "memory");
+    if (c + C::NS - 1 < nch) SK3_STAGE(c + C::NS - 1);
+    const char* st = smem + (c % C::NS) * C::STAGE;
+    bf16x8 a[2], b[2][NT];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int q = 4 * s + g;  // 16-B chunk of the 128-B line
+      a[s] = *reinterpret_cast<const bf16x8*>(st + arow_l * 128 + ((q ^ (arow_l & 7)) << 4));
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int br = 16 * j + l16;
+        b[s][j] = *reinterpret_cast<const bf16x8*>(st + 8192 + br * 128 + ((q ^ (br & 7)) << 4));
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 av = a[s];
+      if constexpr (DROP) {
+        const uint32_t k0 = (uint32_t)(k_begin + 64 * c + 32 * s + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool keep = drop_hash(drow + k0 + (uint32_t)e, dseed) >= dthresh;
+          av[e] = keep ? f2bf(bf2f(av[e]) * dscale) : f2bf(0.f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = MFMA(bok[j] ? b[s][j] : bf16x8{}, av, acc[j]);  // D[16j+4g+q][m]
+    }
+  }
+  const int m = m0 + arow_l;
+  const int ctot = 16 * tiles_total;
+  if (splits > 1) {
+    if (m < M_pad) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        *reinterpret_cast<f32x4*>(ws + ((long)z * M_pad + m) * ctot + 16 * (tbase + j) + 4 * g) = acc[j];
+    }
+    return;
+  }
+  if (m < M_out) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      uint2 pk;
+      if (m < M) {
+        pk.x = pack2(acc[j][0] * scale, acc[j][1] * scale);
+        pk.y = pack2(acc[j][2] * scale, acc[j][3] * scale);
+      } else {
+        pk.x = pk.y = 0u;
+      }
+      *reinterpret_cast<uint2*>(out + (long)m * ldo + 16 * (tbase + j) + 4 * g) = pk;
+    }
+    if (mod == gridDim.z - 1 && g == 0) {
+      for (int cc = ctot; cc < out_cols; ++cc) out[(long)m * ldo + cc] = f2bf(0.f);
+    }
+  }
+}
 }  // namespace
 
 // K splits: enough workgroups to keep every CU streaming (>= ~4 per CU), each
@@ -294,9 +452,11 @@ struct SkDropArgs {
 };
 
 #ifdef OSPO_ABLATION
-static int g_skinny_variant = 3;  // 1 = 16-row skinny loop, 2 = 64-row LDS-shared, 3 = 2 with whole-chunk splits (default)
+static int g_skinny_variant = 4;  // 1 = 16-row skinny loop, 2 = 64-row LDS-shared, 3 = 2 with whole-chunk splits, 4 = v3 (default)
+static int g_sk3_wgs = 512;       // v3: target workgroups per launch
 #else
-constexpr int g_skinny_variant = 3;  // the product library runs the whole-chunk-split v2 kernels
+constexpr int g_skinny_variant = 4;  // the product library runs v3 (v2 where v3's 32-bit buffer offsets do not reach)
+constexpr int g_sk3_wgs = 512;
 #endif
 
 // v2 K split: ~1024 workgroups over (64-row blocks x modules), each split >= one chunk.
@@ -332,12 +492,26 @@ extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
     }
     if (nz == n_tiles) break;
   }
+  // v3: at most max(g_sk3_wgs, 1024) workgroups' worth of splits over one module's row blocks
+  {
+    const long blocks = (M_out + 63) / 64;
+    const long wgs = g_sk3_wgs > 1024 ? g_sk3_wgs : 1024;
+    long sp3 = (wgs + blocks - 1) / blocks;
+    sp3 = sp3 > K / 64 ? K / 64 : sp3;
+    const size_t b = sp3 > 1 ? (size_t)sp3 * (size_t)((M_out + 63) / 64 * 64) * 16 * n_tiles * 4 : 0;
+    v2 = b > v2 ? b : v2;
+  }
   return (v1 > v2 ? v1 : v2) + 16;
 }
 
 #ifdef OSPO_ABLATION
 extern "C" int ospo_set_skinny_variant(int v) {
-  if (v < 1 || v > 3) return OSPO_ERR_ARG;
+  if (v >= 100) {  // v3 with a target of v - 100 workgroups per launch
+    g_skinny_variant = 4;
+    g_sk3_wgs = v - 100;
+    return OSPO_OK;
+  }
+  if (v < 1 || v > 4) return OSPO_ERR_ARG;
   g_skinny_variant = v;
   return OSPO_OK;
 }
@@ -359,6 +533,42 @@ static int launch_skinny2(const bf16* a, int lda, const bf16* b, int ldb, int b_
   else
     hipLaunchKernelGGL((skinny2_kernel<NT, false>), grid, dim3(256), 0, stream, a, lda, b, ldb, b_rows, M, M_out, K,
                        kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad, 0u, 0u, 0.f, nullptr, 0);
+  OSPO_CHECK_LAUNCH();
+  if (splits > 1) {
+    const long n = (long)M_out * (out_cols / 4);
+    hipLaunchKernelGGL(skinny2_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, part, splits,
+                       M, M_out, M_pad, 16 * tiles_total, scale, o, ldo, out_cols);
+    OSPO_CHECK_LAUNCH();
+  }
+  return OSPO_OK;
+}
+
+
+// v3 split: ~2 workgroups per CU over (64-row blocks x modules), whole 64-k chunks per split
+template <int NT>
+static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_rows, int M, int M_out, int K,
+                          int a_koff, int nz, int tiles_total, float scale, bf16* o, int ldo, int out_cols, float* part,
+                          size_t ws_bytes, hipStream_t stream, const SkDropArgs& dr) {
+  const int blocks = (M_out + 63) / 64 * nz;
+  const int chunks = K / 64;
+  int splits = (g_sk3_wgs + blocks - 1) / blocks;
+  splits = splits < 1 ? 1 : (splits > chunks ? chunks : splits);
+  const int cps = (chunks + splits - 1) / splits;
+  const int kper = cps * 64;
+  splits = (K + kper - 1) / kper;
+  const int M_pad = (M_out + 63) / 64 * 64;
+  if (splits > 1 && ws_bytes < (size_t)splits * M_pad * 16 * tiles_total * 4) return OSPO_ERR_SHAPE;
+  const long a_bytes = (long)(M - 1) * lda * 2 + (long)((nz - 1) * a_koff + K) * 2;
+  const long b_bytes = (long)(b_rows - 1) * ldb * 2 + (long)K * 2;
+  const dim3 grid(M_pad / 64, splits, nz);
+  if (dr.scale > 0.f)
+    hipLaunchKernelGGL((skinny3_kernel<NT, true>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb, b_rows,
+                       (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad,
+                       dr.seed, dr.thresh, dr.scale);
+  else
+    hipLaunchKernelGGL((skinny3_kernel<NT, false>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb, b_rows,
+                       (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad, 0u,
+                       0u, 0.f);
   OSPO_CHECK_LAUNCH();
   if (splits > 1) {
     const long n = (long)M_out * (out_cols / 4);
@@ -429,6 +639,23 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
   const bf16* b = (const bf16*)Bt;
   bf16* o = (bf16*)out;
   f32x4* part = (f32x4*)ws;
+  const bool sk3_ok = K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+                      (long)(M - 1) * lda * 2 + (long)(nmods * (a_koff > 0 ? a_koff : 0) + K) * 2 < (1L << 31) &&
+                      (long)b_rows * ldb * 2 < (1L << 31);
+  if (g_skinny_variant == 4 && sk3_ok && out_cols % 4 == 0 && !dr.xd) {  // (the masked-copy output is v2's)
+    const int nz = a_koff > 0 ? nmods : 1;
+    const int nt = a_koff > 0 ? module_tiles : n_tiles;
+    float* p2 = (float*)ws;
+    switch (nt) {
+      case 1: return launch_skinny3<1>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 2: return launch_skinny3<2>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 3: return launch_skinny3<3>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 4: return launch_skinny3<4>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 6: return launch_skinny3<6>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 8: return launch_skinny3<8>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      default: break;
+    }
+  }
   if (g_skinny_variant >= 2 && out_cols % 4 == 0 && K >= 128) {
     // dense: one workgroup column over all n-tiles; block-diagonal: grid z = module
     const int nz = a_koff > 0 ? nmods : 1;

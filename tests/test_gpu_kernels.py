@@ -515,6 +515,25 @@ def test_lora_skinny_dropout(M, K, used):
     assert relerr(out.float(), ref) < 8e-3
 
 
+@pytest.mark.parametrize("M,K,used", [(4800, 4096, 48), (4800, 11008, 16), (130, 4096, 32), (600, 4096, 96)])
+def test_lora_skinny_dropout_streamed(M, K, used):
+    """The step's form (no masked copy requested): the LDS-line streaming kernel masks x in registers."""
+    from ospo_amd import dropout as Dm
+    p, seed = 0.05, 424243
+    Rp = 64 if used <= 64 else 128
+    x = rnd(M, K)
+    Acat = torch.zeros(Rp, K, device=DEV, dtype=torch.bfloat16)
+    Acat[:used] = rnd(used, K, s=0.05)
+    M_out = (M + 63) // 64 * 64
+    out = torch.full((M_out, Rp), 7.0, device=DEV, dtype=torch.bfloat16)
+    ops().lora_skinny(x, Acat, out, M, M_out, K, (used + 15) // 16, 0, 2.0, b_rows=used, dropout=(seed, p))
+    keep = torch.from_numpy(Dm.keep_mask(M, K, seed, p)).to(DEV)
+    xd = torch.where(keep, (x.float() / (1 - p)).to(torch.bfloat16), torch.zeros((), dtype=torch.bfloat16, device=DEV))
+    ref = 2.0 * (xd.float() @ Acat.float().T)
+    assert relerr(out[:M].float(), ref) < 8e-3
+    assert torch.all(out[M:] == 0) and torch.all(out[:M, 16 * ((used + 15) // 16):] == 0)
+
+
 @pytest.mark.parametrize("M,N,K,K2", [(300, 512, 256, 64), (4800, 4096, 4096, 64), (600, 1024, 512, 128)])
 def test_gemm_dropout_backward(M, N, K, K2):
     """dX = dy.W + mask (.) (g.A) / (1-p): the K-extension is masked like the adapter input."""
