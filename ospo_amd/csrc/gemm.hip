@@ -926,51 +926,81 @@ template <int NTHR>
 __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem, int m0, int n0) {
   constexpr int BM = 256, BN = 256, CPITCH = BN * 2 + 16;
   constexpr int CPR = BN / 8;
+  constexpr int ITERS = BM * CPR / NTHR;  // 16-B chunks per thread
+  constexpr int BATCH = 4;                // chunks whose global loads are in flight together
+  static_assert(ITERS % BATCH == 0, "epilogue batch");
   bf16* C = reinterpret_cast<bf16*>(args.C);
-  for (int c = threadIdx.x; c < BM * CPR; c += NTHR) {
-    const int r2 = c / CPR, cc = c % CPR;
-    const int m = m0 + r2;
-    if (m >= args.M) continue;
-    u32x4 v = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + cc * 16);
-    if (n0 + cc * 8 < args.rope_cols) {
-      // RoPE on the bf16-rounded product, rounding per op like HF: x*cos + rotate_half(x)*sin.
-      // The tile holds two whole heads, so the partner (+-64 columns) is in the same LDS row.
-      const int d = (cc * 8) & 127;
-      const bool lo = d < 64;
-      const u32x4 pv = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + (lo ? cc + 8 : cc - 8) * 16);
-      const int t = m % args.rope_T, dd = lo ? d : d - 64;
-      const u32x4 cw = *reinterpret_cast<const u32x4*>(args.rope_cs + (long)t * 64 + dd);
-      const u32x4 sw = *reinterpret_cast<const u32x4*>(args.rope_sn + (long)t * 64 + dd);
-      u32x4 o;
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        float r[2];
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int sh = 16 * hh;
-          const float x = bits2f((v[qq] >> sh) & 0xffff), p = bits2f((pv[qq] >> sh) & 0xffff);
-          const float cf = bits2f((cw[qq] >> sh) & 0xffff), sf = bits2f((sw[qq] >> sh) & 0xffff);
-          // lo half: x1*c + (-x2)*s ; hi half: x2*c + x1*s
-          r[hh] = lo ? round_bf(x * cf) + round_bf(-p * sf) : round_bf(x * cf) + round_bf(p * sf);
-        }
-        o[qq] = pack2(r[0], r[1]);
-      }
-      v = o;
-    }
-    if (args.res) {
-      const u32x4 rv = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + cc * 8);
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const float lo = bits2f(v[qq] & 0xffff) + bits2f(rv[qq] & 0xffff);
-        const float hi = bits2f(v[qq] >> 16) + bits2f(rv[qq] >> 16);
-        v[qq] = pack2(lo, hi);
-      }
-    }
-    if (args.swg_gu) {
+  if (args.swg_gu) {  // fused SwiGLU backward: one chunk at a time (reads gate|up, writes dgate|dup)
+    for (int c = threadIdx.x; c < BM * CPR; c += NTHR) {
+      const int r2 = c / CPR, cc = c % CPR;
+      const int m = m0 + r2;
+      if (m >= args.M) continue;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + cc * 16);
       swiglu_bwd_store8(args, m, n0 + cc * 8, v);
-      continue;
     }
-    *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8) = v;
+    return;
+  }
+  // The residual and RoPE-table loads of BATCH chunks are issued before any of their stores: a load
+  // after a store to C (which the compiler cannot prove disjoint from res) would wait for it, and one
+  // chunk at a time the epilogue ran latency-bound (~9 us per 256 x 256 tile with a residual).
+  // the epilogue's index math starts here: keeps the compiler from hoisting it above the K loop (registers)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid), "+v"(m0), "+v"(n0));
+  const bool rope_tile = n0 < args.rope_cols;  // (rope_cols % 128 == 0: a chunk's partner is in the tile)
+#pragma unroll 1
+  for (int b0 = 0; b0 < ITERS; b0 += BATCH) {
+    u32x4 rv[BATCH], cw[BATCH], sw[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int c = tid + (b0 + u) * NTHR;
+      const int r2 = c / CPR, cc = c % CPR;
+      const int m = min(m0 + r2, args.M - 1);
+      if (args.res) rv[u] = *reinterpret_cast<const u32x4*>(args.res + (long)m * args.ldr + n0 + cc * 8);
+      if (rope_tile) {
+        const int d = (cc * 8) & 127;
+        const int t = m % args.rope_T, dd = d < 64 ? d : d - 64;
+        cw[u] = *reinterpret_cast<const u32x4*>(args.rope_cs + (long)t * 64 + dd);
+        sw[u] = *reinterpret_cast<const u32x4*>(args.rope_sn + (long)t * 64 + dd);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int c = tid + (b0 + u) * NTHR;
+      const int r2 = c / CPR, cc = c % CPR;
+      const int m = m0 + r2;
+      u32x4 v = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + cc * 16);
+      if (rope_tile && n0 + cc * 8 < args.rope_cols) {
+        // RoPE on the bf16-rounded product, rounding per op like HF: x*cos + rotate_half(x)*sin.
+        // The tile holds two whole heads, so the partner (+-64 columns) is in the same LDS row.
+        const int d = (cc * 8) & 127;
+        const bool lo = d < 64;
+        const u32x4 pv = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + (lo ? cc + 8 : cc - 8) * 16);
+        u32x4 o;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          float r[2];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int sh = 16 * hh;
+            const float x = bits2f((v[qq] >> sh) & 0xffff), p = bits2f((pv[qq] >> sh) & 0xffff);
+            const float cf = bits2f((cw[u][qq] >> sh) & 0xffff), sf = bits2f((sw[u][qq] >> sh) & 0xffff);
+            // lo half: x1*c + (-x2)*s ; hi half: x2*c + x1*s
+            r[hh] = lo ? round_bf(x * cf) + round_bf(-p * sf) : round_bf(x * cf) + round_bf(p * sf);
+          }
+          o[qq] = pack2(r[0], r[1]);
+        }
+        v = o;
+      }
+      if (args.res) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const float lo = bits2f(v[qq] & 0xffff) + bits2f(rv[u][qq] & 0xffff);
+          const float hi = bits2f(v[qq] >> 16) + bits2f(rv[u][qq] >> 16);
+          v[qq] = pack2(lo, hi);
+        }
+      }
+      if (m < args.M) *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8) = v;
+    }
   }
 }
 
@@ -985,6 +1015,9 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   constexpr int LDS_BYTES = (MAIN_BYTES > BM * CPITCH) ? MAIN_BYTES : BM * CPITCH;
   static_assert(LDS_BYTES <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  // DBG 5 (ablation): s_memrealtime (100 MHz) stamps of the workgroup's phases, wave 0
+  uint64_t rt[6] = {};
+  if constexpr (DBG == 5) rt[0] = __builtin_amdgcn_s_memrealtime();
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1139,6 +1172,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
+  if constexpr (DBG == 5) rt[1] = __builtin_amdgcn_s_memrealtime();
   if constexpr (EARLYB) {  // B0 of tile 0 (landed per the prologue wait; retired by the first lgkmcnt(0))
 #pragma unroll
     for (int n = 0; n < 2; ++n)
@@ -1559,6 +1593,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (DBG == 5) rt[2] = __builtin_amdgcn_s_memrealtime();
   if constexpr (DBG == 4) {
     if (args.dbg && lane < 10) args.dbg[((long)blockIdx.x * 8 + wave) * 16 + lane] = stp[lane / 5][lane % 5];
   }
@@ -1606,7 +1641,17 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
     }
   }
   __syncthreads();
+  if constexpr (DBG == 5) rt[3] = __builtin_amdgcn_s_memrealtime();
   epi_rows<512>(args, smem, m0, n0);
+  if constexpr (DBG == 5) {
+    rt[4] = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    rt[5] = __builtin_amdgcn_s_memrealtime();
+    if (args.dbg && wave == 0 && lane < 6) {
+      const uint64_t v = lane == 0 ? rt[0] : lane == 1 ? rt[1] : lane == 2 ? rt[2] : lane == 3 ? rt[3] : lane == 4 ? rt[4] : rt[5];
+      reinterpret_cast<uint64_t*>(args.dbg)[(long)blockIdx.x * 8 + lane] = v;
+    }
+  }
 }
 
 // sum the split partials of each tail tile, apply alpha / bias / residual, write bf16
@@ -1836,6 +1881,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 27: return launch_v5<0, false, false, 8>(a, stream, true);  // SP5 unrolled by 2
     case 28: return launch_v5<0, false, false, 9>(a, stream, true);  // SP8 + B0 of the next tile read early
     case 29: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<4, false, false, 8>(d, stream, false); }  // SP8 + stamps
+    case 30: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<5, false, false, 8>(d, stream, false); }  // SP8 + phase stamps
     case 17: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
     default: return launch_v5<0, false, false, 8>(a, stream, true);               // SP8 + split-K tail
   }
@@ -1986,7 +2032,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || v > 29 || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23) return OSPO_ERR_ARG;
+  if (v < 0 || v > 30 || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23) return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;
