@@ -273,6 +273,20 @@ int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows
                      int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed, float drop_p,
                      void* xd, int ld_xd, hipStream_t stream);
 
+/* Fused LoRA backward over one stream of dy, LoRA rank 16 (replaces ospo_lora_skinny's g plus the
+ * dB = dy^T u ospo_gemm_f32acc of the same group; ospo/wrapper/train.py:352 through peft lora.Linear's
+ * backward):
+ *   out[m][16 j + c] = scale * sum_k dy[m][j*Nmod + k] * Bt[16 j + c][k]   (m < M; rows M..M_out-1 and
+ *                      columns 16*nmods..out_cols-1 written zero) -- g, bf16
+ *   dB[j*Nmod + k][c] += sum_{m<M} dy[m][j*Nmod + k] * u[m][16 j + c]       -- fp32 atomic adds
+ * dy [M, >= nmods*Nmod], Bt [nmods*16, Nmod] (ldb), u [M, >= 16*nmods].  Nmod % 128 == 0, nmods <= 4.
+ * ws (>= ospo_lora_gdb_ws_bytes(M, nmods, Nmod) bytes): the fp32 partials of g, summed by a second
+ * launch; calls sharing a ws must be ordered (same stream). */
+size_t ospo_lora_gdb_ws_bytes(int M, int nmods, int Nmod);
+int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M, int M_out,
+                  int nmods, int Nmod, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
+                  size_t ws_bytes, hipStream_t stream);
+
 /* ------------------------------------------------------------ MXFP8 variant ---
  * BASELINE config 5 / SURVEY §8f rank 1: the frozen Linears of the SimPO step
  * (q|k|v, o, gate|up, down; forward and dX backward -- the products that

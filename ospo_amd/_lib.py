@@ -57,6 +57,8 @@ SIGNATURES = {
     "ospo_simpo_fwd": [P, I, F, F, F, I, P, P, P, P],
     "ospo_simpo_bwd": [P, I, F, F, F, I, P, P, P],
     "ospo_lora_pack": [P, P, I, I, I, I, I, P, P, P, P, I, L, P],
+    "ospo_lora_gdb": [P, I, P, I, P, I, I, I, I, I, F, P, I, I, P, P, Z, P],
+    "ospo_lora_gdb_ws_bytes": [I, I, I],
     "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, U, F, P, I, P],
     "ospo_lora_skinny_ws_bytes": [I, I, I],
     "ospo_decode_gemv_ws_bytes": [I, I, I],
@@ -89,7 +91,7 @@ SIGNATURES = {
 ABLATION_SIGNATURES = {"ospo_set_gemm_variant": [I], "ospo_set_gemv_variant": [I], "ospo_set_gemv_splits": [I],
                        "ospo_set_skinny_variant": [I], "ospo_gemm_set_debug_buffer": [P]}
 
-RESTYPES = {"ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
+RESTYPES = {"ospo_lora_gdb_ws_bytes": c_size_t, "ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 

@@ -433,6 +433,185 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
     }
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Fused backward over one stream of dy (LoRA r = 16): g = s dy.B (the dX GEMM's K-extension operand)
+// and dB += dy^T.u (the adapter B gradient), which before read dy twice (the g product on the main
+// stream, dB as a separate f32-atomic GEMM on the side stream).  Workgroup = 4 waves over 64*RSB rows x
+// 64*nch columns of one module.  dy sub-tiles of 64 rows x 64 columns stream through a 4-stage LDS ring
+// (128-B lines, XOR-swizzled); the module's Bt columns and u rows of the workgroup are staged once.
+//   g : row sub-block rb belongs to wave rb & 3 (2 per wave at RSB 8); MFMA D[j][m] (as the skinny kernels),
+//       fp32 partials per column block -> gdb_reduce_kernel.
+//   dB: wave w owns columns 16w..16w+15 of each 64-column chunk, D[n][j] over the workgroup's rows from
+//       transposed reads of the dy image (ds_read_b64_tr_b16) and of u; one f32 atomic add per element
+//       and chunk.  u rows >= M are zeroed in the fragment (dy rows are clamped, so finite).
+// Transposed LDS reads as inline asm: the builtin makes hipcc drain vmcnt(0) -- every LDS-DMA of the
+// prefetched sub-tiles -- before it (it cannot tell them apart); the caller waits lgkmcnt with the
+// destinations tied (tr4_wait) and fences the schedule.
+__device__ __forceinline__ void tr4_issue(const char* p, i16x4& v) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)((LDS_AS const char*)p)));
+}
+__device__ __forceinline__ void tr4_wait(i16x4& a, i16x4& b, i16x4& c, i16x4& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int RSB>
+__global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ dy, int ldy, const bf16* __restrict__ Bt,
+                                                       int ldb, const bf16* __restrict__ u, int ldu, int M, int Nmod,
+                                                       int nch, float* __restrict__ ws, int Mw,
+                                                       float* __restrict__ dB) {
+  constexpr int NS = 4, STAGE = 8192;
+  constexpr int BT_OFF = NS * STAGE, BT_BYTES = 16 * 4 * 128;  // up to nch = 4
+  constexpr int U_OFF = BT_OFF + BT_BYTES;
+  constexpr int ROWS = 64 * RSB;
+  __shared__ __attribute__((aligned(16))) char smem[U_OFF + ROWS * 32];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4, r8 = lane >> 3, c8 = lane & 7;
+  const int rb0 = blockIdx.x * ROWS;
+  const int nsplit = Nmod / (64 * nch);
+  const int mod = blockIdx.y / nsplit, sp = blockIdx.y % nsplit;
+  const int kc0 = sp * 64 * nch;             // first column of the workgroup within its module
+  const long col0 = (long)mod * Nmod + kc0;  // ... within dy
+  const int btrow = nch * 128;               // bytes per Bt image row
+
+  // Bt image [16 j][nch*64 k]: 16-B chunk q of row j at physical chunk q ^ j (source-side swizzle)
+  {
+    const int rpp = 1024 / btrow;  // rows per 1-KiB piece (2 or 4)
+    for (int p = wave; p < 2 * nch; p += 4) {
+      const int off = lane * 16;
+      const int j = p * rpp + off / btrow, pc = (off % btrow) >> 4;
+      const int q = pc ^ j;
+      __builtin_amdgcn_global_load_lds(Bt + (long)(mod * 16 + j) * ldb + kc0 + q * 8,
+                                       (LDS_AS void*)(smem + BT_OFF + p * 1024), 16, 0, 0);
+    }
+  }
+  // u image [ROWS][16] (32 B per row), rows clamped (masked at the fragment)
+#pragma unroll
+  for (int p = wave; p < ROWS / 32; p += 4) {
+    const int row = min(rb0 + p * 32 + (lane >> 1), M - 1);
+    __builtin_amdgcn_global_load_lds(u + (long)row * ldu + mod * 16 + (lane & 1) * 8,
+                                     (LDS_AS void*)(smem + U_OFF + p * 1024), 16, 0, 0);
+  }
+  auto stage = [&](int t) {  // sub-tile t = (chunk t / RSB, row sub-block t % RSB): 2 pieces per wave
+    char* st = smem + (t % NS) * STAGE;
+    const int cc = t / RSB, rb = t % RSB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = wave * 2 + i;
+      const int row = min(rb0 + rb * 64 + p * 8 + r8, M - 1);
+      __builtin_amdgcn_global_load_lds(dy + (long)row * ldy + col0 + cc * 64 + ((c8 ^ r8) << 3),
+                                       (LDS_AS void*)(st + p * 1024), 16, 0, 0);
+    }
+  };
+  const int T = nch * RSB;
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) stage(t);
+
+  f32x4 accg[RSB / 4][4];
+#pragma unroll
+  for (int a = 0; a < RSB / 4; ++a)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) accg[a][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int li = l16, q4 = li >> 2, p4 = li & 3;
+
+  auto gpart = [&](const char* st, int cc, f32x4 (&acc)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int qk = cc * 8 + 4 * s + g;  // Bt chunk (8 bf16) of this lane's k group
+      const bf16x8 bt = *reinterpret_cast<const bf16x8*>(smem + BT_OFF + l16 * btrow + ((qk ^ l16) << 4));
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int row = 16 * f + l16;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + row * 128 + (((4 * s + g) ^ (row & 7)) << 4));
+        acc[f] = MFMA(bt, a, acc[f]);  // D[j = 4g..][m = l16]
+      }
+    }
+  };
+  for (int t = 0; t < T; ++t) {
+    const int cc = t / RSB, rb = t % RSB;
+    const int newer = min(NS - 2, T - 1 - t);
+    if (newer >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (newer == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + NS - 1 < T) stage(t + NS - 1);
+    const char* st = smem + (t % NS) * STAGE;
+    // g: this sub-block's 64 rows belong to wave rb & 3 (its accumulator set rb >> 2)
+    if (wave == (rb & 3)) {
+      static_assert(RSB == 8, "two accumulator sets");
+      if (rb < 4) gpart(st, cc, accg[0]);
+      else gpart(st, cc, accg[1]);
+    }
+    // dB: columns 16 wave .. +15 of the chunk, the sub-block's 64 rows as K
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r1 = 32 * s + 8 * g + q4, r2 = r1 + 4;
+      const int x = 2 * wave + (p4 >> 1), h = (p4 & 1) << 3;
+      const int ur = rb * 64 + 32 * s + 8 * g;  // u image row of element 0
+      i16x4 lo, hi, ulo, uhi;
+      tr4_issue(st + r1 * 128 + ((x ^ (r1 & 7)) << 4) + h, lo);
+      tr4_issue(st + r2 * 128 + ((x ^ (r2 & 7)) << 4) + h, hi);
+      tr4_issue(smem + U_OFF + (ur + q4) * 32 + p4 * 8, ulo);
+      tr4_issue(smem + U_OFF + (ur + 4 + q4) * 32 + p4 * 8, uhi);
+      tr4_wait(lo, hi, ulo, uhi);
+      const int mrow = rb0 + ur;  // global row of element 0
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ulo[e] = (mrow + e < M) ? ulo[e] : (short)0;
+        uhi[e] = (mrow + 4 + e < M) ? uhi[e] : (short)0;
+      }
+      const i16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const i16x8 bv = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+      accb = MFMA(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), accb);  // D[n = 4g+i][j = l16]
+    }
+    if (rb == RSB - 1) {  // the chunk's dB over the workgroup's rows
+      const long n0 = col0 + cc * 64 + 16 * wave + 4 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[i]);
+      accb = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  // g partials of this column block: ws [mod][sp][Mw][16]
+#pragma unroll
+  for (int a = 0; a < RSB / 4; ++a) {
+    const int rb = wave + 4 * a;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int m = rb0 + rb * 64 + 16 * f + l16;
+      if (m < Mw) *reinterpret_cast<f32x4*>(ws + (((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[a][f];
+    }
+  }
+}
+
+// out[m][16 mod + c] = bf16(scale * sum_sp ws[mod][sp][m][c]) (m < M; 0 for M <= m < M_out), pad columns 0
+__global__ void gdb_reduce_kernel(const float* __restrict__ ws, int nmods, int nsplit, int Mw, int M, int M_out,
+                                  float scale, bf16* __restrict__ out, int ldo, int out_cols) {
+  const int cq = out_cols / 4;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (long)M_out * cq) return;
+  const int m = (int)(tid / cq), c = (int)(tid % cq) * 4;
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int mod = c / 16;
+  if (m < M && mod < nmods) {
+    for (int s0 = 0; s0 < nsplit; s0 += 8) {
+      f32x4 p[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (s0 + k < nsplit) p[k] = *reinterpret_cast<const f32x4*>(ws + (((long)mod * nsplit + s0 + k) * Mw + m) * 16 + (c & 15));
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (s0 + k < nsplit) v += p[k];
+    }
+  }
+  uint2 pk;
+  pk.x = pack2(v[0] * scale, v[1] * scale);
+  pk.y = pack2(v[2] * scale, v[3] * scale);
+  *reinterpret_cast<uint2*>(out + (long)m * ldo + c) = pk;
+}
 }  // namespace
 
 // K splits: enough workgroups to keep every CU streaming (>= ~4 per CU), each
@@ -695,5 +874,44 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
       if (rs) return rs;
     }
   }
+  return OSPO_OK;
+}
+
+// ---------------------------------------------------------------------------------- lora_gdb
+static int gdb_nch(int M, int nmods, int Nmod) {
+  const int rbk = (M + 511) / 512;
+  if (Nmod % 256 == 0 && (long)rbk * nmods * (Nmod / 256) >= 256) return 4;
+  return 2;
+}
+
+extern "C" size_t ospo_lora_gdb_ws_bytes(int M, int nmods, int Nmod) {
+  if (M <= 0 || nmods <= 0 || Nmod <= 0 || Nmod % 128) return 0;
+  const size_t Mw = (size_t)(M + 63) / 64 * 64;
+  return (size_t)nmods * (Nmod / 128) * Mw * 16 * sizeof(float) + 16;  // the nch = 2 worst case
+}
+
+extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M, int M_out,
+                             int nmods, int Nmod, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
+                             size_t ws_bytes, hipStream_t stream) {
+  if (!dy || !Bt || !u || !out || !dB || !ws) return OSPO_ERR_ARG;
+  if (M <= 0 || M_out < M || nmods < 1 || nmods > 4 || Nmod <= 0 || Nmod % 128) return OSPO_ERR_SHAPE;
+  if (ldy < nmods * Nmod || ldb < Nmod || ldu < 16 * nmods || ldo < out_cols || out_cols < 16 * nmods ||
+      out_cols % 4 || ldy % 8 || ldb % 8 || ldu % 8 || ldo % 4)
+    return OSPO_ERR_SHAPE;
+  if (ws_bytes < ospo_lora_gdb_ws_bytes(M, nmods, Nmod)) return OSPO_ERR_SHAPE;
+  if (!aligned16(dy) || !aligned16(Bt) || !aligned16(u) || !aligned16(ws) || ((uintptr_t)dB & 3) ||
+      ((uintptr_t)out & 7))
+    return OSPO_ERR_ALIGN;
+  const int nch = gdb_nch(M, nmods, Nmod);
+  const int nsplit = Nmod / (64 * nch);
+  const int Mw = (M + 63) / 64 * 64;
+  const dim3 grid((M + 511) / 512, nmods * nsplit);
+  hipLaunchKernelGGL((lora_gdb_kernel<8>), grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
+                     (const bf16*)u, ldu, M, Nmod, nch, (float*)ws, Mw, dB);
+  OSPO_CHECK_LAUNCH();
+  const long n = (long)M_out * (out_cols / 4);
+  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)ws,
+                     nmods, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
+  OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

@@ -77,7 +77,7 @@ class SimPOEngine:
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_pairs: int = 4,
                  max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
                  dropout_seed: int = 42, linear_dtype: str = "bf16", fuse_swiglu_bwd: bool = False,
-                 dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0):
+                 dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0, fuse_gdb: bool = True):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
         if linear_dtype not in ("bf16", "mx8"):
@@ -163,6 +163,10 @@ class SimPOEngine:
         # > 0: the LoRA weight gradients as ospo_lora_wgrad streams of ~wgrad_wgs workgroups; 0: the 64 x 64
         # f32-atomic tiles (faster in isolation, 180.8 vs 198.8 us per layer, tools/lora_grads_bench.py)
         self.wgrad_wgs = int(wgrad_wgs)
+        # fuse_gdb (LoRA r = 16): g = s dy.B and dB += dy^T u of a group in one stream over dy on the main stream
+        # (ospo_lora_gdb); the side stream then runs only dA.  Off: g on the main stream, dB with dA on the side.
+        self.fuse_gdb = bool(fuse_gdb) and dims.lora_r == 16
+        self._gdb_ws = None
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
             raise ValueError("dadb_splits must be four positive split counts")
         self._side = torch.cuda.Stream(device=self.device, priority=int(side_priority))
@@ -299,6 +303,21 @@ class SimPOEngine:
         nt = (used + 15) // 16
         ops.lora_skinny(x, Acat, out_bf16, M, self.Mk, K, nt, 0, self.scale, b_rows=used, ws=self._skinny_ws(K, nt),
                         dropout=drop, xd=xd if drop else None)
+
+    def _lora_g_db(self, dy, g, Bcat, BT, M, par, u, gbase):
+        """(g_s, dB done): with fuse_gdb, g_s = bf16(scale * dy . Bcat) and dB += dy^T . u in one stream over dy
+        (ospo_lora_gdb); else _lora_g and the side stream computes dB."""
+        r = self.layout.r
+        if not (self.fuse_gdb and r == 16 and g.Nmod % 128 == 0 and g.nmods <= 4):
+            return self._lora_g(dy, g, Bcat, BT, M, par), False
+        out = self.gsc2[g.name][par]
+        b_off = gbase + g.b_off
+        dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
+        ws_bytes = max(int(ops.query_gdb_ws(self.Mk, gg.nmods, gg.Nmod)) for gg in self.layout.groups.values())
+        if self._gdb_ws is None or self._gdb_ws.numel() * 4 < ws_bytes:
+            self._gdb_ws = torch.empty((ws_bytes + 15) // 16 * 4, dtype=F32, device=self.device)
+        ops.lora_gdb(dy, BT, u, out, dB, M, self.Mk, g.nmods, g.Nmod, self.scale, ws=self._gdb_ws)
+        return out, True
 
     def _lora_g(self, dy, g, Bcat, BT, M, par=0):
         """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows M..Mk-1 zero), into g buffer copy `par`."""
@@ -458,12 +477,12 @@ class SimPOEngine:
             if ev is not None:
                 main.wait_event(ev)
 
-        def lora_grads_async(name, par, gs, x_in, dy, u, gbase, drop):
+        def lora_grads_async(name, par, gs, x_in, dy, u, gbase, drop, skip_db=False):
             ev = torch.cuda.Event()
             ev.record(main)
             side.wait_event(ev)
             with torch.cuda.stream(side):
-                self._lora_grads(gs, x_in, dy, u, lay.groups[name], gbase, drop)
+                self._lora_grads(gs, x_in, dy, u, lay.groups[name], gbase, drop, skip_db)
             ev2 = torch.cuda.Event()
             ev2.record(side)
             done[(name, par)] = ev2
@@ -477,43 +496,43 @@ class SimPOEngine:
             # ---- down_proj: out = xmid + h W_d^T + s (h A_d^T) B_d^T
             Acat, AcatT, Bcat, BT = pk["down"]
             guard("down", q)  # g buffer copy q (layer i+2's down products read it)
-            gs = self._lora_g(dx, lay.groups["down"], Bcat, BT, M, q)
+            gs, fdb = self._lora_g_db(dx, lay.groups["down"], Bcat, BT, M, q, a["u_d"], gbase)
             dr = self._drop(i, "down")
             if self.fuse_swiglu_bwd:
                 guard("gu", q)  # dgu / g copy q
                 ops.gemm_nt_swiglu_bwd(dx[:M], lw["downT"], a["gu"][:M], dgu[:M], a2=gs[:M], b2=AcatT, dropout=dr)
-                lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr)
+                lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr, fdb)
             else:
                 self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-                lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr)
+                lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr, fdb)
                 guard("gu", q)  # dgu / g copy q
                 ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
             # ---- gate/up
             Acat, AcatT, Bcat, BT = pk["gu"]
-            gs = self._lora_g(dgu, lay.groups["gu"], Bcat, BT, M, q)
+            gs, fdb = self._lora_g_db(dgu, lay.groups["gu"], Bcat, BT, M, q, a["u_gu"], gbase)
             dr = self._drop(i, "gu")
             self._lin(dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("gu", q, gs, a["xn2"], dgu, a["u_gu"], gbase, dr)
+            lora_grads_async("gu", q, gs, a["xn2"], dgu, a["u_gu"], gbase, dr, fdb)
             guard("o", q)  # dxmid / g copy q
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], dxmid[:M],
                             dres=dx[:M], mx=self._mxo(D))
             # ---- o_proj
             Acat, AcatT, Bcat, BT = pk["o"]
-            gs = self._lora_g(dxmid, lay.groups["o"], Bcat, BT, M, q)
+            gs, fdb = self._lora_g_db(dxmid, lay.groups["o"], Bcat, BT, M, q, a["u_o"], gbase)
             dr = self._drop(i, "o")
             self._lin(dxmid[:M], lw["oT"], self.dattn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("o", q, gs, a["attn"], dxmid, a["u_o"], gbase, dr)
+            lora_grads_async("o", q, gs, a["attn"], dxmid, a["u_o"], gbase, dr, fdb)
             # ---- attention + RoPE
             guard("qkv", q)  # dqkv / g copy q
             ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, self.ds_ws,
                                dqkv, S, T, H, hd, scale_attn, rope_cos=self.cos, rope_sin=self.sin)
             # ---- q/k/v
             Acat, AcatT, Bcat, BT = pk["qkv"]
-            gs = self._lora_g(dqkv, lay.groups["qkv"], Bcat, BT, M, q)
+            gs, fdb = self._lora_g_db(dqkv, lay.groups["qkv"], Bcat, BT, M, q, a["u_qkv"], gbase)
             dr = self._drop(i, "qkv")
             if i > 0:
                 self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
-            lora_grads_async("qkv", q, gs, a["xn1"], dqkv, a["u_qkv"], gbase, dr)
+            lora_grads_async("qkv", q, gs, a["xn1"], dqkv, a["u_qkv"], gbase, dr, fdb)
             if i > 0:
                 guard("down", 1 - q)  # dx copy 1-q: layer i+1's down products read it
                 ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[1 - q][:M],
@@ -526,7 +545,7 @@ class SimPOEngine:
                     on_layer_grads(gbase, gbase + lay.per_layer)
         main.wait_stream(side)
 
-    def _lora_grads(self, gs, x_in, dy, u, g, gbase, drop=None):
+    def _lora_grads(self, gs, x_in, dy, u, g, gbase, drop=None, skip_db=False):
         """dA = g_s^T . dropout(x_in)  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal), each one
         stream over its big operand (ospo_lora_wgrad); with LoRA dropout the mask is recomputed on x_in
         (the forward keeps no masked copy)."""
@@ -540,15 +559,17 @@ class SimPOEngine:
         if self.wgrad_wgs > 0 and r % 16 == 0 and g.Rp in (64, 128):
             sa, sb = self._wgrad_splits(g.Kin), self._wgrad_splits(g.nmods * g.Nmod)
             ops.lora_wgrad(x_in[:Mk], gs[:Mk], dA, mode=0, s_cols=used, splits=sa, dropout=drop)
-            ops.lora_wgrad(dy[:Mk], u[:Mk], dB, mode=1, s_cols=used, splits=sb, nmod=g.Nmod, r=r)
+            if not skip_db:
+                ops.lora_wgrad(dy[:Mk], u[:Mk], dB, mode=1, s_cols=used, splits=sb, nmod=g.Nmod, r=r)
             return
         # other ranks: the 64 x 64 f32-atomic tiles (K splits measured on the 7B shapes, profiles/r01/
         # lora_grads_sweep.jsonl)
         sa_small, sa_big, sb_multi, sb_single = self._dadb_splits
         ops.gemm_f32acc(gs[:Mk, :used], x_in[:Mk], dA, a_kmajor=True, b_kmajor=True,
                         k_splits=sa_big if g.Kin > 8192 else sa_small, b_dropout=drop)
-        ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True, k_splits=sb_multi if g.nmods > 1 else sb_single,
-                        diag=(g.Nmod, r))
+        if not skip_db:  # (with fuse_gdb, ospo_lora_gdb produced dB with g on the main stream)
+            ops.gemm_f32acc(dy[:Mk], u[:Mk], dB, a_kmajor=True, b_kmajor=True,
+                            k_splits=sb_multi if g.nmods > 1 else sb_single, diag=(g.Nmod, r))
 
     def _wgrad_splits(self, N: int) -> int:
         """K-range splits of a LoRA weight-gradient stream: ~wgrad_wgs workgroups of 256-column stripes."""

@@ -483,6 +483,26 @@ def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=No
          _s())
 
 
+def query_gdb_ws(M, nmods, Nmod) -> int:
+    return int(query("ospo_lora_gdb_ws_bytes", M, nmods, Nmod))
+
+
+def lora_gdb_ws(M, nmods, Nmod, device="cuda") -> torch.Tensor:
+    """Workspace for ospo_lora_gdb's fp32 partials of g."""
+    n = int(query("ospo_lora_gdb_ws_bytes", M, nmods, Nmod))
+    return torch.empty((n + 15) // 16 * 4, dtype=torch.float32, device=device)
+
+
+def lora_gdb(dy, bt, u, out, dB, M, M_out, nmods, Nmod, scale, ws=None):
+    """One stream over dy (LoRA r = 16): out[:M_out] (bf16) = scale * dy . B (block diagonal, as
+    lora_skinny's g; rows M.. and columns 16*nmods.. zero) and dB [nmods*Nmod, 16] (fp32) += dy^T . u."""
+    _chk(dB, torch.float32, "dB")
+    if ws is None:
+        ws = lora_gdb_ws(M, nmods, Nmod, dy.device)
+    call("ospo_lora_gdb", _p(dy), _ld(dy), _p(bt), _ld(bt), _p(u), _ld(u), M, M_out, nmods, Nmod, float(scale),
+         _p(out), _ld(out), out.shape[1], _p(dB), _p(ws), ws.numel() * ws.element_size(), _s())
+
+
 # -------------------------------------------------------------- optimizer
 def sumsq(g, out):
     call("ospo_sumsq", _p(g), g.numel(), _p(out), _s())

@@ -548,6 +548,28 @@ def test_gemm_dropout_backward(M, N, K, K2):
     assert relerr(out.float(), ref) < 4e-3
 
 
+@pytest.mark.parametrize("M,M_out,nm,Nmod", [(4800, 4800, 3, 4096), (4800, 4864, 2, 11008), (777, 832, 1, 4096),
+                                            (100, 128, 1, 1024), (1000, 1024, 4, 512)])
+def test_lora_gdb_exact_integers(M, M_out, nm, Nmod):
+    """The fused g = s dy.B / dB += dy^T u stream: exact on small integers against the two products
+    it replaces (block diagonal over the modules; rows >= M of u and dy ignored, g rows M.. zeroed)."""
+    r = 16
+    dy = ints(M_out, nm * Nmod, lo=-2, hi=3)
+    BT = ints(nm * r, Nmod, lo=-2, hi=3)
+    Rp = 64 if nm * r <= 64 else 128
+    u = ints(M_out, Rp, lo=-2, hi=3)
+    u[M:] = 99.0  # rows past M must not contribute
+    out = torch.full((M_out, Rp), 7.0, device=DEV, dtype=torch.bfloat16)
+    dB = torch.ones(nm * Nmod, r, device=DEV, dtype=torch.float32)  # accumulates onto what is there
+    ops().lora_gdb(dy, BT, u, out, dB, M, M_out, nm, Nmod, 1.0)
+    dyd, Bd, ud = dy[:M].double(), BT.double(), u[:M].double()
+    g_ref = torch.cat([dyd[:, j * Nmod:(j + 1) * Nmod] @ Bd[j * r:(j + 1) * r].T for j in range(nm)], 1)
+    assert torch.equal(out[:M, : nm * r].float(), bf(g_ref.float()).float())
+    assert torch.all(out[M:] == 0) and torch.all(out[:, nm * r:] == 0)
+    dB_ref = torch.cat([dyd[:, j * Nmod:(j + 1) * Nmod].T @ ud[:, j * r:(j + 1) * r] for j in range(nm)], 0) + 1.0
+    assert torch.equal(dB.double(), dB_ref)
+
+
 @pytest.mark.parametrize("M,nm,Nmod,r", [(4800, 3, 4096, 16), (640, 2, 11008, 16), (100, 1, 4096, 16),
                                          (300, 3, 1024, 32), (200, 2, 2048, 32)])
 def test_lora_skinny_up_blockdiag(M, nm, Nmod, r):
