@@ -327,7 +327,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
 // sweeps the query tiles at/after its block.  Q / dO tiles (+ lse, delta) are
 // double-buffered in LDS through global_load_lds; no atomics.
 // DBG (A/B decomposition only, results invalid): 1 = no softmax VALU (P = S, dS = dP),
-// 2 = no dV/dK products, 3 = no S/dP products, 4 = no Q/dO loads after the first tile
+// 2 = no dV/dK products, 3 = no S/dP products, 4 = no Q/dO loads after the first tile, 5 = no dS^T stores
 template <int NW, int DBG = 0>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
                                                             int vc, const bf16* __restrict__ dout, int ldd,
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
         dp[a][j] = px * (dp[a][j] - dq4[j]) * scale;
         dp[a][j + 1] = py * (dp[a][j + 1] - dq4[j + 1]) * scale;
       }
-      if (dsrow) {  // dS^T[key][q .. q+3] in bf16, the values the dK product below rounds to (8 B per lane)
+      if (dsrow && DBG != 5) {  // dS^T[key][q .. q+3] in bf16, the values the dK product below rounds to (8 B per lane)
         uint2 pk;
         pk.x = pack2(dp[a][0], dp[a][1]);
         pk.y = pack2(dp[a][2], dp[a][3]);
@@ -826,6 +826,7 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
   if (nw == 8 && dkdv_dbg == 2) dkdv = attn_bwd_dkdv_kernel<8, 2>;
   if (nw == 8 && dkdv_dbg == 3) dkdv = attn_bwd_dkdv_kernel<8, 3>;
   if (nw == 8 && dkdv_dbg == 4) dkdv = attn_bwd_dkdv_kernel<8, 4>;
+  if (nw == 8 && dkdv_dbg == 5) dkdv = attn_bwd_dkdv_kernel<8, 5>;  // no dS^T stores
 #else
   auto dkdv = attn_bwd_dkdv_kernel<8>;
 #endif

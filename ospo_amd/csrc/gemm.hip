@@ -1099,15 +1099,17 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   // SP >= 5 (bf16): the main (non-extension) tiles are staged by buffer_load_dwordx4 ... lds from per-lane
   // byte offsets fixed for the whole launch, the K advance riding in the scalar soffset: no VALU address math
   // and no per-piece operand selects in the loop (SP 6: the same schedule with the generic staging, for A/B).
-  static_assert(!(SP >= 5 && MX), "SP 5-7 are bf16 schedules");
+  static_assert(!((SP == 6 || SP == 7 || SP == 9) && MX), "SP 6, 7, 9 are bf16 schedules");
   constexpr bool FAST = (SP == 5 || SP == 7 || SP == 8 || SP == 9);  // buffer-offset staging of the main tiles
   constexpr bool BAL = (SP == 5 || SP == 6 || SP == 8 || SP == 9);  // 4 + 4 refills per K-tile
   constexpr bool UNR2 = (SP == 8 || SP == 9);             // steady loop unrolled by 2 (slot parity constant)
   constexpr bool EARLYB = (SP == 9);                      // B0 of tile t+1 read in R(t,1): 12 + 12 fragment reads
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)args.A, 0, (int)((long)Mlast * args.lda * 2 + args.K * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)args.B, 0, (int)((long)Nlast * args.ldb * 2 + args.K * 2), 0x00020000);
+  // main-operand element bytes: 2 (bf16) or 1 (MXFP8: lda / ldb are in bytes, a K-tile row is 128 B either way)
+  constexpr int EB = MX ? 1 : 2;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)args.A, 0, (int)(((long)Mlast * args.lda + args.K) * EB), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)args.B, 0, (int)(((long)Nlast * args.ldb + args.K) * EB), 0x00020000);
   uint32_t voff[4][2] = {};
   if constexpr (FAST) {
 #pragma unroll
@@ -1117,13 +1119,13 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
         const bool isA = h < 2;
         const int row = (h & 1) * 128 + (wave * 2 + i) * 8 + rr8;
         const int g = min((isA ? m0 : n0) + row, isA ? Mlast : Nlast);
-        voff[h][i] = (uint32_t)g * (uint32_t)(isA ? args.lda : args.ldb) * 2u + ((c8 ^ rr8) << 4);
+        voff[h][i] = (uint32_t)g * (uint32_t)(isA ? args.lda : args.ldb) * (uint32_t)EB + ((c8 ^ rr8) << 4);
       }
   }
   auto is_ext = [&](int tl) { return abs_tile(tl) >= nt1; };
   auto stage_fast = [&](int tl, int h, int par = -1) __attribute__((always_inline)) {
     char* dst = smem + (par >= 0 ? par : (tl & 1)) * SLOT + h * HALF;
-    const int kb = abs_tile(tl) * (BK * 2);
+    const int kb = abs_tile(tl) * 128;  // one 128-B row per K-tile (64 bf16 or 128 e4m3)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (LDS_AS void*)(dst + (wave * 2 + i) * 1024), 16,
@@ -1151,10 +1153,14 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   i32x8 b8sp[2][2];    // SP + MX: [B half][n]
 
   // prologue: tile 0 complete, A0 of tile 1 in flight (SP: tile 0 only)
-  if constexpr (BAL) {  // tile 0 complete; B0 B1 of tile 1 in flight (its A0 A1 are staged in R(0,0))
-    if (nt > 0) { stage_any(0, 2); stage_any(0, 3); stage_any(0, 0); stage_any(0, 1); }
-    if (nt > 1) { stage_any(1, 2); stage_any(1, 3); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (BAL) {  // tile 0 complete; B0 B1 (+ scales) of tile 1 in flight (its A0 A1 are staged in R(0,0))
+    if (nt > 0) { stage_scales(0); stage_any(0, 2); stage_any(0, 3); stage_any(0, 0); stage_any(0, 1); }
+    if (nt > 1) {
+      stage_scales(1); stage_any(1, 2); stage_any(1, 3);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MX ? 5 : 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   } else {
   if (nt > 0) {
     stage_scales(0);
@@ -1315,11 +1321,23 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   // barrier that opens g0's first read): A1(t) before R(t,1) -- 8 newer pieces (B(t+1), A(t+1)); A0 B of t+1
   // before R(t+1,0) -- 6 newer (A1(t+1), B(t+2)).  STEADY: t+1 and t+2 exist and are main tiles, so the waits
   // are constants and staging takes the fast path with no branch.
-  auto run_tile_sp5 = [&](int t, auto steady, auto parity) __attribute__((always_inline)) {
+  auto run_tile_sp5 = [&](int t, auto steady, auto parity, auto mxt) __attribute__((always_inline)) {
     constexpr bool ST = decltype(steady)::value;
     constexpr int PAR = decltype(parity)::value;  // slot parity of tile t when known at compile time, else -1
+    constexpr bool mx_tile = MX && decltype(mxt)::value;
+    constexpr int SC = MX ? 1 : 0;                // MX: the scales of tile t+2 ride with its B0 B1
     const char* slot = smem + (PAR >= 0 ? PAR : (t & 1)) * SLOT;
     const bool n1 = ST || t + 1 < nt, n2 = ST || t + 2 < nt;
+    uint32_t scA[2] = {0u, 0u}, scB[2] = {0u, 0u};
+    if constexpr (mx_tile) {  // staged with tile t's B0 B1: landed per the waits before R(t,0)
+      const char* sc = smem + SC_BASE + (PAR >= 0 ? PAR : (t & 1)) * SC_SLOT;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        scA[h] = *reinterpret_cast<const uint32_t*>(sc + (h * 2 + wm) * 256 + lane * 4);
+        scB[h] = *reinterpret_cast<const uint32_t*>(sc + 1024 + (h * 2 + (wn >> 1)) * 256 + lane * 4) >>
+                 (16 * (wn & 1));
+      }
+    }
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       uint32_t st_raw[5];
@@ -1331,57 +1349,76 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   }
       STAMP(0);
       const char* la = slot + p * HALF;
+      if constexpr (mx_tile) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
-      if (EARLYB) {
-        if (p == 0) {  // B0(t) came with R(t-1,1); B1(t) now
-#pragma unroll
-          for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              bsp[0][n][s] = b0n[n][s];
-              bsp[1][n][s] = *reinterpret_cast<const bf16x8*>(slot + 3 * HALF +
-                                                               mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
-            }
-        } else if (n1) {
-          const char* nslot = smem + (PAR >= 0 ? 1 - PAR : ((t + 1) & 1)) * SLOT;
-#pragma unroll
-          for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-              b0n[n][s] = *reinterpret_cast<const bf16x8*>(nslot + 2 * HALF +
-                                                          mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+        for (int i = 0; i < 4; ++i) {
+          a8[i].lo = *reinterpret_cast<const i32x4*>(la + mmaj_off(wm * 64 + i * 16 + frow, fcol));
+          a8[i].hi = *reinterpret_cast<const i32x4*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 + fcol));
         }
-      } else if (p == 0) {
+        if (p == 0) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+          for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int n = 0; n < 2; ++n)
+            for (int n = 0; n < 2; ++n) {
+              const char* lb = slot + (2 + h) * HALF;
+              b8sp[h][n].lo = *reinterpret_cast<const i32x4*>(lb + mmaj_off(wn * 32 + n * 16 + frow, fcol));
+              b8sp[h][n].hi = *reinterpret_cast<const i32x4*>(lb + mmaj_off(wn * 32 + n * 16 + frow, 4 + fcol));
+            }
+        }
+      } else {
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-              bsp[h][n][s] = *reinterpret_cast<const bf16x8*>(slot + (2 + h) * HALF +
-                                                               mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
+        if (EARLYB) {
+          if (p == 0) {  // B0(t) came with R(t-1,1); B1(t) now
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int s = 0; s < 2; ++s) {
+                bsp[0][n][s] = b0n[n][s];
+                bsp[1][n][s] = *reinterpret_cast<const bf16x8*>(slot + 3 * HALF +
+                                                                 mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+              }
+          } else if (n1) {
+            const char* nslot = smem + (PAR >= 0 ? 1 - PAR : ((t + 1) & 1)) * SLOT;
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int s = 0; s < 2; ++s)
+                b0n[n][s] = *reinterpret_cast<const bf16x8*>(nslot + 2 * HALF +
+                                                            mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+          }
+        } else if (p == 0) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int s = 0; s < 2; ++s)
+                bsp[h][n][s] = *reinterpret_cast<const bf16x8*>(slot + (2 + h) * HALF +
+                                                                 mmaj_off(wn * 32 + n * 16 + frow, 4 * s + fcol));
+        }
       }
       if (ST && FAST) {
         if (p == 0) { stage_fast(t + 1, 0, PAR >= 0 ? 1 - PAR : -1); stage_fast(t + 1, 1, PAR >= 0 ? 1 - PAR : -1); }
-        if (p == 1) { stage_fast(t + 2, 2, PAR); stage_fast(t + 2, 3, PAR); }
+        if (p == 1) { stage_scales(t + 2); stage_fast(t + 2, 2, PAR); stage_fast(t + 2, 3, PAR); }
       } else if (ST) {
         if (p == 0) { stage_half(t + 1, 0); stage_half(t + 1, 1); }
-        if (p == 1) { stage_half(t + 2, 2); stage_half(t + 2, 3); }
+        if (p == 1) { stage_scales(t + 2); stage_half(t + 2, 2); stage_half(t + 2, 3); }
       } else {
         if (p == 0 && n1) { stage_any(t + 1, 0); stage_any(t + 1, 1); }
-        if (p == 1 && n2) { stage_any(t + 2, 2); stage_any(t + 2, 3); }
+        if (p == 1 && n2) { stage_scales(t + 2); stage_any(t + 2, 2); stage_any(t + 2, 3); }
       }
+      // counted waits: p 0 -> A1(t) (+ EARLYB: B0(t+1)); p 1 -> A0 B (+ scales) of t+1
       auto waits = [&]() __attribute__((always_inline)) {
         if (ST) {
-          if (p == 0 && !EARLYB) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // EARLYB p 0: A1(t) and B0(t+1)
+          if (p == 0 && !EARLYB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + SC) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + SC) : "memory");  // EARLYB p 0: A1(t) and B0(t+1)
         } else {
-          if (p == 0) wait_vmcnt_exact(n1 ? (EARLYB ? 6 : 8) : 0);
-          if (p == 1 && n1) wait_vmcnt_exact(n2 ? 6 : 2);
+          if (p == 0) wait_vmcnt_exact(n1 ? (EARLYB ? 6 : 8 + SC) : 0);
+          if (p == 1 && n1) wait_vmcnt_exact(n2 ? 6 + SC : 2);
         }
       };
       if (g1) waits();
@@ -1392,17 +1429,37 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       __builtin_amdgcn_sched_barrier(0);
       STAMP(2);
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (mx_tile) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int j = 2 * p + q;
-        const int ib = (j == 1 || j == 2) ? 1 : 0;
+        for (int q = 0; q < 2; ++q) {
+          const int j = 2 * p + q;
+          const int ib = (j == 1 || j == 2) ? 1 : 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int n = 0; n < 2; ++n)
+            for (int n = 0; n < 2; ++n)
+              acc[j][i][n] = mx_mfma(b8sp[ib][n], a8[i], acc[j][i][n], n, scB[ib], i, scA[p]);
+        }
+        // keep the scaled MFMAs inside their phase (see the 8-phase loop)
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-              acc[j][i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bsp[ib][n][s], af[i][s], acc[j][i][n], 0, 0, 0);
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int n = 0; n < 2; ++n) asm volatile("" : "+v"(acc[2 * p + q][i][n]));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int j = 2 * p + q;
+          const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int s = 0; s < 2; ++s)
+                acc[j][i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bsp[ib][n][s], af[i][s], acc[j][i][n], 0, 0, 0);
+        }
       }
       __builtin_amdgcn_s_setprio(0);
       STAMP(3);
@@ -1419,7 +1476,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   };
   auto run_tile = [&](int t, auto mxt) __attribute__((always_inline)) {
     if constexpr (BAL) {
-      run_tile_sp5(t, std::integral_constant<bool, false>{}, std::integral_constant<int, -1>{});
+      run_tile_sp5(t, std::integral_constant<bool, false>{}, std::integral_constant<int, -1>{}, mxt);
       return;
     }
     if constexpr (SP) {
@@ -1564,7 +1621,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
       }
     }
   }
-  if constexpr (MX) {  // main (fp8) tiles, then any bf16 extension tiles of this K-range
+  if constexpr (MX && !BAL) {  // main (fp8) tiles, then any bf16 extension tiles of this K-range
     const int main_end = DROP ? nt : min(nt, max(pre, nt1 - tb));
     for (int t = pre; t < main_end; ++t) run_tile(t, MXT{});
     for (int t = main_end; t < nt; ++t) run_tile(t, BFT{});
@@ -1574,16 +1631,18 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
     using STT = std::integral_constant<bool, true>;
     using STF = std::integral_constant<bool, false>;
     using PRT = std::integral_constant<int, -1>;
+    using MT = std::integral_constant<bool, MX>;  // the main tiles' MFMA form
     int t = pre;
     if constexpr (UNR2) {
-      if ((t & 1) && t < main_lim - 2) run_tile_sp5(t++, STT{}, PRT{});
+      if ((t & 1) && t < main_lim - 2) run_tile_sp5(t++, STT{}, PRT{}, MT{});
       for (; t + 1 < main_lim - 2; t += 2) {
-        run_tile_sp5(t, STT{}, std::integral_constant<int, 0>{});
-        run_tile_sp5(t + 1, STT{}, std::integral_constant<int, 1>{});
+        run_tile_sp5(t, STT{}, std::integral_constant<int, 0>{}, MT{});
+        run_tile_sp5(t + 1, STT{}, std::integral_constant<int, 1>{}, MT{});
       }
     }
-    for (; t < main_lim - 2; ++t) run_tile_sp5(t, STT{}, PRT{});
-    for (; t < nt; ++t) run_tile_sp5(t, STF{}, PRT{});
+    for (; t < main_lim - 2; ++t) run_tile_sp5(t, STT{}, PRT{}, MT{});
+    for (; t < main_lim; ++t) run_tile_sp5(t, STF{}, PRT{}, MT{});
+    for (; t < nt; ++t) run_tile_sp5(t, STF{}, PRT{}, BFT{});  // (non-dropout: the extension tiles come last)
   } else {
     for (int t = pre; t < nt; ++t) run_tile(t, BFT{});
   }
@@ -1829,6 +1888,16 @@ int launch_default(const GemmArgs& a, hipStream_t s) {
   return launch_v5<0, DROP, false, 8>(a, s);
 }
 
+// the MXFP8 256 x 256 schedule (the ablation build can switch it: 17 = 8-phase, 14 = SP1)
+template <bool DROP>
+int launch_mx(const GemmArgs& a, hipStream_t s) {
+#ifdef OSPO_ABLATION
+  if (g_gemm_variant == 17) return launch_v5<0, DROP, true>(a, s);
+  if (g_gemm_variant == 14) return launch_v5<0, DROP, true, 1>(a, s);
+#endif
+  return launch_v5<0, DROP, true, 8>(a, s);
+}
+
 // NT tile: 256 x 256 (8-phase, split-K tail) whenever N % 256 == 0, else the 64 x 64 simple kernel.
 int pick_nt_tile(int M, int N) {
   (void)M;
@@ -1999,16 +2068,16 @@ extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const 
     a.rope_sn = (const bf16*)rope_sin;
     a.rope_T = rope_T;
     a.rope_cols = rope_cols;
-    return g_gemm_variant == 17 ? launch_v5<0, false, true>(a, stream) : launch_v5<0, false, true, 1>(a, stream);
+    return launch_mx<false>(a, stream);
   }
   if (drop) {
     a.drop_seed = drop_seed;
     a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
     a.drop_scale = 1.f / (1.f - drop_p);
     a.drop_ld = N;
-    return g_gemm_variant == 17 ? launch_v5<0, true, true>(a, stream) : launch_v5<0, true, true, 1>(a, stream);
+    return launch_mx<true>(a, stream);
   }
-  return g_gemm_variant == 17 ? launch_v5<0, false, true>(a, stream) : launch_v5<0, false, true, 1>(a, stream);
+  return launch_mx<false>(a, stream);
 }
 
 extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {

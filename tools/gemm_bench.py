@@ -20,6 +20,7 @@ SHAPES = [  # name, M, N, K, K2
 VARIANTS = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1").split(",") if v != ""]
 MX8 = os.environ.get("GB_MX8", "0") == "1"  # also time the block-scaled fp8 GEMM (+ its A quantization)
 SPLITS = [int(v) for v in os.environ.get("GB_SPLITS", "").split(",") if v != ""]  # forced tail splits (v0)
+DROP = os.environ.get("GB_DROP", "0") == "1"  # also time the dropout-masked extension form (the dX GEMMs)
 ROUNDS, ITERS = 5, 10
 
 
@@ -62,6 +63,9 @@ def main():
                 call("ospo_set_gemm_variant", v)
                 res[f"v{v}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
             res["hipblaslt"].append(timeit(lambda: torch.matmul(a, b.t(), out=ref)))
+            if DROP and k2:
+                call("ospo_set_gemm_variant", 0)
+                res.setdefault("v0_dropout", []).append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(77, 0.05))))
             for sp in SPLITS:
                 call("ospo_gemm_force_split", sp)
                 res[f"split{sp}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
