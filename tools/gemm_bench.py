@@ -20,7 +20,8 @@ SHAPES = [  # name, M, N, K, K2
 VARIANTS = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1").split(",") if v != ""]
 MX8 = os.environ.get("GB_MX8", "0") == "1"  # also time the block-scaled fp8 GEMM (+ its A quantization)
 SPLITS = [int(v) for v in os.environ.get("GB_SPLITS", "").split(",") if v != ""]  # forced tail splits (v0)
-DROP = os.environ.get("GB_DROP", "0") == "1"  # also time the dropout-masked extension form (the dX GEMMs)
+DROP = os.environ.get("GB_DROP", "0") == "1"
+RES = os.environ.get("GB_RES", "0") == "1"  # bias + residual epilogue on every variant (bit-equality covers it)  # also time the dropout-masked extension form (the dX GEMMs)
 ROUNDS, ITERS = 5, 10
 
 
@@ -44,6 +45,8 @@ def main():
         b2 = (torch.rand(n, k2, device="cuda") * 2 - 1).bfloat16() if k2 else None
         out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
         ref = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        ex = {"bias": (torch.rand(n, device="cuda") - 0.5).bfloat16(),
+              "residual": (torch.rand(m, n, device="cuda") - 0.5).bfloat16()} if RES else {}
         res = {f"v{v}": [] for v in VARIANTS}
         res["hipblaslt"] = []
         for sp in SPLITS:
@@ -61,7 +64,7 @@ def main():
                 res["mx8_quantA"].append(timeit(lambda: ops.quant_mx8(a, a8)))
             for v in VARIANTS:
                 call("ospo_set_gemm_variant", v)
-                res[f"v{v}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
+                res[f"v{v}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2, **ex)))
             res["hipblaslt"].append(timeit(lambda: torch.matmul(a, b.t(), out=ref)))
             if DROP and k2:
                 call("ospo_set_gemm_variant", 0)
@@ -73,11 +76,11 @@ def main():
         exp = a.float() @ b.float().t() + (a2.float() @ b2.float().t() if k2 else 0)
         errs, same = {}, {}
         call("ospo_set_gemm_variant", 0)
-        ops.gemm_nt(a, b, ref, a2=a2, b2=b2)
+        ops.gemm_nt(a, b, ref, a2=a2, b2=b2, **ex)
         for v in VARIANTS:
             call("ospo_set_gemm_variant", v)
             out.zero_()
-            ops.gemm_nt(a, b, out, a2=a2, b2=b2)
+            ops.gemm_nt(a, b, out, a2=a2, b2=b2, **ex)
             errs[f"v{v}"] = float((out.float() - exp).norm() / exp.norm())
             same[f"v{v}"] = bool(torch.equal(out, ref))
         call("ospo_set_gemm_variant", 0)
