@@ -25,9 +25,15 @@ int ospo_set_skinny_variant(int v);
 int ospo_set_gemv_variant(int v);
 /* Force the K-split count of GEMV schedules 2 / 3 (0 = automatic). */
 int ospo_set_gemv_splits(int s);
+/* Pipelined dK/dV kernel phase stamps (s_memtime sums per wave: first LDS wait, S/dP + softmax
+ * sub-phases, dV/dK sub-phases, vmcnt drain, barrier, tile count): 2 banks of 8 uint64 per wave,
+ * [kb][S][H][waves][8]; nullptr turns them off. */
+int ospo_attn_set_stamps(void* buf);
 /* Environment (read once): OSPO_ATTN_WAVES=4 (64-row attention workgroups), OSPO_ATTN_DBG and
- * OSPO_ATTN_DKDV_DBG=1..4 (attention decompositions, results INVALID), OSPO_F32ACC_LEGACY (old
- * tile rule of ospo_gemm_f32acc). */
+ * OSPO_ATTN_DKDV_DBG=1..5 (attention decompositions of the 8-wave round-2 dK/dV kernel, results
+ * INVALID; set OSPO_ATTN_DKDV_WAVES=8 with them), OSPO_ATTN_DKDV_R2 (the unpipelined round-2 dK/dV
+ * kernel), OSPO_ATTN_DKDV_WAVES=8 (8-wave dK/dV workgroups), OSPO_ATTN_DQ_2SLOT (the 2-slot dQ
+ * kernel), OSPO_F32ACC_LEGACY (old tile rule of ospo_gemm_f32acc). */
 
 #ifdef __cplusplus
 }

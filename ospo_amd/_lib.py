@@ -89,7 +89,8 @@ SIGNATURES = {
 
 # include/ospo_hip_ablation.h: only in libospo_hip_ablation.so (tools/ A/B runs, OSPO_HIP_LIB=...)
 ABLATION_SIGNATURES = {"ospo_set_gemm_variant": [I], "ospo_set_gemv_variant": [I], "ospo_set_gemv_splits": [I],
-                       "ospo_set_skinny_variant": [I], "ospo_gemm_set_debug_buffer": [P]}
+                       "ospo_set_skinny_variant": [I], "ospo_gemm_set_debug_buffer": [P],
+                       "ospo_attn_set_stamps": [P]}
 
 RESTYPES = {"ospo_lora_gdb_ws_bytes": c_size_t, "ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 

@@ -173,6 +173,32 @@ __device__ __forceinline__ float grp_sum(float x) {
 // RoPE backward (transpose of the rotate-half rotation) on fp32 accumulators whose lane
 // holds d = 16dt + 4g + j, dt = 0..7: d < 64 pairs with d + 64 (dt + 4) in the same lane.
 // cs / sn: bf16 [T][64] tables, t = the row's position in its sequence.
+// The same split in two: the table loads (issued early, so their latency hides under MFMA work) and
+// the rotation of the accumulators (bit-identical to rope_bwd_acc).
+struct RopeRow {
+  uint2 c[4], s[4];
+};
+__device__ __forceinline__ void rope_load(RopeRow& r, const bf16* cs, const bf16* sn, int t, int g) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    r.c[dt] = *reinterpret_cast<const uint2*>(cs + (long)t * 64 + 16 * dt + 4 * g);
+    r.s[dt] = *reinterpret_cast<const uint2*>(sn + (long)t * 64 + 16 * dt + 4 * g);
+  }
+}
+__device__ __forceinline__ void rope_apply(f32x4 (&v)[8], const RopeRow& r) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const uint2 cw = r.c[dt], sw = r.s[dt];
+    const float c[4] = {bits2f(cw.x & 0xffff), bits2f(cw.x >> 16), bits2f(cw.y & 0xffff), bits2f(cw.y >> 16)};
+    const float sv[4] = {bits2f(sw.x & 0xffff), bits2f(sw.x >> 16), bits2f(sw.y & 0xffff), bits2f(sw.y >> 16)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = v[dt][j], b = v[dt + 4][j];
+      v[dt][j] = a * c[j] + b * sv[j];
+      v[dt + 4][j] = b * c[j] - a * sv[j];
+    }
+  }
+}
 __device__ __forceinline__ void rope_bwd_acc(f32x4 (&v)[8], const bf16* cs, const bf16* sn, int t, int g) {
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
@@ -329,7 +355,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
 // DBG (A/B decomposition only, results invalid): 1 = no softmax VALU (P = S, dS = dP),
 // 2 = no dV/dK products, 3 = no S/dP products, 4 = no Q/dO loads after the first tile, 5 = no dS^T stores
 template <int NW, int DBG = 0>
-__global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc,
                                                             int vc, const bf16* __restrict__ dout, int ldd,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, bf16* __restrict__ dqkv,
@@ -383,6 +409,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
   };
 
   const int qt0 = (kb * KBW) / QB;  // first query tile with a row >= the block's first key
+  // The dQ kernel reads dS^T in 128-query blocks: a 64-key block that starts mid-block (NW = 4, odd
+  // qt0) writes the causal zeros of the block's first 64 queries, which its sweep does not reach.
+  if (dsrow && DBG != 5 && (qt0 & 1)) {
+    const uint4 z = {0u, 0u, 0u, 0u};
+    *reinterpret_cast<uint4*>(dsrow + (qt0 - 1) * QB + 16 * g) = z;
+    *reinterpret_cast<uint4*>(dsrow + (qt0 - 1) * QB + 16 * g + 8) = z;
+  }
   stage(qt0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -492,6 +525,401 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dkdv_kernel(const bf16* __re
       *reinterpret_cast<uint2*>(kp + 16 * dt + 4 * g) = a;
       *reinterpret_cast<uint2*>(vp + 16 * dt + 4 * g) = b;
     }
+  }
+}
+
+// 1-D grid -> (group = s * H + h, block j of nb).  Workgroup i is dispatched to XCD i % 8, so with
+// this map the nb blocks of a group run back to back on ONE XCD and the group's operands (re-read by
+// every block) stay in that XCD's L2; with the (head, sequence, block) grid the blocks of a group were
+// a whole chip-wide round apart and re-read their tiles from HBM.  Blocks of a group come in order
+// 0 .. nb - 1 (callers put the longest sweep first).
+// gm = 0: block-major instead (every group's block 0 first, chip-wide: heaviest sweeps first, no L2 reuse).
+__device__ __forceinline__ void group_major(int nb, int ngroups, int& grp, int& j, int gm = 1) {
+  const int i = blockIdx.x;
+  if (!gm) {
+    j = i / ngroups;
+    grp = i - j * ngroups;
+  } else if ((ngroups & 7) == 0) {
+    const int q = i >> 3;
+    grp = (q / nb) * 8 + (i & 7);
+    j = q - (q / nb) * nb;
+  } else {
+    grp = i / nb;
+    j = i - grp * nb;
+  }
+}
+
+// Store a wave's 16-row accumulator tile (lane: row l16, columns 16 dt + 4 g + j) as bf16 rows through
+// a 16 x 272-B LDS scratch (16-B pad: the 16 rows' 8-B writes land on distinct banks): 4 stores of
+// 16 B per lane, each 4 whole 256-B rows, instead of 8 x 8-B stores touching 16 rows each (a row-per-
+// lane store tail is store-ISSUE bound).  Rows r with row0 + r >= row_lim are not stored.
+constexpr int SCR_PITCH = ROWB + 16;
+constexpr int SCR_BYTES = 16 * SCR_PITCH;  // 4352 B per wave and matrix
+__device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf16* dst, long ld, int row0,
+                                             int row_lim, int lane) {
+  const int g = lane >> 4, l16 = lane & 15;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    uint2 pk;
+    pk.x = pack2(v[dt][0], v[dt][1]);
+    pk.y = pack2(v[dt][2], v[dt][3]);
+    *reinterpret_cast<uint2*>(scr + l16 * SCR_PITCH + (16 * dt + 4 * g) * 2) = pk;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = 4 * k + (lane >> 4);
+    const uint4 x = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + (lane & 15) * 16);
+    if (row0 + r < row_lim) *reinterpret_cast<uint4*>(dst + (long)(row0 + r) * ld + (lane & 15) * 8) = x;
+  }
+}
+
+// ------------------------------------------------------- dK / dV, pipelined ----
+// LDS reads as inline asm with immediate offsets: the compiler neither drains the in-flight
+// LDS-DMA before them nor splits their batches; each batch is waited once (registers tied).
+template <int OFF>
+__device__ __forceinline__ void lds_rd128(uint32_t a, bf16x8& v) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+}
+template <int OFF>
+__device__ __forceinline__ void lds_rdf4(uint32_t a, f32x4& v) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+}
+template <int OFF>
+__device__ __forceinline__ void lds_rdtr(uint32_t a, i16x4& v) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+}
+// 16 B per lane, buffer -> LDS (a device function: see sk3_lds16 in lora.hip)
+__device__ __forceinline__ void dk_lds16(__amdgpu_buffer_rsrc_t rs, char* dst, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, voff, 0, 0, 0);
+}
+// a batch of 8 row fragments (one query sub-tile) + the lse / delta quads of the previous sub-tile
+struct RowBatch {
+  bf16x8 f[8];
+  f32x4 l, d;
+};
+__device__ __forceinline__ void wait_rows(RowBatch& r) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(r.f[0]), "+v"(r.f[1]), "+v"(r.f[2]), "+v"(r.f[3]), "+v"(r.f[4]), "+v"(r.f[5]), "+v"(r.f[6]),
+                 "+v"(r.f[7]), "+v"(r.l), "+v"(r.d)::"memory");
+}
+// a batch of 8 transposed fragments (dO^T and Q^T, 4 column tiles each), 16 reads (+ lse / delta)
+struct TrBatch {
+  i16x4 lo[8], hi[8];
+  f32x4 l, d;
+};
+__device__ __forceinline__ void wait_tr(TrBatch& t) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(t.lo[0]), "+v"(t.lo[1]), "+v"(t.lo[2]), "+v"(t.lo[3]), "+v"(t.lo[4]), "+v"(t.lo[5]),
+                 "+v"(t.lo[6]), "+v"(t.lo[7]), "+v"(t.hi[0]), "+v"(t.hi[1]), "+v"(t.hi[2]), "+v"(t.hi[3]),
+                 "+v"(t.hi[4]), "+v"(t.hi[5]), "+v"(t.hi[6]), "+v"(t.hi[7])::"memory");
+}
+__device__ __forceinline__ void wait_tr_ld(TrBatch& t) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(t.lo[0]), "+v"(t.lo[1]), "+v"(t.lo[2]), "+v"(t.lo[3]), "+v"(t.lo[4]), "+v"(t.lo[5]),
+                 "+v"(t.lo[6]), "+v"(t.lo[7]), "+v"(t.hi[0]), "+v"(t.hi[1]), "+v"(t.hi[2]), "+v"(t.hi[3]),
+                 "+v"(t.hi[4]), "+v"(t.hi[5]), "+v"(t.hi[6]), "+v"(t.hi[7]), "+v"(t.l), "+v"(t.d)::"memory");
+}
+
+// The same product and outputs as attn_bwd_dkdv_kernel (bit-identical: same MFMA operands and
+// accumulation order, same softmax arithmetic), reorganised as 8 sub-phases per 64-query tile so
+// that no phase waits alone: every sub-phase first waits for the batch of LDS reads issued one
+// sub-phase earlier, issues the next batch, then runs 8 MFMAs next to the VALU work of an earlier
+// sub-tile:
+//   sp0  S, dP of sub-tile 0                    sp4  dV, dK (queries 0-31, d tiles 0-3) | softmax 3
+//   sp1  S, dP of sub-tile 1 | softmax 0        sp5  dV, dK (queries 0-31, d tiles 4-7)
+//   sp2  S, dP of sub-tile 2 | softmax 1        sp6  dV, dK (queries 32-63, d tiles 0-3)
+//   sp3  S, dP of sub-tile 3 | softmax 2        sp7  dV, dK (queries 32-63, d tiles 4-7)
+// (the round-2 kernel ran S/dP, softmax and dV/dK one after another, each LDS batch waited right
+// before its MFMAs: ~18 % MFMA busy at 2 waves per SIMD).  The first batch of a tile is issued
+// right after the tile barrier.
+// DBG 1 (ablation build): s_memtime sums per wave of the tile phases -> dbg[8 per wave]
+template <int NW, int DBG = 0>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv3_kernel(
+    const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, const bf16* __restrict__ dout, int ldd,
+    const float* __restrict__ lse, const float* __restrict__ delta, bf16* __restrict__ dqkv, int ldg, int T, int H,
+    float scale, const bf16* __restrict__ rcs, const bf16* __restrict__ rsn, bf16* __restrict__ dsT, int ds_ld,
+    unsigned long long* __restrict__ dbg, int gm) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES + 4 * 64 * 4];
+  unsigned long long st_acc[7] = {0, 0, 0, 0, 0, 0, 0};  // DBG: first wait, sp0-3, sp4-7, vmcnt, barrier, tiles, stage
+  auto stamp = [&]() -> unsigned long long { return DBG ? __builtin_amdgcn_s_memtime() : 0ull; };
+  const unsigned long long rt_start = DBG ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const unsigned long long mt_start = stamp();
+  float* Lsb = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int KBW = 16 * NW;
+  int grp, kb;  // kb = 0 (the longest sweep) first within the group
+  group_major((T + KBW - 1) / KBW, gridDim.x / ((T + KBW - 1) / KBW), grp, kb, gm);
+  const int h = grp % H, s = grp / H;
+  const int g = lane >> 4, l16 = lane & 15;
+  const long rowbase = (long)s * T;
+  const int nq = (T + QB - 1) / QB;
+  const int key_l = kb * KBW + wave * 16 + l16;
+  const int key_c = key_l < T ? key_l : T - 1;
+  bf16x8 kf[4], vf[4];
+  {
+    const bf16* kp = qkv + (rowbase + key_c) * ldq + kc + h * HD;
+    const bf16* vp = qkv + (rowbase + key_c) * ldq + vc + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      kf[d] = *reinterpret_cast<const bf16x8*>(kp + 32 * d + 8 * g);
+      vf[d] = *reinterpret_cast<const bf16x8*>(vp + 32 * d + 8 * g);
+    }
+  }
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { dk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+  const bf16* qbase = qkv + rowbase * ldq + qc + h * HD;
+  const bf16* obase = dout + rowbase * ldd + h * HD;
+  const float* lse_sh = lse + ((long)s * H + h) * T;
+  const float* del_sh = delta + ((long)s * H + h) * T;
+  bf16* dsrow = dsT ? dsT + ((long)s * H + h) * ds_ld * (long)ds_ld + (long)key_l * ds_ld : nullptr;
+
+  // per-lane LDS byte offsets inside one image (row fragments: 4 d steps; transposed: 8 column tiles)
+  uint32_t rowo[4], tro[8];
+  {
+    const int sw = (l16 & 7) << 1;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) rowo[d] = l16 * ROWB + (((4 * d + g) ^ sw) << 4);
+    const int li = l16, q = li >> 2, p = li & 3;
+    const int r1 = 4 * g + q;  // + 32u (immediate); r1 & 7 does not depend on u
+#pragma unroll
+    for (int d0 = 0; d0 < 8; ++d0) {
+      const int x = 2 * d0 + (p >> 1);
+      tro[d0] = r1 * ROWB + ((x ^ aswz(r1)) << 4) + ((p & 1) << 3);
+    }
+  }
+  {  // absolute LDS addresses; the buffer, sub-tile and image offsets are all immediates
+    const uint32_t smem_a = lds_u32(smem);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) rowo[d] += smem_a;
+#pragma unroll
+    for (int d0 = 0; d0 < 8; ++d0) tro[d0] += smem_a;
+  }
+  const uint32_t la = lds_u32(reinterpret_cast<const char*>(Lsb)) + 16 * g;  // + b*256 (+512 delta) + 64a
+
+  // Q / dO tiles by buffer_load ... lds from per-sequence descriptors: 32-bit per-lane offsets (row
+  // clamped to T - 1), no 64-bit address math per piece (the global_load_lds form kept several 64-bit
+  // bases live and, at 256 VGPRs, a spilled one was reloaded between the DMA issues behind vmcnt(0))
+  const __amdgpu_buffer_rsrc_t rsQ = __builtin_amdgcn_make_buffer_rsrc((void*)qbase, 0, T * ldq * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc((void*)obase, 0, T * ldd * 2, 0x00020000);
+  const int srow = 4 * wave + (lane >> 4);                       // + 16 i: the row of piece wave + 4 i
+  const uint32_t chb = (uint32_t)(((lane & 15) ^ aswz(srow)) << 4);  // aswz(srow + 16 i) == aswz(srow)
+  auto stage = [&](int qt, int b) {
+    char* Qs = smem + b * 2 * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 16 / NW; ++i) {
+      int r = qt * QB + 16 * i + srow;
+      r = r < T ? r : T - 1;
+      dk_lds16(rsQ, Qs + (wave + NW * i) * 1024, (uint32_t)r * (uint32_t)(ldq * 2) + chb);
+      dk_lds16(rsO, Qs + TILE_BYTES + (wave + NW * i) * 1024, (uint32_t)r * (uint32_t)(ldd * 2) + chb);
+    }
+    if (wave < 2) {
+      int q = qt * QB + lane;
+      q = q < T ? q : T - 1;
+      const float* src = (wave == 0 ? lse_sh : del_sh) + q;
+      __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(Lsb + (wave * 2 + b) * 64), 4, 0, 0);
+    }
+  };
+  // batch issue: Q and dO row fragments of sub-tile A (4 d steps each) + its lse / delta quads
+  auto issue_rows = [&](auto b_c, auto a_c, RowBatch& r) {
+    constexpr int B = decltype(b_c)::value, A = decltype(a_c)::value;
+    constexpr int O = B * 2 * TILE_BYTES + A * 16 * ROWB;
+    lds_rd128<O>(rowo[0], r.f[0]);
+    lds_rd128<O + TILE_BYTES>(rowo[0], r.f[4]);
+    lds_rd128<O>(rowo[1], r.f[1]);
+    lds_rd128<O + TILE_BYTES>(rowo[1], r.f[5]);
+    lds_rd128<O>(rowo[2], r.f[2]);
+    lds_rd128<O + TILE_BYTES>(rowo[2], r.f[6]);
+    lds_rd128<O>(rowo[3], r.f[3]);
+    lds_rd128<O + TILE_BYTES>(rowo[3], r.f[7]);
+    if constexpr (A > 0) {  // lse / delta of sub-tile A - 1, whose softmax runs beside S / dP of A
+      lds_rdf4<B * 256 + (A - 1) * 64>(la, r.l);
+      lds_rdf4<B * 256 + (A - 1) * 64 + 512>(la, r.d);
+    }
+  };
+  // batch issue: dO^T and Q^T fragments of query half U, column tiles 4*DH .. 4*DH + 3
+  auto issue_tr = [&](auto b_c, auto u_c, auto dh_c, TrBatch& t) {
+    constexpr int B = decltype(b_c)::value, U = decltype(u_c)::value, DH = decltype(dh_c)::value;
+    constexpr int O = B * 2 * TILE_BYTES + U * 32 * ROWB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lds_rdtr<O + TILE_BYTES>(tro[4 * DH + i], t.lo[i]);
+      lds_rdtr<O + TILE_BYTES + 16 * ROWB>(tro[4 * DH + i], t.hi[i]);
+      lds_rdtr<O>(tro[4 * DH + i], t.lo[4 + i]);
+      lds_rdtr<O + 16 * ROWB>(tro[4 * DH + i], t.hi[4 + i]);
+    }
+  };
+
+  const int qt0 = (kb * KBW) / QB;
+  if (dsrow && (qt0 & 1)) {  // causal zeros of the dQ kernel's 128-query block (see attn_bwd_dkdv_kernel)
+    const uint4 z = {0u, 0u, 0u, 0u};
+    *reinterpret_cast<uint4*>(dsrow + (qt0 - 1) * QB + 16 * g) = z;
+    *reinterpret_cast<uint4*>(dsrow + (qt0 - 1) * QB + 16 * g + 8) = z;
+  }
+  stage(qt0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const unsigned long long mt_loop = stamp();
+
+  // RoPE tables of this lane's key: loaded inside the last tile (sp5), applied after the loop
+  RopeRow rr;
+  const bf16* rcs_ = rcs ? rcs : qkv;  // any readable rows when there is no RoPE (not applied)
+  const bf16* rsn_ = rcs ? rsn : qkv;
+  auto tile = [&](const int qt, auto diag_c, auto b_c, auto last_c) {
+    constexpr bool DIAG = decltype(diag_c)::value;
+    constexpr bool LAST = decltype(last_c)::value;
+    constexpr int b = decltype(b_c)::value;
+    const unsigned long long cs0 = stamp();
+    if (qt + 1 < nq) stage(qt + 1, b ^ 1);
+    const int lo = key_l - (qt * QB + 4 * g), hi = T - (qt * QB + 4 * g);
+    f32x4 sv[4], dp[4];
+    bf16x8 pb[2], sb[2];
+
+    auto sdp = [&](auto a_c, RowBatch& r) {  // S, dP of sub-tile A: 8 MFMAs
+      constexpr int A = decltype(a_c)::value;
+      sv[A] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[A] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        sv[A] = MFMA(r.f[d], kf[d], sv[A]);
+        dp[A] = MFMA(r.f[4 + d], vf[d], dp[A]);
+      }
+    };
+    auto softmax = [&](auto a_c, const f32x4& lq, const f32x4& dq4) {
+      constexpr int A = decltype(a_c)::value;
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        float x = sv[A][j], y = sv[A][j + 1];
+        hf_scores2(x, y, scale);
+        if (DIAG) {
+          const int e = 16 * A + j;
+          x = (e < lo || e >= hi) ? -INFINITY : x;
+          y = (e + 1 < lo || e + 1 >= hi) ? -INFINITY : y;
+        }
+        const float px = __builtin_amdgcn_exp2f((x - lq[j]) * L2E);
+        const float py = __builtin_amdgcn_exp2f((y - lq[j + 1]) * L2E);
+        sv[A][j] = px;
+        sv[A][j + 1] = py;
+        dp[A][j] = px * (dp[A][j] - dq4[j]) * scale;
+        dp[A][j + 1] = py * (dp[A][j + 1] - dq4[j + 1]) * scale;
+      }
+      {  // dsT is required here (the 5-product path): no branch inside the sub-phase
+        uint2 pk;
+        pk.x = pack2(dp[A][0], dp[A][1]);
+        pk.y = pack2(dp[A][2], dp[A][3]);
+        *reinterpret_cast<uint2*>(dsrow + qt * QB + 16 * A + 4 * g) = pk;
+      }
+    };
+    auto dvdk = [&](auto u_c, auto dh_c, TrBatch& t) {  // 8 MFMAs
+      constexpr int U = decltype(u_c)::value, DH = decltype(dh_c)::value;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dv[4 * DH + i] = MFMA(trp_join(t.lo[i], t.hi[i]), pb[U], dv[4 * DH + i]);
+        dk[4 * DH + i] = MFMA(trp_join(t.lo[4 + i], t.hi[4 + i]), sb[U], dk[4 * DH + i]);
+      }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    RowBatch r0, r1;
+    TrBatch t0, t1;
+    const unsigned long long c0 = stamp();
+    issue_rows(b_c, I0{}, r0);
+    r0.l = r0.d = f32x4{0.f, 0.f, 0.f, 0.f};
+    wait_rows(r0);                                     // sp0
+    const unsigned long long c1 = stamp();
+    issue_rows(b_c, I1{}, r1);
+    sdp(I0{}, r0);
+    wait_rows(r1);                                     // sp1
+    issue_rows(b_c, I2{}, r0);
+    sdp(I1{}, r1);
+    softmax(I0{}, r1.l, r1.d);
+    wait_rows(r0);                                     // sp2
+    issue_rows(b_c, I3{}, r1);
+    sdp(I2{}, r0);
+    softmax(I1{}, r0.l, r0.d);
+    pb[0] = pack_perm(sv[0], sv[1]);
+    sb[0] = pack_perm(dp[0], dp[1]);
+    wait_rows(r1);                                     // sp3
+    issue_tr(b_c, I0{}, I0{}, t0);
+    lds_rdf4<b * 256 + 3 * 64>(la, t0.l);
+    lds_rdf4<b * 256 + 3 * 64 + 512>(la, t0.d);
+    sdp(I3{}, r1);
+    softmax(I2{}, r1.l, r1.d);
+    const unsigned long long c2 = stamp();
+    wait_tr_ld(t0);                                    // sp4
+    const f32x4 l3 = t0.l, d3 = t0.d;
+    issue_tr(b_c, I0{}, I1{}, t1);
+    dvdk(I0{}, I0{}, t0);
+    softmax(I3{}, l3, d3);
+    pb[1] = pack_perm(sv[2], sv[3]);
+    sb[1] = pack_perm(dp[2], dp[3]);
+    wait_tr(t1);                                       // sp5
+    issue_tr(b_c, I1{}, I0{}, t0);
+    dvdk(I0{}, I1{}, t1);
+    wait_tr(t0);                                       // sp6
+    issue_tr(b_c, I1{}, I1{}, t1);
+    dvdk(I1{}, I0{}, t0);
+    wait_tr(t1);                                       // sp7
+    if constexpr (LAST) rope_load(rr, rcs_, rsn_, key_c, g);
+    dvdk(I1{}, I1{}, t1);
+    const unsigned long long c3 = stamp();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long c4 = stamp();
+    __syncthreads();
+    if constexpr (DBG != 0) {
+      const unsigned long long c5 = stamp();
+      st_acc[0] += c1 - c0; st_acc[1] += c2 - c1; st_acc[2] += c3 - c2; st_acc[3] += c4 - c3; st_acc[4] += c5 - c4;
+      st_acc[5] += 1;
+      st_acc[6] += c0 - cs0;
+    }
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  for (int qt = qt0; qt < nq - 1; ++qt) {
+    const bool diag = qt * QB < kb * KBW + KBW || (qt + 1) * QB > T;
+    if ((qt - qt0) & 1) {
+      if (diag) tile(qt, std::true_type{}, B1{}, std::false_type{});
+      else tile(qt, std::false_type{}, B1{}, std::false_type{});
+    } else {
+      if (diag) tile(qt, std::true_type{}, B0{}, std::false_type{});
+      else tile(qt, std::false_type{}, B0{}, std::false_type{});
+    }
+  }
+  // the last tile: masks applied (exact for any tile), RoPE tables fetched under its MFMAs
+  if ((nq - 1 - qt0) & 1)
+    tile(nq - 1, std::true_type{}, B1{}, std::true_type{});
+  else
+    tile(nq - 1, std::true_type{}, B0{}, std::true_type{});
+
+  if constexpr (DBG != 0) {
+    if (lane == 0) {
+      const long w = ((long)kb * (gridDim.x / ((T + KBW - 1) / KBW)) + grp) * NW + wave;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) dbg[w * 8 + i] = st_acc[i];
+      dbg[w * 8 + 6 + (long)gridDim.x * NW * 8] = st_acc[6];  // second bank
+      dbg[w * 8 + 5] = ((mt_loop - mt_start) << 32) | ((stamp() - mt_start) & 0xffffffffull);  // prologue | whole
+      const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+      const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+      dbg[w * 8 + 6] = rt_start;
+      dbg[w * 8 + 7] = (rt_end << 32) | ((st_acc[5] & 0xff) << 20) | ((unsigned long long)(xcc & 0xf) << 16) |
+                       (hwid & 0xffff);
+    }
+  }
+  // the tile buffers are free after the last tile's barrier: each wave stages its dK, dV rows there
+  if (rcs) rope_apply(dk, rr);
+  {
+    char* scr = smem + wave * 2 * SCR_BYTES;
+    const int key0 = kb * KBW + wave * 16;
+    store_rows16(dk, scr, dqkv + rowbase * ldg + kc + h * HD, ldg, key0, T, lane);
+    store_rows16(dv, scr + SCR_BYTES, dqkv + rowbase * ldg + vc + h * HD, ldg, key0, T, lane);
   }
 }
 
@@ -628,25 +1056,40 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
 
 
 // delta[s, h, t] = rowsum(dO * O) over the head's 128 columns (fp32): the softmax-backward term the
-// dK/dV kernel reads.  One workgroup per row s*T + t; 16 lanes per head, 8 columns (16 B) per lane.
+// dK/dV kernel reads.  16 lanes per (row, head), 8 columns (16 B) per lane; a workgroup covers
+// 1024 such 16-B chunks with all 8 loads of a lane issued before the first product.
+constexpr int DELTA_CH = 4;  // chunks per lane
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16* __restrict__ dout, int ldd,
                                                              const bf16* __restrict__ o, int ldo,
-                                                             float* __restrict__ delta, int T, int H) {
-  const long row = blockIdx.x;
-  const int s = (int)(row / T), t = (int)(row % T);
-  for (int c = threadIdx.x; c < H * 16; c += 256) {
-    const int h = c >> 4;
-    const u32x4 a = *reinterpret_cast<const u32x4*>(dout + row * ldd + c * 8);
-    const u32x4 b = *reinterpret_cast<const u32x4*>(o + row * ldo + c * 8);
+                                                             float* __restrict__ delta, int T, int H, long n_chunks) {
+  const int cpr = H * 16;  // chunks per row
+  u32x4 a[DELTA_CH], b[DELTA_CH];
+  long row[DELTA_CH];
+  int cc[DELTA_CH];
+#pragma unroll
+  for (int i = 0; i < DELTA_CH; ++i) {
+    long c = (long)blockIdx.x * (256 * DELTA_CH) + i * 256 + threadIdx.x;
+    c = c < n_chunks ? c : n_chunks - 1;  // clamped lanes recompute the last chunk, store nothing
+    row[i] = c / cpr;
+    cc[i] = (int)(c - row[i] * cpr);
+    a[i] = *reinterpret_cast<const u32x4*>(dout + row[i] * ldd + cc[i] * 8);
+    b[i] = *reinterpret_cast<const u32x4*>(o + row[i] * ldo + cc[i] * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < DELTA_CH; ++i) {
     float fa[8], fb[8];
-    unpack8(a, fa);
-    unpack8(b, fb);
+    unpack8(a[i], fa);
+    unpack8(b[i], fb);
     float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v += fa[i] * fb[i];
+    for (int k = 0; k < 8; ++k) v += fa[k] * fb[k];
 #pragma unroll
     for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 16);
-    if ((c & 15) == 0) delta[((long)s * H + h) * T + t] = v;
+    const long c = (long)blockIdx.x * (256 * DELTA_CH) + i * 256 + threadIdx.x;
+    if ((cc[i] & 15) == 0 && c < n_chunks) {
+      const int s = (int)(row[i] / T), t = (int)(row[i] - (long)s * T);
+      delta[((long)s * H + (cc[i] >> 4)) * T + t] = v;
+    }
   }
 }
 
@@ -752,6 +1195,110 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ds_kernel(const bf16* __r
   }
 }
 
+// Stage 32 rows x 128 bf16 (clamped to [0, row_lim)): 8 pieces of 1 KiB (4 rows each) over the NW waves.
+template <int NW>
+__device__ __forceinline__ void stage32(const bf16* base, int ld, int row0, int row_lim, int col0, char* lds,
+                                        int wave, int lane) {
+#pragma unroll
+  for (int p = wave; p < 8; p += NW) {
+    const int row = p * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ aswz(row);
+    int gr = row0 + row;
+    gr = gr < row_lim ? gr : row_lim - 1;
+    glds16(base + (long)gr * ld + col0 + ch * 8, lds + p * 1024);
+  }
+}
+
+// dQ = dS . K, ring form: the same product and tile shape as attn_bwd_dq_ds_kernel, but the K / dS^T
+// tiles are 32 keys deep and staged through a 4-slot LDS ring (3 stages in flight while one is read):
+// the 2-slot form waits for each 32-KiB tile right after one tile of MFMA work, so at T = 600 it ran
+// at ~2 TB/s of dS^T reads, load-latency bound.  Iteration kt: wait for stage kt (own DMA, counted),
+// barrier (every wave's stage-kt pieces landed, every wave done reading slot kt - 1), refill slot kt - 1
+// with stage kt + 3, then 16 MFMAs per wave from 10 transposed fragments.  Same accumulation order as
+// the 2-slot kernel (keys ascending, 32 per MFMA), so bit-identical.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ring_kernel(const bf16* __restrict__ qkv, int ldq, int qc,
+                                                               int kc, const bf16* __restrict__ dsT, int ds_ld,
+                                                               bf16* __restrict__ dqkv, int ldg, int T, int H,
+                                                               const bf16* __restrict__ rcs,
+                                                               const bf16* __restrict__ rsn, int gm) {
+  constexpr int SLOT = 2 * 32 * ROWB;  // K [32][128] | dS^T [32][128 queries]: 16 KiB
+  constexpr int NSLOT = 4;
+  constexpr int PIECES = 2 * (8 / NW);  // DMA pieces per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int RB = 32 * NW;
+  const int nqb = (T + RB - 1) / RB;
+  int grp, j;
+  group_major(nqb, gridDim.x / nqb, grp, j, gm);
+  const int qb = nqb - 1 - j;  // the longest sweep first within the group
+  const int h = grp % H, s = grp / H;
+  const int g = lane >> 4, l16 = lane & 15;
+  const long rowbase = (long)s * T;
+  const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
+  const bf16* dbase = dsT + ((long)s * H + h) * ds_ld * (long)ds_ld;
+
+  f32x4 dq[2][8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dq[a][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // RoPE tables of this lane's two query rows, fetched before the sweep (applied at the end)
+  RopeRow rr[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int qrow = qb * RB + wave * 32 + 16 * a + l16;
+    rope_load(rr[a], rcs ? rcs : qkv, rcs ? rsn : qkv, qrow < T ? qrow : T - 1, g);
+  }
+  const int last = (qb * RB + RB - 1 < T ? qb * RB + RB - 1 : T - 1);
+  const int n_st = last / 32 + 1;  // 32-key stages up to the block's last query
+  auto stage = [&](int st) {
+    char* Ks = smem + (st % NSLOT) * SLOT;
+    stage32<NW>(kbase, ldq, st * 32, T, 0, Ks, wave, lane);
+    stage32<NW>(dbase, ds_ld, st * 32, ds_ld, qb * RB, Ks + 32 * ROWB, wave, lane);
+  };
+#pragma unroll
+  for (int st = 0; st < NSLOT - 1; ++st)
+    if (st < n_st) stage(st);
+  for (int kt = 0; kt < n_st; ++kt) {
+    // own pieces of stage kt landed: the stages issued after it may stay in flight
+    const int newer = n_st - 1 - kt < NSLOT - 2 ? n_st - 1 - kt : NSLOT - 2;
+    if (newer >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
+    else if (newer == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + NSLOT - 1 < n_st) stage(kt + NSLOT - 1);
+    const char* Ks = smem + (kt % NSLOT) * SLOT;
+    const char* Ds = Ks + 32 * ROWB;
+    i16x4 blo[2], bhi[2], lo[8], hi[8];
+    trn_issue(Ds, 0, wave * 32, lane, blo[0], bhi[0]);
+    trn_issue(Ds, 0, wave * 32 + 16, lane, blo[1], bhi[1]);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) trn_issue(Ks, 0, 16 * d, lane, lo[d], hi[d]);
+    trp_wait2(blo, bhi);
+    trp_wait8(lo, hi);
+    const bf16x8 b0 = trp_join(blo[0], bhi[0]), b1 = trp_join(blo[1], bhi[1]);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const bf16x8 a = trp_join(lo[d], hi[d]);
+      dq[0][d] = MFMA(a, b0, dq[0][d]);
+      dq[1][d] = MFMA(a, b1, dq[1][d]);
+    }
+  }
+  __syncthreads();  // every wave done with the ring: its slots become the store scratch
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    if (rcs) rope_apply(dq[a], rr[a]);
+    store_rows16(dq[a], smem + (wave * 2 + a) * SCR_BYTES, dqkv + rowbase * ldg + qc + h * HD, ldg,
+                 qb * RB + wave * 32 + 16 * a, T, lane);
+  }
+}
+
 // dS^T rows / columns per (sequence, head): T rounded up to the dQ kernel's 128-query blocks
 int ds_pitch(int T) { return (T + 127) / 128 * 128; }
 
@@ -768,8 +1315,31 @@ int attn_waves() {
   return 8;
 #endif
 }
+// dK/dV workgroup of the 5-product backward: 4 waves (64 keys, <= 256 VGPRs), so two workgroups share
+// a CU and their tile barriers interleave (8 waves: one workgroup per CU, both waves of a SIMD in step;
+// 212-217 vs 229-230 us per layer at the step shape, tools/attn_bench.py).  Ablation: OSPO_ATTN_DKDV_WAVES=8.
+void* g_attn_stamps = nullptr;  // ablation: dK/dV phase stamps (ospo_attn_set_stamps)
+int dkdv_waves() {
+#ifdef OSPO_ABLATION
+  static const int nw = [] {
+    const char* e = getenv("OSPO_ATTN_DKDV_WAVES");
+    return (e && atoi(e) == 8) ? 8 : 4;
+  }();
+  return nw;
+#else
+  return 4;
+#endif
+}
 
 }  // namespace
+
+#ifdef OSPO_ABLATION
+// ablation only: buffer for the pipelined dK/dV kernel's phase stamps (2 banks of 8 x u64 per wave), nullptr = off
+extern "C" int ospo_attn_set_stamps(void* buf) {
+  g_attn_stamps = buf;
+  return OSPO_OK;
+}
+#endif
 
 extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
                                    int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
@@ -830,19 +1400,54 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
 #else
   auto dkdv = attn_bwd_dkdv_kernel<8>;
 #endif
-  if (ds_ws && nw == 8) {
+  if (ds_ws) {
     // delta, then dK/dV (which also stores dS^T), then dQ = dS . K: 5 MFMA products instead of 7
     const int p = ds_pitch(T);
-    hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3(S * T), dim3(256), 0, stream, (const bf16*)dout, ld_do,
-                       (const bf16*)o, ld_o, delta_ws, T, n_heads);
+    const int nwd = dkdv_waves();
+    if (nwd != nw) {
+      dkdv = nwd == 4 ? attn_bwd_dkdv_kernel<4> : attn_bwd_dkdv_kernel<8>;
+      grid = dim3(n_heads, S, (T + 16 * nwd - 1) / (16 * nwd));
+    }
+    // workgroup order of the 1-D grids (group_major): dK/dV heaviest key blocks first chip-wide (the
+    // group-major order ended on a few heavy workgroups: 152 vs 140 us), dQ group-major
+    int order_dkdv = 0, order_dq = 1;
+#ifdef OSPO_ABLATION
+    if (const char* e = getenv("OSPO_ATTN_ORDER")) order_dkdv = order_dq = atoi(e);  // A/B: 0 block-, 1 group-major
+#endif
+    using DkdvFn = decltype(&attn_bwd_dkdv3_kernel<4>);
+    DkdvFn dkdv3 = attn_bwd_dkdv3_kernel<4>;
+#ifdef OSPO_ABLATION
+    static const bool dkdv_r2 = getenv("OSPO_ATTN_DKDV_R2") != nullptr;  // A/B: the unpipelined round-2 kernel
+    if (nwd == 8) dkdv3 = attn_bwd_dkdv3_kernel<8>;
+    if (g_attn_stamps) dkdv3 = nwd == 4 ? attn_bwd_dkdv3_kernel<4, 1> : attn_bwd_dkdv3_kernel<8, 1>;
+    if (dkdv_r2 || dkdv_dbg != 0) dkdv3 = nullptr;
+#endif
+    const long n_chunks = (long)S * T * n_heads * 16;
+    hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)((n_chunks + 256 * DELTA_CH - 1) / (256 * DELTA_CH))),
+                       dim3(256), 0, stream, (const bf16*)dout, ld_do, (const bf16*)o, ld_o, delta_ws, T, n_heads,
+                       n_chunks);
     OSPO_CHECK_LAUNCH();
-    hipLaunchKernelGGL(dkdv, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
-                       (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
-                       (bf16*)ds_ws, p);
+    if (dkdv3)
+      hipLaunchKernelGGL(dkdv3, dim3(S * n_heads * ((T + 16 * nwd - 1) / (16 * nwd))), dim3(64 * nwd), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+                         (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
+                         (bf16*)ds_ws, p, (unsigned long long*)g_attn_stamps, order_dkdv);
+    else
+      hipLaunchKernelGGL(dkdv, grid, dim3(64 * nwd), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+                         (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
+                         (bf16*)ds_ws, p);
     OSPO_CHECK_LAUNCH();
-    dim3 gq(n_heads, S, (T + 127) / 128);
-    hipLaunchKernelGGL(attn_bwd_dq_ds_kernel<4>, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
-                       (const bf16*)ds_ws, p, (bf16*)dqkv, ld_dqkv, T, n_heads, rc, rs);
+    dim3 gq(S * n_heads * ((T + 127) / 128));  // group-major 1-D grid (see group_major)
+    bool dq_two_slot = false;
+#ifdef OSPO_ABLATION
+    dq_two_slot = getenv("OSPO_ATTN_DQ_2SLOT") != nullptr;  // A/B: the round-2 2-slot dQ kernel (3-D grid)
+#endif
+    if (!dq_two_slot)
+      hipLaunchKernelGGL(attn_bwd_dq_ring_kernel<4>, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+                         (const bf16*)ds_ws, p, (bf16*)dqkv, ld_dqkv, T, n_heads, rc, rs, order_dq);
+    else
+      hipLaunchKernelGGL(attn_bwd_dq_ds_kernel<4>, dim3(n_heads, S, (T + 127) / 128), dim3(256), 0, stream,
+                         (const bf16*)qkv, ld_qkv, q_col, k_col, (const bf16*)ds_ws, p, (bf16*)dqkv, ld_dqkv, T,
+                         n_heads, rc, rs);
     OSPO_CHECK_LAUNCH();
     return OSPO_OK;
   }
