@@ -599,6 +599,24 @@ struct RowBatch {
   bf16x8 f[8];
   f32x4 l, d;
 };
+// half of a transposed batch: 4 dO^T (or Q^T) fragments, 8 reads (+ lse / delta quads in the first)
+struct TrHalf {
+  i16x4 lo[4], hi[4];
+  f32x4 l, d;
+};
+__device__ __forceinline__ void wait_trh(TrHalf& t) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(t.lo[0]), "+v"(t.lo[1]), "+v"(t.lo[2]), "+v"(t.lo[3]), "+v"(t.hi[0]), "+v"(t.hi[1]),
+                 "+v"(t.hi[2]), "+v"(t.hi[3]), "+v"(t.l), "+v"(t.d)::"memory");
+}
+// half of a row batch: the 4 Q (or dO) fragments of one sub-tile + one quad (lse or delta)
+struct HalfBatch {
+  bf16x8 f[4];
+  f32x4 x;
+};
+__device__ __forceinline__ void wait_half(HalfBatch& r) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r.f[0]), "+v"(r.f[1]), "+v"(r.f[2]), "+v"(r.f[3]), "+v"(r.x)::"memory");
+}
 __device__ __forceinline__ void wait_rows(RowBatch& r) {
   asm volatile("s_waitcnt lgkmcnt(0)"
                : "+v"(r.f[0]), "+v"(r.f[1]), "+v"(r.f[2]), "+v"(r.f[3]), "+v"(r.f[4]), "+v"(r.f[5]), "+v"(r.f[6]),
@@ -726,6 +744,26 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
   };
   // batch issue: Q and dO row fragments of sub-tile A (4 d steps each) + its lse / delta quads
+  // half batches: Q (IMG 0) or dO (IMG 1) fragments of sub-tile A + lse (IMG 0) / delta (IMG 1) of A - 1
+  auto issue_half = [&](auto b_c, auto a_c, auto img_c, HalfBatch& r) {
+    constexpr int B = decltype(b_c)::value, A = decltype(a_c)::value, IMG = decltype(img_c)::value;
+    constexpr int O = B * 2 * TILE_BYTES + A * 16 * ROWB + IMG * TILE_BYTES;
+    lds_rd128<O>(rowo[0], r.f[0]);
+    lds_rd128<O>(rowo[1], r.f[1]);
+    lds_rd128<O>(rowo[2], r.f[2]);
+    lds_rd128<O>(rowo[3], r.f[3]);
+    if constexpr (A > 0) lds_rdf4<B * 256 + (A - 1) * 64 + IMG * 512>(la, r.x);
+  };
+  // transposed half batches: dO^T (IMG 1, for dV) or Q^T (IMG 0, for dK), query half U, column tiles 4 DH ..
+  auto issue_trh = [&](auto b_c, auto u_c, auto dh_c, auto img_c, TrHalf& t) {
+    constexpr int B = decltype(b_c)::value, U = decltype(u_c)::value, DH = decltype(dh_c)::value;
+    constexpr int O = B * 2 * TILE_BYTES + U * 32 * ROWB + decltype(img_c)::value * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lds_rdtr<O>(tro[4 * DH + i], t.lo[i]);
+      lds_rdtr<O + 16 * ROWB>(tro[4 * DH + i], t.hi[i]);
+    }
+  };
   auto issue_rows = [&](auto b_c, auto a_c, RowBatch& r) {
     constexpr int B = decltype(b_c)::value, A = decltype(a_c)::value;
     constexpr int O = B * 2 * TILE_BYTES + A * 16 * ROWB;
@@ -780,6 +818,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     f32x4 sv[4], dp[4];
     bf16x8 pb[2], sb[2];
 
+    auto s_only = [&](auto a_c, HalfBatch& r) {  // S of sub-tile A: 4 MFMAs
+      constexpr int A = decltype(a_c)::value;
+      sv[A] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) sv[A] = MFMA(r.f[d], kf[d], sv[A]);
+    };
+    auto dp_only = [&](auto a_c, HalfBatch& r) {  // dP of sub-tile A: 4 MFMAs
+      constexpr int A = decltype(a_c)::value;
+      dp[A] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) dp[A] = MFMA(r.f[d], vf[d], dp[A]);
+    };
     auto sdp = [&](auto a_c, RowBatch& r) {  // S, dP of sub-tile A: 8 MFMAs
       constexpr int A = decltype(a_c)::value;
       sv[A] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -815,6 +865,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
         *reinterpret_cast<uint2*>(dsrow + qt * QB + 16 * A + 4 * g) = pk;
       }
     };
+    auto dvdk_h = [&](auto u_c, auto dh_c, auto img_c, TrHalf& t) {  // 4 MFMAs: dV (IMG 1) or dK (IMG 0)
+      constexpr int U = decltype(u_c)::value, DH = decltype(dh_c)::value;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (decltype(img_c)::value == 1)
+          dv[4 * DH + i] = MFMA(trp_join(t.lo[i], t.hi[i]), pb[U], dv[4 * DH + i]);
+        else
+          dk[4 * DH + i] = MFMA(trp_join(t.lo[i], t.hi[i]), sb[U], dk[4 * DH + i]);
+      }
+    };
     auto dvdk = [&](auto u_c, auto dh_c, TrBatch& t) {  // 8 MFMAs
       constexpr int U = decltype(u_c)::value, DH = decltype(dh_c)::value;
 #pragma unroll
@@ -827,52 +887,91 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
-    RowBatch r0, r1;
-    TrBatch t0, t1;
+    // S / dP in half sub-phases of 4 MFMAs, two 20-register half batches in flight (a whole row batch
+    // of 8 fragments double-buffered held 80 registers and spilled a K/V fragment, whose reload's
+    // compiler vmcnt(0) then drained the next tile's DMA and the dS^T stores mid-tile)
+    using IQ = std::integral_constant<int, 0>;
+    using IO = std::integral_constant<int, 1>;
+    HalfBatch h0, h1;
     const unsigned long long c0 = stamp();
-    issue_rows(b_c, I0{}, r0);
-    r0.l = r0.d = f32x4{0.f, 0.f, 0.f, 0.f};
-    wait_rows(r0);                                     // sp0
+    issue_half(b_c, I0{}, IQ{}, h0);
+    h0.x = f32x4{0.f, 0.f, 0.f, 0.f};
+    wait_half(h0);                                     // sp0a
     const unsigned long long c1 = stamp();
-    issue_rows(b_c, I1{}, r1);
-    sdp(I0{}, r0);
-    wait_rows(r1);                                     // sp1
-    issue_rows(b_c, I2{}, r0);
-    sdp(I1{}, r1);
-    softmax(I0{}, r1.l, r1.d);
-    wait_rows(r0);                                     // sp2
-    issue_rows(b_c, I3{}, r1);
-    sdp(I2{}, r0);
-    softmax(I1{}, r0.l, r0.d);
+    issue_half(b_c, I0{}, IO{}, h1);
+    s_only(I0{}, h0);
+    h1.x = f32x4{0.f, 0.f, 0.f, 0.f};
+    wait_half(h1);                                     // sp0b
+    issue_half(b_c, I1{}, IQ{}, h0);
+    dp_only(I0{}, h1);
+    wait_half(h0);                                     // sp1a
+    const f32x4 l0 = h0.x;
+    issue_half(b_c, I1{}, IO{}, h1);
+    s_only(I1{}, h0);
+    wait_half(h1);                                     // sp1b
+    const f32x4 d0 = h1.x;
+    issue_half(b_c, I2{}, IQ{}, h0);
+    dp_only(I1{}, h1);
+    softmax(I0{}, l0, d0);
+    wait_half(h0);                                     // sp2a
+    const f32x4 l1 = h0.x;
+    issue_half(b_c, I2{}, IO{}, h1);
+    s_only(I2{}, h0);
+    wait_half(h1);                                     // sp2b
+    const f32x4 d1 = h1.x;
+    issue_half(b_c, I3{}, IQ{}, h0);
+    dp_only(I2{}, h1);
+    softmax(I1{}, l1, d1);
     pb[0] = pack_perm(sv[0], sv[1]);
     sb[0] = pack_perm(dp[0], dp[1]);
-    wait_rows(r1);                                     // sp3
-    issue_tr(b_c, I0{}, I0{}, t0);
-    lds_rdf4<b * 256 + 3 * 64>(la, t0.l);
-    lds_rdf4<b * 256 + 3 * 64 + 512>(la, t0.d);
-    sdp(I3{}, r1);
-    softmax(I2{}, r1.l, r1.d);
+    wait_half(h0);                                     // sp3a
+    const f32x4 l2 = h0.x;
+    issue_half(b_c, I3{}, IO{}, h1);
+    s_only(I3{}, h0);
+    wait_half(h1);                                     // sp3b
+    const f32x4 d2 = h1.x;
+    TrHalf ta, tb;  // dV / dK phase in half sub-phases of 4 MFMAs, two 8-read half batches in flight
+    issue_trh(b_c, I0{}, I0{}, IO{}, ta);
+    lds_rdf4<b * 256 + 3 * 64>(la, ta.l);
+    lds_rdf4<b * 256 + 3 * 64 + 512>(la, ta.d);
+    dp_only(I3{}, h1);
+    softmax(I2{}, l2, d2);
     const unsigned long long c2 = stamp();
-    wait_tr_ld(t0);                                    // sp4
-    const f32x4 l3 = t0.l, d3 = t0.d;
-    issue_tr(b_c, I0{}, I1{}, t1);
-    dvdk(I0{}, I0{}, t0);
+    wait_trh(ta);                                      // s4a
+    const f32x4 l3 = ta.l, d3 = ta.d;
+    issue_trh(b_c, I0{}, I0{}, IQ{}, tb);
+    dvdk_h(I0{}, I0{}, IO{}, ta);
     softmax(I3{}, l3, d3);
+    wait_trh(tb);                                      // s4b
+    issue_trh(b_c, I0{}, I1{}, IO{}, ta);
+    dvdk_h(I0{}, I0{}, IQ{}, tb);
     pb[1] = pack_perm(sv[2], sv[3]);
     sb[1] = pack_perm(dp[2], dp[3]);
-    wait_tr(t1);                                       // sp5
-    issue_tr(b_c, I1{}, I0{}, t0);
-    dvdk(I0{}, I1{}, t1);
-    wait_tr(t0);                                       // sp6
-    issue_tr(b_c, I1{}, I1{}, t1);
-    dvdk(I1{}, I0{}, t0);
-    wait_tr(t1);                                       // sp7
+    wait_trh(ta);                                      // s5a
+    issue_trh(b_c, I0{}, I1{}, IQ{}, tb);
+    dvdk_h(I0{}, I1{}, IO{}, ta);
+    wait_trh(tb);                                      // s5b
+    issue_trh(b_c, I1{}, I0{}, IO{}, ta);
+    dvdk_h(I0{}, I1{}, IQ{}, tb);
+    wait_trh(ta);                                      // s6a
+    issue_trh(b_c, I1{}, I0{}, IQ{}, tb);
+    dvdk_h(I1{}, I0{}, IO{}, ta);
+    wait_trh(tb);                                      // s6b
+    issue_trh(b_c, I1{}, I1{}, IO{}, ta);
+    dvdk_h(I1{}, I0{}, IQ{}, tb);
+    wait_trh(ta);                                      // s7a
+    issue_trh(b_c, I1{}, I1{}, IQ{}, tb);
+    dvdk_h(I1{}, I1{}, IO{}, ta);
+    wait_trh(tb);                                      // s7b
     if constexpr (LAST) rope_load(rr, rcs_, rsn_, key_c, g);
-    dvdk(I1{}, I1{}, t1);
+    dvdk_h(I1{}, I1{}, IQ{}, tb);
     const unsigned long long c3 = stamp();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the next tile's DMA pieces were issued before this tile's 4 dS^T stores: vmcnt counts in issue
+    // order, so vmcnt(4) leaves only the stores in flight; raw s_barrier (__syncthreads would drain
+    // vmcnt(0) for its fence; this wave's LDS reads are all waited by the sp7 batch wait)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     const unsigned long long c4 = stamp();
-    __syncthreads();
+    __builtin_amdgcn_s_barrier();
     if constexpr (DBG != 0) {
       const unsigned long long c5 = stamp();
       st_acc[0] += c1 - c0; st_acc[1] += c2 - c1; st_acc[2] += c3 - c2; st_acc[3] += c4 - c3; st_acc[4] += c5 - c4;
@@ -1408,9 +1507,11 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
       dkdv = nwd == 4 ? attn_bwd_dkdv_kernel<4> : attn_bwd_dkdv_kernel<8>;
       grid = dim3(n_heads, S, (T + 16 * nwd - 1) / (16 * nwd));
     }
-    // workgroup order of the 1-D grids (group_major): dK/dV heaviest key blocks first chip-wide (the
-    // group-major order ended on a few heavy workgroups: 152 vs 140 us), dQ group-major
-    int order_dkdv = 0, order_dq = 1;
+    // workgroup order of the 1-D grids (group_major): heaviest blocks first chip-wide for both kernels.
+    // Group-major (a group's blocks back to back on one XCD) cut the dK/dV kernel's HBM fetch 2.2x
+    // (206 -> 92 MB) but ended on a few heavy workgroups: 215-221 vs 206-209 us per layer for the whole
+    // backward (profiles/r02/attn)
+    int order_dkdv = 0, order_dq = 0;
 #ifdef OSPO_ABLATION
     if (const char* e = getenv("OSPO_ATTN_ORDER")) order_dkdv = order_dq = atoi(e);  // A/B: 0 block-, 1 group-major
 #endif
@@ -1436,7 +1537,7 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
                          (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
                          (bf16*)ds_ws, p);
     OSPO_CHECK_LAUNCH();
-    dim3 gq(S * n_heads * ((T + 127) / 128));  // group-major 1-D grid (see group_major)
+    dim3 gq(S * n_heads * ((T + 127) / 128));  // 1-D grid (see group_major)
     bool dq_two_slot = false;
 #ifdef OSPO_ABLATION
     dq_two_slot = getenv("OSPO_ATTN_DQ_2SLOT") != nullptr;  // A/B: the round-2 2-slot dQ kernel (3-D grid)
