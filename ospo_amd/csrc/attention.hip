@@ -215,6 +215,32 @@ __device__ __forceinline__ void rope_bwd_acc(f32x4 (&v)[8], const bf16* cs, cons
   }
 }
 
+// Store a wave's 16-row accumulator tile (lane: row l16, columns 16 dt + 4 g + j) as bf16 rows through
+// a 16 x 272-B LDS scratch (16-B pad: the 16 rows' 8-B writes land on distinct banks): 4 stores of
+// 16 B per lane, each 4 whole 256-B rows, instead of 8 x 8-B stores touching 16 rows each (a row-per-
+// lane store tail is store-ISSUE bound).  Rows r with row0 + r >= row_lim are not stored.
+constexpr int SCR_PITCH = ROWB + 16;
+constexpr int SCR_BYTES = 16 * SCR_PITCH;  // 4352 B per wave and matrix
+__device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf16* dst, long ld, int row0,
+                                             int row_lim, int lane) {
+  const int g = lane >> 4, l16 = lane & 15;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    uint2 pk;
+    pk.x = pack2(v[dt][0], v[dt][1]);
+    pk.y = pack2(v[dt][2], v[dt][3]);
+    *reinterpret_cast<uint2*>(scr + l16 * SCR_PITCH + (16 * dt + 4 * g) * 2) = pk;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = 4 * k + (lane >> 4);
+    const uint4 x = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + (lane & 15) * 16);
+    if (row0 + r < row_lim) *reinterpret_cast<uint4*>(dst + (long)(row0 + r) * ld + (lane & 15) * 8) = x;
+  }
+}
+
 // ============================================================== forward ====
 template <int NW, int DBG = 0>  // DBG 1: no K/V loads after the first tile (ablation, results invalid)
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
@@ -333,17 +359,13 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
     __syncthreads();
   }
 
-  if (qrow < T) {
+  // O rows through LDS (the K/V buffers are free after the last tile's barrier): 16-B row stores
+  {
     const float inv = 1.f / l_run;
-    bf16* op = out + (rowbase + qrow) * ldo + h * HD;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      uint2 pk;
-      pk.x = pack2(o[dt][0] * inv, o[dt][1] * inv);
-      pk.y = pack2(o[dt][2] * inv, o[dt][3] * inv);
-      *reinterpret_cast<uint2*>(op + 16 * dt + 4 * g) = pk;
-    }
-    if (g == 0) lse[((long)s * H + h) * T + qrow] = m_run + __logf(l_run);
+    for (int dt = 0; dt < 8; ++dt) o[dt] *= inv;
+    store_rows16(o, smem + wave * SCR_BYTES, out + rowbase * ldo + h * HD, ldo, qb * RB + wave * 16, T, lane);
+    if (qrow < T && g == 0) lse[((long)s * H + h) * T + qrow] = m_run + __logf(l_run);
   }
 }
 
@@ -546,32 +568,6 @@ __device__ __forceinline__ void group_major(int nb, int ngroups, int& grp, int& 
   } else {
     grp = i / nb;
     j = i - grp * nb;
-  }
-}
-
-// Store a wave's 16-row accumulator tile (lane: row l16, columns 16 dt + 4 g + j) as bf16 rows through
-// a 16 x 272-B LDS scratch (16-B pad: the 16 rows' 8-B writes land on distinct banks): 4 stores of
-// 16 B per lane, each 4 whole 256-B rows, instead of 8 x 8-B stores touching 16 rows each (a row-per-
-// lane store tail is store-ISSUE bound).  Rows r with row0 + r >= row_lim are not stored.
-constexpr int SCR_PITCH = ROWB + 16;
-constexpr int SCR_BYTES = 16 * SCR_PITCH;  // 4352 B per wave and matrix
-__device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf16* dst, long ld, int row0,
-                                             int row_lim, int lane) {
-  const int g = lane >> 4, l16 = lane & 15;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    uint2 pk;
-    pk.x = pack2(v[dt][0], v[dt][1]);
-    pk.y = pack2(v[dt][2], v[dt][3]);
-    *reinterpret_cast<uint2*>(scr + l16 * SCR_PITCH + (16 * dt + 4 * g) * 2) = pk;
-  }
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int r = 4 * k + (lane >> 4);
-    const uint4 x = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + (lane & 15) * 16);
-    if (row0 + r < row_lim) *reinterpret_cast<uint4*>(dst + (long)(row0 + r) * ld + (lane & 15) * 8) = x;
   }
 }
 

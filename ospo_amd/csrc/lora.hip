@@ -13,6 +13,8 @@
 // through LDS and written as bf16 -- no fp32 atomics, no zero-fill, no
 // separate convert pass.  Any permutation of k is legal as long as A and B
 // agree, so each lane streams its own 16-B chunk of the row.
+#include <cstdlib>
+
 #include "common.h"
 #include "skinny.h"
 
@@ -880,7 +882,11 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
 // ---------------------------------------------------------------------------------- lora_gdb
 static int gdb_nch(int M, int nmods, int Nmod) {
   const int rbk = (M + 511) / 512;
-  if (Nmod % 256 == 0 && (long)rbk * nmods * (Nmod / 256) >= 256) return 4;
+  int min_wgs = 256;
+#ifdef OSPO_ABLATION
+  if (const char* e = getenv("OSPO_GDB_MINWG")) min_wgs = atoi(e);  // A/B: grid size below which nch = 2
+#endif
+  if (Nmod % 256 == 0 && (long)rbk * nmods * (Nmod / 256) >= min_wgs) return 4;
   return 2;
 }
 
