@@ -473,6 +473,32 @@ def test_lora_pack():
     assert torch.equal(Ac2[1, : nm * r], A2) and torch.equal(BT2[1], torch.cat([B2[i].T for i in range(nm)], 0))
 
 
+@pytest.mark.parametrize("pad", [40, 41], ids=["vector8", "scalar"])
+def test_lora_pack_r8_paths(pad):
+    """r = 8 over 4 modules, 3 layers: the 16-B kernel (layer stride a multiple of 8 elements) and the
+    element-wise fallback (odd stride) give the same exact copies."""
+    nm, r, Kin, Nmod, Rp, L = 4, 8, 128, 64, 32, 3
+    na, nb = nm * r * Kin, nm * Nmod * r
+    stride = na + nb + pad
+    flat = torch.zeros(L * stride + 8, device=DEV, dtype=torch.bfloat16)
+    As, Bs = [rnd(nm * r, Kin) for _ in range(L)], [rnd(nm, Nmod, r) for _ in range(L)]
+    for l in range(L):
+        flat[l * stride: l * stride + na] = As[l].reshape(-1)
+        flat[l * stride + na: l * stride + na + nb] = Bs[l].reshape(-1)
+    Ac = torch.empty(L, Rp, Kin, device=DEV, dtype=torch.bfloat16)
+    AT = torch.empty(L, Kin, Rp, device=DEV, dtype=torch.bfloat16)
+    Bc = torch.empty(L, nm * Nmod, Rp, device=DEV, dtype=torch.bfloat16)
+    BT = torch.empty(L, nm * r, Nmod, device=DEV, dtype=torch.bfloat16)
+    ops().lora_pack(flat, flat[na:], nm, r, Kin, Nmod, Rp, Ac, AT, Bc, BT, n_layers=L, layer_stride=stride)
+    for l in range(L):
+        assert torch.equal(Ac[l], As[l]) and torch.equal(AT[l], As[l].T)
+        expB = torch.zeros(nm * Nmod, Rp, device=DEV, dtype=torch.bfloat16)
+        for i in range(nm):
+            expB[i * Nmod:(i + 1) * Nmod, i * r:(i + 1) * r] = Bs[l][i]
+        assert torch.equal(Bc[l], expB)
+        assert torch.equal(BT[l], torch.cat([Bs[l][i].T for i in range(nm)], 0))
+
+
 @pytest.mark.parametrize("M,K,used", [(4800, 4096, 48), (300, 11008, 16), (77, 512, 32), (1, 256, 64),
                                       (600, 4096, 96)])
 def test_lora_skinny_down(M, K, used):
