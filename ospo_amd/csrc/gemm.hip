@@ -947,6 +947,60 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem,
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid), "+v"(m0), "+v"(n0));
   const bool rope_tile = n0 < args.rope_cols;  // (rope_cols % 128 == 0: a chunk's partner is in the tile)
+  if (rope_tile && !args.res) {
+    // RoPE tiles: one thread per (row, head, 8-column group j < 8) computes BOTH outputs of the rotate-half
+    // pair -- columns 8j.. and 64 + 8j.. -- from one unpack of x1, x2 and of the shared cos / sin entry
+    // (HF's tables repeat freqs: cos[d + 64] = cos[d]); the per-chunk form unpacked every value and table
+    // entry twice (once per partner) and the epilogue was VALU bound (qkv_fwd: +36 us per launch).  Same
+    // roundings, bit-identical.  Heads at or past rope_cols are copied.
+    constexpr int UNITS = BM * 2 * 8, PITERS = UNITS / NTHR, PB = 4;
+    static_assert(PITERS % PB == 0, "rope epilogue batch");
+#pragma unroll 1
+    for (int b0 = 0; b0 < PITERS; b0 += PB) {
+      u32x4 cw[PB], sw[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int un = tid + (b0 + u) * NTHR;
+        const int j = un & 7, r2 = un >> 4;
+        const int t = min(m0 + r2, args.M - 1) % args.rope_T;
+        cw[u] = *reinterpret_cast<const u32x4*>(args.rope_cs + (long)t * 64 + 8 * j);
+        sw[u] = *reinterpret_cast<const u32x4*>(args.rope_sn + (long)t * 64 + 8 * j);
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int un = tid + (b0 + u) * NTHR;
+        const int j = un & 7, hd = (un >> 3) & 1, r2 = un >> 4;
+        const int m = m0 + r2;
+        const int cl = hd * 16 + j;  // 16-B chunk of columns 8j.. of head hd; its partner is cl + 8
+        u32x4 v1 = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + cl * 16);
+        u32x4 v2 = *reinterpret_cast<const u32x4*>(smem + r2 * CPITCH + (cl + 8) * 16);
+        if (n0 + hd * 128 < args.rope_cols) {
+          u32x4 o1, o2;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            float r1[2], r2v[2];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const int sh = 16 * hh;
+              const float x1 = bits2f((v1[qq] >> sh) & 0xffff), x2 = bits2f((v2[qq] >> sh) & 0xffff);
+              const float cf = bits2f((cw[u][qq] >> sh) & 0xffff), sf = bits2f((sw[u][qq] >> sh) & 0xffff);
+              r1[hh] = round_bf(x1 * cf) + round_bf(-x2 * sf);
+              r2v[hh] = round_bf(x2 * cf) + round_bf(x1 * sf);
+            }
+            o1[qq] = pack2(r1[0], r1[1]);
+            o2[qq] = pack2(r2v[0], r2v[1]);
+          }
+          v1 = o1;
+          v2 = o2;
+        }
+        if (m < args.M) {
+          *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cl * 8) = v1;
+          *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + (cl + 8) * 8) = v2;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll 1
   for (int b0 = 0; b0 < ITERS; b0 += BATCH) {
     u32x4 rv[BATCH], cw[BATCH], sw[BATCH];

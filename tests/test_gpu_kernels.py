@@ -210,6 +210,29 @@ def test_gemm_rope_fused_equals_unfused(M, H, T):
     assert torch.equal(out, ref)
 
 
+def test_gemm_rope_half_tile():
+    """rope_cols = 128 mod 256 (H = 3, q heads only): the last RoPE tile rotates one head and copies
+    the other; checked against a torch statement of HF's rounding points."""
+    M, H, T, hd, K = 300, 3, 150, 128, 256
+    D = H * hd
+    N = 4 * D
+    a, b = rnd(M, K), rnd(N, K, s=0.05)
+    cos, sin = ops().rope_tables(T, hd, 1e4, DEV)
+    plain = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(a, b, plain)
+    out = torch.empty_like(plain)
+    ops().gemm_nt(a, b, out, rope=(cos, sin, T, D))
+    assert torch.equal(out[:, D:], plain[:, D:])
+    t = torch.arange(M, device=DEV) % T
+    c, s_ = cos[t].float()[:, None, :], sin[t].float()[:, None, :]  # [M, 1, 64]
+    x = plain[:, :D].float().view(M, H, hd)
+    x1, x2 = x[..., :64], x[..., 64:]
+    bf = lambda z: z.bfloat16().float()
+    lo = (bf(x1 * c) + bf(-x2 * s_)).bfloat16()
+    hi = (bf(x2 * c) + bf(x1 * s_)).bfloat16()
+    assert torch.equal(out[:, :D].view(M, H, hd), torch.cat([lo, hi], -1))
+
+
 def test_rope_fwd_bwd():
     S, T, H, hd = 2, 72, 3, 128
     D = H * hd

@@ -21,7 +21,8 @@ VARIANTS = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1").split(",") if v
 MX8 = os.environ.get("GB_MX8", "0") == "1"  # also time the block-scaled fp8 GEMM (+ its A quantization)
 SPLITS = [int(v) for v in os.environ.get("GB_SPLITS", "").split(",") if v != ""]  # forced tail splits (v0)
 DROP = os.environ.get("GB_DROP", "0") == "1"
-RES = os.environ.get("GB_RES", "0") == "1"  # bias + residual epilogue on every variant (bit-equality covers it)  # also time the dropout-masked extension form (the dX GEMMs)
+RES = os.environ.get("GB_RES", "0") == "1"
+ROPE = os.environ.get("GB_ROPE", "0") == "1"  # also time qkv_fwd with the RoPE epilogue (T = 600, q|k columns)  # bias + residual epilogue on every variant (bit-equality covers it)  # also time the dropout-masked extension form (the dX GEMMs)
 ROUNDS, ITERS = 5, 10
 
 
@@ -66,6 +67,11 @@ def main():
                 call("ospo_set_gemm_variant", v)
                 res[f"v{v}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2, **ex)))
             res["hipblaslt"].append(timeit(lambda: torch.matmul(a, b.t(), out=ref)))
+            if ROPE and name == "qkv_fwd":
+                if "rope_tab" not in locals():
+                    rope_tab = ops.rope_tables(600, 128, 1e4, "cuda")
+                call("ospo_set_gemm_variant", 0)
+                res.setdefault("v0_rope", []).append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2, rope=(rope_tab[0], rope_tab[1], 600, 8192))))
             if DROP and k2:
                 call("ospo_set_gemm_variant", 0)
                 res.setdefault("v0_dropout", []).append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(77, 0.05))))
