@@ -458,12 +458,13 @@ __device__ __forceinline__ void tr4_wait(i16x4& a, i16x4& b, i16x4& c, i16x4& d)
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int RSB>
+template <int RSB, int NS = 4>
 __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ dy, int ldy, const bf16* __restrict__ Bt,
                                                        int ldb, const bf16* __restrict__ u, int ldu, int M, int Nmod,
                                                        int nch, float* __restrict__ ws, int Mw,
                                                        float* __restrict__ dB) {
-  constexpr int NS = 4, STAGE = 8192;
+  // NS-stage ring of 8-KiB dy sub-tiles, NS - 1 in flight (a 6-stage ring measured 10-30 % slower)
+  constexpr int STAGE = 8192;
   constexpr int BT_OFF = NS * STAGE, BT_BYTES = 16 * 4 * 128;  // up to nch = 4
   constexpr int U_OFF = BT_OFF + BT_BYTES;
   constexpr int ROWS = 64 * RSB;
@@ -511,81 +512,75 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t) stage(t);
 
-  f32x4 accg[RSB / 4][4];
+  // g: every wave computes its 16-row group (rows 16 wave .. +15) of every 64-row sub-block, 2 MFMAs per
+  // sub-tile (the sub-block's 64 rows used to go to one wave, 8 MFMAs while the other three waited at
+  // the next barrier); same per-row accumulation order (chunks, then k steps), bit-identical partials
+  f32x4 accg[RSB];
 #pragma unroll
-  for (int a = 0; a < RSB / 4; ++a)
-#pragma unroll
-    for (int f = 0; f < 4; ++f) accg[a][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int a = 0; a < RSB; ++a) accg[a] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
   const int li = l16, q4 = li >> 2, p4 = li & 3;
-
-  auto gpart = [&](const char* st, int cc, f32x4 (&acc)[4]) __attribute__((always_inline)) {
+  const int grow = 16 * wave + l16;  // this lane's row of the g product inside a sub-tile
+  for (int cc = 0; cc < nch; ++cc) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int qk = cc * 8 + 4 * s + g;  // Bt chunk (8 bf16) of this lane's k group
-      const bf16x8 bt = *reinterpret_cast<const bf16x8*>(smem + BT_OFF + l16 * btrow + ((qk ^ l16) << 4));
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const int row = 16 * f + l16;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + row * 128 + (((4 * s + g) ^ (row & 7)) << 4));
-        acc[f] = MFMA(bt, a, acc[f]);  // D[j = 4g..][m = l16]
+    for (int rb = 0; rb < RSB; ++rb) {
+      const int t = cc * RSB + rb;
+      const int newer = min(NS - 2, T - 1 - t);  // stages issued after t that may stay in flight (2 pieces each)
+      switch (newer) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
       }
-    }
-  };
-  for (int t = 0; t < T; ++t) {
-    const int cc = t / RSB, rb = t % RSB;
-    const int newer = min(NS - 2, T - 1 - t);
-    if (newer >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (newer == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + NS - 1 < T) stage(t + NS - 1);
-    const char* st = smem + (t % NS) * STAGE;
-    // g: this sub-block's 64 rows belong to wave rb & 3 (its accumulator set rb >> 2)
-    if (wave == (rb & 3)) {
-      static_assert(RSB == 8, "two accumulator sets");
-      if (rb < 4) gpart(st, cc, accg[0]);
-      else gpart(st, cc, accg[1]);
-    }
-    // dB: columns 16 wave .. +15 of the chunk, the sub-block's 64 rows as K
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + NS - 1 < T) stage(t + NS - 1);
+      const char* st = smem + (t % NS) * STAGE;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int r1 = 32 * s + 8 * g + q4, r2 = r1 + 4;
-      const int x = 2 * wave + (p4 >> 1), h = (p4 & 1) << 3;
-      const int ur = rb * 64 + 32 * s + 8 * g;  // u image row of element 0
-      i16x4 lo, hi, ulo, uhi;
-      tr4_issue(st + r1 * 128 + ((x ^ (r1 & 7)) << 4) + h, lo);
-      tr4_issue(st + r2 * 128 + ((x ^ (r2 & 7)) << 4) + h, hi);
-      tr4_issue(smem + U_OFF + (ur + q4) * 32 + p4 * 8, ulo);
-      tr4_issue(smem + U_OFF + (ur + 4 + q4) * 32 + p4 * 8, uhi);
-      tr4_wait(lo, hi, ulo, uhi);
-      const int mrow = rb0 + ur;  // global row of element 0
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        ulo[e] = (mrow + e < M) ? ulo[e] : (short)0;
-        uhi[e] = (mrow + 4 + e < M) ? uhi[e] : (short)0;
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int qk = cc * 8 + 4 * s2 + g;  // Bt chunk (8 bf16) of this lane's k group
+        const bf16x8 bt = *reinterpret_cast<const bf16x8*>(smem + BT_OFF + l16 * btrow + ((qk ^ l16) << 4));
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + grow * 128 + (((4 * s2 + g) ^ (grow & 7)) << 4));
+        accg[rb] = MFMA(bt, a, accg[rb]);  // D[j = 4g..][m = l16]
       }
-      const i16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const i16x8 bv = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
-      accb = MFMA(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), accb);  // D[n = 4g+i][j = l16]
-    }
-    if (rb == RSB - 1) {  // the chunk's dB over the workgroup's rows
-      const long n0 = col0 + cc * 64 + 16 * wave + 4 * g;
+      // dB: columns 16 wave .. +15 of the chunk, the sub-block's 64 rows as K
 #pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[i]);
-      accb = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < 2; ++s) {
+        const int r1 = 32 * s + 8 * g + q4, r2 = r1 + 4;
+        const int x = 2 * wave + (p4 >> 1), h = (p4 & 1) << 3;
+        const int ur = rb * 64 + 32 * s + 8 * g;  // u image row of element 0
+        i16x4 lo, hi, ulo, uhi;
+        tr4_issue(st + r1 * 128 + ((x ^ (r1 & 7)) << 4) + h, lo);
+        tr4_issue(st + r2 * 128 + ((x ^ (r2 & 7)) << 4) + h, hi);
+        tr4_issue(smem + U_OFF + (ur + q4) * 32 + p4 * 8, ulo);
+        tr4_issue(smem + U_OFF + (ur + 4 + q4) * 32 + p4 * 8, uhi);
+        tr4_wait(lo, hi, ulo, uhi);
+        const int mrow = rb0 + ur;  // global row of element 0
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ulo[e] = (mrow + e < M) ? ulo[e] : (short)0;
+          uhi[e] = (mrow + 4 + e < M) ? uhi[e] : (short)0;
+        }
+        const i16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const i16x8 bv = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+        accb = MFMA(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), accb);  // D[n = 4g+i][j = l16]
+      }
+      if (rb == RSB - 1) {  // the chunk's dB over the workgroup's rows
+        const long n0 = col0 + cc * 64 + 16 * wave + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[i]);
+        accb = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   }
   // g partials of this column block: ws [mod][sp][Mw][16]
 #pragma unroll
-  for (int a = 0; a < RSB / 4; ++a) {
-    const int rb = wave + 4 * a;
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int m = rb0 + rb * 64 + 16 * f + l16;
-      if (m < Mw) *reinterpret_cast<f32x4*>(ws + (((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[a][f];
-    }
+  for (int rb = 0; rb < RSB; ++rb) {
+    const int m = rb0 + rb * 64 + grow;
+    if (m < Mw) *reinterpret_cast<f32x4*>(ws + (((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[rb];
   }
 }
 
@@ -912,7 +907,11 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   const int nsplit = Nmod / (64 * nch);
   const int Mw = (M + 63) / 64 * 64;
   const dim3 grid((M + 511) / 512, nmods * nsplit);
-  hipLaunchKernelGGL((lora_gdb_kernel<8>), grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
+  auto kfn = lora_gdb_kernel<8, 4>;
+#ifdef OSPO_ABLATION
+  if (getenv("OSPO_GDB_NS6")) kfn = lora_gdb_kernel<8, 6>;  // A/B: a 6-stage ring
+#endif
+  hipLaunchKernelGGL(kfn, grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
                      (const bf16*)u, ldu, M, Nmod, nch, (float*)ws, Mw, dB);
   OSPO_CHECK_LAUNCH();
   const long n = (long)M_out * (out_cols / 4);
