@@ -85,7 +85,8 @@ int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* B, int ldb,
                                  float drop_p, hipStream_t stream);
 
 /* The LoRA dropout mask hash (host copy of the device function): element idx of an
- * adapter input is kept iff ospo_dropout_hash(idx, seed) >= p * 2^32. */
+ * adapter input is kept iff the 16-bit half (idx & 1) of ospo_dropout_hash(idx >> 1, seed)
+ * is >= p * 2^16 (one hash per two adjacent elements; adapter input widths are even). */
 unsigned ospo_dropout_hash(unsigned idx, unsigned seed);
 
 /* Split-K workspace for the GEMM's tail round (tiles % CUs leftover tiles are split

@@ -24,8 +24,8 @@ __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }  // RNE, NaN-p
 __device__ __forceinline__ float round_bf(float x) { return (float)(bf16)x; }
 
 // LoRA dropout mask (counter-based; ospo_amd/dropout.py restates it bit for bit):
-// element idx = row * ncols + col of the adapter input, keep iff hash >= thresh,
-// thresh = p * 2^32; kept values become bf16(x / (1 - p)).
+// element idx = row * ncols + col of the adapter input, kept iff drop_keep(idx) (below);
+// kept values become bf16(x / (1 - p)).
 __host__ __device__ __forceinline__ uint32_t drop_hash(uint32_t idx, uint32_t seed) {
   uint32_t x = idx * 0x9E3779B1u + seed;
   x ^= x >> 16;
@@ -35,6 +35,27 @@ __host__ __device__ __forceinline__ uint32_t drop_hash(uint32_t idx, uint32_t se
   x ^= x >> 16;
   return x;
 }
+
+// Keep decision of mask element idx: the 16-bit half (idx & 1) of drop_hash(idx >> 1), kept iff it is
+// >= thr = p * 2^16 -- one hash per two adjacent elements of a row (the hash's integer multiplies are
+// quarter-rate VALU, and each adapter input's mask is regenerated three times per step: the forward's u
+// product, the dX GEMM's extension, the dA product).  Callers that decide 2n consecutive elements start
+// at an even index (row widths are even: the launchers check) and hash n times.
+__host__ __device__ __forceinline__ bool drop_keep(uint32_t idx, uint32_t seed, uint32_t thr) {
+  const uint32_t h = drop_hash(idx >> 1, seed);
+  return ((idx & 1u) ? (h >> 16) : (h & 0xffffu)) >= thr;
+}
+// keep bits of elements idx0 .. idx0 + 2N - 1, idx0 even
+template <int N>
+__device__ __forceinline__ void drop_keep_pairs(uint32_t idx0, uint32_t seed, uint32_t thr, bool (&keep)[2 * N]) {
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    const uint32_t h = drop_hash((idx0 >> 1) + (uint32_t)q, seed);
+    keep[2 * q] = (h & 0xffffu) >= thr;
+    keep[2 * q + 1] = (h >> 16) >= thr;
+  }
+}
+static inline uint32_t drop_threshold(double p) { return (uint32_t)(p * 65536.0); }
 
 __device__ __forceinline__ float bits2f(unsigned short b) { return __uint_as_float(((unsigned)b) << 16); }
 __device__ __forceinline__ unsigned short f2bits(float x) {

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) 
   };
 
   // LoRA dropout recomputed on a K-major B operand (the dA product's activations): the landed tile
-  // is masked in LDS, element (m = reduction row, n) kept iff drop_hash(m * drop_ld + n) >= thresh and
+  // is masked in LDS, element (m = reduction row, n) kept iff drop_keep(m * drop_ld + n) and
   // scaled by 1/(1-p) with the bf16 rounding of the forward's masked copy -- the same bf16 values the
   // forward's skinny product multiplied, without storing them.
   auto mask_b = [&](int t, int buf) {
@@ -220,11 +220,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) 
           const int x = (ln % LPR) ^ kmaj_swz<ROWB>(row);
           const uint32_t base = (uint32_t)(t * BK + row) * (uint32_t)args.drop_ld + (uint32_t)(n0 + x * 8);
           bf16x8 v = *reinterpret_cast<const bf16x8*>(lb + c * 16);
+          bool keep[8];
+          drop_keep_pairs<4>(base, args.drop_seed, args.drop_thresh, keep);  // base even (drop_ld even)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const bool keep = drop_hash(base + e, args.drop_seed) >= args.drop_thresh;
-            v[e] = keep ? f2bf(bf2f(v[e]) * args.drop_scale) : f2bf(0.f);
-          }
+          for (int e = 0; e < 8; ++e) v[e] = keep[e] ? f2bf(bf2f(v[e]) * args.drop_scale) : f2bf(0.f);
           *reinterpret_cast<bf16x8*>(lb + c * 16) = v;
         }
         __syncthreads();
@@ -455,7 +454,7 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const bf16* __restrict_
           const uint32_t n = (uint32_t)(n0 + wave * (TN / 4) + 16 * f + l16);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const bool keep = drop_hash((mrow + e) * (uint32_t)drop_ld + n, dseed) >= dthresh;
+            const bool keep = drop_keep((mrow + e) * (uint32_t)drop_ld + n, dseed, dthresh);
             bx[f][e] = keep ? f2bf(bf2f(bx[f][e]) * dscale) : f2bf(0.f);
           }
         }
@@ -509,7 +508,7 @@ extern "C" int ospo_lora_wgrad(const void* X, int ldx, int N, const void* S, int
   if (!aligned16(X) || !aligned16(S)) return OSPO_ERR_ALIGN;
   if (drop_p < 0.f || drop_p >= 1.f) return OSPO_ERR_ARG;
   const bool drop = drop_p > 0.f;
-  const uint32_t thresh = (uint32_t)((double)drop_p * 4294967296.0);
+  const uint32_t thresh = drop_threshold(drop_p);
   const float dscale = drop ? 1.f / (1.f - drop_p) : 0.f;
   const bf16* x = (const bf16*)X;
   const bf16* sp = (const bf16*)S;
@@ -1665,11 +1664,10 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
             for (int n = 0; n < 2; ++n) {
               const uint32_t m = (uint32_t)(m0 + ia * 128 + wm * 64 + i * 16 + lq);
               const uint32_t c = (uint32_t)(n0 + ib * 128 + wn * 32 + n * 16 + 4 * gq);
+              bool keep[4];
+              drop_keep_pairs<2>(m * (uint32_t)args.drop_ld + c, args.drop_seed, args.drop_thresh, keep);  // c % 4 == 0
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const bool keep = drop_hash(m * (uint32_t)args.drop_ld + c + e, args.drop_seed) >= args.drop_thresh;
-                acc[j][i][n][e] *= keep ? args.drop_scale : 0.f;
-              }
+              for (int e = 0; e < 4; ++e) acc[j][i][n][e] *= keep[e] ? args.drop_scale : 0.f;
             }
         }
       }
@@ -2055,8 +2053,9 @@ extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, 
              M, N, K, K2, 1.f, nullptr, nullptr, 0, C, ldc, 1, 0, 0};
   if (drop_p == 0.f)
     return launch_default<false>(a, stream);
+  if (N & 1) return OSPO_ERR_SHAPE;  // mask pairs (drop_keep) start at even indices
   a.drop_seed = drop_seed;
-  a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
+  a.drop_thresh = drop_threshold(drop_p);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = N;
   return launch_default<true>(a, stream);
@@ -2086,7 +2085,7 @@ extern "C" int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* 
   if (drop_p == 0.f)
     return launch_default<false>(a, stream);
   a.drop_seed = drop_seed;
-  a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
+  a.drop_thresh = drop_threshold(drop_p);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = F;
   return launch_default<true>(a, stream);
@@ -2126,7 +2125,7 @@ extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const 
   }
   if (drop) {
     a.drop_seed = drop_seed;
-    a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
+    a.drop_thresh = drop_threshold(drop_p);
     a.drop_scale = 1.f / (1.f - drop_p);
     a.drop_ld = N;
     return launch_mx<true>(a, stream);
@@ -2199,8 +2198,9 @@ static int gemm_f32acc_impl(const void* A, int lda, int a_kmajor, const void* B,
   GemmArgs a{(const bf16*)A, (const bf16*)B, nullptr, nullptr, lda, ldb, 0, 0, M, N, K, 0, alpha,
              nullptr, nullptr, 0, C, ldc, k_splits, diag_nblk, diag_r};
   if (drop_p > 0.f) {  // mask on B [K, N] (K-major), index m * N + n
+    if (N & 1) return OSPO_ERR_SHAPE;  // mask pairs (drop_keep) start at even indices
     a.drop_seed = drop_seed;
-    a.drop_thresh = (uint32_t)((double)drop_p * 4294967296.0);
+    a.drop_thresh = drop_threshold(drop_p);
     a.drop_scale = 1.f / (1.f - drop_p);
     a.drop_ld = N;
   }

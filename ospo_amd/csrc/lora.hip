@@ -206,11 +206,10 @@ __global__ __launch_bounds__(256) void skinny2_kernel(const bf16* __restrict__ A
         bf16x8 a = av[s];
         if constexpr (DROP) {
           const int k0 = kc + 32 * s + 8 * g;
+          bool keep[8];
+          drop_keep_pairs<4>((uint32_t)mr * (uint32_t)K + (uint32_t)k0, dseed, dthresh, keep);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const bool keep = drop_hash((uint32_t)mr * (uint32_t)K + (uint32_t)(k0 + e), dseed) >= dthresh;
-            a[e] = keep ? f2bf(bf2f(a[e]) * dscale) : f2bf(0.f);
-          }
+          for (int e = 0; e < 8; ++e) a[e] = keep[e] ? f2bf(bf2f(a[e]) * dscale) : f2bf(0.f);
           if (xd && m < M) *reinterpret_cast<bf16x8*>(xd + (long)m * ldxd + k0) = a;
         }
 #pragma unroll
@@ -398,11 +397,10 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
       bf16x8 av = a[s];
       if constexpr (DROP) {
         const uint32_t k0 = (uint32_t)(k_begin + 64 * c + 32 * s + 8 * g);
+        bool keep[8];
+        drop_keep_pairs<4>(drow + k0, dseed, dthresh, keep);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const bool keep = drop_hash(drow + k0 + (uint32_t)e, dseed) >= dthresh;
-          av[e] = keep ? f2bf(bf2f(av[e]) * dscale) : f2bf(0.f);
-        }
+        for (int e = 0; e < 8; ++e) av[e] = keep[e] ? f2bf(bf2f(av[e]) * dscale) : f2bf(0.f);
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[j] = MFMA(bok[j] ? b[s][j] : bf16x8{}, av, acc[j]);  // D[16j+4g+q][m]
@@ -795,9 +793,10 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
   if (drop_p > 0.f) {
     if (a_koff != 0) return OSPO_ERR_UNSUPPORTED;  // dropout acts on the adapter input (dense u product)
     if ((long)M * K > 0xFFFFFFFFL) return OSPO_ERR_SHAPE;  // 32-bit mask index
+    if (K & 1) return OSPO_ERR_SHAPE;                       // mask pairs (drop_keep) start at even indices
     if (xd && (ld_xd < K || ld_xd % 8 || !aligned16(xd))) return OSPO_ERR_SHAPE;
     dr.seed = drop_seed;
-    dr.thresh = (uint32_t)((double)drop_p * 4294967296.0);
+    dr.thresh = drop_threshold(drop_p);
     dr.scale = 1.f / (1.f - drop_p);
     dr.xd = (bf16*)xd;
     dr.ldxd = ld_xd;

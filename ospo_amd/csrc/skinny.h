@@ -46,11 +46,10 @@ __device__ __forceinline__ void sk_loop(const bf16* arow, const bf16* const (&bp
       bf16x8 av = (batch * SK_U + u < n_i) ? a[u] : bf16x8{};
       if constexpr (DROP) {
         const int k = dp.k0 + 32 * (wave + (batch * SK_U + u) * SK_WAVES);
+        bool keep[8];
+        drop_keep_pairs<4>(dp.rowidx + (uint32_t)k, dp.seed, dp.thresh, keep);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const bool keep = drop_hash(dp.rowidx + (uint32_t)(k + e), dp.seed) >= dp.thresh;
-          av[e] = keep ? f2bf(bf2f(av[e]) * dp.scale) : f2bf(0.f);
-        }
+        for (int e = 0; e < 8; ++e) av[e] = keep[e] ? f2bf(bf2f(av[e]) * dp.scale) : f2bf(0.f);
         if (dp.xd && batch * SK_U + u < n_i) *reinterpret_cast<bf16x8*>(dp.xd + k) = av;
       }
 #pragma unroll

@@ -3,9 +3,11 @@ ospo/utils/model.py:50-57 with configs/peft/lora.yaml lora_dropout).
 
 The mask is counter based, so the forward (skinny u kernel) and the backward (dX
 GEMM epilogue, dA on the stored masked input) regenerate the same bits without
-storing them: element (m, k) of a [M, K] adapter input is kept iff
-drop_hash(m * K + k, seed) >= p * 2^32, kept values become bf16(x / (1 - p)).
-``drop_hash`` restates ``ospo_amd/csrc/common.h`` bit for bit (numpy uint32).
+storing them: element idx = m * K + k of a [M, K] adapter input is kept iff the
+16-bit half (idx & 1) of drop_hash(idx >> 1, seed) is >= p * 2^16 (one hash per two
+adjacent elements; K is even), kept values become bf16(x / (1 - p)).
+``drop_hash`` / ``keep_bits`` restate ``ospo_amd/csrc/common.h`` (drop_hash, drop_keep)
+bit for bit (numpy uint32).
 
 One mask per adapter INPUT per layer and step: q/k/v share the mask of the
 attention-norm output and gate/up that of the MLP-norm output (their LoRA A's are
@@ -33,7 +35,16 @@ def drop_hash(idx, seed):
 
 
 def threshold(p: float) -> int:
-    return int(float(p) * 4294967296.0)
+    """16-bit keep threshold (common.h drop_threshold)."""
+    return int(float(p) * 65536.0)
+
+
+def keep_bits(idx, seed, p: float):
+    """bool keep decision of flat element indices idx (array) -- common.h drop_keep."""
+    idx = np.asarray(idx, dtype=np.uint32)
+    h = drop_hash(idx >> np.uint32(1), seed)
+    half = np.where((idx & np.uint32(1)) != 0, h >> np.uint32(16), h & np.uint32(0xFFFF))
+    return half >= np.uint32(threshold(p))
 
 
 def layer_seed(base: int, call: int, layer: int, group: str) -> int:
@@ -45,4 +56,4 @@ def layer_seed(base: int, call: int, layer: int, group: str) -> int:
 def keep_mask(M: int, K: int, seed: int, p: float) -> np.ndarray:
     """bool [M, K] keep mask of an adapter input (test / oracle use)."""
     idx = np.arange(M * K, dtype=np.uint64).astype(np.uint32).reshape(M, K)
-    return drop_hash(idx, seed) >= np.uint32(threshold(p))
+    return keep_bits(idx, seed, p)

@@ -302,6 +302,13 @@ def test_dropout_hash_host_c_and_numpy_agree(lib):
     assert np.array_equal(ref, np.array([D.drop_hash(i, int(s)) for i, s in zip(idx, seeds)], dtype=np.uint32))
     m = D.keep_mask(512, 4096, D.layer_seed(42, 1, 0, "qkv"), 0.05)
     assert abs(m.mean() - 0.95) < 2e-3
+    # one hash per two adjacent elements: the halves of one hash are independent decisions
+    pairs = m.reshape(-1, 2)
+    assert abs((pairs[:, 0] & pairs[:, 1]).mean() - 0.95 ** 2) < 3e-3
+    s0 = D.layer_seed(42, 1, 0, "qkv")
+    k = D.keep_bits(np.arange(10, dtype=np.uint32), s0, 0.05)
+    h = [int(D.drop_hash(np.uint32(i), s0)) for i in range(5)]
+    assert list(k) == [((h[i // 2] >> (16 * (i & 1))) & 0xFFFF) >= D.threshold(0.05) for i in range(10)]
     m2 = D.keep_mask(512, 4096, D.layer_seed(42, 1, 0, "o"), 0.05)
     assert 0.90 < (m == m2).mean() < 0.91  # independent masks agree where both keep or both drop
     assert D.layer_seed(42, 1, 3, "gu") != D.layer_seed(42, 2, 3, "gu")
