@@ -474,6 +474,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       if constexpr (DBG == 1) break;
       // this lane's 4 queries of sub-tile a are consecutive: one 16-B LDS read each for lse, delta
       const f32x4 lq = *reinterpret_cast<const f32x4*>(Ls + 16 * a + 4 * g);
+      const f32x4 lq2 = lq * L2E;
       const f32x4 dq4 = *reinterpret_cast<const f32x4*>(Dl + 16 * a + 4 * g);
 #pragma unroll
       for (int j = 0; j < 4; j += 2) {
@@ -484,8 +485,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
           x = (e < lo || e >= hi) ? -INFINITY : x;
           y = (e + 1 < lo || e + 1 >= hi) ? -INFINITY : y;
         }
-        const float px = __builtin_amdgcn_exp2f((x - lq[j]) * L2E);
-        const float py = __builtin_amdgcn_exp2f((y - lq[j + 1]) * L2E);
+        const float px = __builtin_amdgcn_exp2f(fmaf(x, L2E, -lq2[j]));  // one FMA: lse pre-scaled per quad
+        const float py = __builtin_amdgcn_exp2f(fmaf(y, L2E, -lq2[j + 1]));
         sv[a][j] = px;
         sv[a][j + 1] = py;
         dp[a][j] = px * (dp[a][j] - dq4[j]) * scale;
@@ -838,6 +839,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     };
     auto softmax = [&](auto a_c, const f32x4& lq, const f32x4& dq4) {
       constexpr int A = decltype(a_c)::value;
+      const f32x4 lq2 = lq * L2E;
 #pragma unroll
       for (int j = 0; j < 4; j += 2) {
         float x = sv[A][j], y = sv[A][j + 1];
@@ -847,8 +849,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
           x = (e < lo || e >= hi) ? -INFINITY : x;
           y = (e + 1 < lo || e + 1 >= hi) ? -INFINITY : y;
         }
-        const float px = __builtin_amdgcn_exp2f((x - lq[j]) * L2E);
-        const float py = __builtin_amdgcn_exp2f((y - lq[j + 1]) * L2E);
+        const float px = __builtin_amdgcn_exp2f(fmaf(x, L2E, -lq2[j]));  // one FMA: lse pre-scaled per quad
+        const float py = __builtin_amdgcn_exp2f(fmaf(y, L2E, -lq2[j + 1]));
         sv[A][j] = px;
         sv[A][j + 1] = py;
         dp[A][j] = px * (dp[A][j] - dq4[j]) * scale;
