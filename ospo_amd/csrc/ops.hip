@@ -291,13 +291,15 @@ __global__ void rope_kernel(bf16* __restrict__ x, int ld, int q_col, int k_col, 
 }
 
 // ------------------------------------------------------------------- SwiGLU
+// Grid (column blocks of 128 chunks, rows): no 64-bit division of a flat index (it was ~50 of the
+// kernels' ~350 instructions per thread); consecutive threads still take consecutive 8-column chunks
+// of one row (the MXFP8 stores need 4 of them per 32-block).
 __global__ void swiglu_fwd_kernel(const bf16* __restrict__ gu, int ldg, bf16* __restrict__ h, int ldh, long M, int F,
                                   const Mx8Out mo) {
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cpr = F / 8;
-  if (tid >= M * cpr) return;
-  const long m = tid / cpr;
-  const int c = tid % cpr;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cpr) return;
+  const long m = blockIdx.y;
   float g[8], u[8], o[8];
   unpack8(*reinterpret_cast<const u32x4*>(gu + m * ldg + c * 8), g);
   unpack8(*reinterpret_cast<const u32x4*>(gu + m * ldg + F + c * 8), u);
@@ -313,11 +315,10 @@ __global__ void swiglu_fwd_kernel(const bf16* __restrict__ gu, int ldg, bf16* __
 
 __global__ void swiglu_bwd_kernel(const bf16* __restrict__ dh, int lddh, const bf16* __restrict__ gu, int ldg,
                                   bf16* __restrict__ dgu, int lddg, long M, int F, const Mx8Out mo) {
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cpr = F / 8;
-  if (tid >= M * cpr) return;
-  const long m = tid / cpr;
-  const int c = tid % cpr;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cpr) return;
+  const long m = blockIdx.y;
   float d[8], g[8], u[8], dg[8], du[8];
   unpack8(*reinterpret_cast<const u32x4*>(dh + m * lddh + c * 8), d);
   unpack8(*reinterpret_cast<const u32x4*>(gu + m * ldg + c * 8), g);
@@ -812,9 +813,9 @@ static int swiglu_fwd_impl(const void* gu, int ld_gu, void* h, int ld_h, int M, 
   if (!gu || !h) return OSPO_ERR_ARG;
   if (M <= 0 || F % 8 || ld_gu < 2 * F || ld_h < F || ld_gu % 8 || ld_h % 8) return OSPO_ERR_SHAPE;
   if (!aligned16(gu) || !aligned16(h)) return OSPO_ERR_ALIGN;
-  const long n = (long)M * (F / 8);
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(blocks(n)), dim3(256), 0, st, (const bf16*)gu, ld_gu, (bf16*)h, ld_h,
-                     (long)M, F, mo);
+  if (M > 65535) return OSPO_ERR_SHAPE;  // rows on grid.y
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(blocks(F / 8, 128), M), dim3(128), 0, st, (const bf16*)gu, ld_gu,
+                     (bf16*)h, ld_h, (long)M, F, mo);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
@@ -824,9 +825,9 @@ static int swiglu_bwd_impl(const void* dh, int ld_dh, const void* gu, int ld_gu,
   if (M <= 0 || F % 8 || ld_gu < 2 * F || ld_dgu < 2 * F || ld_dh < F || ld_dh % 8 || ld_gu % 8 || ld_dgu % 8)
     return OSPO_ERR_SHAPE;
   if (!aligned16(dh) || !aligned16(gu) || !aligned16(dgu)) return OSPO_ERR_ALIGN;
-  const long n = (long)M * (F / 8);
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(blocks(n)), dim3(256), 0, st, (const bf16*)dh, ld_dh, (const bf16*)gu,
-                     ld_gu, (bf16*)dgu, ld_dgu, (long)M, F, mo);
+  if (M > 65535) return OSPO_ERR_SHAPE;  // rows on grid.y
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(blocks(F / 8, 128), M), dim3(128), 0, st, (const bf16*)dh, ld_dh,
+                     (const bf16*)gu, ld_gu, (bf16*)dgu, ld_dgu, (long)M, F, mo);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
