@@ -1161,16 +1161,16 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16* __restr
                                                              float* __restrict__ delta, int T, int H, long n_chunks) {
   const int cpr = H * 16;  // chunks per row
   u32x4 a[DELTA_CH], b[DELTA_CH];
-  long row[DELTA_CH];
+  int row[DELTA_CH];  // 32-bit index math: n_chunks < 2^31 (host check)
   int cc[DELTA_CH];
 #pragma unroll
   for (int i = 0; i < DELTA_CH; ++i) {
-    long c = (long)blockIdx.x * (256 * DELTA_CH) + i * 256 + threadIdx.x;
-    c = c < n_chunks ? c : n_chunks - 1;  // clamped lanes recompute the last chunk, store nothing
-    row[i] = c / cpr;
-    cc[i] = (int)(c - row[i] * cpr);
-    a[i] = *reinterpret_cast<const u32x4*>(dout + row[i] * ldd + cc[i] * 8);
-    b[i] = *reinterpret_cast<const u32x4*>(o + row[i] * ldo + cc[i] * 8);
+    int c = (int)blockIdx.x * (256 * DELTA_CH) + i * 256 + (int)threadIdx.x;
+    c = c < (int)n_chunks ? c : (int)n_chunks - 1;  // clamped lanes recompute the last chunk, store nothing
+    row[i] = (int)((unsigned)c / (unsigned)cpr);
+    cc[i] = c - row[i] * cpr;
+    a[i] = *reinterpret_cast<const u32x4*>(dout + (long)row[i] * ldd + cc[i] * 8);
+    b[i] = *reinterpret_cast<const u32x4*>(o + (long)row[i] * ldo + cc[i] * 8);
   }
 #pragma unroll
   for (int i = 0; i < DELTA_CH; ++i) {
@@ -1522,6 +1522,7 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
     if (dkdv_r2 || dkdv_dbg != 0) dkdv3 = nullptr;
 #endif
     const long n_chunks = (long)S * T * n_heads * 16;
+    if (n_chunks >= (1L << 31) - 256 * DELTA_CH) return OSPO_ERR_SHAPE;
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)((n_chunks + 256 * DELTA_CH - 1) / (256 * DELTA_CH))),
                        dim3(256), 0, stream, (const bf16*)dout, ld_do, (const bf16*)o, ld_o, delta_ws, T, n_heads,
                        n_chunks);

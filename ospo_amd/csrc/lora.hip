@@ -252,9 +252,9 @@ __global__ __launch_bounds__(256) void skinny2_kernel(const bf16* __restrict__ A
 // out[m][c] = bf16(scale * sum_z ws[z][m][c]) for c < ctot, 0 for ctot <= c < out_cols; rows >= M zero
 __global__ void skinny2_reduce_kernel(const float* __restrict__ ws, int splits, int M, int M_out, int M_pad, int ctot,
                                       float scale, bf16* __restrict__ out, int ldo, int out_cols) {
-  const int cq = out_cols / 4;
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= (long)M_out * cq) return;
+  const unsigned cq = (unsigned)out_cols / 4;  // 32-bit index math: M_out * cq < 2^31 (host check)
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (unsigned)M_out * cq) return;
   const int m = (int)(tid / cq), c = (int)(tid % cq) * 4;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   if (m < M && c < ctot) {
@@ -585,9 +585,9 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
 // out[m][16 mod + c] = bf16(scale * sum_sp ws[mod][sp][m][c]) (m < M; 0 for M <= m < M_out), pad columns 0
 __global__ void gdb_reduce_kernel(const float* __restrict__ ws, int nmods, int nsplit, int Mw, int M, int M_out,
                                   float scale, bf16* __restrict__ out, int ldo, int out_cols) {
-  const int cq = out_cols / 4;
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= (long)M_out * cq) return;
+  const unsigned cq = (unsigned)out_cols / 4;  // 32-bit index math: M_out * cq < 2^31 (host check)
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (unsigned)M_out * cq) return;
   const int m = (int)(tid / cq), c = (int)(tid % cq) * 4;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   const int mod = c / 16;
@@ -710,6 +710,7 @@ static int launch_skinny2(const bf16* a, int lda, const bf16* b, int ldb, int b_
   OSPO_CHECK_LAUNCH();
   if (splits > 1) {
     const long n = (long)M_out * (out_cols / 4);
+    if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
     hipLaunchKernelGGL(skinny2_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, part, splits,
                        M, M_out, M_pad, 16 * tiles_total, scale, o, ldo, out_cols);
     OSPO_CHECK_LAUNCH();
@@ -746,6 +747,7 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   OSPO_CHECK_LAUNCH();
   if (splits > 1) {
     const long n = (long)M_out * (out_cols / 4);
+    if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
     hipLaunchKernelGGL(skinny2_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, part, splits,
                        M, M_out, M_pad, 16 * tiles_total, scale, o, ldo, out_cols);
     OSPO_CHECK_LAUNCH();
@@ -914,6 +916,7 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
                      (const bf16*)u, ldu, M, Nmod, nch, (float*)ws, Mw, dB);
   OSPO_CHECK_LAUNCH();
   const long n = (long)M_out * (out_cols / 4);
+  if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
   hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)ws,
                      nmods, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
   OSPO_CHECK_LAUNCH();
