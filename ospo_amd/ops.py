@@ -86,7 +86,8 @@ def gemm_workspace(device=None) -> torch.Tensor:
     ws = _GEMM_WS.get(dev.index)
     if ws is None:
         ws = _GEMM_WS[dev.index] = torch.empty(256 * 65536, dtype=torch.float32, device=dev)
-        call("ospo_gemm_set_workspace", ws.data_ptr(), ws.numel() * 4)
+        with torch.cuda.device(dev):  # ospo_gemm_set_workspace registers for the current device
+            call("ospo_gemm_set_workspace", ws.data_ptr(), ws.numel() * 4)
     return ws
 
 
@@ -106,7 +107,7 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
         K2 = a2.shape[1]
         if a2.shape[0] != M or b2.shape != (N, K2):
             raise ValueError("gemm_nt K-extension shape mismatch")
-    if not _GEMM_WS:
+    if a.device.index not in _GEMM_WS:  # per device (the library keys the workspace by the current device)
         gemm_workspace(a.device)
     st = torch.cuda.current_stream()
     e0 = _TIMER.start(st) if _TIMER is not None else None
@@ -154,7 +155,7 @@ def gemm_nt_swiglu_bwd(a: torch.Tensor, b: torch.Tensor, gu: torch.Tensor, dgu: 
     seed, p = (0, 0.0) if dropout is None else (int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]))
     if p > 0 and a2 is None:
         raise ValueError("gemm_nt_swiglu_bwd: dropout needs a2/b2")
-    if not _GEMM_WS:
+    if a.device.index not in _GEMM_WS:  # per device (the library keys the workspace by the current device)
         gemm_workspace(a.device)
     st = torch.cuda.current_stream()
     e0 = _TIMER.start(st) if _TIMER is not None else None
@@ -212,7 +213,7 @@ def gemm_nt_mx8(a: MX8, b: MX8, out: torch.Tensor, *, a2=None, b2=None, alpha: f
         K2 = a2.shape[1]
         if a2.shape[0] != M or b2.shape != (N, K2):
             raise ValueError("gemm_nt_mx8 K-extension shape mismatch")
-    if not _GEMM_WS:
+    if out.device.index not in _GEMM_WS:  # per device
         gemm_workspace(out.device)
     cos = sin = None
     T = ncols = 0
