@@ -316,6 +316,10 @@ int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, i
  * (pos_dev = position of the current query, step_dev = image-token index).
  * ospo_decode_gemv: out[r][n] = act(x[r] . W[n] + bias[n]) (+ residual[r][n]), R <= 64 rows,
  *   W [N, ldw] (nn.Linear layout), act = GELU(erf) when gelu; ws >= ospo_decode_gemv_ws_bytes.
+ *   ldw = 0 (here and in the fused entries below): W is in the MFMA-tiled decode layout, 1-KiB tiles
+ *   of 16 rows x 32 k at ((n/16) * (K/32) + k/32) * 512 elements, element 8 * (16 g + l16) + e =
+ *   W[16 (n/16) + l16][32 (k/32) + 8 g + e] (ospo_amd.ops.tile_decode_weight); needs R <= 32 and
+ *   N % 128 == 0 (OSPO_ERR_UNSUPPORTED otherwise); results bit-identical to the row-major W.
  * ospo_kv_store: q|k|v rows [R][nq] (position pos0 + i, pos0 = *pos_dev or 0): optional
  *   rotate-half RoPE on q and k, k / v into the caches [R][H][Tmax][head_dim], q to q_out.
  * ospo_attn_cache: causal attention of query (r, i) over cached keys [start[r], pos0 + i]

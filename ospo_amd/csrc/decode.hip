@@ -198,8 +198,14 @@ __global__ __launch_bounds__(256) void gemv2_reduce_kernel(const f32x4* __restri
 
 // GEMV v3: v2's schedule with 8 waves = 128 weight rows per workgroup: half the x staging per
 // weight byte.  Split partials as v2 (summed by gemv2_reduce_kernel).
+//
+// TL (round 2): W in the MFMA-tiled decode layout (ospo_decode_gemv with ldw = 0): tile (nb, ks) =
+// rows 16 nb .. +15 x k 32 ks .. +31 is 1 KiB at ((nb * K/32 + ks) * 512) elements, lane-ordered
+// (element 8 * (16 g + l16) + e = W[16 nb + l16][32 ks + 8 g + e]), so each 16-B fragment load of a
+// wave reads one contiguous KiB (8 whole 128-B lines) instead of 16 rows x 64 B (half lines) of the
+// row-major weight.  Same fragments, same MFMA order: bit-identical to the row-major form.
 constexpr int G3_WAVES = 8, G3_ROWS = 16 * G3_WAVES;
-template <int NT>
+template <int NT, bool TL = false>
 __global__ __launch_bounds__(64 * G3_WAVES) void gemv3_kernel(const bf16* __restrict__ W, int ldw,
                                                               const bf16* __restrict__ X, int ldx, int R, int K,
                                                               int kper, const bf16* __restrict__ bias, int gelu,
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(64 * G3_WAVES) void gemv3_kernel(const bf16* __rest
   const int n = blockIdx.x * G3_ROWS + wave * 16 + l16;
   const int z = blockIdx.y, splits = gridDim.y;
   const int k_begin = z * kper, k_end = min(K, k_begin + kper);
-  const bf16* wrow = W + (long)n * ldw;
+  const bf16* wrow = TL ? W + ((long)(n >> 4) * (K >> 5) * 64 + lane) * 8 : W + (long)n * ldw;
   f32x4 acc[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -227,8 +233,12 @@ __global__ __launch_bounds__(64 * G3_WAVES) void gemv3_kernel(const bf16* __rest
     bf16x8 wv[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int k = kc + 32 * min(s, nsteps - 1) + 8 * g;
-      wv[s] = *reinterpret_cast<const bf16x8*>(wrow + k);
+      if (TL) {
+        wv[s] = *reinterpret_cast<const bf16x8*>(wrow + (long)((kc >> 5) + min(s, nsteps - 1)) * 512);
+      } else {
+        const int k = kc + 32 * min(s, nsteps - 1) + 8 * g;
+        wv[s] = *reinterpret_cast<const bf16x8*>(wrow + k);
+      }
     }
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this wave's x DMA (issued first) has landed
     __syncthreads();
@@ -793,12 +803,10 @@ static int gemv3_partials(const bf16* w, int ldw, const bf16* x, int ldx, int R,
   splits = (K + kper - 1) / kper;
   if (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws)) return OSPO_ERR_ARG;
   const dim3 grid(N / G3_ROWS, splits);
-  if (R <= 16)
-    hipLaunchKernelGGL((gemv3_kernel<1>), grid, dim3(64 * G3_WAVES), 0, stream, w, ldw, x, ldx, R, K, kper, nullptr,
-                       0, nullptr, 0, nullptr, 0, ws);
-  else
-    hipLaunchKernelGGL((gemv3_kernel<2>), grid, dim3(64 * G3_WAVES), 0, stream, w, ldw, x, ldx, R, K, kper, nullptr,
-                       0, nullptr, 0, nullptr, 0, ws);
+  auto kfn = R <= 16 ? (ldw == 0 ? gemv3_kernel<1, true> : gemv3_kernel<1, false>)
+                     : (ldw == 0 ? gemv3_kernel<2, true> : gemv3_kernel<2, false>);
+  hipLaunchKernelGGL(kfn, grid, dim3(64 * G3_WAVES), 0, stream, w, ldw, x, ldx, R, K, kper, nullptr, 0, nullptr, 0,
+                     nullptr, 0, ws);
   return OSPO_OK;
 }
 
@@ -810,7 +818,7 @@ extern "C" int ospo_decode_gemv_kv(const void* W, int ldw, const void* X, int ld
   if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
   const int N = 3 * n_heads * HD;
   if (!ospo_decode_gemv_fusable(R, N, K)) return OSPO_ERR_UNSUPPORTED;
-  if (ldw < K || ldx < K || ldw % 8 || ldx % 8 || ldq < n_heads * HD || Tmax <= 0) return OSPO_ERR_SHAPE;
+  if ((ldw != 0 && ldw < K) || ldx < K || ldw % 8 || ldx % 8 || ldq < n_heads * HD || Tmax <= 0) return OSPO_ERR_SHAPE;
   if (!aligned16(W) || !aligned16(X)) return OSPO_ERR_ALIGN;
   int splits = 0;
   const int rc = gemv3_partials((const bf16*)W, ldw, (const bf16*)X, ldx, R, N, K, (f32x4*)ws, ws_bytes, stream, splits);
@@ -833,7 +841,7 @@ extern "C" int ospo_decode_gemv_swiglu(const void* W, int ldw, const void* X, in
   if (!W || !X || !h) return OSPO_ERR_ARG;
   const int N = 2 * F;
   if (F % 64 || !ospo_decode_gemv_fusable(R, N, K)) return OSPO_ERR_UNSUPPORTED;
-  if (ldw < K || ldx < K || ldw % 8 || ldx % 8 || ldh < F) return OSPO_ERR_SHAPE;
+  if ((ldw != 0 && ldw < K) || ldx < K || ldw % 8 || ldx % 8 || ldh < F) return OSPO_ERR_SHAPE;
   if (!aligned16(W) || !aligned16(X)) return OSPO_ERR_ALIGN;
   int splits = 0;
   const int rc = gemv3_partials((const bf16*)W, ldw, (const bf16*)X, ldx, R, N, K, (f32x4*)ws, ws_bytes, stream, splits);
@@ -854,7 +862,8 @@ extern "C" int ospo_decode_gemv(const void* W, int ldw, const void* X, int ldx, 
                                 hipStream_t stream) {
   if (!W || !X || !out) return OSPO_ERR_ARG;
   if (R <= 0 || R > 64 || N <= 0 || N % 16 || K <= 0 || K % 32) return OSPO_ERR_SHAPE;
-  if (ldw < K || ldx < K || ldo < N || ldw % 8 || ldx % 8 || (residual && (ldr < N))) return OSPO_ERR_SHAPE;
+  if (ldw == 0 && (g_gemv_variant != 3 || R > 32 || N % G3_ROWS)) return OSPO_ERR_UNSUPPORTED;  // tiled: v3 only
+  if ((ldw != 0 && ldw < K) || ldx < K || ldo < N || ldw % 8 || ldx % 8 || (residual && (ldr < N))) return OSPO_ERR_SHAPE;
   if (!aligned16(W) || !aligned16(X)) return OSPO_ERR_ALIGN;
   const int nt = (R + 15) / 16, nb = N / 16;
   const bf16 *w = (const bf16*)W, *x = (const bf16*)X, *bs = (const bf16*)bias, *rs = (const bf16*)residual;
@@ -866,8 +875,11 @@ extern "C" int ospo_decode_gemv(const void* W, int ldw, const void* X, int ldx, 
     if (splits > 1 && (!ws || ws_bytes < ospo_decode_gemv_ws_bytes(R, N, K) || !aligned16(ws))) return OSPO_ERR_ARG;
     const dim3 grid(N / G3_ROWS, splits);
 #define GEMV3(NT_)                                                                                                \
-  hipLaunchKernelGGL((gemv3_kernel<NT_>), grid, dim3(64 * G3_WAVES), 0, stream, w, ldw, x, ldx, R, K, kper, bs, gelu, \
-                     rs, ldr, o, ldo, wsp);                                                                         \
+  {                                                                                                               \
+    auto kfn = ldw == 0 ? gemv3_kernel<NT_, true> : gemv3_kernel<NT_, false>;                                     \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * G3_WAVES), 0, stream, w, ldw, x, ldx, R, K, kper, bs, gelu, rs, ldr, o,  \
+                       ldo, wsp);                                                                                 \
+  }                                                                                                               \
   if (splits > 1)                                                                                                 \
     hipLaunchKernelGGL((gemv2_reduce_kernel<NT_>), dim3((nb + 3) / 4), dim3(256), 0, stream, wsp, splits, nb, R, bs,    \
                        gelu, rs, ldr, o, ldo);

@@ -47,7 +47,8 @@ class T2IGenerator:
 
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_batch: int = 16,
                  max_prompt_len: int = 64, n_img_tokens: int = 576, cfg_weight: float = 5.0,
-                 temperature: float = 1.0, pad_id: int = PAD_ID, vq_weights: Optional[Dict[str, torch.Tensor]] = None):
+                 temperature: float = 1.0, pad_id: int = PAD_ID, vq_weights: Optional[Dict[str, torch.Tensor]] = None,
+                 tiled_weights: bool = True):
         if dims.head_dim != 128:
             raise ValueError("head_dim must be 128 (Janus-Pro)")
         if 2 * max_batch > 64:
@@ -85,6 +86,18 @@ class T2IGenerator:
         self.al_w1, self.al_b1 = _dev(w["gen_aligner.w1"], dev), _dev(w["gen_aligner.b1"], dev)
         self.al_w2, self.al_b2 = _dev(w["gen_aligner.w2"], dev), _dev(w["gen_aligner.b2"], dev)
         self.gen_embed = _dev(w["gen_embed"], dev)
+        # decode-step copies of the weight streams in the MFMA-tiled layout (ops.tile_decode_weight: every
+        # fragment load reads whole 128-B lines; bit-identical results).  The prefill keeps the row-major
+        # weights (256x256 GEMM).  Needs R = 2 max_batch <= 32 and N % 128 == 0, else row-major.
+        self.tiled = bool(tiled_weights) and 2 * max_batch <= 32
+
+        def dw(t):
+            return ops.tile_decode_weight(t) if self.tiled and t.shape[0] % 128 == 0 and t.shape[1] % 32 == 0 else t
+
+        for lw in self.layers:
+            for k in ("qkv", "o", "gu", "down"):
+                lw[k + "_d"] = dw(lw[k])
+        self.gh_w1_d, self.gh_w2_d, self.al_w2_d = dw(self.gh_w1), dw(self.gh_w2), dw(self.al_w2)
         # ---- KV cache and decode-step buffers (R = 2 * max_batch rows)
         self.max_batch, self.max_prompt = max_batch, max_prompt_len
         self.Tmax = max_prompt_len + n_img_tokens
@@ -167,8 +180,8 @@ class T2IGenerator:
         """gen_head on the last position, CFG + sampling, next input embeds (aligner)."""
         dims = self.dims
         ops.rmsnorm_fwd(last, self.norm, self.hf[:R], self.rstd[:R], dims.rms_eps)
-        ops.decode_gemv(self.hf[:R], self.gh_w1, self.zg[:R], bias=self.gh_b1, gelu=True, ws=self.gws)
-        ops.decode_gemv(self.zg[:R], self.gh_w2, self.logits[:R], bias=self.gh_b2, ws=self.gws)
+        ops.decode_gemv(self.hf[:R], self.gh_w1_d, self.zg[:R], bias=self.gh_b1, gelu=True, ws=self.gws)
+        ops.decode_gemv(self.zg[:R], self.gh_w2_d, self.logits[:R], bias=self.gh_b2, ws=self.gws)
         B = R // 2
         probs = None
         if self.probs is not None:
@@ -176,7 +189,7 @@ class T2IGenerator:
         ops.cfg_sample(self.logits[:R], B, self.cfg_weight, self.temperature, self.u, self.step, self.n_img,
                        self.tokens[:B], self.next_ids[:R], probs)
         ops.gen_aligner_in(self.next_ids[:R], self.gen_embed, self.al_w1, self.al_b1, self.e1[:R])
-        ops.decode_gemv(self.e1[:R], self.al_w2, self.x[:R], bias=self.al_b2, ws=self.gws)
+        ops.decode_gemv(self.e1[:R], self.al_w2_d, self.x[:R], bias=self.al_b2, ws=self.gws)
         ops.decode_advance(self.pos, self.step)
 
     def _decode_step(self, R: int):
@@ -193,22 +206,22 @@ class T2IGenerator:
         for i, lw in enumerate(self.layers):
             ops.rmsnorm_fwd(x, lw["ln_in"], self.xn[:R], self.rstd[:R], dims.rms_eps)
             if fuse_qkv:
-                ops.decode_gemv_kv(self.xn[:R], lw["qkv"], g, self.pos, (self.cos, self.sin), self.kc[i], self.vc[i],
+                ops.decode_gemv_kv(self.xn[:R], lw["qkv_d"], g, self.pos, (self.cos, self.sin), self.kc[i], self.vc[i],
                                    H, self.Tmax, self.q[:R])
             else:
-                ops.decode_gemv(self.xn[:R], lw["qkv"], self.qkv[:R], ws=g)
+                ops.decode_gemv(self.xn[:R], lw["qkv_d"], self.qkv[:R], ws=g)
                 ops.kv_store(self.qkv[:R], R, 1, self.pos, self.kc[i], self.vc[i], H, self.Tmax,
                              rope=(self.cos, self.sin), q_out=self.q[:R])
             ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos, scale,
                            self.attn[:R])
-            ops.decode_gemv(self.attn[:R], lw["o"], self.xmid[:R], residual=x, ws=g)
+            ops.decode_gemv(self.attn[:R], lw["o_d"], self.xmid[:R], residual=x, ws=g)
             ops.rmsnorm_fwd(self.xmid[:R], lw["ln_post"], self.xn2[:R], self.rstd[:R], dims.rms_eps)
             if fuse_gu:
-                ops.decode_gemv_swiglu(self.xn2[:R], lw["gu"], g, self.h[:R])
+                ops.decode_gemv_swiglu(self.xn2[:R], lw["gu_d"], g, self.h[:R])
             else:
-                ops.decode_gemv(self.xn2[:R], lw["gu"], self.gu[:R], ws=g)
+                ops.decode_gemv(self.xn2[:R], lw["gu_d"], self.gu[:R], ws=g)
                 ops.swiglu_fwd(self.gu[:R], self.h[:R])
-            ops.decode_gemv(self.h[:R], lw["down"], xo, residual=self.xmid[:R], ws=g)
+            ops.decode_gemv(self.h[:R], lw["down_d"], xo, residual=self.xmid[:R], ws=g)
             x, xo = xo, x
         self._head_and_sample(x, R)
 

@@ -520,16 +520,38 @@ def decode_gemv_ws(R: int, N: int, K: int, device) -> torch.Tensor:
     return torch.zeros(max(nbytes // 4, 4), dtype=torch.float32, device=device)
 
 
+def tile_decode_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] nn.Linear weight -> the MFMA-tiled decode layout [N/16, K/32, 512] (include/ospo_hip.h,
+    ospo_decode_gemv with ldw = 0): tile (nb, ks) holds rows 16 nb.., k 32 ks.. lane-ordered, element
+    8 (16 g + l16) + e = w[16 nb + l16, 32 ks + 8 g + e].  A one-time layout copy of a frozen weight."""
+    if w.dtype != BF16 or w.dim() != 2:
+        raise ValueError(f"tile_decode_weight: expected a 2-D bf16 weight, got {w.dtype} {tuple(w.shape)}")
+    N, K = w.shape
+    if N % 16 or K % 32:
+        raise ValueError(f"tile_decode_weight: [{N}, {K}] needs N % 16 == 0 and K % 32 == 0")
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N // 16, K // 32, 512)
+
+
+def _decode_w(w: torch.Tensor):
+    """(N, K, ldw) of a decode weight: row-major [N, K] or tiled [N/16, K/32, 512] (ldw = 0)."""
+    if w.dim() == 3:
+        if w.shape[2] != 512 or not w.is_contiguous():
+            raise ValueError(f"tiled decode weight must be a contiguous [N/16, K/32, 512] tensor, got {tuple(w.shape)}")
+        return w.shape[0] * 16, w.shape[1] * 32, 0
+    return w.shape[0], w.shape[1], _ld(w)
+
+
 def decode_gemv(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, gelu: bool = False, residual=None,
                 ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out[R, N] = act(x . w^T + bias) (+ residual), R <= 64 (weight-streaming decode GEMV)."""
+    """out[R, N] = act(x . w^T + bias) (+ residual), R <= 64 (weight-streaming decode GEMV); w row-major
+    [N, K] or tiled by ``tile_decode_weight``."""
     for t, n in ((x, "x"), (w, "w"), (out, "out")):
         _chk(t, BF16, n)
     R, K = x.shape
-    N = w.shape[0]
-    if w.shape[1] != K or out.shape != (R, N):
+    N, Kw, ldw = _decode_w(w)
+    if Kw != K or out.shape != (R, N):
         raise ValueError(f"decode_gemv shape mismatch x{tuple(x.shape)} w{tuple(w.shape)} out{tuple(out.shape)}")
-    call("ospo_decode_gemv", _p(w), _ld(w), _p(x), _ld(x), R, N, K, _p(bias), int(gelu), _p(residual),
+    call("ospo_decode_gemv", _p(w), ldw, _p(x), _ld(x), R, N, K, _p(bias), int(gelu), _p(residual),
          _ld(residual) if residual is not None else 0, _p(out), _ld(out), _p(ws), 0 if ws is None else ws.numel() * 4,
          _s())
     return out
@@ -544,8 +566,11 @@ def decode_gemv_kv(x, w, ws, pos_dev, rope, k_cache, v_cache, n_heads, Tmax, q_o
     _chk(x, BF16, "x")
     _chk(w, BF16, "w")
     R, K = x.shape
+    N, Kw, ldw = _decode_w(w)
+    if Kw != K or N != 3 * n_heads * 128:
+        raise ValueError(f"decode_gemv_kv shape mismatch x{tuple(x.shape)} w{tuple(w.shape)}")
     cos, sin = rope
-    call("ospo_decode_gemv_kv", _p(w), _ld(w), _p(x), _ld(x), R, n_heads, 128, K, _p(ws), ws.numel() * 4,
+    call("ospo_decode_gemv_kv", _p(w), ldw, _p(x), _ld(x), R, n_heads, 128, K, _p(ws), ws.numel() * 4,
          _p(pos_dev), _p(cos), _p(sin), _p(k_cache), _p(v_cache), Tmax, _p(q_out), _ld(q_out), _s())
 
 
@@ -555,10 +580,11 @@ def decode_gemv_swiglu(x, w, ws, h):
     _chk(w, BF16, "w")
     _chk(h, BF16, "h")
     R, K = x.shape
-    F = w.shape[0] // 2
-    if h.shape[0] < R or h.shape[1] != F:
-        raise ValueError(f"decode_gemv_swiglu: h{tuple(h.shape)} for R={R}, F={F}")
-    call("ospo_decode_gemv_swiglu", _p(w), _ld(w), _p(x), _ld(x), R, F, K, _p(ws), ws.numel() * 4, _p(h), _ld(h),
+    N, Kw, ldw = _decode_w(w)
+    F = N // 2
+    if Kw != K or h.shape[0] < R or h.shape[1] != F:
+        raise ValueError(f"decode_gemv_swiglu: h{tuple(h.shape)} w{tuple(w.shape)} for R={R}, F={F}")
+    call("ospo_decode_gemv_swiglu", _p(w), ldw, _p(x), _ld(x), R, F, K, _p(ws), ws.numel() * 4, _p(h), _ld(h),
          _s())
     return h
 

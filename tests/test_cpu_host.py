@@ -363,3 +363,23 @@ def test_checkpoint_keys_resolve_in_the_reference_module_tree(tmp_path):
         assert isinstance(m, torch.nn.Linear), name
         assert tuple(t.shape) == ((r, m.in_features) if ab.startswith("A") else (m.out_features, r)), k
         assert name.split(".")[-1] in lc["target_modules"]
+
+
+def test_tile_decode_weight_layout():
+    """ops.tile_decode_weight is the layout include/ospo_hip.h states for ospo_decode_gemv ldw = 0:
+    element 8 (16 g + l16) + e of tile (nb, ks) = w[16 nb + l16, 32 ks + 8 g + e]."""
+    import torch
+    from ospo_amd import ops
+    N, K = 48, 96
+    w = torch.arange(N * K, dtype=torch.float32).reshape(N, K).bfloat16()  # exact up to 256: compare indices below
+    idx = torch.arange(N * K, dtype=torch.int64).reshape(N, K)
+    t = ops.tile_decode_weight(w)
+    assert t.shape == (N // 16, K // 32, 512) and t.is_contiguous()
+    ti = idx.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(N // 16, K // 32, 512)
+    for nb in range(N // 16):
+        for ks in range(K // 32):
+            for g in range(4):
+                for l16 in range(16):
+                    for e in (0, 7):
+                        assert int(ti[nb, ks, 8 * (16 * g + l16) + e]) == (16 * nb + l16) * K + 32 * ks + 8 * g + e
+    assert torch.equal(t, w.flatten()[ti.flatten()].reshape(t.shape))

@@ -309,3 +309,64 @@ def test_decode_gemv_fused_consumers_equal_unfused(R):
     ops().swiglu_fwd(gu, h1)
     ops().decode_gemv_swiglu(x, wg, ws, h2)
     assert torch.equal(h1, h2)
+
+
+@pytest.mark.parametrize("R,N,K", [(32, 4096, 4096), (32, 12288, 4096), (32, 4096, 11008), (16, 16384, 4096),
+                                   (12, 256, 608), (32, 128, 96)])
+def test_decode_gemv_tiled_weight_bit_identical(R, N, K):
+    """The MFMA-tiled decode layout (ops.tile_decode_weight, ldw = 0) gives the row-major GEMV's bits:
+    plain, K-split with bias + GELU, and with a residual (the o / down / gen_head calls of the step)."""
+    x = torch.randn(R, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16()
+    res = torch.randn(R, N, device=DEV).bfloat16()
+    wt = ops().tile_decode_weight(w)
+    assert wt.shape == (N // 16, K // 32, 512)
+    ws = ops().decode_gemv_ws(R, N, K, DEV)
+    for kw in ({}, {"bias": b, "gelu": True}, {"residual": res}):
+        o1 = torch.full((R, N), float("nan"), device=DEV).bfloat16()
+        o2 = o1.clone()
+        ops().decode_gemv(x, w, o1, ws=ws, **kw)
+        ops().decode_gemv(x, wt, o2, ws=ws, **kw)
+        assert torch.equal(o1, o2), kw
+    ref = x.float() @ w.float().T
+    assert relerr(o2.float() - res.float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("R", [32, 12])
+def test_decode_gemv_tiled_fused_consumers_bit_identical(R):
+    """q|k|v + RoPE/KV store and gate|up + SwiGLU from tiled weights equal the row-major forms."""
+    H, D, F, Tmax, p = 32, 4096, 11008, 96, 41
+    x = torch.randn(R, D, device=DEV).bfloat16()
+    wq = (torch.randn(3 * D, D, device=DEV) * 0.02).bfloat16()
+    wg = (torch.randn(2 * F, D, device=DEV) * 0.02).bfloat16()
+    ws = torch.zeros(max(ops().decode_gemv_ws(R, 2 * F, D, DEV).numel(), ops().decode_gemv_ws(R, 3 * D, D, DEV).numel()),
+                     device=DEV)
+    pos = torch.tensor([p], dtype=torch.int32, device=DEV)
+    cos, sin = ops().rope_tables(Tmax, 128, 1e4, DEV)
+    z = lambda *sh: torch.zeros(*sh, dtype=torch.bfloat16, device=DEV)  # noqa: E731
+    out = []
+    for wqq in (wq, ops().tile_decode_weight(wq)):
+        kc, vc, q = z(R, H, Tmax, 128), z(R, H, Tmax, 128), z(R, D)
+        ops().decode_gemv_kv(x, wqq, ws, pos, (cos, sin), kc, vc, H, Tmax, q)
+        out.append((kc, vc, q))
+    assert all(torch.equal(a, b) for a, b in zip(*out))
+    h = []
+    for wgg in (wg, ops().tile_decode_weight(wg)):
+        h.append(z(R, F))
+        ops().decode_gemv_swiglu(x, wgg, ws, h[-1])
+    assert torch.equal(h[0], h[1])
+
+
+def test_decode_gemv_tiled_rejects_unsupported():
+    """Tiled weights need R <= 32 and N % 128 == 0: other shapes fail loudly, never fall back."""
+    x = torch.randn(40, 256, device=DEV).bfloat16()
+    w = torch.randn(256, 256, device=DEV).bfloat16()
+    with pytest.raises(RuntimeError):
+        ops().decode_gemv(x, ops().tile_decode_weight(w), torch.empty(40, 256, device=DEV).bfloat16(),
+                          ws=ops().decode_gemv_ws(40, 256, 256, DEV))
+    x = torch.randn(8, 256, device=DEV).bfloat16()
+    w = torch.randn(208, 256, device=DEV).bfloat16()
+    with pytest.raises(RuntimeError):
+        ops().decode_gemv(x, ops().tile_decode_weight(w), torch.empty(8, 208, device=DEV).bfloat16(),
+                          ws=ops().decode_gemv_ws(8, 208, 256, DEV))
