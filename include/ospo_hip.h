@@ -192,6 +192,20 @@ int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v
                         float* delta_ws, void* ds_ws, void* dqkv, int ld_dqkv, int S, int T,
                         int n_heads, int head_dim, float scale, const void* rope_cos,
                         const void* rope_sin, hipStream_t stream);
+/* BASELINE config 5 (MXFP8 decoder Linears): the same kernels also write the MXFP8 copy of what they store,
+ * byte-identical to ospo_quant_mx8 of the bf16 output, so the o_proj forward GEMM (operand: the attention
+ * output, K8 = n_heads * head_dim) and the q|k|v dX GEMM (operand: dqkv, K8 = its column count) need no
+ * quantize pass: q8 e4m3 [S*T, ldq8 bytes], s8 the scales of a [S*T, K8] matrix in ospo_quant_mx8's layout
+ * (K8 % 128 == 0; every stored column < K8).  The backward form needs ds_ws (5-product kernels) and
+ * q/k/v column offsets that are multiples of 128. */
+int ospo_flash_attn_fwd_mx8(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o, int ld_o,
+                            float* lse, int S, int T, int n_heads, int head_dim, float scale, void* q8, int ldq8,
+                            void* s8, int K8, hipStream_t stream);
+int ospo_flash_attn_bwd_mx8(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, const void* o,
+                            int ld_o, const void* dout, int ld_do, const float* lse, float* delta_ws, void* ds_ws,
+                            void* dqkv, int ld_dqkv, int S, int T, int n_heads, int head_dim, float scale,
+                            const void* rope_cos, const void* rope_sin, void* q8, int ldq8, void* s8, int K8,
+                            hipStream_t stream);
 
 /* ------------------------------------------------------- embed / gather ---
  * preprocess_batch (ospo/wrapper/train.py:224-239, 267-277) + concatenated_inputs

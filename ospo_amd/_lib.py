@@ -46,6 +46,8 @@ SIGNATURES = {
     "ospo_flash_attn_fwd": [P, I, I, I, I, P, I, P, I, I, I, I, F, P],
     "ospo_flash_attn_bwd": [P, I, I, I, I, P, I, P, I, P, P, P, P, I, I, I, I, I, F, P, P, P],
     "ospo_flash_attn_bwd_ws_bytes": [I, I, I],
+    "ospo_flash_attn_fwd_mx8": [P, I, I, I, I, P, I, P, I, I, I, I, F, P, I, P, I, P],
+    "ospo_flash_attn_bwd_mx8": [P, I, I, I, I, P, I, P, I, P, P, P, P, I, I, I, I, I, F, P, P, P, I, P, I, P],
     "ospo_assemble_inputs": [P, I, I, P, I, P, I, I, P, P],
     "ospo_gen_aligner_in": [P, I, P, I, I, P, P, I, P, P],
     "ospo_gather_rows": [P, I, I, I, I, I, I, P, P],

@@ -24,6 +24,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "mx8.h"
 
 namespace {
 
@@ -221,8 +222,13 @@ __device__ __forceinline__ void rope_bwd_acc(f32x4 (&v)[8], const bf16* cs, cons
 // lane store tail is store-ISSUE bound).  Rows r with row0 + r >= row_lim are not stored.
 constexpr int SCR_PITCH = ROWB + 16;
 constexpr int SCR_BYTES = 16 * SCR_PITCH;  // 4352 B per wave and matrix
+// With mo.q != nullptr the stored bf16 rows also go out as MXFP8 (config 5: the attention output is the o_proj
+// GEMM's operand, dq|dk|dv the q|k|v dX GEMM's): row grow0 + row0 + r, columns 8 (c8_0 + lane & 15) ..; the
+// 16 lanes of a row hold its 128 columns, so 4 consecutive lanes hold one 32-block (mx8_store8), bytes
+// identical to ospo_quant_mx8 of the bf16 output.
 __device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf16* dst, long ld, int row0,
-                                             int row_lim, int lane) {
+                                             int row_lim, int lane, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0},
+                                             long grow0 = 0, int c8_0 = 0) {
   const int g = lane >> 4, l16 = lane & 15;
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) {
@@ -237,7 +243,14 @@ __device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf1
   for (int k = 0; k < 4; ++k) {
     const int r = 4 * k + (lane >> 4);
     const uint4 x = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + (lane & 15) * 16);
-    if (row0 + r < row_lim) *reinterpret_cast<uint4*>(dst + (long)(row0 + r) * ld + (lane & 15) * 8) = x;
+    if (row0 + r < row_lim) {  // uniform over the 16 lanes of a row
+      *reinterpret_cast<uint4*>(dst + (long)(row0 + r) * ld + (lane & 15) * 8) = x;
+      if (mo.q) {
+        const float f[8] = {bits2f(x.x & 0xffff), bits2f(x.x >> 16), bits2f(x.y & 0xffff), bits2f(x.y >> 16),
+                            bits2f(x.z & 0xffff), bits2f(x.z >> 16), bits2f(x.w & 0xffff), bits2f(x.w >> 16)};
+        mx8_store8(mo, grow0 + row0 + r, c8_0 + (lane & 15), f);
+      }
+    }
   }
 }
 
@@ -245,7 +258,8 @@ __device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf1
 template <int NW, int DBG = 0>  // DBG 1: no K/V loads after the first tile (ablation, results invalid)
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
                                                        bf16* __restrict__ out, int ldo, float* __restrict__ lse,
-                                                       int T, int H, float scale) {
+                                                       int T, int H, float scale,
+                                                       const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0}) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -364,7 +378,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
     const float inv = 1.f / l_run;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) o[dt] *= inv;
-    store_rows16(o, smem + wave * SCR_BYTES, out + rowbase * ldo + h * HD, ldo, qb * RB + wave * 16, T, lane);
+    store_rows16(o, smem + wave * SCR_BYTES, out + rowbase * ldo + h * HD, ldo, qb * RB + wave * 16, T, lane, mo,
+                 rowbase, h * (HD / 8));
     if (qrow < T && g == 0) lse[((long)s * H + h) * T + qrow] = m_run + __logf(l_run);
   }
 }
@@ -655,7 +670,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, const bf16* __restrict__ dout, int ldd,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16* __restrict__ dqkv, int ldg, int T, int H,
     float scale, const bf16* __restrict__ rcs, const bf16* __restrict__ rsn, bf16* __restrict__ dsT, int ds_ld,
-    unsigned long long* __restrict__ dbg, int gm) {
+    unsigned long long* __restrict__ dbg, int gm, const Mx8Out mo) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES + 4 * 64 * 4];
   unsigned long long st_acc[7] = {0, 0, 0, 0, 0, 0, 0};  // DBG: first wait, sp0-3, sp4-7, vmcnt, barrier, tiles, stage
   auto stamp = [&]() -> unsigned long long { return DBG ? __builtin_amdgcn_s_memtime() : 0ull; };
@@ -1015,8 +1030,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   {
     char* scr = smem + wave * 2 * SCR_BYTES;
     const int key0 = kb * KBW + wave * 16;
-    store_rows16(dk, scr, dqkv + rowbase * ldg + kc + h * HD, ldg, key0, T, lane);
-    store_rows16(dv, scr + SCR_BYTES, dqkv + rowbase * ldg + vc + h * HD, ldg, key0, T, lane);
+    store_rows16(dk, scr, dqkv + rowbase * ldg + kc + h * HD, ldg, key0, T, lane, mo, rowbase, (kc + h * HD) / 8);
+    store_rows16(dv, scr + SCR_BYTES, dqkv + rowbase * ldg + vc + h * HD, ldg, key0, T, lane, mo, rowbase,
+                 (vc + h * HD) / 8);
   }
 }
 
@@ -1318,7 +1334,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ring_kernel(const bf16* _
                                                                int kc, const bf16* __restrict__ dsT, int ds_ld,
                                                                bf16* __restrict__ dqkv, int ldg, int T, int H,
                                                                const bf16* __restrict__ rcs,
-                                                               const bf16* __restrict__ rsn, int gm) {
+                                                               const bf16* __restrict__ rsn, int gm,
+                                                               const Mx8Out mo) {
   constexpr int SLOT = 2 * 32 * ROWB;  // K [32][128] | dS^T [32][128 queries]: 16 KiB
   constexpr int NSLOT = 4;
   constexpr int PIECES = 2 * (8 / NW);  // DMA pieces per wave per stage
@@ -1392,7 +1409,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ring_kernel(const bf16* _
   for (int a = 0; a < 2; ++a) {
     if (rcs) rope_apply(dq[a], rr[a]);
     store_rows16(dq[a], smem + (wave * 2 + a) * SCR_BYTES, dqkv + rowbase * ldg + qc + h * HD, ldg,
-                 qb * RB + wave * 32 + 16 * a, T, lane);
+                 qb * RB + wave * 32 + 16 * a, T, lane, mo, rowbase, (qc + h * HD) / 8);
   }
 }
 
@@ -1438,9 +1455,9 @@ extern "C" int ospo_attn_set_stamps(void* buf) {
 }
 #endif
 
-extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
-                                   int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
-                                   hipStream_t stream) {
+static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o, int ld_o,
+                          float* lse, int S, int T, int n_heads, int head_dim, float scale, const Mx8Out mo,
+                          hipStream_t stream) {
   if (!qkv || !o || !lse) return OSPO_ERR_ARG;
   if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
   if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || q_col % 8 || k_col % 8 || v_col % 8)
@@ -1455,9 +1472,35 @@ extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k
   auto kfn = attn_fwd_kernel<8, 0>;
 #endif
   hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
-                     (bf16*)o, ld_o, lse, T, n_heads, scale);
+                     (bf16*)o, ld_o, lse, T, n_heads, scale, mo);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
+}
+
+extern "C" int ospo_flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
+                                   int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
+                                   hipStream_t stream) {
+  return flash_attn_fwd(qkv, ld_qkv, q_col, k_col, v_col, o, ld_o, lse, S, T, n_heads, head_dim, scale,
+                        Mx8Out{nullptr, 0, nullptr, 0}, stream);
+}
+
+// The MXFP8 copy of an attention output's bf16 rows (q8 [S*T, ldq8] e4m3 + s8 scales in ospo_quant_mx8's
+// layout for K8 columns): every column an output kernel stores must lie below K8 (K8 % 128 == 0).
+static int mx8_target(void* q8, int ldq8, void* s8, int K8, int max_col, Mx8Out& mo) {
+  if (!q8 || !s8) return OSPO_ERR_ARG;
+  if (K8 <= 0 || K8 % 128 || ldq8 < K8 || ldq8 % 16 || max_col > K8) return OSPO_ERR_SHAPE;
+  if (!aligned16(q8)) return OSPO_ERR_ALIGN;
+  mo = Mx8Out{(uint8_t*)q8, ldq8, (uint8_t*)s8, K8};
+  return OSPO_OK;
+}
+
+extern "C" int ospo_flash_attn_fwd_mx8(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, void* o,
+                                       int ld_o, float* lse, int S, int T, int n_heads, int head_dim, float scale,
+                                       void* q8, int ldq8, void* s8, int K8, hipStream_t stream) {
+  Mx8Out mo;
+  const int rc = mx8_target(q8, ldq8, s8, K8, n_heads * head_dim, mo);
+  if (rc != OSPO_OK) return rc;
+  return flash_attn_fwd(qkv, ld_qkv, q_col, k_col, v_col, o, ld_o, lse, S, T, n_heads, head_dim, scale, mo, stream);
 }
 
 extern "C" size_t ospo_flash_attn_bwd_ws_bytes(int S, int T, int n_heads) {
@@ -1466,12 +1509,12 @@ extern "C" size_t ospo_flash_attn_bwd_ws_bytes(int S, int T, int n_heads) {
   return (size_t)S * n_heads * p * p * sizeof(bf16);
 }
 
-extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, const void* o,
-                                   int ld_o, const void* dout, int ld_do, const float* lse, float* delta_ws,
-                                   void* ds_ws, void* dqkv, int ld_dqkv, int S, int T, int n_heads,
-                                   int head_dim, float scale, const void* rope_cos, const void* rope_sin,
-                                   hipStream_t stream) {
+static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, const void* o, int ld_o,
+                          const void* dout, int ld_do, const float* lse, float* delta_ws, void* ds_ws, void* dqkv,
+                          int ld_dqkv, int S, int T, int n_heads, int head_dim, float scale, const void* rope_cos,
+                          const void* rope_sin, const Mx8Out mo, hipStream_t stream) {
   if (!qkv || !o || !dout || !lse || !delta_ws || !dqkv) return OSPO_ERR_ARG;
+  if (mo.q && !ds_ws) return OSPO_ERR_UNSUPPORTED;  // the MXFP8 copy comes from the 5-product kernels' stores
   if (head_dim != HD) return OSPO_ERR_UNSUPPORTED;
   if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || ld_do % 8 || ld_dqkv % 8) return OSPO_ERR_SHAPE;
   if (q_col % 8 || k_col % 8 || v_col % 8) return OSPO_ERR_SHAPE;
@@ -1520,6 +1563,7 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
     if (nwd == 8) dkdv3 = attn_bwd_dkdv3_kernel<8>;
     if (g_attn_stamps) dkdv3 = nwd == 4 ? attn_bwd_dkdv3_kernel<4, 1> : attn_bwd_dkdv3_kernel<8, 1>;
     if (dkdv_r2 || dkdv_dbg != 0) dkdv3 = nullptr;
+    if (mo.q && (!dkdv3 || getenv("OSPO_ATTN_DQ_2SLOT"))) return OSPO_ERR_UNSUPPORTED;  // ablation kernels: no MX copy
 #endif
     const long n_chunks = (long)S * T * n_heads * 16;
     if (n_chunks >= (1L << 31) - 256 * DELTA_CH) return OSPO_ERR_SHAPE;
@@ -1530,7 +1574,7 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
     if (dkdv3)
       hipLaunchKernelGGL(dkdv3, dim3(S * n_heads * ((T + 16 * nwd - 1) / (16 * nwd))), dim3(64 * nwd), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                          (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
-                         (bf16*)ds_ws, p, (unsigned long long*)g_attn_stamps, order_dkdv);
+                         (bf16*)ds_ws, p, (unsigned long long*)g_attn_stamps, order_dkdv, mo);
     else
       hipLaunchKernelGGL(dkdv, grid, dim3(64 * nwd), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                          (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
@@ -1543,7 +1587,7 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
 #endif
     if (!dq_two_slot)
       hipLaunchKernelGGL(attn_bwd_dq_ring_kernel<4>, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
-                         (const bf16*)ds_ws, p, (bf16*)dqkv, ld_dqkv, T, n_heads, rc, rs, order_dq);
+                         (const bf16*)ds_ws, p, (bf16*)dqkv, ld_dqkv, T, n_heads, rc, rs, order_dq, mo);
     else
       hipLaunchKernelGGL(attn_bwd_dq_ds_kernel<4>, dim3(n_heads, S, (T + 127) / 128), dim3(256), 0, stream,
                          (const bf16*)qkv, ld_qkv, q_col, k_col, (const bf16*)ds_ws, p, (bf16*)dqkv, ld_dqkv, T,
@@ -1562,4 +1606,27 @@ extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k
                      (bf16*)nullptr, 0);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
+}
+
+extern "C" int ospo_flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, const void* o,
+                                   int ld_o, const void* dout, int ld_do, const float* lse, float* delta_ws,
+                                   void* ds_ws, void* dqkv, int ld_dqkv, int S, int T, int n_heads,
+                                   int head_dim, float scale, const void* rope_cos, const void* rope_sin,
+                                   hipStream_t stream) {
+  return flash_attn_bwd(qkv, ld_qkv, q_col, k_col, v_col, o, ld_o, dout, ld_do, lse, delta_ws, ds_ws, dqkv, ld_dqkv,
+                        S, T, n_heads, head_dim, scale, rope_cos, rope_sin, Mx8Out{nullptr, 0, nullptr, 0}, stream);
+}
+
+extern "C" int ospo_flash_attn_bwd_mx8(const void* qkv, int ld_qkv, int q_col, int k_col, int v_col, const void* o,
+                                       int ld_o, const void* dout, int ld_do, const float* lse, float* delta_ws,
+                                       void* ds_ws, void* dqkv, int ld_dqkv, int S, int T, int n_heads,
+                                       int head_dim, float scale, const void* rope_cos, const void* rope_sin,
+                                       void* q8, int ldq8, void* s8, int K8, hipStream_t stream) {
+  Mx8Out mo;
+  const int max_col = std::max(q_col, std::max(k_col, v_col)) + n_heads * head_dim;
+  const int rc = mx8_target(q8, ldq8, s8, K8, max_col, mo);
+  if (rc != OSPO_OK) return rc;
+  if (q_col % 128 || k_col % 128 || v_col % 128) return OSPO_ERR_SHAPE;  // whole 32-blocks per head
+  return flash_attn_bwd(qkv, ld_qkv, q_col, k_col, v_col, o, ld_o, dout, ld_do, lse, delta_ws, ds_ws, dqkv, ld_dqkv,
+                        S, T, n_heads, head_dim, scale, rope_cos, rope_sin, mo, stream);
 }

@@ -391,10 +391,10 @@ class SimPOEngine:
             else:
                 self._lin(a["xn1"][:M], lw["qkv"], a["qkv"][:M], pre=True, a2=a["u_qkv"][:M], b2=Bcat)
                 ops.rope(a["qkv"], 0, D, S, T, H, hd, self.cos, self.sin)
-            ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn)
+            ops.flash_attn_fwd(a["qkv"], 0, D, 2 * D, a["attn"], a["lse"], S, T, H, hd, scale_attn, mx=self._mxo(D))
             Acat, _, Bcat, _ = pk["o"]
             self._lora_down(a["attn"], Acat, a["u_o"], M, lay.groups["o"].nmods, self._drop(i, "o"))
-            self._lin(a["attn"][:M], lw["o"], a["xmid"][:M], a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
+            self._lin(a["attn"][:M], lw["o"], a["xmid"][:M], pre=True, a2=a["u_o"][:M], b2=Bcat, residual=x[:M])
             ops.rmsnorm_fwd(a["xmid"][:M], lw["ln_post"], a["xn2"][:M], a["rstd2"][:M], dims.rms_eps,
                             mx=self._mxo(D))
             Acat, _, Bcat, _ = pk["gu"]
@@ -525,13 +525,14 @@ class SimPOEngine:
             # ---- attention + RoPE
             guard("qkv", q)  # dqkv / g copy q
             ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, self.ds_ws,
-                               dqkv, S, T, H, hd, scale_attn, rope_cos=self.cos, rope_sin=self.sin)
+                               dqkv, S, T, H, hd, scale_attn, rope_cos=self.cos, rope_sin=self.sin,
+                               mx=self._mxo(3 * D) if i > 0 else None)  # layer 0 runs no q|k|v dX GEMM
             # ---- q/k/v
             Acat, AcatT, Bcat, BT = pk["qkv"]
             gs, fdb = self._lora_g_db(dqkv, lay.groups["qkv"], Bcat, BT, M, q, a["u_qkv"], gbase)
             dr = self._drop(i, "qkv")
             if i > 0:
-                self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], a2=gs[:M], b2=AcatT, dropout=dr)
+                self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
             lora_grads_async("qkv", q, gs, a["xn1"], dqkv, a["u_qkv"], gbase, dr, fdb)
             if i > 0:
                 guard("down", 1 - q)  # dx copy 1-q: layer i+1's down products read it

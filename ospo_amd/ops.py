@@ -360,9 +360,16 @@ def swiglu_bwd(dh, gu, dgu, mx: "MX8 | None" = None):
 
 
 # -------------------------------------------------------------- attention
-def flash_attn_fwd(qkv, q_col, k_col, v_col, o, lse, S, T, n_heads, head_dim, scale):
-    call("ospo_flash_attn_fwd", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(lse), S, T, n_heads,
-         head_dim, float(scale), _s())
+def flash_attn_fwd(qkv, q_col, k_col, v_col, o, lse, S, T, n_heads, head_dim, scale, mx: "MX8 | None" = None):
+    """Causal flash attention; with mx, also mx <- MXFP8(o) from the output stores (== quant_mx8(o, mx))."""
+    if mx is None:
+        call("ospo_flash_attn_fwd", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(lse), S, T, n_heads,
+             head_dim, float(scale), _s())
+        return o, lse
+    _mx_target(mx, S * T, n_heads * head_dim, "flash_attn_fwd")
+    call("ospo_flash_attn_fwd_mx8", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(lse), S, T, n_heads,
+         head_dim, float(scale), _p(mx.q), mx.q.stride(0), _p(mx.s), mx.K, _s())
+    mx.m = S * T
     return o, lse
 
 
@@ -376,15 +383,23 @@ def flash_attn_bwd_ws(S: int, T: int, n_heads: int, device) -> torch.Tensor:
 
 
 def flash_attn_bwd(qkv, q_col, k_col, v_col, o, dout, lse, delta_ws, ds_ws, dqkv, S, T, n_heads, head_dim, scale,
-                   rope_cos=None, rope_sin=None):
+                   rope_cos=None, rope_sin=None, mx: "MX8 | None" = None):
     """Attention backward; with rope_cos/rope_sin the RoPE backward is fused into the dq/dk stores.
     ds_ws (flash_attn_bwd_ws): dK/dV store dS^T and dQ = dS.K reads it (5 MFMA products); None: the
-    dQ kernel recomputes S and dP (7 products)."""
+    dQ kernel recomputes S and dP (7 products).  With mx (needs ds_ws), also mx <- MXFP8 of the dqkv
+    matrix's first mx.K columns from the dq / dk / dv stores (== quant_mx8(dqkv, mx))."""
     if ds_ws is not None and ds_ws.numel() * 2 < flash_attn_bwd_ws_bytes(S, T, n_heads):
         raise ValueError("flash_attn_bwd: dS workspace too small")
-    call("ospo_flash_attn_bwd", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(dout), _ld(dout),
+    if mx is None:
+        call("ospo_flash_attn_bwd", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(dout), _ld(dout),
+             _p(lse), _p(delta_ws), _p(ds_ws), _p(dqkv), _ld(dqkv), S, T, n_heads, head_dim, float(scale),
+             _p(rope_cos), _p(rope_sin), _s())
+        return dqkv
+    _mx_target(mx, S * T, dqkv.shape[1], "flash_attn_bwd")
+    call("ospo_flash_attn_bwd_mx8", _p(qkv), _ld(qkv), q_col, k_col, v_col, _p(o), _ld(o), _p(dout), _ld(dout),
          _p(lse), _p(delta_ws), _p(ds_ws), _p(dqkv), _ld(dqkv), S, T, n_heads, head_dim, float(scale),
-         _p(rope_cos), _p(rope_sin), _s())
+         _p(rope_cos), _p(rope_sin), _p(mx.q), mx.q.stride(0), _p(mx.s), mx.K, _s())
+    mx.m = S * T
     return dqkv
 
 

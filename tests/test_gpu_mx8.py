@@ -230,3 +230,39 @@ def test_mx8_producers_reject_bad_targets():
         ops().rmsnorm_fwd(x, w, y, rstd, 1e-6, mx=ops().MX8(64, 384, DEV))
     with pytest.raises(ValueError):  # too few rows
         ops().rmsnorm_fwd(x, w, y, rstd, 1e-6, mx=ops().MX8(32, 256, DEV))
+
+
+@pytest.mark.parametrize("S,T,H", [(2, 200, 4), (8, 600, 2)])
+def test_flash_attention_mx8_outputs_equal_quantized_outputs(S, T, H):
+    """Config 5: attention forward / backward with an MXFP8 copy of their stores (the o_proj and the q|k|v
+    dX GEMM operands) write the plain kernels' bf16 outputs, and the copies == quant_mx8 of them, byte for
+    byte (elements + scales); the backward with the fused RoPE as in the step."""
+    import math
+    hd = 128
+    D = H * hd
+    M = S * T
+    qkv = rnd(M, 3 * D)
+    cos, sin = ops().rope_tables(T, hd, 1e4, DEV)
+    scale = 1 / math.sqrt(hd)
+    o_ref, o = (torch.zeros(M, D, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    lse = torch.empty(S * H * T, device=DEV)
+    ops().flash_attn_fwd(qkv, 0, D, 2 * D, o_ref, lse, S, T, H, hd, scale)
+    mx = ops().MX8(M, D, DEV)
+    ops().flash_attn_fwd(qkv, 0, D, 2 * D, o, torch.empty_like(lse), S, T, H, hd, scale, mx=mx)
+    assert torch.equal(o, o_ref)
+    q = ops().quant_mx8(o_ref, ops().MX8(M, D, DEV))
+    assert mx.m == M and torch.equal(mx.q[:M], q.q[:M]) and torch.equal(mx.s, q.s)
+    do = rnd(M, D)
+    delta = torch.empty(S * H * T, device=DEV)
+    dsw = ops().flash_attn_bwd_ws(S, T, H, DEV)
+    g_ref, g = (torch.zeros(M, 3 * D, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o_ref, do, lse, delta, dsw, g_ref, S, T, H, hd, scale,
+                         rope_cos=cos, rope_sin=sin)
+    mx3 = ops().MX8(M, 3 * D, DEV)
+    ops().flash_attn_bwd(qkv, 0, D, 2 * D, o_ref, do, lse, delta, dsw, g, S, T, H, hd, scale,
+                         rope_cos=cos, rope_sin=sin, mx=mx3)
+    assert torch.equal(g, g_ref)
+    q3 = ops().quant_mx8(g_ref, ops().MX8(M, 3 * D, DEV))
+    assert torch.equal(mx3.q[:M], q3.q[:M]) and torch.equal(mx3.s, q3.s)
+    with pytest.raises(RuntimeError):  # the MXFP8 copy needs the 5-product (dS workspace) kernels
+        ops().flash_attn_bwd(qkv, 0, D, 2 * D, o_ref, do, lse, delta, None, g, S, T, H, hd, scale, mx=mx3)
