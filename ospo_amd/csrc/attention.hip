@@ -255,7 +255,7 @@ __device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf1
 }
 
 // ============================================================== forward ====
-template <int NW, int DBG = 0>  // DBG 1: no K/V loads after the first tile (ablation, results invalid)
+template <int NW, int DBG = 0, bool MXO = false>  // MXO: also the MXFP8 copy of O (config 5)
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
                                                        bf16* __restrict__ out, int ldo, float* __restrict__ lse,
                                                        int T, int H, float scale,
@@ -378,8 +378,11 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
     const float inv = 1.f / l_run;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) o[dt] *= inv;
-    store_rows16(o, smem + wave * SCR_BYTES, out + rowbase * ldo + h * HD, ldo, qb * RB + wave * 16, T, lane, mo,
-                 rowbase, h * (HD / 8));
+    if constexpr (MXO)
+      store_rows16(o, smem + wave * SCR_BYTES, out + rowbase * ldo + h * HD, ldo, qb * RB + wave * 16, T, lane, mo,
+                   rowbase, h * (HD / 8));
+    else
+      store_rows16(o, smem + wave * SCR_BYTES, out + rowbase * ldo + h * HD, ldo, qb * RB + wave * 16, T, lane);
     if (qrow < T && g == 0) lse[((long)s * H + h) * T + qrow] = m_run + __logf(l_run);
   }
 }
@@ -665,7 +668,7 @@ __device__ __forceinline__ void wait_tr_ld(TrBatch& t) {
 // before its MFMAs: ~18 % MFMA busy at 2 waves per SIMD).  The first batch of a tile is issued
 // right after the tile barrier.
 // DBG 1 (ablation build): s_memtime sums per wave of the tile phases -> dbg[8 per wave]
-template <int NW, int DBG = 0>
+template <int NW, int DBG = 0, bool MXO = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv3_kernel(
     const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, const bf16* __restrict__ dout, int ldd,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16* __restrict__ dqkv, int ldg, int T, int H,
@@ -1030,9 +1033,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   {
     char* scr = smem + wave * 2 * SCR_BYTES;
     const int key0 = kb * KBW + wave * 16;
-    store_rows16(dk, scr, dqkv + rowbase * ldg + kc + h * HD, ldg, key0, T, lane, mo, rowbase, (kc + h * HD) / 8);
-    store_rows16(dv, scr + SCR_BYTES, dqkv + rowbase * ldg + vc + h * HD, ldg, key0, T, lane, mo, rowbase,
-                 (vc + h * HD) / 8);
+    if constexpr (MXO) {
+      store_rows16(dk, scr, dqkv + rowbase * ldg + kc + h * HD, ldg, key0, T, lane, mo, rowbase, (kc + h * HD) / 8);
+      store_rows16(dv, scr + SCR_BYTES, dqkv + rowbase * ldg + vc + h * HD, ldg, key0, T, lane, mo, rowbase,
+                   (vc + h * HD) / 8);
+    } else {
+      store_rows16(dk, scr, dqkv + rowbase * ldg + kc + h * HD, ldg, key0, T, lane);
+      store_rows16(dv, scr + SCR_BYTES, dqkv + rowbase * ldg + vc + h * HD, ldg, key0, T, lane);
+    }
   }
 }
 
@@ -1329,7 +1337,7 @@ __device__ __forceinline__ void stage32(const bf16* base, int ld, int row0, int 
 // barrier (every wave's stage-kt pieces landed, every wave done reading slot kt - 1), refill slot kt - 1
 // with stage kt + 3, then 16 MFMAs per wave from 10 transposed fragments.  Same accumulation order as
 // the 2-slot kernel (keys ascending, 32 per MFMA), so bit-identical.
-template <int NW>
+template <int NW, bool MXO = false>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ring_kernel(const bf16* __restrict__ qkv, int ldq, int qc,
                                                                int kc, const bf16* __restrict__ dsT, int ds_ld,
                                                                bf16* __restrict__ dqkv, int ldg, int T, int H,
@@ -1408,8 +1416,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ring_kernel(const bf16* _
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
     if (rcs) rope_apply(dq[a], rr[a]);
-    store_rows16(dq[a], smem + (wave * 2 + a) * SCR_BYTES, dqkv + rowbase * ldg + qc + h * HD, ldg,
-                 qb * RB + wave * 32 + 16 * a, T, lane, mo, rowbase, (qc + h * HD) / 8);
+    if constexpr (MXO)
+      store_rows16(dq[a], smem + (wave * 2 + a) * SCR_BYTES, dqkv + rowbase * ldg + qc + h * HD, ldg,
+                   qb * RB + wave * 32 + 16 * a, T, lane, mo, rowbase, (qc + h * HD) / 8);
+    else
+      store_rows16(dq[a], smem + (wave * 2 + a) * SCR_BYTES, dqkv + rowbase * ldg + qc + h * HD, ldg,
+                   qb * RB + wave * 32 + 16 * a, T, lane);
   }
 }
 
@@ -1471,6 +1483,12 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
 #else
   auto kfn = attn_fwd_kernel<8, 0>;
 #endif
+  if (mo.q) {
+#ifdef OSPO_ABLATION
+    if (dbg || nw != 8) return OSPO_ERR_UNSUPPORTED;  // ablation forms: no MXFP8 copy
+#endif
+    kfn = attn_fwd_kernel<8, 0, true>;
+  }
   hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                      (bf16*)o, ld_o, lse, T, n_heads, scale, mo);
   OSPO_CHECK_LAUNCH();
@@ -1563,7 +1581,8 @@ static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
     if (nwd == 8) dkdv3 = attn_bwd_dkdv3_kernel<8>;
     if (g_attn_stamps) dkdv3 = nwd == 4 ? attn_bwd_dkdv3_kernel<4, 1> : attn_bwd_dkdv3_kernel<8, 1>;
     if (dkdv_r2 || dkdv_dbg != 0) dkdv3 = nullptr;
-    if (mo.q && (!dkdv3 || getenv("OSPO_ATTN_DQ_2SLOT"))) return OSPO_ERR_UNSUPPORTED;  // ablation kernels: no MX copy
+    if (mo.q && (!dkdv3 || nwd != 4 || g_attn_stamps || getenv("OSPO_ATTN_DQ_2SLOT")))
+      return OSPO_ERR_UNSUPPORTED;  // ablation kernels: no MX copy
 #endif
     const long n_chunks = (long)S * T * n_heads * 16;
     if (n_chunks >= (1L << 31) - 256 * DELTA_CH) return OSPO_ERR_SHAPE;
@@ -1571,6 +1590,7 @@ static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
                        dim3(256), 0, stream, (const bf16*)dout, ld_do, (const bf16*)o, ld_o, delta_ws, T, n_heads,
                        n_chunks);
     OSPO_CHECK_LAUNCH();
+    if (dkdv3 && mo.q) dkdv3 = attn_bwd_dkdv3_kernel<4, 0, true>;  // (the ablation forms are refused above)
     if (dkdv3)
       hipLaunchKernelGGL(dkdv3, dim3(S * n_heads * ((T + 16 * nwd - 1) / (16 * nwd))), dim3(64 * nwd), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                          (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
@@ -1585,8 +1605,9 @@ static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
 #ifdef OSPO_ABLATION
     dq_two_slot = getenv("OSPO_ATTN_DQ_2SLOT") != nullptr;  // A/B: the round-2 2-slot dQ kernel (3-D grid)
 #endif
+    auto dq_ring = mo.q ? attn_bwd_dq_ring_kernel<4, true> : attn_bwd_dq_ring_kernel<4, false>;
     if (!dq_two_slot)
-      hipLaunchKernelGGL(attn_bwd_dq_ring_kernel<4>, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+      hipLaunchKernelGGL(dq_ring, gq, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
                          (const bf16*)ds_ws, p, (bf16*)dqkv, ld_dqkv, T, n_heads, rc, rs, order_dq, mo);
     else
       hipLaunchKernelGGL(attn_bwd_dq_ds_kernel<4>, dim3(n_heads, S, (T + 127) / 128), dim3(256), 0, stream,
