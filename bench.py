@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import statistics
 import math
 import os
 import sys
@@ -82,7 +83,8 @@ def cpu_baseline(Lt=24, N=576, L=30, reps=2):
     full Janus-Pro-7B shapes, fwd + bwd through ALL L decoder layers, gen_head, log-probs and the
     SimPO loss.  The L layers share one layer's frozen weights (aliased dict entries): the
     arithmetic per layer is identical and the 7B-sized weight init on CPU would take longer than
-    the measurement.  Median of ``reps`` timed passes after one untimed warm-up pass."""
+    the measurement.  Median of ``reps`` timed passes after one untimed full-size warm-up pass (the
+    first full-size pass runs ~25 % slower: the round-2 runs measured 10-12 s against 8-9 s for the next)."""
     from oracle import simpo_ref as O
     threads, host_cpus, model = host_cpu_info()
     torch.set_num_threads(threads)
@@ -96,13 +98,13 @@ def cpu_baseline(Lt=24, N=576, L=30, reps=2):
         if k.startswith("layers.0."):
             for i in range(1, L):
                 w[f"layers.{i}." + k[len("layers.0."):]] = w[k]
-    O.simpo_step(text, ch[:, :64], rj[:, :64], w, dims, dtype=torch.bfloat16)  # warm-up (short sequence)
+    O.simpo_step(text, ch, rj, w, dims, dtype=torch.bfloat16)  # warm-up (full size)
     times = []
     for _ in range(reps):
         t0 = time.perf_counter()
         O.simpo_step(text, ch, rj, w, dims, dtype=torch.bfloat16)
         times.append(time.perf_counter() - t0)
-    t_pair = sorted(times)[len(times) // 2]
+    t_pair = statistics.median(times)
     return {"value": round(1.0 / t_pair, 5), "unit": "pairs/s", "cores": threads, "kind": "port",
             "host_cpus": host_cpus, "cpu_model": model,
             "sample": f"1 pair (T={Lt + N}), oracle bf16 fwd+bwd through all {L} full-size 7B decoder layers "
