@@ -370,3 +370,21 @@ def test_decode_gemv_tiled_rejects_unsupported():
     with pytest.raises(RuntimeError):
         ops().decode_gemv(x, ops().tile_decode_weight(w), torch.empty(8, 208, device=DEV).bfloat16(),
                           ws=ops().decode_gemv_ws(8, 208, 256, DEV))
+
+
+def test_generate_tiled_weights_same_tokens():
+    """The sampler on MFMA-tiled decode weights (the default) draws exactly the tokens of the
+    row-major weights, eager and hipGraph."""
+    from ospo_amd.engine import ModelDims
+    from ospo_amd.generate import T2IGenerator
+    dims, w, prompts = _small_case()
+    toks = []
+    for tiled in (True, False):
+        gen = T2IGenerator(ModelDims.from_any(dims), w, device=DEV, max_batch=4, max_prompt_len=16, n_img_tokens=24,
+                           cfg_weight=5.0, temperature=1.0, pad_id=7, tiled_weights=tiled)
+        assert gen.tiled == tiled
+        if tiled:
+            assert any(lw["gu_d"].dim() == 3 for lw in gen.layers)
+        toks.append(gen.generate(prompts, seed=5, use_graph=False).cpu().clone())
+        toks.append(gen.generate(prompts, seed=5, use_graph=True).cpu().clone())
+    assert all(torch.equal(t, toks[0]) for t in toks[1:])
