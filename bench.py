@@ -53,6 +53,25 @@ def synthetic_batch(B, Lt, N, vocab, img_vocab, seed, device):
     return text.to(device), chosen.to(device), rejected.to(device)
 
 
+def simpo_setup(layers=30, lora_r=16, pairs=4, text_len=24, img_tokens=576, lora_dropout=0.05,
+                linear_dtype="bf16", rank=0, device="cuda", wgrad_wgs=0):
+    """The bench's SimPO workload: Janus-Pro-7B-shaped synthetic weights (seed 0, LoRA seed 1, identical
+    on every rank), the engine, and rank's 4 synthetic batches (seeds 1000 * rank + i).  Returns
+    (dims, engine, batches, weights); tests/test_gpu_step.py builds the same workload to check the
+    bench's first-step loss against the oracle."""
+    from ospo_amd.engine import JANUS_PRO_7B, SimPOEngine, synthetic_weights
+    dev = torch.device(device)
+    dims = JANUS_PRO_7B.__class__(**{**JANUS_PRO_7B.__dict__, "n_layers": layers, "lora_r": lora_r,
+                                     "lora_alpha": 2 * lora_r})
+    weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)
+    eng = SimPOEngine(dims, weights, device=dev, max_pairs=pairs, max_text_len=text_len, n_img_tokens=img_tokens,
+                      lora_dropout=lora_dropout, dropout_seed=42, linear_dtype=linear_dtype, wgrad_wgs=wgrad_wgs)
+    # each rank draws its own pairs (the DistributedSampler shard of the global batch)
+    batches = [synthetic_batch(pairs, text_len, img_tokens, dims.vocab, dims.img_vocab, seed=1000 * rank + i,
+                               device=dev) for i in range(4)]
+    return dims, eng, batches, weights
+
+
 def host_cpu_info():
     """(usable CPUs, host CPU count, CPU model).  Usable = the affinity mask, capped by the cgroup
     CPU quota when one is set (a GPU box shows the whole machine in os.cpu_count() but grants a
@@ -373,9 +392,11 @@ def timed_region(step, warmup, steps, barrier, sync, world, device, on_last=None
     barrier()
     sync()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device=device, dtype=torch.float64)
+    t = torch.tensor([dt], dtype=torch.float64)
     if world > 1:
         import torch.distributed as tdist
+        if tdist.get_backend() != "gloo":
+            t = t.to(device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
     return float(t.item()), out
 
@@ -438,6 +459,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--wgrad-wgs", type=int, default=0)  # A/B: LoRA weight grads as ospo_lora_wgrad streams
+    # process-group backend for N > 1: RCCL ("nccl", default on GPUs); "gloo" lets N ranks share one GPU
+    # (the multi-rank rehearsal of tests/test_gpu_dp_overlap.py on a one-GPU box)
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default=None)
     args = ap.parse_args()
     if launch_ranks(args):
         sys.exit(args.child_rc)
@@ -452,35 +476,34 @@ def main():
 
     from ospo_amd import dist as odist
     from ospo_amd import ops
-    from ospo_amd.engine import JANUS_PRO_7B, SimPOEngine, synthetic_weights
     from ospo_amd.simpo import SimPOConfig, SimPOLossBuffers, train_step
 
-    world, rank, local = odist.init()
+    world, rank, local = odist.init(backend=args.backend)
     dev = torch.device("cuda", local)
     backend = "none"
     if world > 1:
         import torch.distributed as tdist
         backend = tdist.get_backend()
-    dims = JANUS_PRO_7B.__class__(**{**JANUS_PRO_7B.__dict__, "n_layers": args.layers, "lora_r": args.lora_r,
-                                     "lora_alpha": 2 * args.lora_r})
     B, Lt, N = args.pairs_per_gpu or default_pairs_per_gpu(world), args.text_len, args.img_tokens
-    weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)  # identical on every rank (same seeds)
-    eng = SimPOEngine(dims, weights, device=dev, max_pairs=B, max_text_len=Lt, n_img_tokens=N,
-                      lora_dropout=args.lora_dropout, dropout_seed=42, linear_dtype=args.linear_dtype,
-                      wgrad_wgs=args.wgrad_wgs)
+    dims, eng, batches, weights = simpo_setup(layers=args.layers, lora_r=args.lora_r, pairs=B, text_len=Lt,
+                                              img_tokens=N, lora_dropout=args.lora_dropout,
+                                              linear_dtype=args.linear_dtype, rank=rank, device=dev,
+                                              wgrad_wgs=args.wgrad_wgs)
     del weights
     torch.cuda.empty_cache()
     cfg = SimPOConfig()
     buf = SimPOLossBuffers(B, dev)
     allreduce = odist.GradAllReduce(world) if world > 1 else None
-    # each rank draws its own pairs (the DistributedSampler shard of the global batch)
-    batches = [synthetic_batch(B, Lt, N, dims.vocab, dims.img_vocab, seed=1000 * rank + i, device=dev)
-               for i in range(4)]
 
     timer = None if args.no_kernel_timer else ops.KernelTimer()
+    first = {}
 
     def step(i):
-        return train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
+        out = train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
+        if not first:  # the first step's loss (fresh weights): tests/test_gpu_step.py reproduces it
+            first["loss"] = out["loss"].clone()
+            first["logps"] = out["logps"].clone()
+        return out
 
     # per-launch HIP events on the last timed step only: an event pair around every GEMM costs ~1 %
     # of the step (128.8 vs 127.5 ms), so recording them on all K steps would depress `value`; one
@@ -491,6 +514,14 @@ def main():
     loss = float(out["loss"].item())
     if not math.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
+    checks = None
+    if world > 1:  # the all-reduced grads and the updated LoRA params must be identical on every rank
+        import torch.distributed as tdist
+        c = torch.stack([eng.grads.double().sum(), eng.grads.double().abs().sum(), eng.lora.double().sum()])
+        c = c.cpu() if backend == "gloo" else c
+        every = [torch.zeros_like(c) for _ in range(world)]
+        tdist.all_gather(every, c)
+        checks = [[float(v) for v in e.cpu()] for e in every]
     if rank != 0:
         return
     global_batch = B * world
@@ -532,6 +563,8 @@ def main():
                    "backend": backend, "algorithmic_tflop_per_pair": round(flops_pair / 1e12, 3)},
         "roofline": roof,
         "loss": round(loss, 5),
+        "loss_first_step": round(float(first["loss"].item()), 6),
+        "rank_checksums": checks,
         "gemm_kernels": {k: {"count": v["count"], "ms": round(v["ms"], 2),
                              "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)} for k, v in kern.items()},
     }

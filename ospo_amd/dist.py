@@ -20,15 +20,22 @@ def env_world():
 
 
 def init(backend: Optional[str] = None):
+    """Join the process group of a torchrun-style launch; returns (world, rank, device index).
+    backend None: RCCL ("nccl") when a GPU is present, else gloo.  With gloo the ranks may share
+    GPUs (device = LOCAL_RANK mod device count): the multi-rank rehearsal on a one-GPU box."""
     world, rank, local = env_world()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "gloo" and torch.cuda.is_available():
+        local = local % max(1, torch.cuda.device_count())
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group(backend, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+            if torch.cuda.is_available():
+                torch.cuda.set_device(local)
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     return world, rank, local

@@ -52,3 +52,16 @@ def step_outputs(z):
 def rel_err(a: torch.Tensor, b: torch.Tensor) -> float:
     a, b = a.double(), b.double()
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def golden_vq_pixels(z, i):
+    """f32 [1, 3, s, s] pixels of vq_golden image i made by ospo_amd.data.VLMImageProcessor from the
+    stored uint8 image -- byte-identical to the reference processor's tensor the golden ids were
+    encoded from (its sha256 is in the golden)."""
+    import hashlib
+    from PIL import Image
+    from ospo_amd.data import VLMImageProcessor
+    u8 = z[f"img{i}_u8"]
+    x = VLMImageProcessor(image_size=u8.shape[0])([Image.fromarray(u8)])["pixel_values"]
+    assert hashlib.sha256(x.numpy().tobytes()).hexdigest() == str(z[f"img{i}_px_sha256"])
+    return x

@@ -6,10 +6,13 @@ Loads ``janus/models/vq_model.py`` from the reference tree (importlib; it depend
 builds ``VQModel(ModelArgs())`` (the VQ-16 gen_vision_model of Janus-Pro), loads the seeded weights of
 ``oracle.vq_ref.init_vq_weights`` into it (no checkpoint exists offline; the decoder keeps its own
 init and is not used) and runs ``encode`` in fp32, eval mode, on example PNGs of the reference
-(``examples/step3/...``): two at 128 px (bicubic) and one at 384 px.
+(``examples/step3/...``): two at 128 px and one at 384 px.  The pixels are the reference's own
+``VLMImageProcessor`` output (``image_processing_vlm.py:127-192`` at image_size 128 / 384, mean = std
+= 0.5; loaded as ``make_golden_image.py`` loads it): bicubic resize, then x/255 in f64 -> f32,
+then (x - 0.5) / 0.5 in f32.
 
-Output ``tests/golden/vq_golden.npz`` (data only): the uint8 pixels actually fed (after resize), the
-weight seed, the reference's indices (``encode(x)[2][2]``, what train.py:257-258 keeps), its
+Output ``tests/golden/vq_golden.npz`` (data only): the uint8 pixels after the processor's resize,
+the sha256 of the f32 pixel tensor the processor made of them, the weight seed, the reference's indices (``encode(x)[2][2]``, what train.py:257-258 keeps), its
 quant_conv output z and the top-2 distance margin per token.
 
 Decoder (step 3, ``image_generation.py:174-181``): with ``oracle.vq_ref.init_vq_decoder_weights(DEC_SEED)``
@@ -19,6 +22,7 @@ into ``tests/golden/vq_decode_golden.npz``.
 """
 from __future__ import annotations
 
+import hashlib
 import importlib.util
 import os
 import sys
@@ -31,6 +35,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 from oracle import vq_ref as V  # noqa: E402
+
+sys.path.insert(0, HERE)
+from make_golden_image import load_reference_processor  # noqa: E402
 
 IMAGES = [("examples/step3/negative/layout/1000003/01.png", 128),
           ("examples/step3/negative/layout/1000005/00.png", 128),
@@ -52,13 +59,17 @@ def main():
     assert all(k.startswith("quantize.codebook_used") for k in missing), missing
     out = {"seed": np.int64(SEED)}
     torch.set_num_threads(8)
+    ip = load_reference_processor()
     for i, (rel, size) in enumerate(IMAGES):
         from PIL import Image
         im = Image.open(os.path.join(REF, rel)).convert("RGB")
-        if im.size != (size, size):
-            im = im.resize((size, size), Image.BICUBIC)
-        u8 = np.asarray(im, dtype=np.uint8).copy()
-        x = (torch.from_numpy(u8).permute(2, 0, 1).float()[None] / 255.0 - 0.5) / 0.5
+        # the reference's own VLMImageProcessor at image_size = size (Janus-Pro mean = std = 0.5)
+        proc = ip.VLMImageProcessor(image_size=size, image_mean=ip.IMAGENET_INCEPTION_MEAN,
+                                    image_std=ip.IMAGENET_INCEPTION_STD, do_normalize=True)
+        u8 = np.ascontiguousarray(proc.resize(im).transpose(1, 2, 0)).astype(np.uint8)
+        x = torch.as_tensor(proc([im])["pixel_values"])
+        assert x.dtype == torch.float32 and tuple(x.shape) == (1, 3, size, size)
+        out[f"img{i}_px_sha256"] = np.array(hashlib.sha256(x.numpy().tobytes()).hexdigest())
         with torch.no_grad():
             h = model.quant_conv(model.encoder(x))
             _, _, info = model.quantize(h)

@@ -383,3 +383,31 @@ def test_tile_decode_weight_layout():
                     for e in (0, 7):
                         assert int(ti[nb, ks, 8 * (16 * g + l16) + e]) == (16 * nb + l16) * K + 32 * ks + 8 * g + e
     assert torch.equal(t, w.flatten()[ti.flatten()].reshape(t.shape))
+
+
+def test_image_processor_equals_reference_processor_bytes():
+    """ospo_amd.data.VLMImageProcessor against the reference's own
+    janus/models/image_processing_vlm.py VLMImageProcessor (resize :127-162, preprocess :164-192,
+    Janus-Pro mean = std = 0.5), run by tests/golden/make_golden_image.py: the f32 pixel tensors
+    are byte-identical on the example PNGs (identity resize) and on a landscape 500x320 image
+    (bicubic downsample + top/bottom padding), a 512x512 image (downsample) and a portrait 200x300
+    image (upsample + left/right padding)."""
+    import hashlib
+    import numpy as np
+    from PIL import Image
+    from ospo_amd.data import VLMImageProcessor
+    from tests import fixtures as FX
+    z = FX.load("image_golden.npz")
+    proc = VLMImageProcessor()
+    names = [str(n) for n in z["names"]]
+    assert len(names) == 8 and sum(not n.endswith(".png") for n in names) == 3
+    for i, name in enumerate(names):
+        if name.endswith(".png"):
+            with Image.open(os.path.join(FX.GOLDEN, name)) as im:
+                img = im.convert("RGB")
+        else:
+            img = Image.fromarray(z[f"in{i}"])
+        x = proc([img])["pixel_values"].numpy()
+        assert x.dtype == np.float32 and x.shape == (1, 3, 384, 384), name
+        np.testing.assert_array_equal(x.reshape(-1)[::331], z[f"px{i}_sample"], err_msg=name)
+        assert hashlib.sha256(x.tobytes()).hexdigest() == str(z[f"px{i}_sha256"]), name

@@ -95,3 +95,31 @@ def test_overlapped_allreduce_equals_post_backward_and_union_batch():
     g_union = _grads(eng, text, chosen, rejected)
     err = rel(res[0][1], g_union)
     assert err < 1e-4, err
+
+
+def test_bench_two_ranks_gloo_share_one_gpu():
+    """The multi-rank bench path the 8-GPU scaling run takes, short of RCCL
+    itself: ``bench.py --gpus 2 --backend gloo`` spawns two ranks on this box's one GPU, each
+    running the real HIP engine (2 layers of Janus-Pro-7B shapes) on 8 pairs (config 3's per-GPU
+    batch) with the LoRA-grad all-reduce overlapped with the backward, times the region with
+    barrier + max over ranks, and prints one JSON line from rank 0.  Both ranks must end with the
+    same all-reduced grads and the same AdamW-updated LoRA params."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--layers", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    ln = lines[0]
+    print("\n" + json.dumps({k: ln[k] for k in ("value", "ms_per_step", "n_gpus", "loss", "rank_checksums")}))
+    assert ln["n_gpus"] == 2 and ln["config"]["backend"] == "gloo" and ln["config"]["parallelism"] == "dp2"
+    assert ln["config"]["pairs_per_gpu"] == 8 and ln["config"]["global_batch"] == 16
+    assert ln["value"] > 0 and ln["loss"] == ln["loss"]
+    c0, c1 = ln["rank_checksums"]
+    assert c0 == c1, (c0, c1)
+    assert c0[1] > 0  # the grads are live

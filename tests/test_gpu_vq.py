@@ -8,6 +8,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from tests import fixtures as FX
+
 from oracle import vq_ref as V
 
 pytestmark = pytest.mark.gpu
@@ -113,8 +115,7 @@ def test_encoder_matches_reference_golden_ids():
     z = np.load(GOLD)
     enc = VQEncoder(V.init_vq_weights(int(z["seed"])), device=DEV)
     for i in range(3):
-        u8 = torch.from_numpy(z[f"img{i}_u8"])
-        x = (u8.permute(2, 0, 1).float()[None] / 255.0 - 0.5) / 0.5
+        x = FX.golden_vq_pixels(z, i)  # the reference processor's pixels (sha256-checked)
         ids, zq, _ = enc.encode(x, return_z=True)
         ref_ids = torch.from_numpy(z[f"img{i}_ids"])
         ref_z = torch.from_numpy(z[f"img{i}_z"])  # [8, h, w]

@@ -5,6 +5,8 @@ import os
 import numpy as np
 import torch
 
+from tests import fixtures as FX
+
 from oracle import vq_ref as V
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "vq_golden.npz")
@@ -15,8 +17,7 @@ def test_vq_oracle_matches_reference_golden():
     w = V.init_vq_weights(int(z["seed"]))
     torch.set_num_threads(max(1, min(8, torch.get_num_threads())))
     for i in range(3):
-        u8 = torch.from_numpy(z[f"img{i}_u8"])
-        x = (u8.permute(2, 0, 1).float()[None] / 255.0 - 0.5) / 0.5
+        x = FX.golden_vq_pixels(z, i)  # the reference processor's pixels (sha256-checked)
         ids, zq, margin = V.encode_ref(x, w)
         assert torch.equal(ids.reshape(-1), torch.from_numpy(z[f"img{i}_ids"]))
         ref = torch.from_numpy(z[f"img{i}_z"])
