@@ -47,11 +47,22 @@ int ospo_abi_version(void);
  * nn.Linear weight layout [out,in]).  A2/B2 is the LoRA K-extension
  * (A2 = scaling * lora_A(x), B2 = block-diagonal lora_B), may be NULL (K2 = 0).
  * Requires N % 256 == 0 (or N % 64 == 0 for N <= 256), K % 64 == 0, K2 % 64 == 0;
- * M arbitrary.  MFMA bf16 (v_mfma_f32_16x16x32_bf16), fp32 accumulation. */
+ * M arbitrary.  MFMA bf16 (v_mfma_f32_16x16x32_bf16), fp32 accumulation.
+ *
+ * Split-K tail (every 256x256 GEMM entry point below): the tiles of the last, partial
+ * round (tiles % CUs) may be split along K into fp32 partial tiles that a fixup launch sums
+ * and epilogues.  ws (16-B aligned, >= ospo_gemm_nt_ws_bytes(M, N, K, K2, mx, tail_split)
+ * bytes) holds the partials; NULL or too small = no split.  The caller owns it; calls
+ * sharing a ws must be stream-ordered.  tail_split: 0 = the library's cost model, 1 = never
+ * split, 2..8 = that split (bounded by one round of pieces and K / 4 K-tiles per piece).
+ * The split changes the order of the fp32 sum only. */
 int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                       const void* A2, int lda2, const void* B2, int ldb2, int K2, float alpha,
                       const void* bias, const void* residual, int ldr, void* C, int ldc,
-                      hipStream_t stream);
+                      int tail_split, void* ws, size_t ws_bytes, hipStream_t stream);
+/* Bytes of split-K workspace a 256x256 GEMM of this shape uses (0: no split); mx = 1 for
+ * ospo_gemm_nt_mx8 (K in fp8 elements). */
+size_t ospo_gemm_nt_ws_bytes(int M, int N, int K, int K2, int mx, int tail_split);
 
 /* ospo_gemm_nt_bf16 (alpha 1, no bias / residual, N % 256 == 0) with the RoPE
  * forward (ospo_rope_fwd semantics: HF rotate-half, bf16 rounding per op) fused
@@ -62,7 +73,7 @@ int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int
 int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                            const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
                            const void* rope_cos, const void* rope_sin, int T, int rope_cols,
-                           hipStream_t stream);
+                           int tail_split, void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* LoRA-dropout backward of a frozen Linear with its adapter (peft lora.Linear,
  * dropout before lora_A): C = A.B^T + mask (.) (A2.B2^T) / (1 - drop_p), with
@@ -71,7 +82,8 @@ int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M
  * dX = dy.W + dropout'(g . A_cat).  N % 256 == 0, K2 > 0, no bias / residual. */
 int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                               const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
-                              unsigned drop_seed, float drop_p, hipStream_t stream);
+                              unsigned drop_seed, float drop_p, int tail_split, void* ws, size_t ws_bytes,
+                              hipStream_t stream);
 
 /* down_proj backward fused with the SwiGLU backward (replaces ospo_gemm_nt_dropout_bf16 into dh +
  * ospo_swiglu_bwd; the autograd of `down_proj(act_fn(gate_proj(x)) * up_proj(x))` in HF
@@ -82,20 +94,12 @@ int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, in
 int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* B, int ldb, int M, int F, int K,
                                  const void* A2, int lda2, const void* B2, int ldb2, int K2,
                                  const void* gu, int ld_gu, void* dgu, int ld_dgu, unsigned drop_seed,
-                                 float drop_p, hipStream_t stream);
+                                 float drop_p, int tail_split, void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* The LoRA dropout mask hash (host copy of the device function): element idx of an
  * adapter input is kept iff the 16-bit half (idx & 1) of ospo_dropout_hash(idx >> 1, seed)
  * is >= p * 2^16 (one hash per two adjacent elements; adapter input widths are even). */
 unsigned ospo_dropout_hash(unsigned idx, unsigned seed);
-
-/* Split-K workspace for the GEMM's tail round (tiles % CUs leftover tiles are split
- * along K into fp32 partial tiles, then summed + epilogued by a fixup launch), registered
- * for the CURRENT device (hipGetDevice): each device has its own, and a GEMM uses the one of
- * the device it runs on.  bytes >= 256 KiB x CU count uses the split everywhere it pays; NULL
- * disables it.  The library keeps the pointer: it must outlive every later GEMM call on that
- * device, and GEMMs sharing it must be stream-ordered. */
-int ospo_gemm_set_workspace(void* ws, size_t bytes);
 
 /* Row count of the tile ospo_gemm_nt_bf16 uses for an M x N output (256 or 64). */
 int ospo_gemm_nt_tile(int M, int N);
@@ -225,6 +229,17 @@ int ospo_gather_rows(const void* src, int ld_src, int S, int T, int t0, int N, i
 int ospo_scatter_rows(const void* src, int S, int T, int t0, int N, int D, void* dst, int ld_dst,
                       int total_rows, hipStream_t stream);
 
+/* Grouped row-vector sums (the logits/* metrics of get_batch_loss_metrics, ospo/wrapper/train.py:441-442,
+ * without the [S, T, V] logits: sum_v logits = z . colsum(W2) + sum(b2)):
+ *   out[g] = (accumulate ? out[g] : 0) + sum_{r < rows_per_group} x[g*rows_per_group + r] . w
+ *            [+ add_scale * add[0] when add != NULL]
+ * x bf16 rows of D (ldx elements apart), w fp32 [D]; D % 8 == 0.  fp32, deterministic order; ws >=
+ * ospo_row_dot_sum_ws_bytes (the per-chunk partials).  Also colsum(W2) = W2^T rows . ones, and sum(b2). */
+size_t ospo_row_dot_sum_ws_bytes(int n_groups, int rows_per_group, int D);
+int ospo_row_dot_sum(const void* x, long ldx, int n_groups, int rows_per_group, int D, const float* w,
+                     const float* add, float add_scale, int accumulate, float* out, void* ws, size_t ws_bytes,
+                     hipStream_t stream);
+
 /* y = bf16(gelu(x)); dx = bf16(dy * gelu'(x_pre)) -- gen_head GELU (modeling_vlm.py:49). */
 int ospo_gelu_fwd(const void* x, void* y, long n, hipStream_t stream);
 int ospo_gelu_bwd(const void* dy, const void* x_pre, void* dx, long n, hipStream_t stream);
@@ -320,7 +335,8 @@ int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, i
                      int M, int N, int K, const void* A2, int lda2, const void* B2, int ldb2, int K2,
                      float alpha, const void* bias, const void* residual, int ldr, void* C, int ldc,
                      const void* rope_cos, const void* rope_sin, int rope_T, int rope_cols,
-                     unsigned drop_seed, float drop_p, hipStream_t stream);
+                     unsigned drop_seed, float drop_p, int tail_split, void* ws, size_t ws_bytes,
+                     hipStream_t stream);
 
 /* ------------------------------------------------------ step-3 T2I decode ---
  * BASELINE config 4 / SURVEY §8f rank 2: the sampling loop of
@@ -357,9 +373,6 @@ int ospo_cfg_sample(const void* logits, int ldl, int V, int B, float cfg_weight,
                     hipStream_t stream);
 int ospo_embed_rows(const int* ids, long n, const void* table, int vocab, int D, void* out, hipStream_t stream);
 int ospo_decode_advance(int* pos_dev, int* step_dev, hipStream_t stream);
-/* Test / A-B knob of the 256x256 GEMMs: 0 = cost-model split of the tail round (default), 2..8 = force
- * that split-K factor on the tail tiles (bounded by K / 4 K-tiles per piece). */
-int ospo_gemm_force_split(int s);
 /* Decode-step fusions of the GEMV split sum with its consumer (bit-identical to the unfused
  * ospo_decode_gemv + consumer; need ospo_decode_gemv_fusable(R, N, K), else OSPO_ERR_UNSUPPORTED):
  * ospo_decode_gemv_kv: q|k|v = X . W^T (W [3 H 128, K]) then RoPE + KV-cache store as ospo_kv_store

@@ -20,15 +20,15 @@ P, I, L, F, Z, U = c_void_p, c_int, c_long, c_float, c_size_t, c_uint
 SIGNATURES = {
     "ospo_abi_version": [],
     "ospo_dropout_hash": [U, U],
-    "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P],
+    "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, I, P, Z, P],
+    "ospo_gemm_nt_ws_bytes": [I, I, I, I, I, I],
     "ospo_gemm_nt_tile": [I, I],
-    "ospo_gemm_nt_dropout_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, U, F, P],
-    "ospo_gemm_nt_swiglu_bwd_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, I, U, F, P],
-    "ospo_gemm_nt_rope_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, P, I, I, P],
+    "ospo_gemm_nt_dropout_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, U, F, I, P, Z, P],
+    "ospo_gemm_nt_swiglu_bwd_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, I, U, F, I, P, Z, P],
+    "ospo_gemm_nt_rope_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, P, I, I, I, P, Z, P],
     "ospo_mx8_scale_bytes": [I, I],
     "ospo_quant_mx8": [P, I, I, I, P, I, P, P],
-    "ospo_gemm_nt_mx8": [P, I, P, P, I, P, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P, P, I, I, U, F, P],
-    "ospo_gemm_set_workspace": [P, Z],
+    "ospo_gemm_nt_mx8": [P, I, P, P, I, P, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P, P, I, I, U, F, I, P, Z, P],
     "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],
     "ospo_gemm_f32acc_bdrop": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, U, F, P],
     "ospo_lora_wgrad": [P, I, I, P, I, I, I, I, I, I, P, I, I, U, F, P],
@@ -52,6 +52,8 @@ SIGNATURES = {
     "ospo_gen_aligner_in": [P, I, P, I, I, P, P, I, P, P],
     "ospo_gather_rows": [P, I, I, I, I, I, I, P, P],
     "ospo_scatter_rows": [P, I, I, I, I, I, P, I, I, P],
+    "ospo_row_dot_sum": [P, L, I, I, I, P, P, F, I, P, P, Z, P],
+    "ospo_row_dot_sum_ws_bytes": [I, I, I],
     "ospo_gelu_fwd": [P, P, L, P],
     "ospo_gelu_bwd": [P, P, P, L, P],
     "ospo_logprob_fwd": [P, I, P, I, I, P, P, P, P],
@@ -73,7 +75,6 @@ SIGNATURES = {
     "ospo_cfg_sample": [P, I, I, I, F, F, P, P, I, P, P, P, P],
     "ospo_embed_rows": [P, L, P, I, I, P, P],
     "ospo_decode_advance": [P, P, P],
-    "ospo_gemm_force_split": [I],
     "ospo_vq_conv2d": [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, P, P, P],
     "ospo_vq_bmm_nt": [P, P, I, I, I, I, P, P],
     "ospo_vq_groupnorm_ws_bytes": [I, I],
@@ -94,7 +95,7 @@ ABLATION_SIGNATURES = {"ospo_set_gemm_variant": [I], "ospo_set_gemv_variant": [I
                        "ospo_set_skinny_variant": [I], "ospo_gemm_set_debug_buffer": [P],
                        "ospo_attn_set_stamps": [P]}
 
-RESTYPES = {"ospo_lora_gdb_ws_bytes": c_size_t, "ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
+RESTYPES = {"ospo_gemm_nt_ws_bytes": c_size_t, "ospo_row_dot_sum_ws_bytes": c_size_t, "ospo_lora_gdb_ws_bytes": c_size_t, "ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 

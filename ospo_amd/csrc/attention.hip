@@ -1444,7 +1444,11 @@ int attn_waves() {
 // dK/dV workgroup of the 5-product backward: 4 waves (64 keys, <= 256 VGPRs), so two workgroups share
 // a CU and their tile barriers interleave (8 waves: one workgroup per CU, both waves of a SIMD in step;
 // 212-217 vs 229-230 us per layer at the step shape, tools/attn_bench.py).  Ablation: OSPO_ATTN_DKDV_WAVES=8.
+#ifdef OSPO_ABLATION
 void* g_attn_stamps = nullptr;  // ablation: dK/dV phase stamps (ospo_attn_set_stamps)
+#else
+constexpr void* g_attn_stamps = nullptr;  // the product library records no stamps
+#endif
 int dkdv_waves() {
 #ifdef OSPO_ABLATION
   static const int nw = [] {

@@ -16,7 +16,9 @@
 //    fusing alpha, bias and the bf16 residual add of the decoder layer.
 //  * The LoRA update x.A^T.B^T*s is one more K segment (A2 = s*u, B2 = packed
 //    block-diagonal lora_B), so the adapter costs Rp/K extra MFMAs, no pass.
+#include <cstdint>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 #include "common.h"
@@ -1831,77 +1833,83 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
   *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(args.C) + (long)m * args.ldc + n0 + c) = o;
 }
 
-// Per-device state: the caller-owned split-K workspace registered for each device (ospo_gemm_set_workspace
-// registers it for the current device) and the device's CU count.  A launch uses the current device's.
+// The device's CU count: an immutable property, read once per device (std::call_once), so the
+// library holds no mutable state -- the split-K workspace comes with every call (SplitOpts).
 constexpr int kMaxDevices = 64;
-struct DeviceState {
-  float* ws = nullptr;
-  size_t ws_bytes = 0;
-  int cus = 0;
-};
-DeviceState g_dev[kMaxDevices];
-int g_force_split = 0;  // test knob: > 0 forces that split of the tail round (still bounded below)
-
-DeviceState& dev_state() {
+int device_cus() {
+  static std::once_flag once[kMaxDevices];
+  static int cus[kMaxDevices];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
-  DeviceState& d = g_dev[dev];
-  if (!d.cus) {
+  std::call_once(once[dev], [dev] {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    d.cus = n;
+    cus[dev] = n;
+  });
+  return cus[dev];
+}
+
+// Per call: the caller's split-K workspace and an optional pinned split of the tail round.
+struct SplitOpts {
+  int split = 0;              // 0: the cost model's choice; 1: no split; 2..8: that split (bounded below)
+  float* ws = nullptr;        // fp32 partial tiles (256 KiB each); NULL: no split
+  size_t ws_bytes = 0;
+};
+
+struct SplitPlan {
+  int dp, split, tail;
+};
+
+// The tail round (tiles % CUs leftover tiles) as pieces of 1/s of a tile: ceil(tail s / cus) waves of T / s,
+// plus the fp32 partials (256 KiB per piece, written here and read by the fixup: ~0.13 us each at ~4 TB/s).
+// T = one tile's K loop, ~1.9 us per bf16 K-tile (2.3 per MX K-tile) at the measured rate.  At most one
+// round of pieces (tail s <= CUs) and as many as ws_bytes holds.
+SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus, int pinned, size_t ws_bytes) {
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  SplitPlan pl{tiles, 1, 0};
+  if (tiles <= cus || pinned == 1) return pl;
+  const int tail = tiles % cus;
+  if (!tail) return pl;
+  const long ws_pieces = (long)(ws_bytes / (65536 * sizeof(float)));
+  const int sp_max = (int)std::min<long>(std::min(std::min(8, ntot / 4), cus / tail), ws_pieces / tail);
+  int split = 1;
+  if (pinned > 1) {
+    split = std::max(1, std::min(pinned, sp_max));
+  } else {
+    const double T = ntot * (mx ? 2.3 : 1.9);
+    double best = T;
+    for (int sp = 2; sp <= sp_max; ++sp) {
+      const double cost = (double)((tail * sp + cus - 1) / cus) / sp * T + 0.13 * tail * sp;
+      if (cost < best - 1e-9) {
+        best = cost;
+        split = sp;
+      }
+    }
   }
-  return d;
+  // (with dropout every extension tile must sit in K-range 0, which applies the mask)
+  const bool drop_ok = !drop || (long)(K2 / BK) * split <= ntot;
+  if (split >= 2 && ntot >= 16 && drop_ok) pl = SplitPlan{tiles - tail, split, tail};
+  return pl;
 }
 
 template <int DBG = 0, bool DROP = false, bool MX = false, int SP = 0>
-int launch_v5(const GemmArgs& a, hipStream_t s, bool allow_split = true) {
+int launch_v5(const GemmArgs& a, hipStream_t s, const SplitOpts& so, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
   if constexpr (SP == 5 || SP >= 7) {  // 32-bit buffer offsets: operands beyond 2 GiB take the generic staging
     if ((long)a.M * a.lda * 2 >= (1L << 31) || (long)a.N * a.ldb * 2 >= (1L << 31))
-      return launch_v5<DBG, DROP, MX, (SP == 5 ? 6 : 1)>(a, s, allow_split);
+      return launch_v5<DBG, DROP, MX, (SP == 5 ? 6 : 1)>(a, s, so, allow_split);
   }
-  const int tm = (a.M + 255) / 256, tn = a.N / 256, tiles = tm * tn;
+  const int tm = (a.M + 255) / 256, tn = a.N / 256;
   const int ntot = (MX ? a.K / 128 : a.K / BK) + a.K2 / BK;
-  DeviceState& ds = dev_state();
-  const int cus = ds.cus;
-  int dp = tiles, split = 1, tail = 0;
-  if (allow_split && tiles > cus) {
-    tail = tiles % cus;
-    // The tail round as pieces of 1/s of a tile: ceil(tail s / cus) waves of T / s, plus the fp32 partials
-    // (256 KiB per piece, written here and read by the fixup: ~0.13 us each at ~4 TB/s).  T = one tile's
-    // K loop, ~1.9 us per bf16 K-tile (2.3 per MX K-tile) at the measured 8-phase rate.  s = 1: a full T.
-    split = 1;
-    if (tail) {
-      const double T = ntot * (MX ? 2.3 : 1.9);
-      double best = T;
-      const int sp_max = std::min(std::min(8, ntot / 4), (int)(ds.ws_bytes / (65536 * sizeof(float)) / tail));
-      for (int sp = 2; sp <= sp_max; ++sp) {
-        const double cost = (double)((tail * sp + cus - 1) / cus) / sp * T + 0.13 * tail * sp;
-        if (cost < best - 1e-9) {
-          best = cost;
-          split = sp;
-        }
-      }
-      if (g_force_split > 0) split = std::max(1, std::min(g_force_split, sp_max));
-    }
-    const size_t need = (size_t)tail * split * 65536 * sizeof(float);
-    // (with dropout every extension tile must sit in K-range 0, which applies the mask)
-    const bool drop_ok = !DROP || (long)(a.K2 / BK) * split <= ntot;
-    if (tail && split >= 2 && ntot >= 16 && drop_ok && ds.ws && need <= ds.ws_bytes) {
-      dp = tiles - tail;
-    } else {
-      split = 1;
-      tail = 0;
-    }
-  }
-  const int grid = dp + tail * split;
-  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP, MX, SP>), dim3(grid), dim3(512), 0, s, a, tm, tn, dp, split,
-                     ds.ws, g_v5_gm);
+  const SplitPlan pl = plan_split(a.M, a.N, ntot, a.K2, MX, DROP, device_cus(), allow_split ? so.split : 1,
+                                  so.ws ? so.ws_bytes : 0);
+  const int grid = pl.dp + pl.tail * pl.split;
+  hipLaunchKernelGGL((gemm_nt_v5_kernel<DBG, DROP, MX, SP>), dim3(grid), dim3(512), 0, s, a, tm, tn, pl.dp, pl.split,
+                     so.ws, g_v5_gm);
   OSPO_CHECK_LAUNCH();
-  if (tail) {
-    hipLaunchKernelGGL(splitk_fixup_kernel, dim3(tail * 32), dim3(256), 0, s, a, tm, tn, dp, split,
-                       (const float*)ds.ws, g_v5_gm);
+  if (pl.tail) {
+    hipLaunchKernelGGL(splitk_fixup_kernel, dim3(pl.tail * 32), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split,
+                       (const float*)so.ws, g_v5_gm);
     OSPO_CHECK_LAUNCH();
   }
   return OSPO_OK;
@@ -1927,27 +1935,27 @@ constexpr int g_gemm_variant = 0;  // the product library runs the default sched
 
 // the bf16 256 x 256 schedule every entry point runs (the ablation build can switch it for A/B)
 template <bool DROP>
-int launch_default(const GemmArgs& a, hipStream_t s) {
+int launch_default(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
 #ifdef OSPO_ABLATION
-  if (g_gemm_variant == 17) return launch_v5<0, DROP>(a, s);
-  if (g_gemm_variant == 14) return launch_v5<0, DROP, false, 1>(a, s);
-  if (g_gemm_variant == 24) return launch_v5<0, DROP, false, 5>(a, s);
-  if (g_gemm_variant == 25) return launch_v5<0, DROP, false, 6>(a, s);
-  if (g_gemm_variant == 26) return launch_v5<0, DROP, false, 7>(a, s);
-  if (g_gemm_variant == 27) return launch_v5<0, DROP, false, 8>(a, s);
-  if (g_gemm_variant == 28) return launch_v5<0, DROP, false, 9>(a, s);
+  if (g_gemm_variant == 17) return launch_v5<0, DROP>(a, s, so);
+  if (g_gemm_variant == 14) return launch_v5<0, DROP, false, 1>(a, s, so);
+  if (g_gemm_variant == 24) return launch_v5<0, DROP, false, 5>(a, s, so);
+  if (g_gemm_variant == 25) return launch_v5<0, DROP, false, 6>(a, s, so);
+  if (g_gemm_variant == 26) return launch_v5<0, DROP, false, 7>(a, s, so);
+  if (g_gemm_variant == 27) return launch_v5<0, DROP, false, 8>(a, s, so);
+  if (g_gemm_variant == 28) return launch_v5<0, DROP, false, 9>(a, s, so);
 #endif
-  return launch_v5<0, DROP, false, 8>(a, s);
+  return launch_v5<0, DROP, false, 8>(a, s, so);
 }
 
 // the MXFP8 256 x 256 schedule (the ablation build can switch it: 17 = 8-phase, 14 = SP1)
 template <bool DROP>
-int launch_mx(const GemmArgs& a, hipStream_t s) {
+int launch_mx(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
 #ifdef OSPO_ABLATION
-  if (g_gemm_variant == 17) return launch_v5<0, DROP, true>(a, s);
-  if (g_gemm_variant == 14) return launch_v5<0, DROP, true, 1>(a, s);
+  if (g_gemm_variant == 17) return launch_v5<0, DROP, true>(a, s, so);
+  if (g_gemm_variant == 14) return launch_v5<0, DROP, true, 1>(a, s, so);
 #endif
-  return launch_v5<0, DROP, true, 8>(a, s);
+  return launch_v5<0, DROP, true, 8>(a, s, so);
 }
 
 // NT tile: 256 x 256 (8-phase, split-K tail) whenever N % 256 == 0, else the 64 x 64 simple kernel.
@@ -1960,9 +1968,11 @@ int pick_nt_tile(int M, int N) {
 
 extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                                  const void* A2, int lda2, const void* B2, int ldb2, int K2, float alpha,
-                                 const void* bias, const void* residual, int ldr, void* C, int ldc,
-                                 hipStream_t stream) {
+                                 const void* bias, const void* residual, int ldr, void* C, int ldc, int tail_split,
+                                 void* ws, size_t ws_bytes, hipStream_t stream) {
   if (!A || !B || !C) return OSPO_ERR_ARG;
+  if (tail_split < 0 || tail_split > 8 || (ws && !aligned16(ws))) return OSPO_ERR_ARG;
+  const SplitOpts so{tail_split, (float*)ws, ws ? ws_bytes : 0};
   if (M <= 0 || N <= 0 || K <= 0 || K % BK || K2 < 0 || K2 % BK || N % 64) return OSPO_ERR_SHAPE;
   if (K2 > 0 && (!A2 || !B2)) return OSPO_ERR_ARG;
   if (lda < K || ldb < K || ldc < N || (lda % 8) || (ldb % 8) || (ldc % 8)) return OSPO_ERR_SHAPE;
@@ -1976,7 +1986,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   const int tile = pick_nt_tile(M, N);
   if (tile == 64) return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
 #ifndef OSPO_ABLATION
-  return launch_v5<0, false, false, 8>(a, stream, true);  // SP8 (4 + 4 refills, buffer-offset staging, 2-tile unroll) + split-K tail
+  return launch_v5<0, false, false, 8>(a, stream, so, true);  // SP8 (4 + 4 refills, buffer-offset staging, 2-tile unroll) + split-K tail
 #else
   switch (g_gemm_variant) {
     // A/B alternatives (tools/gemm_bench.py); results identical, schedules differ
@@ -1984,42 +1994,38 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 2: return launch<2, 4, 5, 4, false, false, EPI_BF16>(a, stream);            // simple, 160 x 256
     case 3: return launch_v3<8, 2, true, true>(a, stream);                           // v3 register-prefetch
     case 4: return launch_v4<8, 3>(a, stream);                                       // v4 BK=32 ring
-    case 5: return launch_v5<0>(a, stream, false);                                   // 8-phase, no split tail
+    case 5: return launch_v5<0>(a, stream, so, false);                                   // 8-phase, no split tail
     // decompositions (results invalid): 10 no loads / 11 no MFMA (simple); 12 no loads / 13 no MFMA (8-phase)
     case 10: return launch<2, 4, 8, 4, false, false, EPI_BF16, 1>(a, stream);
     case 11: return launch<2, 4, 8, 4, false, false, EPI_BF16, 2>(a, stream);
-    case 12: return launch_v5<1>(a, stream, false);
-    case 13: return launch_v5<2>(a, stream, false);
+    case 12: return launch_v5<1>(a, stream, so, false);
+    case 13: return launch_v5<2>(a, stream, so, false);
     // SP schedule (2 phases of 32 MFMAs per K-tile): 14 + split tail, 15 no loads, 16 no MFMA
-    case 14: return launch_v5<0, false, false, 1>(a, stream, true);  // SP1 (2 + 6 refills, generic staging)
-    case 15: return launch_v5<1, false, false, 1>(a, stream, false);
-    case 16: return launch_v5<2, false, false, 1>(a, stream, false);
-    case 18: return launch_v5<0, false, false, 2>(a, stream, true);  // SP without s_setprio
-    case 19: return launch_v5<0, false, false, 3>(a, stream, true);  // SP, refills ahead of the reads
-    case 24: return launch_v5<0, false, false, 5>(a, stream, true);  // SP5: 4 + 4 refills, buffer-offset staging
-    case 25: return launch_v5<0, false, false, 6>(a, stream, true);  // SP, 4 + 4 refills, generic staging
-    case 26: return launch_v5<0, false, false, 7>(a, stream, true);  // SP, 2 + 6 refills, buffer-offset staging
-    case 27: return launch_v5<0, false, false, 8>(a, stream, true);  // SP5 unrolled by 2
-    case 28: return launch_v5<0, false, false, 9>(a, stream, true);  // SP8 + B0 of the next tile read early
-    case 29: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<4, false, false, 8>(d, stream, false); }  // SP8 + stamps
-    case 30: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<5, false, false, 8>(d, stream, false); }  // SP8 + phase stamps
-    case 17: return launch_v5<0>(a, stream, true);                                   // 8-phase + split-K tail
-    default: return launch_v5<0, false, false, 8>(a, stream, true);               // SP8 + split-K tail
+    case 14: return launch_v5<0, false, false, 1>(a, stream, so, true);  // SP1 (2 + 6 refills, generic staging)
+    case 15: return launch_v5<1, false, false, 1>(a, stream, so, false);
+    case 16: return launch_v5<2, false, false, 1>(a, stream, so, false);
+    case 18: return launch_v5<0, false, false, 2>(a, stream, so, true);  // SP without s_setprio
+    case 19: return launch_v5<0, false, false, 3>(a, stream, so, true);  // SP, refills ahead of the reads
+    case 24: return launch_v5<0, false, false, 5>(a, stream, so, true);  // SP5: 4 + 4 refills, buffer-offset staging
+    case 25: return launch_v5<0, false, false, 6>(a, stream, so, true);  // SP, 4 + 4 refills, generic staging
+    case 26: return launch_v5<0, false, false, 7>(a, stream, so, true);  // SP, 2 + 6 refills, buffer-offset staging
+    case 27: return launch_v5<0, false, false, 8>(a, stream, so, true);  // SP5 unrolled by 2
+    case 28: return launch_v5<0, false, false, 9>(a, stream, so, true);  // SP8 + B0 of the next tile read early
+    case 29: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<4, false, false, 8>(d, stream, so, false); }  // SP8 + stamps
+    case 30: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<5, false, false, 8>(d, stream, so, false); }  // SP8 + phase stamps
+    case 17: return launch_v5<0>(a, stream, so, true);                                   // 8-phase + split-K tail
+    default: return launch_v5<0, false, false, 8>(a, stream, so, true);               // SP8 + split-K tail
   }
 #endif
 }
 
-extern "C" int ospo_gemm_force_split(int s) {
-  if (s < 0 || s > 8) return OSPO_ERR_ARG;
-  g_force_split = s;
-  return OSPO_OK;
-}
-
 extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                                       const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
-                                      const void* rope_cos, const void* rope_sin, int T, int rope_cols,
-                                      hipStream_t stream) {
+                                      const void* rope_cos, const void* rope_sin, int T, int rope_cols, int tail_split,
+                                      void* ws, size_t ws_bytes, hipStream_t stream) {
   if (!A || !B || !C || !rope_cos || !rope_sin) return OSPO_ERR_ARG;
+  if (tail_split < 0 || tail_split > 8 || (ws && !aligned16(ws))) return OSPO_ERR_ARG;
+  const SplitOpts so{tail_split, (float*)ws, ws ? ws_bytes : 0};
   if (M <= 0 || N <= 0 || K <= 0 || K % BK || K2 < 0 || K2 % BK || N % 256 || T <= 0) return OSPO_ERR_SHAPE;
   if (rope_cols < 0 || rope_cols % 128 || rope_cols > N) return OSPO_ERR_SHAPE;
   if (K2 > 0 && (!A2 || !B2)) return OSPO_ERR_ARG;
@@ -2035,13 +2041,16 @@ extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int
   a.rope_T = T;
   a.rope_cols = rope_cols;
   // split-K tail fixups apply the RoPE epilogue too
-  return launch_default<false>(a, stream);
+  return launch_default<false>(a, stream, so);
 }
 
 extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                                          const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
-                                         unsigned drop_seed, float drop_p, hipStream_t stream) {
+                                         unsigned drop_seed, float drop_p, int tail_split, void* ws, size_t ws_bytes,
+                                         hipStream_t stream) {
   if (!A || !B || !C || !A2 || !B2) return OSPO_ERR_ARG;
+  if (tail_split < 0 || tail_split > 8 || (ws && !aligned16(ws))) return OSPO_ERR_ARG;
+  const SplitOpts so{tail_split, (float*)ws, ws ? ws_bytes : 0};
   if (drop_p < 0.f || drop_p >= 1.f) return OSPO_ERR_ARG;
   if (M <= 0 || N <= 0 || K <= 0 || K % BK || K2 <= 0 || K2 % BK) return OSPO_ERR_SHAPE;
   if (N % 256) return OSPO_ERR_UNSUPPORTED;
@@ -2052,20 +2061,23 @@ extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, 
   GemmArgs a{(const bf16*)A, (const bf16*)B, (const bf16*)A2, (const bf16*)B2, lda, ldb, lda2, ldb2,
              M, N, K, K2, 1.f, nullptr, nullptr, 0, C, ldc, 1, 0, 0};
   if (drop_p == 0.f)
-    return launch_default<false>(a, stream);
+    return launch_default<false>(a, stream, so);
   if (N & 1) return OSPO_ERR_SHAPE;  // mask pairs (drop_keep) start at even indices
   a.drop_seed = drop_seed;
   a.drop_thresh = drop_threshold(drop_p);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = N;
-  return launch_default<true>(a, stream);
+  return launch_default<true>(a, stream, so);
 }
 
 extern "C" int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* B, int ldb, int M, int F, int K,
                                             const void* A2, int lda2, const void* B2, int ldb2, int K2,
                                             const void* gu, int ld_gu, void* dgu, int ld_dgu, unsigned drop_seed,
-                                            float drop_p, hipStream_t stream) {
+                                            float drop_p, int tail_split, void* ws, size_t ws_bytes,
+                                            hipStream_t stream) {
   if (!A || !B || !gu || !dgu || (K2 > 0 && (!A2 || !B2))) return OSPO_ERR_ARG;
+  if (tail_split < 0 || tail_split > 8 || (ws && !aligned16(ws))) return OSPO_ERR_ARG;
+  const SplitOpts so{tail_split, (float*)ws, ws ? ws_bytes : 0};
   if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && K2 <= 0)) return OSPO_ERR_ARG;
   if (M <= 0 || F <= 0 || K <= 0 || K % BK || K2 < 0 || K2 % BK) return OSPO_ERR_SHAPE;
   if (F % 256) return OSPO_ERR_UNSUPPORTED;
@@ -2083,20 +2095,23 @@ extern "C" int ospo_gemm_nt_swiglu_bwd_bf16(const void* A, int lda, const void* 
   a.ld_gu = ld_gu;
   a.ld_dgu = ld_dgu;
   if (drop_p == 0.f)
-    return launch_default<false>(a, stream);
+    return launch_default<false>(a, stream, so);
   a.drop_seed = drop_seed;
   a.drop_thresh = drop_threshold(drop_p);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = F;
-  return launch_default<true>(a, stream);
+  return launch_default<true>(a, stream, so);
 }
 
 extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const void* B8, int ldb, const void* Bsc,
                                 int M, int N, int K, const void* A2, int lda2, const void* B2, int ldb2, int K2,
                                 float alpha, const void* bias, const void* residual, int ldr, void* C, int ldc,
                                 const void* rope_cos, const void* rope_sin, int rope_T, int rope_cols,
-                                unsigned drop_seed, float drop_p, hipStream_t stream) {
+                                unsigned drop_seed, float drop_p, int tail_split, void* ws, size_t ws_bytes,
+                                hipStream_t stream) {
   if (!A8 || !Asc || !B8 || !Bsc || !C) return OSPO_ERR_ARG;
+  if (tail_split < 0 || tail_split > 8 || (ws && !aligned16(ws))) return OSPO_ERR_ARG;
+  const SplitOpts so{tail_split, (float*)ws, ws ? ws_bytes : 0};
   if (M <= 0 || N <= 0 || K <= 0 || K % 128 || K2 < 0 || K2 % BK) return OSPO_ERR_SHAPE;
   if (N % 256) return OSPO_ERR_UNSUPPORTED;
   if (K2 > 0 && (!A2 || !B2)) return OSPO_ERR_ARG;
@@ -2121,24 +2136,24 @@ extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const 
     a.rope_sn = (const bf16*)rope_sin;
     a.rope_T = rope_T;
     a.rope_cols = rope_cols;
-    return launch_mx<false>(a, stream);
+    return launch_mx<false>(a, stream, so);
   }
   if (drop) {
     a.drop_seed = drop_seed;
     a.drop_thresh = drop_threshold(drop_p);
     a.drop_scale = 1.f / (1.f - drop_p);
     a.drop_ld = N;
-    return launch_mx<true>(a, stream);
+    return launch_mx<true>(a, stream, so);
   }
-  return launch_mx<false>(a, stream);
+  return launch_mx<false>(a, stream, so);
 }
 
-extern "C" int ospo_gemm_set_workspace(void* ws, size_t bytes) {
-  if (bytes && (!ws || !aligned16(ws))) return OSPO_ERR_ARG;
-  DeviceState& d = dev_state();
-  d.ws = (float*)ws;
-  d.ws_bytes = ws ? bytes : 0;
-  return OSPO_OK;
+extern "C" size_t ospo_gemm_nt_ws_bytes(int M, int N, int K, int K2, int mx, int tail_split) {
+  if (M <= 0 || N <= 0 || N % 256 || K <= 0 || K2 < 0 || tail_split < 0 || tail_split > 8) return 0;
+  const int ntot = (mx ? K / 128 : K / BK) + K2 / BK;
+  // with dropout the plan can only shrink (drop_ok), so the plan without it bounds the bytes
+  const SplitPlan pl = plan_split(M, N, ntot, K2, mx != 0, false, device_cus(), tail_split, SIZE_MAX);
+  return (size_t)pl.tail * pl.split * 65536 * sizeof(float);
 }
 
 #ifdef OSPO_ABLATION

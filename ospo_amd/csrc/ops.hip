@@ -7,6 +7,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace {
 
 // block-wide sum for 256-thread blocks
@@ -698,7 +700,78 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ s, bf16* __restrict
 
 inline unsigned blocks(long n, int per = 256) { return (unsigned)((n + per - 1) / per); }
 
+// ---------------------------------------------------- grouped row . vector sums
+// partial[g][c] = sum over rows [c*rpc, min((c+1)*rpc, rpg)) of group g of x[row] . w (fp32, fixed order:
+// each thread its 16-B column chunks of every row, then the block tree); the finish kernel adds a group's
+// partials in chunk order, so the result is deterministic.
+__global__ __launch_bounds__(256) void row_dot_partial_kernel(const bf16* __restrict__ x, long ldx, int rpg, int rpc,
+                                                              int D, const float* __restrict__ w,
+                                                              float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int g = blockIdx.y, c = blockIdx.x;
+  const int r0 = c * rpc, r1 = min(rpg, r0 + rpc);
+  const int nch = D / 8;
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const u32x4* xr = reinterpret_cast<const u32x4*>(x + ((long)g * rpg + r) * ldx);
+    for (int ch = threadIdx.x; ch < nch; ch += 256) {
+      float f[8];
+      unpack8(xr[ch], f);
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + ch * 8);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(w + ch * 8 + 4);
+      acc += f[0] * w0[0] + f[1] * w0[1] + f[2] * w0[2] + f[3] * w0[3] + f[4] * w1[0] + f[5] * w1[1] +
+             f[6] * w1[2] + f[7] * w1[3];
+    }
+  }
+  const float tot = block_sum256(acc, red);
+  if (threadIdx.x == 0) partial[(long)g * gridDim.x + c] = tot;
+}
+
+__global__ void row_dot_finish_kernel(const float* __restrict__ partial, int nc, int G, const float* __restrict__ add,
+                                      float add_scale, int accumulate, float* __restrict__ out) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  float s = accumulate ? out[g] : 0.f;
+  float p = 0.f;
+  for (int c = 0; c < nc; ++c) p += partial[(long)g * nc + c];
+  s += p;
+  if (add) s += add_scale * add[0];
+  out[g] = s;
+}
+
+int row_dot_chunks(int rpg, int D, int* rpc) {
+  const int r = std::max(1, std::min(rpg, 65536 / std::max(D, 1)));  // ~64K elements per workgroup
+  *rpc = r;
+  return (rpg + r - 1) / r;
+}
+
 }  // namespace
+
+extern "C" size_t ospo_row_dot_sum_ws_bytes(int n_groups, int rows_per_group, int D) {
+  if (n_groups <= 0 || rows_per_group <= 0 || D <= 0) return 0;
+  int rpc = 0;
+  const int nc = row_dot_chunks(rows_per_group, D, &rpc);
+  return (size_t)n_groups * nc * sizeof(float);
+}
+
+extern "C" int ospo_row_dot_sum(const void* x, long ldx, int n_groups, int rows_per_group, int D, const float* w,
+                                const float* add, float add_scale, int accumulate, float* out, void* ws,
+                                size_t ws_bytes, hipStream_t st) {
+  if (!x || !w || !out || !ws) return OSPO_ERR_ARG;
+  if (n_groups <= 0 || rows_per_group <= 0 || D <= 0 || D % 8 || ldx < D || ldx % 8) return OSPO_ERR_SHAPE;
+  if (!aligned16(x) || !aligned16(w) || !aligned16(ws)) return OSPO_ERR_ALIGN;
+  if (ws_bytes < ospo_row_dot_sum_ws_bytes(n_groups, rows_per_group, D)) return OSPO_ERR_ARG;
+  if (n_groups > 65535) return OSPO_ERR_SHAPE;
+  int rpc = 0;
+  const int nc = row_dot_chunks(rows_per_group, D, &rpc);
+  hipLaunchKernelGGL(row_dot_partial_kernel, dim3(nc, n_groups), dim3(256), 0, st, (const bf16*)x, ldx,
+                     rows_per_group, rpc, D, w, (float*)ws);
+  OSPO_CHECK_LAUNCH();
+  hipLaunchKernelGGL(row_dot_finish_kernel, dim3(blocks(n_groups)), dim3(256), 0, st, (const float*)ws, nc, n_groups,
+                     add, add_scale, accumulate, out);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
 
 // =================================================================== C ABI
 extern "C" const char* ospo_strerror(int s) {

@@ -166,7 +166,6 @@ class SimPOEngine:
         # fuse_gdb (LoRA r = 16): g = s dy.B and dB += dy^T u of a group in one stream over dy on the main stream
         # (ospo_lora_gdb); the side stream then runs only dA.  Off: g on the main stream, dB with dA on the side.
         self.fuse_gdb = bool(fuse_gdb) and dims.lora_r == 16
-        self._gdb_ws = None
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
             raise ValueError("dadb_splits must be four positive split counts")
         self._side = torch.cuda.Stream(device=self.device, priority=int(side_priority))
@@ -231,6 +230,13 @@ class SimPOEngine:
         self.ds_ws = ops.flash_attn_bwd_ws(S, Tm, H, dev)
         self.dz = z(R, Dg)
         self.dhsel = z(R, D)
+        # fp32 g partials of the fused g / dB stream (ospo_lora_gdb, r = 16), sized once for the capacity
+        # (the size grows with the rows); every group's call fits
+        self._gdb_ws = None
+        if self.layout.r == 16:
+            nb = max(int(ops.query_gdb_ws(Mc, g.nmods, g.Nmod)) for g in self.layout.groups.values()
+                     if g.Nmod % 128 == 0)
+            self._gdb_ws = torch.empty((nb + 15) // 16 * 4, dtype=F32, device=dev)
         # MXFP8 activation operands, one per contraction size (main-stream GEMMs only, reused in order)
         self._mx = {K: ops.MX8(Mc, K, dev) for K in {D, Fd, 2 * Fd, 3 * D}} if self.linear_dtype == "mx8" else {}
 
@@ -313,9 +319,6 @@ class SimPOEngine:
         out = self.gsc2[g.name][par]
         b_off = gbase + g.b_off
         dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
-        ws_bytes = max(int(ops.query_gdb_ws(self.Mk, gg.nmods, gg.Nmod)) for gg in self.layout.groups.values())
-        if self._gdb_ws is None or self._gdb_ws.numel() * 4 < ws_bytes:
-            self._gdb_ws = torch.empty((ws_bytes + 15) // 16 * 4, dtype=F32, device=self.device)
         ops.lora_gdb(dy, BT, u, out, dB, M, self.Mk, g.nmods, g.Nmod, self.scale, ws=self._gdb_ws)
         return out, True
 
@@ -424,21 +427,48 @@ class SimPOEngine:
         position T-1 out (train.py:422 rebinds the logits to [..., :-1, :] when sft_weight > 0).
         Call after forward() and before backward()."""
         S, T, Lt, N, D = self.S, self.T, self.Lt, self.N, self.dims.d_model
-        if not hasattr(self, "_w2sum"):
-            self._w2sum = self.gh_w2.float().sum(0)
-            self._b2sum = self.gh_b2.float().sum()
-        seq = torch.mv(self.zact[: S * N].float(), self._w2sum).view(S, N).sum(1)
-        pos = list(range(Lt - 1)) + ([] if skip_last else [T - 1])
-        if pos:
-            rows = (torch.arange(S, device=self.device)[:, None] * T +
-                    torch.tensor(pos, device=self.device)[None, :]).reshape(-1)
-            hx = self.hf.index_select(0, rows)
-            zp = torch.empty(hx.shape[0], self.dims.gen_head_dim, dtype=BF16, device=self.device)
+        Dg, V, dev = self.dims.gen_head_dim, self.dims.img_vocab, self.device
+        if not hasattr(self, "_w2sum"):  # colsum(W2) = rows of W2^T . 1, sum(b2) (frozen: once)
+            ones = torch.ones(V, dtype=F32, device=dev)
+            self._w2sum = torch.empty(Dg, dtype=F32, device=dev)
+            self._b2sum = torch.empty(1, dtype=F32, device=dev)
+            ops.row_dot_sum(self.gh_w2T, ones, self._w2sum, 1)
+            ops.row_dot_sum(self.gh_b2.view(1, V), ones, self._b2sum, 1)
+        nt = Lt - 1  # text positions 0 .. Lt-2 (position Lt-1 is the first predicting one)
+        nl = 0 if skip_last else 1
+        seq = torch.empty(S, dtype=F32, device=dev)
+        ops.row_dot_sum(self.zact[: S * N], self._w2sum, seq, N, add=self._b2sum, add_scale=float(N + nt + nl))
+        rows = S * (nt + nl)
+        if rows:
+            hx = torch.empty(rows, D, dtype=BF16, device=dev)
+            if nt:
+                ops.gather_rows(self.hf, S, T, 0, nt, hx[: S * nt])
+            if nl:
+                ops.gather_rows(self.hf, S, T, T - 1, 1, hx[S * nt:])
+            zp = torch.empty(rows, Dg, dtype=BF16, device=dev)
             ops.gemm_nt(hx, self.gh_w1, zp, bias=self.gh_b1)
             za = torch.empty_like(zp)
             ops.gelu_fwd(zp, za)
-            seq = seq + torch.mv(za.float(), self._w2sum).view(S, len(pos)).sum(1)
-        return seq + (N + len(pos)) * self._b2sum
+            if nt:
+                ops.row_dot_sum(za[: S * nt], self._w2sum, seq, nt, accumulate=True)
+            if nl:
+                ops.row_dot_sum(za[S * nt:], self._w2sum, seq, 1, accumulate=True)
+        return seq
+
+    def full_logits(self) -> torch.Tensor:
+        """gen_head over EVERY position: bf16 [S, T, V], what the reference's concatenated_forward
+        returns (train.py:356-357, 367-368).  A new tensor; call after forward() (backward() leaves
+        the final hidden state alone).  The loss path never needs it: the N predicting positions'
+        logits are computed in forward() and the logits/* metrics come from logit_sums()."""
+        S, T, Dg, V, dev = self.S, self.T, self.dims.gen_head_dim, self.dims.img_vocab, self.device
+        M = S * T
+        zp = torch.empty(M, Dg, dtype=BF16, device=dev)
+        ops.gemm_nt(self.hf[:M], self.gh_w1, zp, bias=self.gh_b1)
+        za = torch.empty_like(zp)
+        ops.gelu_fwd(zp, za)
+        out = torch.empty(M, V, dtype=BF16, device=dev)
+        ops.gemm_nt(za, self.gh_w2, out, bias=self.gh_b2)
+        return out.view(S, T, V)
 
     # ------------------------------------------------------------ backward
     def zero_grad(self):

@@ -142,7 +142,8 @@ class JanusProPolicy:
         return self._vq
 
     def vq_encode(self, pixels: torch.Tensor) -> torch.Tensor:
-        """f32 [n, 3, 384, 384] -> int32 [n, 576] VQ ids on the device (fp32 encode, exact ids)."""
+        """f32 [n, 3, 384, 384] -> int32 [n, 576] VQ ids on the device (fp32 encode: the ids of the
+        reference's vq_model.py run in fp32, not of its bf16 run)."""
         return self.gen_vision_model.encode(pixels)
 
     def named_lora_parameters(self):

@@ -78,24 +78,41 @@ def _ld(t: torch.Tensor) -> int:
 _GEMM_WS = {}
 
 
-def gemm_workspace(device=None) -> torch.Tensor:
-    """Process-lifetime split-K workspace of the NT GEMM (256 partial tiles = 64 MiB),
-    registered with the library on first use and never freed, so the library's pointer
-    cannot dangle.  One per device; GEMMs are issued on one stream per device."""
+def gemm_ws_bytes(M: int, N: int, K: int, K2: int = 0, mx: bool = False, split: int = 0) -> int:
+    """Split-K workspace bytes a 256x256 GEMM of this shape uses (ospo_gemm_nt_ws_bytes; 0: no split)."""
+    return int(query("ospo_gemm_nt_ws_bytes", M, N, K, K2, int(mx), int(split)))
+
+
+def gemm_workspace(device=None, stream=None) -> torch.Tensor:
+    """The split-K workspace the GEMM wrappers pass when the caller gives none: one per (device,
+    stream), so GEMMs that share it are stream-ordered.  The library splits at most one round of
+    tail pieces (tail x split <= CUs), so CUs x 256 KiB covers every shape; allocated once, on
+    the stream that uses it (the caching allocator reuses freed memory stream-ordered)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    ws = _GEMM_WS.get(dev.index)
+    st = torch.cuda.current_stream(dev) if stream is None else stream
+    key = (dev.index, st.cuda_stream)
+    ws = _GEMM_WS.get(key)
     if ws is None:
-        ws = _GEMM_WS[dev.index] = torch.empty(256 * 65536, dtype=torch.float32, device=dev)
-        with torch.cuda.device(dev):  # ospo_gemm_set_workspace registers for the current device
-            call("ospo_gemm_set_workspace", ws.data_ptr(), ws.numel() * 4)
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        with torch.cuda.stream(st):
+            ws = _GEMM_WS[key] = torch.empty(cus * 65536, dtype=torch.float32, device=dev)
     return ws
 
 
+def _ws_args(ws: Optional[torch.Tensor], device, stream):
+    if ws is None:
+        ws = gemm_workspace(device, stream)
+    _chk(ws, torch.float32, "ws")
+    return ws.data_ptr(), ws.numel() * 4
+
+
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0,
-            bias=None, residual=None, rope=None, dropout=None) -> torch.Tensor:
+            bias=None, residual=None, rope=None, dropout=None, split: int = 0, ws=None) -> torch.Tensor:
     """out[M,N] = bf16(alpha*(a.b^T + a2.b2^T) + bias) [+ residual]  (nn.Linear layout b=[N,K]).
     rope=(cos, sin, T, ncols): RoPE forward fused on output columns < ncols (ospo_gemm_nt_rope_bf16).
-    dropout=(seed, p): the a2.b2^T term is masked like the adapter input's dropout (ospo_gemm_nt_dropout_bf16)."""
+    dropout=(seed, p): the a2.b2^T term is masked like the adapter input's dropout (ospo_gemm_nt_dropout_bf16).
+    split: the tail round's split-K (0 = the library's cost model, 1 = none, 2..8 pinned); ws: the fp32
+    split-K workspace (default: gemm_workspace of the current stream)."""
     for t, n in ((a, "a"), (b, "b"), (out, "out")):
         _chk(t, BF16, n)
     M, K = a.shape
@@ -107,26 +124,27 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
         K2 = a2.shape[1]
         if a2.shape[0] != M or b2.shape != (N, K2):
             raise ValueError("gemm_nt K-extension shape mismatch")
-    if a.device.index not in _GEMM_WS:  # per device (the library keys the workspace by the current device)
-        gemm_workspace(a.device)
     st = torch.cuda.current_stream()
+    wsp, wsb = _ws_args(ws, a.device, st)
     e0 = _TIMER.start(st) if _TIMER is not None else None
     if dropout is not None and dropout[1] > 0:
         if bias is not None or residual is not None or alpha != 1.0 or rope is not None or a2 is None:
             raise ValueError("gemm_nt: dropout needs a2/b2 and excludes bias / residual / alpha / rope")
         call("ospo_gemm_nt_dropout_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K, _p(a2), _ld(a2), _p(b2), _ld(b2),
-             K2, _p(out), _ld(out), int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]), st.cuda_stream)
+             K2, _p(out), _ld(out), int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]), int(split), wsp, wsb,
+             st.cuda_stream)
     elif rope is not None:
         if bias is not None or residual is not None or alpha != 1.0:
             raise ValueError("gemm_nt: rope excludes bias / residual / alpha")
         cos, sin, T, ncols = rope
         call("ospo_gemm_nt_rope_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K,
              _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2,
-             _p(out), _ld(out), _p(cos), _p(sin), int(T), int(ncols), st.cuda_stream)
+             _p(out), _ld(out), _p(cos), _p(sin), int(T), int(ncols), int(split), wsp, wsb, st.cuda_stream)
     else:
         call("ospo_gemm_nt_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K,
              _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2, float(alpha),
-             _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), st.cuda_stream)
+             _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), int(split),
+             wsp, wsb, st.cuda_stream)
     if e0 is not None:
         # algorithmic flops: the frozen product only (the LoRA K-extension is not counted)
         # algorithmic bytes: A, B, C once each (+ the bf16 residual read)
@@ -136,7 +154,7 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
 
 
 def gemm_nt_swiglu_bwd(a: torch.Tensor, b: torch.Tensor, gu: torch.Tensor, dgu: torch.Tensor, *, a2=None, b2=None,
-                       dropout=None) -> torch.Tensor:
+                       dropout=None, split: int = 0, ws=None) -> torch.Tensor:
     """dgu[M, 2F] = SwiGLU backward of dh = bf16(a.b^T + a2.b2^T) (b = down_proj's W^T, [F, K]) at gu [M, 2F],
     without storing dh (ospo_gemm_nt_swiglu_bwd_bf16; bit-identical to gemm_nt(..., dropout) + swiglu_bwd).
     dropout=(seed, p): the a2.b2^T term is masked as in gemm_nt."""
@@ -155,13 +173,12 @@ def gemm_nt_swiglu_bwd(a: torch.Tensor, b: torch.Tensor, gu: torch.Tensor, dgu: 
     seed, p = (0, 0.0) if dropout is None else (int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]))
     if p > 0 and a2 is None:
         raise ValueError("gemm_nt_swiglu_bwd: dropout needs a2/b2")
-    if a.device.index not in _GEMM_WS:  # per device (the library keys the workspace by the current device)
-        gemm_workspace(a.device)
     st = torch.cuda.current_stream()
+    wsp, wsb = _ws_args(ws, a.device, st)
     e0 = _TIMER.start(st) if _TIMER is not None else None
     call("ospo_gemm_nt_swiglu_bwd_bf16", _p(a), _ld(a), _p(b), _ld(b), M, F, K,
          _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2,
-         _p(gu), _ld(gu), _p(dgu), _ld(dgu), seed, p, st.cuda_stream)
+         _p(gu), _ld(gu), _p(dgu), _ld(dgu), seed, p, int(split), wsp, wsb, st.cuda_stream)
     if e0 is not None:
         # algorithmic: the frozen product's flops; bytes A, B once, gu read and dgu written (2F columns each)
         nbytes = 2.0 * (M * K + F * K + 4 * M * F)
@@ -201,7 +218,7 @@ def quant_mx8(x: torch.Tensor, out: MX8) -> MX8:
 
 
 def gemm_nt_mx8(a: MX8, b: MX8, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0, bias=None,
-                residual=None, rope=None, dropout=None) -> torch.Tensor:
+                residual=None, rope=None, dropout=None, split: int = 0, ws=None) -> torch.Tensor:
     """out[M, N] = bf16(alpha*(deq(a).deq(b)^T + a2.b2^T) + bias) [+ residual] on block-scaled fp8 MFMA;
     M = a.m rows (the last quant_mx8), b = the weight [N, K].  rope / dropout as gemm_nt."""
     _chk(out, BF16, "out")
@@ -213,19 +230,18 @@ def gemm_nt_mx8(a: MX8, b: MX8, out: torch.Tensor, *, a2=None, b2=None, alpha: f
         K2 = a2.shape[1]
         if a2.shape[0] != M or b2.shape != (N, K2):
             raise ValueError("gemm_nt_mx8 K-extension shape mismatch")
-    if out.device.index not in _GEMM_WS:  # per device
-        gemm_workspace(out.device)
     cos = sin = None
     T = ncols = 0
     if rope is not None:
         cos, sin, T, ncols = rope
     seed, p = (0, 0.0) if dropout is None else (int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]))
     st = torch.cuda.current_stream()
+    wsp, wsb = _ws_args(ws, out.device, st)
     e0 = _TIMER.start(st) if _TIMER is not None else None
     call("ospo_gemm_nt_mx8", _p(a.q), a.q.stride(0), _p(a.s), _p(b.q), b.q.stride(0), _p(b.s), M, N, K,
          _p(a2), _ld(a2) if a2 is not None else 0, _p(b2), _ld(b2) if b2 is not None else 0, K2, float(alpha),
          _p(bias), _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out),
-         _p(cos), _p(sin), int(T), int(ncols), seed, p, st.cuda_stream)
+         _p(cos), _p(sin), int(T), int(ncols), seed, p, int(split), wsp, wsb, st.cuda_stream)
     if e0 is not None:
         nbytes = 1.0 * (M * K + N * K) + 2.0 * (M * N + (M * N if residual is not None else 0))
         _TIMER.add("gemm_nt_mx8_256x256", 2.0 * M * N * K, e0, st, nbytes)
@@ -425,6 +441,24 @@ def gather_rows(src, S, T, t0, N, dst):
 def scatter_rows(src, S, T, t0, N, dst):
     call("ospo_scatter_rows", _p(src), S, T, t0, N, src.shape[1], _p(dst), _ld(dst), dst.shape[0], _s())
     return dst
+
+
+def row_dot_sum(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, rows_per_group: int, *, add=None,
+                add_scale: float = 1.0, accumulate: bool = False) -> torch.Tensor:
+    """out[g] (fp32) (+)= sum over rows_per_group rows of x (bf16 [G * rows_per_group, D]) of row . w (fp32 [D])
+    [+ add_scale * add[0]] -- ospo_row_dot_sum (deterministic fp32 reduction)."""
+    _chk(x, BF16, "x")
+    _chk(w, torch.float32, "w")
+    _chk(out, torch.float32, "out")
+    R, D = x.shape
+    if R % rows_per_group or out.numel() < R // rows_per_group or w.numel() != D:
+        raise ValueError(f"row_dot_sum: x{tuple(x.shape)} w{tuple(w.shape)} out{tuple(out.shape)} rows {rows_per_group}")
+    G = R // rows_per_group
+    nb = int(query("ospo_row_dot_sum_ws_bytes", G, rows_per_group, D))
+    ws = torch.empty((nb + 15) // 16 * 4, dtype=torch.float32, device=x.device)
+    call("ospo_row_dot_sum", _p(x), _ld(x), G, rows_per_group, D, _p(w), _p(add), float(add_scale), int(accumulate),
+         _p(out), _p(ws), ws.numel() * 4, _s())
+    return out
 
 
 def gelu_fwd(x, y):

@@ -18,7 +18,8 @@ pixel tensors [1, 3, 384, 384], VQ-encoded on the GPU inside ``preprocess_batch`
 images of the step in one encode, train.py:246-261), or as VQ token ids [1, N] (a token cache).
 
 Differences by construction (documented in DESIGN.md):
-  * the VQ encode runs in fp32 (exact ids; the reference's bf16 autocast moves ~10 % of them).
+  * the VQ encode runs in fp32: the ids of the reference's fp32 vq_model.py; its bf16-precision run
+    encodes in bf16 and ~10 % of its ids differ (a documented deviation).
   * the embeddings are assembled inside the fused engine, so preprocess_batch
     returns ids/labels instead of [B, T, D] inputs_embeds.
   * concatenated_forward returns the logits of the N image-token positions (a copy,
@@ -183,7 +184,9 @@ class JanusProTrainWrapper:
         self._buf = SimPOLossBuffers(max(1, self.engine.cap_pairs), self.device)
         self.global_step = 0
         self._logged: Dict[str, float] = {}
-        self._pending: List[Tuple[List[str], torch.Tensor]] = []
+        # name -> (device tensor of one log_dict call, index): only the latest value per name is kept, so a
+        # run that never reads .logged holds one small tensor per log_dict call site, not one per step
+        self._pending: Dict[str, Tuple[torch.Tensor, int]] = {}
         self.trainer = None
         self.log_dir = None
 
@@ -211,10 +214,12 @@ class JanusProTrainWrapper:
     def logged(self) -> Dict[str, float]:
         """The logged scalars as floats (reading them is the only host sync of the logging)."""
         if self._pending:
-            for names, vals in self._pending:
-                for n, v in zip(names, vals.tolist()):
-                    self._logged[n] = v
-            self._pending = []
+            host = {}
+            for n, (vals, i) in self._pending.items():
+                if id(vals) not in host:
+                    host[id(vals)] = vals.tolist()
+                self._logged[n] = host[id(vals)][i]
+            self._pending = {}
         return self._logged
 
     def log(self, name, value, sync_dist: bool = True, **kw):
@@ -226,7 +231,8 @@ class JanusProTrainWrapper:
                              else torch.tensor(float(v), device=self.device)) for v in d.values()])
         if sync_dist:
             odist.all_reduce_mean_(vals)  # one fused all-reduce for all scalars
-        self._pending.append((names, vals))
+        for i, n in enumerate(names):
+            self._pending[n] = (vals, i)
 
     # ------------------------------------------------------------ the step
     def training_step(self, batch, batch_idx):
@@ -299,13 +305,17 @@ class JanusProTrainWrapper:
             "concatenated_text_ids": torch.cat([batch["text_ids"], batch["text_ids"]], 0),
         }
 
-    def concatenated_forward(self, batch):
+    def concatenated_forward(self, batch, return_logits: bool = True):
+        """train.py:345-372: (chosen_logps, rejected_logps, chosen_logits, rejected_logits, chosen_labels), the
+        logits gen_head's [B, T, V] bf16 over every position as the reference returns them (evaluated on
+        request: the loss needs only the N predicting positions, which the engine keeps internally).
+        return_logits=False (get_batch_loss_metrics): the two logits entries are None."""
         len_chosen = batch["chosen_labels"].shape[0]
         all_logps = PolicyLogps.apply(self.model.lora_anchor, self.engine, batch["text_ids"], batch["chosen_ids"],
                                       batch["rejected_ids"])
-        e = self.engine
-        # a copy: the engine's logits buffer becomes d(loss)/d(logits) in backward()
-        logits = e.logits[: e.S * e.N].view(e.S, e.N, -1).clone()
+        if not return_logits:
+            return all_logps[:len_chosen], all_logps[len_chosen:], None, None, batch["chosen_labels"]
+        logits = self.engine.full_logits()  # a new tensor: backward() rewrites only the engine's own buffers
         return (all_logps[:len_chosen], all_logps[len_chosen:], logits[:len_chosen], logits[len_chosen:],
                 batch["chosen_labels"])
 
@@ -339,7 +349,7 @@ class JanusProTrainWrapper:
 
     def get_batch_loss_metrics(self, batch, train_eval: Literal["train", "val"] = "train"):
         prefix = "val" if train_eval == "val" else "train"
-        c, r, _, _, _ = self.concatenated_forward(batch)
+        c, r, _, _, _ = self.concatenated_forward(batch, return_logits=False)
         losses, cr, rr = self.simpo_loss(c, r)
         loss = losses.mean()
         e = self.engine

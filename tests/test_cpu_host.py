@@ -53,16 +53,28 @@ def test_validation_before_launch(lib):
     a = ctypes.addressof(buf)
     # K % 64 != 0
     rc = lib.ospo_gemm_nt_bf16(P(a), 96, P(a), 96, 64, 64, 96, None, 0, None, 0, 0, ctypes.c_float(1.0),
-                               None, None, 0, P(a), 64, None)
+                               None, None, 0, P(a), 64, 0, None, 0, None)
     assert rc == 1
     # misaligned A
     rc = lib.ospo_gemm_nt_bf16(P(a + 2), 64, P(a), 64, 64, 64, 64, None, 0, None, 0, 0, ctypes.c_float(1.0),
-                               None, None, 0, P(a), 64, None)
+                               None, None, 0, P(a), 64, 0, None, 0, None)
     assert rc == 2
     # null output
     rc = lib.ospo_gemm_nt_bf16(P(a), 64, P(a), 64, 64, 64, 64, None, 0, None, 0, 0, ctypes.c_float(1.0),
-                               None, None, 0, None, 64, None)
+                               None, None, 0, None, 64, 0, None, 0, None)
     assert rc == 5
+    # split-K workspace: misaligned, or a tail split outside 0..8
+    rc = lib.ospo_gemm_nt_bf16(P(a), 64, P(a), 64, 64, 256, 64, None, 0, None, 0, 0, ctypes.c_float(1.0),
+                               None, None, 0, P(a), 256, 0, P(a + 4), 4096, None)
+    assert rc == 5
+    rc = lib.ospo_gemm_nt_bf16(P(a), 64, P(a), 64, 64, 256, 64, None, 0, None, 0, 0, ctypes.c_float(1.0),
+                               None, None, 0, P(a), 256, 9, None, 0, None)
+    assert rc == 5
+    # workspace query: M = 4800 x N = 4096 is 304 tiles, a 48-tile tail round that the cost model splits 4
+    # ways on 256 CUs (48 x 4 partial tiles of 256 KiB); a pinned split of 1 needs none
+    assert lib.ospo_gemm_nt_ws_bytes(4800, 4096, 4096, 64, 0, 0) == 48 * 4 * 65536 * 4
+    assert lib.ospo_gemm_nt_ws_bytes(4800, 4096, 4096, 64, 0, 1) == 0
+    assert lib.ospo_gemm_nt_ws_bytes(4096, 4096, 4096, 0, 0, 0) == 0  # exactly one round
     # unknown SimPO loss type -> OSPO_ERR_ARG, like train.py:335-337 raising ValueError
     rc = lib.ospo_simpo_fwd(P(a), 2, ctypes.c_float(10), ctypes.c_float(0.5), ctypes.c_float(0), 7, P(a), P(a),
                             P(a), None)

@@ -61,16 +61,14 @@ def test_gemm_nt_exact_integers(M, N, K):
 def test_gemm_nt_schedule_exact_integers_long_k(M, N, K, K2, split):
     """The default 256x256 schedule over many K-tiles (steady loop), the LoRA extension tiles after the main
     ones, ragged M and split-K tails (workgroups whose K-range starts mid-way): exact on small integers."""
-    from ospo_amd._lib import call
     a, b = ints(M, K, lo=-2, hi=3), ints(N, K, lo=-2, hi=3)
     a2 = ints(M, K2) if K2 else None
     b2 = ints(N, K2) if K2 else None
     out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-    try:
-        call("ospo_gemm_force_split", split)
-        ops().gemm_nt(a, b, out, a2=a2, b2=b2)
-    finally:
-        call("ospo_gemm_force_split", 0)
+    ops().gemm_nt(a, b, out, a2=a2, b2=b2, split=split)
+    # the pinned splits really ran: tail tiles (tiles - 256) x split partial tiles
+    tail = {(4800, 3): 48, (4608, 4): 32}.get((M, split), 0)
+    assert ops().gemm_ws_bytes(M, N, K, K2, split=split) == tail * split * 65536 * 4 or split in (0, 1)
     ref = a.double() @ b.double().T + (a2.double() @ b2.double().T if K2 else 0)
     assert torch.equal(out.float(), bf(ref.float()).float()), (out.float() - ref.float()).abs().max()
 
@@ -662,25 +660,21 @@ def test_clip_adamw_matches_torch():
 def test_gemm_split_tail_equals_unsplit(split):
     """Split-K tail tiles (partials + fixup, RoPE and residual epilogues applied in the fixup) give the
     same bf16 output as the unsplit kernel: exact integers so the fp32 partial order cannot matter."""
-    from ospo_amd._lib import call
-    M, H, T, K = 4800, 16, 600, 1024
+    M, H, T, K = 4800, 10, 600, 1024
     D = H * 128
-    N = 3 * D                                     # 19 x 24 = 456 tiles: a tail round of 200 tiles
+    N = 3 * D                                     # 19 x 15 = 285 tiles: a tail round of 29 tiles
     a, b = ints(M, K), ints(N, K, lo=-1, hi=2)
     a2, b2 = ints(M, 64), ints(N, 64, lo=-1, hi=2)
     cos, sin = ops().rope_tables(T, 128, 1e4, DEV)
     res = ints(M, N)
     outs = {}
-    try:
-        for s in (1, split):
-            call("ospo_gemm_force_split", s if s > 1 else 0)   # 0: the cost model keeps this shape unsplit
-            o1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-            ops().gemm_nt(a, b, o1, a2=a2, b2=b2, rope=(cos, sin, T, 2 * D))
-            o2 = torch.empty_like(o1)
-            ops().gemm_nt(a, b, o2, a2=a2, b2=b2, residual=res)
-            outs[s] = (o1, o2)
-    finally:
-        call("ospo_gemm_force_split", 0)
+    for s in (1, split):  # 1: no split
+        o1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops().gemm_nt(a, b, o1, a2=a2, b2=b2, rope=(cos, sin, T, 2 * D), split=s)
+        o2 = torch.empty_like(o1)
+        ops().gemm_nt(a, b, o2, a2=a2, b2=b2, residual=res, split=s)
+        outs[s] = (o1, o2)
+    assert ops().gemm_ws_bytes(M, N, K, 64, split=split) == 29 * split * 65536 * 4  # the split really ran
     ref = torch.empty_like(outs[1][1])
     ops().gemm_nt(a, b, ref, a2=a2, b2=b2)
     ops().rope(ref, 0, D, M // T, T, H, 128, cos, sin)
@@ -695,23 +689,18 @@ def test_gemm_split_tail_equals_unsplit(split):
 def test_gemm_swiglu_bwd_fused_equals_two_launches(M, F, K, K2, p, split):
     """down_proj dX GEMM with the SwiGLU backward in its epilogue (dh never stored) is bit-identical to
     the dh GEMM (+ masked LoRA extension) followed by swiglu_bwd, on the same split-K decisions."""
-    from ospo_amd._lib import call
     seed = 4242
     dy, w = rnd(M, K), rnd(F, K, s=0.05)
     a2 = rnd(M, K2) if K2 else None
     b2 = rnd(F, K2, s=0.05) if K2 else None
     gu = rnd(M, 2 * F, s=2.0)
     dr = (seed, p) if p > 0 else None
-    try:
-        call("ospo_gemm_force_split", split)
-        dh = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
-        ops().gemm_nt(dy, w, dh, a2=a2, b2=b2, dropout=dr)
-        ref = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
-        ops().swiglu_bwd(dh, gu, ref)
-        out = torch.full((M, 2 * F), float("nan"), device=DEV, dtype=torch.bfloat16)
-        ops().gemm_nt_swiglu_bwd(dy, w, gu, out, a2=a2, b2=b2, dropout=dr)
-    finally:
-        call("ospo_gemm_force_split", 0)
+    dh = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(dy, w, dh, a2=a2, b2=b2, dropout=dr, split=split)
+    ref = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    ops().swiglu_bwd(dh, gu, ref)
+    out = torch.full((M, 2 * F), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt_swiglu_bwd(dy, w, gu, out, a2=a2, b2=b2, dropout=dr, split=split)
     assert torch.equal(out, ref)
     # and against an fp32 statement of the op (HF LlamaMLP: h = bf16(silu(g)) * u)
     g, u, d = gu[:, :F].float(), gu[:, F:].float(), dh.float()

@@ -154,8 +154,7 @@ def test_gemm_mx8_rejects_bad_shapes():
 def test_gemm_mx8_split_tail_rope_equals_unsplit():
     """MX8 rope GEMM with a forced split-K tail (RoPE applied in the fixup) == the unsplit kernel, on
     codes whose products are exact (power-of-two scales, small integers)."""
-    from ospo_amd._lib import call
-    M, H, T, K = 4800, 16, 600, 1024
+    M, H, T, K = 4800, 10, 600, 2048  # 19 x 15 = 285 tiles: 29 in the tail round, 17 K-tiles
     D = H * 128
     x = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
     w = torch.randint(-1, 2, (3 * D, K), device=DEV).to(torch.bfloat16)
@@ -164,14 +163,11 @@ def test_gemm_mx8_split_tail_rope_equals_unsplit():
     cos, sin = ops().rope_tables(T, 128, 10000.0, DEV)
     xa, wb = ops().MX8.of(x), ops().MX8.of(w)
     outs = []
-    try:
-        for s in (0, 3):
-            call("ospo_gemm_force_split", s)
-            o = torch.empty(M, 3 * D, device=DEV, dtype=torch.bfloat16)
-            ops().gemm_nt_mx8(xa, wb, o, a2=a2, b2=b2, rope=(cos, sin, T, 2 * D))
-            outs.append(o)
-    finally:
-        call("ospo_gemm_force_split", 0)
+    for s in (1, 3):  # 1: no split
+        o = torch.empty(M, 3 * D, device=DEV, dtype=torch.bfloat16)
+        ops().gemm_nt_mx8(xa, wb, o, a2=a2, b2=b2, rope=(cos, sin, T, 2 * D), split=s)
+        outs.append(o)
+    assert ops().gemm_ws_bytes(M, 3 * D, K, 64, mx=True, split=3) == 29 * 3 * 65536 * 4  # the split really ran
     assert torch.equal(outs[0], outs[1])
 
 

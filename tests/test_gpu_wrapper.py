@@ -153,7 +153,7 @@ def test_wrapper_sft_weight_and_logits_metrics_vs_oracle(tmp_path):
     """algo.sft_weight > 0 (train.py:421-430) and the reference's logits/* logging (mean over all
     [B, T, V] logits, [B, T-1, V] for chosen with sft) through the wrapper, against the oracle."""
     from oracle import simpo_ref as O
-    cfg, model, dl, w = make(tmp_path, extra=["algo.sft_weight=0.5"])
+    cfg, model, dl, w = make(tmp_path, extra=["algo.sft_weight=0.5", "lora.lora_dropout=0.0"])
     batch = next(iter(dl))
     eng = w.engine
     eng.zero_grad()
@@ -171,10 +171,44 @@ def test_wrapper_sft_weight_and_logits_metrics_vs_oracle(tmp_path):
     ref = O.simpo_step(text, pre["chosen_ids"].cpu().long(), pre["rejected_ids"].cpu().long(), wts, dims,
                        dtype=torch.float32, sft_weight=0.5)
     lg = w.logged
-    assert abs(float(loss) - float(ref.loss)) / abs(float(ref.loss)) < 2e-3
+    assert abs(float(loss) - float(ref.loss)) / abs(float(ref.loss)) < 1e-3
     assert lg["train/sft_loss"] == pytest.approx(ref.metrics["sft_loss"], rel=1e-3)
     for k in ("logits/chosen", "logits/rejected"):
         assert lg["train/" + k] == pytest.approx(ref.metrics[k], rel=2e-2, abs=2e-4), k
     g = eng.grad_tensors()
     errs = [FX.rel_err(g[k].cpu(), v) for k, v in ref.lora_grads.items()]
     assert max(errs) < 5e-2
+
+
+def test_concatenated_forward_returns_full_logits(tmp_path):
+    """train.py:345-372: concatenated_forward returns gen_head's logits over EVERY position, [B, T, V]
+    per side, as the reference does (get_batch_loss_metrics itself skips them).  Against the oracle's
+    gen_head over the final hidden state (fp32), and get_batch_logps of those logits reproduces the
+    engine's log-probs (1e-3, north star)."""
+    from oracle import simpo_ref as O
+    from ospo_amd.engine import synthetic_weights
+    cfg, model, dl, w = make(tmp_path, extra=["lora.lora_dropout=0.0"])  # two forwards below: same masks
+    batch = next(iter(dl))
+    pre = w.preprocess_batch(batch)
+    c, r, cl, rl, lab = w.concatenated_forward(pre)
+    e = w.engine
+    B, T, V = e.B, e.T, e.dims.img_vocab
+    assert cl.shape == (B, T, V) and rl.shape == (B, T, V) and cl.dtype == torch.bfloat16
+    assert lab.shape == (B, T)
+    c2, r2, ncl, nrl, _ = w.concatenated_forward(pre, return_logits=False)
+    assert ncl is None and nrl is None and torch.equal(c, c2) and torch.equal(r, r2)
+    lp = w.get_batch_logps(torch.cat([cl, rl]), torch.cat([lab, pre["rejected_labels"]]))
+    assert FX.rel_err(lp.cpu(), torch.cat([c, r]).detach().cpu()) < 1e-3
+    d = e.dims
+    dims = O.JanusDims(n_layers=d.n_layers, d_model=d.d_model, d_ff=d.d_ff, n_heads=d.n_heads, head_dim=d.head_dim,
+                       vocab=d.vocab, img_vocab=d.img_vocab, img_embed=d.img_embed, gen_head_dim=d.gen_head_dim,
+                       lora_r=d.lora_r, lora_alpha=d.lora_alpha)
+    wts = {k: v.cpu().float() for k, v in synthetic_weights(d, "cuda", seed=0, lora_seed=1).items()}
+    text = [t.to(torch.int32) for t in batch[1]]
+    bt = O.preprocess_batch(text, pre["chosen_ids"].cpu().long(), pre["rejected_ids"].cpu().long(), wts,
+                            torch.float32)
+    cb = O.concatenated_inputs(bt)
+    with torch.no_grad():
+        ref = O.gen_head(O.llama_hidden(cb["concatenated_inputs_embeds"], wts, dims, training=False), wts)
+    got = torch.cat([cl, rl]).float().cpu()
+    assert FX.rel_err(got, ref) < 2e-2  # bf16 logits of a bf16 path vs fp32

@@ -76,9 +76,7 @@ def main():
                 call("ospo_set_gemm_variant", 0)
                 res.setdefault("v0_dropout", []).append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(77, 0.05))))
             for sp in SPLITS:
-                call("ospo_gemm_force_split", sp)
-                res[f"split{sp}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2)))
-            call("ospo_gemm_force_split", 0)
+                res[f"split{sp}"].append(timeit(lambda: ops.gemm_nt(a, b, out, a2=a2, b2=b2, split=sp)))
         exp = a.float() @ b.float().t() + (a2.float() @ b2.float().t() if k2 else 0)
         errs, same = {}, {}
         call("ospo_set_gemm_variant", 0)
