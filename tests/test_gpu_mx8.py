@@ -146,7 +146,8 @@ def test_gemm_mx8_rejects_bad_shapes():
     out = torch.empty(64, 256, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(ValueError):  # K % 128
         call("ospo_gemm_nt_mx8", a.q.data_ptr(), 256, a.s.data_ptr(), b.q.data_ptr(), 256, b.s.data_ptr(), 64, 256,
-             200, None, 0, None, 0, 0, 1.0, None, None, 0, out.data_ptr(), 256, None, None, 0, 0, 0, 0.0, None)
+             200, None, 0, None, 0, 0, 1.0, None, None, 0, out.data_ptr(), 256, None, None, 0, 0, 0, 0.0, 0, None, 0,
+             None)
     with pytest.raises(ValueError):  # MX8 operand K mismatch
         ops().gemm_nt_mx8(a, ops().MX8.of(rnd(256, 384)), out)
 
