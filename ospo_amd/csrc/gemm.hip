@@ -1915,6 +1915,499 @@ int launch_v5(const GemmArgs& a, hipStream_t s, const SplitOpts& so, bool allow_
   return OSPO_OK;
 }
 
+#ifdef OSPO_ABLATION
+// ----------------------------------------------------------------------------
+// v6 (ablation build only, variant 32; rejected): the SP8 schedule as a PERSISTENT kernel with the epilogue
+// inside the ping-pong.  Bit-identical to v5 on every epilogue, but 0.2-4 % slower on the step shapes and
+// 20-30 % on single-round ones (profiles/r03/rejected/gemm_v6_persistent_ab.jsonl).
+//
+// v5 runs one work unit (a 256 x 256 tile, or a split-K piece of a tail tile) per workgroup: each
+// unit pays a prologue (the first K-tiles' DMA, ~1.8 us) and an LDS-staged epilogue (accumulators ->
+// LDS ~2 us, 16-B row stores ~2.2 us, ~10 us with a residual) during which no MFMA runs -- ~15 % of a
+// 4096-deep unit.  Here gridDim.x <= CUs workgroups walk the same unit list (virtual id v = blockIdx.x
+// + k * gridDim.x, mapped to tiles exactly as v5 maps blockIdx, so the XCD placement is unchanged):
+//  * the LDS ring runs on across units: the last two K-tiles of a unit stage the next unit's first
+//    two (the v5 prologue pattern), so a unit starts with its operands landed;
+//  * the epilogue stores straight from the accumulators (8-B bf16 / 16-B fp32 stores per lane, no
+//    LDS, no barrier), each wave group in its own R section right after its last M section, so it
+//    overlaps the other group's MFMAs;
+//  * the B fragments of a wave are columns {n * 64 + wn * 16 + 0..15} of each B half (v5: wn * 32 +
+//    n * 16): a head's RoPE partner columns d and d + 64 sit in the same lane, so the RoPE epilogue
+//    needs no exchange.
+// Every output element gets the same MFMA operands in the same K order as v5: results are
+// bit-identical (the split-K partial tiles and their fixup are v5's).
+// The first wait after an epilogue keeps the standard count (vmcnt counts loads, stores and LDS-DMA together
+// in issue order; the epilogue's stores sit between the next unit's B(1) and A(1) pieces, so the count is
+// stricter there -- it also waits for the older stores -- never looser).
+
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));  // the buffer-intrinsic 8-B operand
+
+// byte offset of the 16-B piece (h, i) of a lane in a main K-tile-0 half (rows clamped, chunks XOR-swizzled);
+// a device function: the same code as a lambda called from another lambda loses the kernel's host stub
+__device__ __forceinline__ uint32_t v6_voff(const GemmArgs& args, int um0, int un0, int h, int i, int wave, int rr8,
+                                            int c8) {
+  const bool isA = h < 2;
+  const int row = (h & 1) * 128 + (wave * 2 + i) * 8 + rr8;
+  const int g = min((isA ? um0 : un0) + row, isA ? args.M - 1 : args.N - 1);
+  return (uint32_t)g * (uint32_t)(isA ? args.lda : args.ldb) * 2u + ((c8 ^ rr8) << 4);
+}
+
+// RES: the residual-add epilogue (o / down projections); else the plain / RoPE one (one instance each keeps
+// the register allocation of the other's epilogue out of the loop).
+template <bool DROP, bool RES>
+__global__ __launch_bounds__(512) void gemm_nt_v6_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
+                                                         int split, float* __restrict__ ws, int GM, int n_units) {
+  constexpr int HALF = 16384, SLOT = 4 * HALF;  // half order in a slot: A0 A1 B0 B1
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool g1 = wave >= 4;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int rr8 = lane >> 3, c8 = lane & 7;
+  const int frow = lane & 15, fcol = lane >> 4;
+  const int nt1 = args.K / BK, nt2 = args.K2 / BK, ntot = nt1 + nt2;
+  const int Mlast = args.M - 1, Nlast = args.N - 1;
+  const int G = gridDim.x;
+
+  // ---- the unit list (v5's blockIdx mapping)
+  int v = blockIdx.x;
+  if (v >= n_units) return;
+  int m0, n0, tb, nt, part;
+  auto unit_of = [&](int vv, int& um0, int& un0, int& utb, int& unt, int& upart) {
+    upart = -1;
+    if (vv < dp) {
+      const int xcd = vv & 7, slot = vv >> 3, q = dp >> 3, r = dp & 7;
+      const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+      v5_tile(L, tiles_m, tiles_n, um0, un0, GM);
+      utb = 0;
+      unt = ntot;
+    } else {
+      const int u = vv - dp, z = u % split;
+      upart = u;
+      v5_tile(dp + u / split, tiles_m, tiles_n, um0, un0, GM);
+      utb = (int)((long)ntot * z / split);
+      unt = (int)((long)ntot * (z + 1) / split) - utb;
+    }
+  };
+  unit_of(v, m0, n0, tb, nt, part);
+
+  // ---- staging: buffer_load ... lds from per-lane offsets (main tiles), global_load_lds (extension tiles)
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)args.A, 0, (int)(((long)Mlast * args.lda + args.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)args.B, 0, (int)(((long)Nlast * args.ldb + args.K) * 2), 0x00020000);
+  // lane-derived values re-derived from an opaque copy of the lane id where used, so the compiler
+  // cannot hoist per-lane 64-bit addresses out of the unit loop (they would be spilled)
+  auto opaque_lane = [&]() __attribute__((always_inline)) {
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    return l;
+  };
+  uint32_t voff[4][2];  // the current unit's main-tile offsets (the next unit's are computed where used)
+  auto make_voff = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) voff[h][i] = v6_voff(args, m0, n0, h, i, wave, rr8, c8);
+  };
+  make_voff();
+  auto abs_t = [&](int utb, int tl) {
+    const int q = utb + tl;
+    return DROP ? (q < nt2 ? nt1 + q : q - nt2) : q;
+  };
+  // one half-tile (2 pieces per wave) of local tile tl of a unit into slot parity par; CUR: the current
+  // unit (precomputed offsets), else the unit at (um0, un0)
+  // (CUR is a plain bool, constant after inlining: a generic lambda here loses the kernel's host stub)
+  auto stage_piece = [&](bool CUR, int um0, int un0, int utb, int tl, int h, int par)
+      __attribute__((always_inline)) {
+    char* dst = smem + par * SLOT + h * HALF;
+    const int t = abs_t(utb, tl);
+    if (t < nt1) {
+      int ol = 0;
+      if (!CUR) ol = opaque_lane();
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (LDS_AS void*)(dst + (wave * 2 + i) * 1024), 16,
+                                                 CUR ? voff[h][i] : v6_voff(args, um0, un0, h, i, wave, (ol >> 3) & 7, ol & 7),
+                                                 t * 128, 0, 0);
+    } else {
+      const int ol = opaque_lane(), rr8 = (ol >> 3) & 7, c8 = ol & 7;
+      const bool isA = h < 2;
+      const bf16* base = isA ? args.A2 : args.B2;
+      const int ld = isA ? args.lda2 : args.ldb2;
+      const int k0 = (t - nt1) * BK;
+      const int row0 = (isA ? um0 : un0) + (h & 1) * 128;
+      const int last = isA ? Mlast : Nlast;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int p = wave * 2 + i;
+        const int g = min(row0 + p * 8 + rr8, last);
+        glds16(base + (long)g * ld + k0 + ((c8 ^ rr8) << 3), dst + p * 1024);
+      }
+    }
+  };
+
+  f32x4 acc[4][4][2];
+  bf16x8 af[4][2];
+  bf16x8 bsp[2][2][2];  // [B half][n][k-substep]: the whole K-tile's B fragments
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // ---- prologue of the first unit: tile 0 complete, B0 B1 of tile 1 in flight (v5 BAL)
+  int gb = 0;  // global index of the current unit's tile 0 (slot parity of its tile t = (gb + t) & 1)
+  stage_piece(true, m0, n0, tb, 0, 2, 0);
+  stage_piece(true, m0, n0, tb, 0, 3, 0);
+  stage_piece(true, m0, n0, tb, 0, 0, 0);
+  stage_piece(true, m0, n0, tb, 0, 1, 0);
+  if (nt > 1) {
+    stage_piece(true, m0, n0, tb, 1, 2, 1);
+    stage_piece(true, m0, n0, tb, 1, 3, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (g1) {  // the ping-pong offset
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  for (;;) {
+    const int vn = v + G;
+    const bool has_next = vn < n_units;
+    int m0n = 0, n0n = 0, tbn = 0, ntn = 0, partn = -1;
+    if (has_next) {
+      unit_of(vn, m0n, n0n, tbn, ntn, partn);
+    }
+    zero_acc();
+
+    // one K-tile = 2 phases of 32 MFMAs per wave (v5 run_tile_sp5).  ST: t+1, t+2 are main tiles of this
+    // unit (constant waits, fast staging, no branch); PAR: slot parity of tile t when known (else -1).
+    auto run_tile = [&](int t, auto steady, auto parity) __attribute__((always_inline)) {
+      constexpr bool ST = decltype(steady)::value;
+      constexpr int PAR = decltype(parity)::value;
+      const int par = PAR >= 0 ? PAR : ((gb + t) & 1);
+      const char* slot = smem + par * SLOT;
+      // tiles t+1 / t+2 in the concatenated sequence: this unit's, else the next unit's first two
+      const bool n1 = ST || t + 1 < nt || has_next;
+      const bool n2 = ST || t + 2 < nt || (has_next && t + 2 - nt < ntn);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const char* la = slot + p * HALF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            af[i][s] = *reinterpret_cast<const bf16x8*>(la + mmaj_off(wm * 64 + i * 16 + frow, 4 * s + fcol));
+        if (p == 0) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int s = 0; s < 2; ++s)
+                bsp[h][n][s] = *reinterpret_cast<const bf16x8*>(slot + (2 + h) * HALF +
+                                                                 mmaj_off(n * 64 + wn * 16 + frow, 4 * s + fcol));
+        }
+        // refills: A0 A1 of tile t+1 in R(t,0), B0 B1 of tile t+2 in R(t,1)
+        if (ST) {
+          if (p == 0) {
+            stage_piece(true, m0, n0, tb, t + 1, 0, PAR >= 0 ? 1 - PAR : 1 - par);
+            stage_piece(true, m0, n0, tb, t + 1, 1, PAR >= 0 ? 1 - PAR : 1 - par);
+          } else {
+            stage_piece(true, m0, n0, tb, t + 2, 2, par);
+            stage_piece(true, m0, n0, tb, t + 2, 3, par);
+          }
+        } else {
+          if (p == 0 && n1) {
+            if (t + 1 < nt) {
+              stage_piece(true, m0, n0, tb, t + 1, 0, 1 - par);
+              stage_piece(true, m0, n0, tb, t + 1, 1, 1 - par);
+            } else {
+              stage_piece(false, m0n, n0n, tbn, t + 1 - nt, 0, 1 - par);
+              stage_piece(false, m0n, n0n, tbn, t + 1 - nt, 1, 1 - par);
+            }
+          }
+          if (p == 1 && n2) {
+            if (t + 2 < nt) {
+              stage_piece(true, m0, n0, tb, t + 2, 2, par);
+              stage_piece(true, m0, n0, tb, t + 2, 3, par);
+            } else {
+              stage_piece(false, m0n, n0n, tbn, t + 2 - nt, 2, par);
+              stage_piece(false, m0n, n0n, tbn, t + 2 - nt, 3, par);
+            }
+          }
+        }
+        // counted waits: p 0 -> A1(t) (8 newer: B(t+1), A(t+1)); 
+        // p 1 -> A0 B of t+1 (6 newer: A1(t+1), B(t+2))
+        auto waits = [&]() __attribute__((always_inline)) {
+          if (ST) {
+            if (p == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          } else {
+            if (p == 0) {
+              // tile 0 after an epilogue: its EPI_STORES stores sit between B(1) and A(1)
+              if (n1 && t == 0 && gb > 0) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // 8 + EPI_STORES
+              else wait_vmcnt_exact(n1 ? 8 : 0);
+            }
+            if (p == 1 && n1) wait_vmcnt_exact(n2 ? 6 : 2);
+          }
+        };
+        if (g1) waits();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int j = 2 * p + q;  // p 0: quadrants j 0 (ia 0, ib 0), 1 (0, 1); p 1: j 2 (1, 1), 3 (1, 0)
+          const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int s = 0; s < 2; ++s)
+                acc[j][i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bsp[ib][n][s], af[i][s], acc[j][i][n], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if (!g1) waits();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    };
+    using PRT = std::integral_constant<int, -1>;
+    using STT = std::integral_constant<bool, true>;
+    using STF = std::integral_constant<bool, false>;
+    // with dropout the extension tiles come first (tb == 0); their masked sum is scaled between the loops
+    const int pre = (DROP && tb == 0) ? (nt2 < nt ? nt2 : nt) : 0;
+    int t = 0;
+    for (; t < pre; ++t) run_tile(t, STF{}, PRT{});
+    if (t == 0) run_tile(t++, STF{}, PRT{});  // tile 0 waits with the previous epilogue's stores counted
+    if (DROP && pre > 0) {
+      const int ol = opaque_lane(), gq = ol >> 4, lq = ol & 15;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ia = (j >= 2) ? 1 : 0;
+        const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const uint32_t m = (uint32_t)(m0 + ia * 128 + wm * 64 + i * 16 + lq);
+            const uint32_t c = (uint32_t)(n0 + ib * 128 + n * 64 + wn * 16 + 4 * gq);
+            bool keep[4];
+            drop_keep_pairs<2>(m * (uint32_t)args.drop_ld + c, args.drop_seed, args.drop_thresh, keep);  // c % 4 == 0
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[j][i][n][e] *= keep[e] ? args.drop_scale : 0.f;
+          }
+      }
+    }
+    // steady tiles: t+1 and t+2 are main tiles of this unit (non-dropout: the extension tiles come last)
+    const int main_lim = DROP ? nt : min(nt, max(0, nt1 - tb));
+    if (((gb + t) & 1) && t < main_lim - 2) run_tile(t++, STT{}, PRT{});
+    for (; t + 1 < main_lim - 2; t += 2) {
+      run_tile(t, STT{}, std::integral_constant<int, 0>{});
+      run_tile(t + 1, STT{}, std::integral_constant<int, 1>{});
+    }
+    for (; t < main_lim - 2; ++t) run_tile(t, STT{}, PRT{});
+    for (; t < nt; ++t) run_tile(t, STF{}, PRT{});
+
+    // ---- epilogue: straight from the accumulators (lane: row m0 + ia*128 + wm*64 + i*16 + l16, columns
+    // n0 + ib*128 + n*64 + wn*16 + 4g .. +3), no LDS, no barrier.  Every wave issues exactly EPI_STORES (32)
+    // stores, unconditionally (bf16 rows >= M: buffer stores past num_records, dropped), and waits for all of its
+    // epilogue loads before its last store: the next unit's first wait counts them (run_tile).
+    {
+      const int ol = opaque_lane(), g = ol >> 4, l16 = ol & 15;
+      if (part >= 0) {  // split-K piece: the raw fp32 partial tile [256][256] (v5's layout)
+        float* wt = ws + (long)part * 65536;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ia = (j >= 2) ? 1 : 0;
+          const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int ml = ia * 128 + wm * 64 + i * 16 + l16;
+              const int nl = ib * 128 + n * 64 + wn * 16 + 4 * g;
+              *reinterpret_cast<f32x4*>(wt + ml * 256 + nl) = acc[j][i][n];
+            }
+        }
+      } else {
+        const __amdgpu_buffer_rsrc_t rsC =
+            __builtin_amdgcn_make_buffer_rsrc(args.C, 0, (int)((long)args.M * args.ldc * 2), 0x00020000);
+        auto st8 = [&](int m, int c, uint2 v) __attribute__((always_inline)) {
+          u32x2v w;
+          w.x = v.x;
+          w.y = v.y;
+          __builtin_amdgcn_raw_buffer_store_b64(w, rsC, (uint32_t)m * (uint32_t)args.ldc * 2u + (uint32_t)c * 2u, 0, 0);
+        };
+        if (!RES && n0 < args.rope_cols) {
+          // RoPE on the bf16-rounded products (HF rotate-half, per-op bf16 rounding as v5's epilogue): the
+          // partner of head column d < 64 (n = 0) is d + 64 (n = 1), same lane.  cos / sin tables [T][64].
+          uint2 cw[2][4], sw[2][4];
+#pragma unroll
+          for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int m = min(m0 + ia * 128 + wm * 64 + i * 16 + l16, Mlast);
+              const int tt = m % args.rope_T;
+              cw[ia][i] = *reinterpret_cast<const uint2*>(args.rope_cs + (long)tt * 64 + wn * 16 + 4 * g);
+              sw[ia][i] = *reinterpret_cast<const uint2*>(args.rope_sn + (long)tt * 64 + wn * 16 + 4 * g);
+            }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ia = (j >= 2) ? 1 : 0;
+            const int ib = (j == 1 || j == 2) ? 1 : 0;
+            const bool rope_half = n0 + ib * 128 < args.rope_cols;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int m = m0 + ia * 128 + wm * 64 + i * 16 + l16;
+              const int c = n0 + ib * 128 + wn * 16 + 4 * g;
+              uint2 o1, o2;
+              o1.x = pack2(acc[j][i][0][0], acc[j][i][0][1]);
+              o1.y = pack2(acc[j][i][0][2], acc[j][i][0][3]);
+              o2.x = pack2(acc[j][i][1][0], acc[j][i][1][1]);
+              o2.y = pack2(acc[j][i][1][2], acc[j][i][1][3]);
+              if (rope_half) {
+                const uint32_t x1w[2] = {o1.x, o1.y}, x2w[2] = {o2.x, o2.y};
+                const uint32_t cww[2] = {cw[ia][i].x, cw[ia][i].y}, sww[2] = {sw[ia][i].x, sw[ia][i].y};
+                uint32_t r1w[2], r2w[2];
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                  float r1[2], r2[2];
+#pragma unroll
+                  for (int hh = 0; hh < 2; ++hh) {
+                    const int sh = 16 * hh;
+                    const float x1 = bits2f((x1w[qq] >> sh) & 0xffff), x2 = bits2f((x2w[qq] >> sh) & 0xffff);
+                    const float cf = bits2f((cww[qq] >> sh) & 0xffff), sf = bits2f((sww[qq] >> sh) & 0xffff);
+                    r1[hh] = round_bf(x1 * cf) + round_bf(-x2 * sf);
+                    r2[hh] = round_bf(x2 * cf) + round_bf(x1 * sf);
+                  }
+                  r1w[qq] = pack2(r1[0], r1[1]);
+                  r2w[qq] = pack2(r2[0], r2[1]);
+                }
+                o1 = uint2{r1w[0], r1w[1]};
+                o2 = uint2{r2w[0], r2w[1]};
+              }
+              st8(m, c, o1);
+              st8(m, c + 64, o2);
+            }
+          }
+        } else {
+          // bias (per column) and alpha before the bf16 rounding; the bf16 residual after it (v5's order)
+          float b4[2][2][4];
+#pragma unroll
+          for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                b4[ib][n][e] = args.bias ? bf2f(args.bias[n0 + ib * 128 + n * 64 + wn * 16 + 4 * g + e]) : 0.f;
+          // residual: quadrant j + 1's 8 loads in flight while quadrant j is stored (rows >= M read as 0)
+          u32x2v rv[2][4][2];
+          __amdgpu_buffer_rsrc_t rsR;
+          auto load_res = [&](int j, u32x2v (&r)[4][2]) __attribute__((always_inline)) {
+            const int ia = (j >= 2) ? 1 : 0;
+            const int ib = (j == 1 || j == 2) ? 1 : 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int n = 0; n < 2; ++n) {
+                const int m = m0 + ia * 128 + wm * 64 + i * 16 + l16;
+                const int c = n0 + ib * 128 + n * 64 + wn * 16 + 4 * g;
+                r[i][n] = __builtin_amdgcn_raw_buffer_load_b64(
+                    rsR, (uint32_t)m * (uint32_t)args.ldr * 2u + (uint32_t)c * 2u, 0, 0);
+              }
+          };
+          if (RES) {
+            rsR = __builtin_amdgcn_make_buffer_rsrc((void*)args.res, 0, (int)((long)args.M * args.ldr * 2),
+                                                    0x00020000);
+            load_res(0, rv[0]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ia = (j >= 2) ? 1 : 0;
+            const int ib = (j == 1 || j == 2) ? 1 : 0;
+            if (RES) {
+              if (j < 3) load_res(j + 1, rv[(j + 1) & 1]);
+              // quadrant j's loads done: newer are (j > 0) quadrant j-1's 8 stores and (j < 3) quadrant j+1's loads
+              if (j == 0 || j == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+              else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int n = 0; n < 2; ++n) {
+                const int m = m0 + ia * 128 + wm * 64 + i * 16 + l16;
+                const int c = n0 + ib * 128 + n * 64 + wn * 16 + 4 * g;
+                const f32x4 a4 = acc[j][i][n];
+                uint2 pk;
+                pk.x = pack2(a4[0] * args.alpha + b4[ib][n][0], a4[1] * args.alpha + b4[ib][n][1]);
+                pk.y = pack2(a4[2] * args.alpha + b4[ib][n][2], a4[3] * args.alpha + b4[ib][n][3]);
+                if (RES) {
+                  const u32x2v r = rv[j & 1][i][n];
+                  pk.x = pack2(bits2f(pk.x & 0xffff) + bits2f(r.x & 0xffff), bits2f(pk.x >> 16) + bits2f(r.x >> 16));
+                  pk.y = pack2(bits2f(pk.y & 0xffff) + bits2f(r.y & 0xffff), bits2f(pk.y >> 16) + bits2f(r.y >> 16));
+                }
+                st8(m, c, pk);
+              }
+          }
+        }
+      }
+    }
+    if (!has_next) break;
+    gb += nt;
+    v = vn;
+    m0 = m0n; n0 = n0n; tb = tbn; nt = ntn; part = partn;
+    make_voff();
+  }
+  if (!g1) {  // re-align the barrier count
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+
+template <bool DROP>
+int launch_v6(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
+  if (a.N % 256) return OSPO_ERR_SHAPE;
+  const int ntot = a.K / BK + a.K2 / BK;
+  // v6 needs 32-bit buffer offsets and >= 2 K-tiles per unit, and has no fused SwiGLU-backward epilogue
+  if (a.swg_gu || ntot < 2 || (long)a.M * a.lda * 2 >= (1L << 31) || (long)a.N * a.ldb * 2 >= (1L << 31) ||
+      ((long)a.M + 256) * a.ldc * 2 >= (1L << 31) || (a.res && ((long)a.M + 256) * a.ldr * 2 >= (1L << 31)))
+    return launch_v5<0, DROP, false, 8>(a, s, so);
+  const int tm = (a.M + 255) / 256, tn = a.N / 256;
+  const int cus = device_cus();
+  const SplitPlan pl = plan_split(a.M, a.N, ntot, a.K2, false, DROP, cus, so.split, so.ws ? so.ws_bytes : 0);
+  const int units = pl.dp + pl.tail * pl.split;
+  const int grid = units > cus ? std::max(8, cus / 8 * 8) : units;  // a multiple of 8: v & 7 = blockIdx.x & 7
+  if (!DROP && a.res)  // (the dropout entry point takes no residual)
+    hipLaunchKernelGGL((gemm_nt_v6_kernel<DROP, !DROP>), dim3(grid), dim3(512), 0, s, a, tm, tn, pl.dp, pl.split,
+                       so.ws, g_v5_gm, units);
+  else
+    hipLaunchKernelGGL((gemm_nt_v6_kernel<DROP, false>), dim3(grid), dim3(512), 0, s, a, tm, tn, pl.dp, pl.split,
+                       so.ws, g_v5_gm, units);
+  OSPO_CHECK_LAUNCH();
+  if (pl.tail) {
+    hipLaunchKernelGGL(splitk_fixup_kernel, dim3(pl.tail * 32), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split,
+                       (const float*)so.ws, g_v5_gm);
+    OSPO_CHECK_LAUNCH();
+  }
+  return OSPO_OK;
+}
+#endif  // OSPO_ABLATION
+
 template <int FM, int STAGES, bool REMAP, bool PRIO, int WM = 2, int WN = 4, int FN = 4, int DBG = 0>
 int launch_v3(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
@@ -1944,6 +2437,7 @@ int launch_default(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
   if (g_gemm_variant == 26) return launch_v5<0, DROP, false, 7>(a, s, so);
   if (g_gemm_variant == 27) return launch_v5<0, DROP, false, 8>(a, s, so);
   if (g_gemm_variant == 28) return launch_v5<0, DROP, false, 9>(a, s, so);
+  if (g_gemm_variant == 32) return launch_v6<DROP>(a, s, so);  // persistent SP8 (rejected)
 #endif
   return launch_v5<0, DROP, false, 8>(a, s, so);
 }
@@ -1986,7 +2480,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   const int tile = pick_nt_tile(M, N);
   if (tile == 64) return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
 #ifndef OSPO_ABLATION
-  return launch_v5<0, false, false, 8>(a, stream, so, true);  // SP8 (4 + 4 refills, buffer-offset staging, 2-tile unroll) + split-K tail
+  return launch_v5<0, false, false, 8>(a, stream, so);  // SP8 (4 + 4 refills, buffer-offset staging) + split-K tail
 #else
   switch (g_gemm_variant) {
     // A/B alternatives (tools/gemm_bench.py); results identical, schedules differ
@@ -2014,6 +2508,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 29: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<4, false, false, 8>(d, stream, so, false); }  // SP8 + stamps
     case 30: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<5, false, false, 8>(d, stream, so, false); }  // SP8 + phase stamps
     case 17: return launch_v5<0>(a, stream, so, true);                                   // 8-phase + split-K tail
+    case 32: return launch_v6<false>(a, stream, so);                                  // persistent SP8 (v6, rejected)
     default: return launch_v5<0, false, false, 8>(a, stream, so, true);               // SP8 + split-K tail
   }
 #endif
@@ -2169,7 +2664,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || v > 30 || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23) return OSPO_ERR_ARG;
+  if (v < 0 || v > 32 || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23) return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;

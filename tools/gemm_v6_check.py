@@ -1,5 +1,5 @@
-"""Persistent GEMM (v6, the default schedule) against the one-unit-per-workgroup SP8 kernel (v5, ablation
-variant 31) on the SimPO step's shapes: bit-equality for every epilogue (plain, bias + residual, RoPE,
+"""Persistent GEMM (v6, ablation variant 32, rejected) against the one-unit-per-workgroup SP8 kernel (v5, the
+default schedule) on the SimPO step's shapes: bit-equality for every epilogue (plain, bias + residual, RoPE,
 dropout-masked extension, pinned split-K tails) and interleaved timings.  Ablation build only.
 One JSON line per case; exits 1 if any case differs."""
 import os as _os; _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "ospo_amd", "libospo_hip_ablation.so"))
@@ -60,29 +60,29 @@ def main():
         if "split" in epi:
             ex["split"] = int(epi[-1])
         outs, times = {}, {}
-        for v in (31, 0):
+        for v in (0, 32):
             call("ospo_set_gemm_variant", v)
             o = torch.full((m, n), float("nan"), device="cuda", dtype=torch.bfloat16)
             ops.gemm_nt(a, b, o, a2=a2, b2=b2, **ex)
             torch.cuda.synchronize()
             outs[v] = o
         for _ in range(ROUNDS):
-            for v in (31, 0):
+            for v in (0, 32):
                 call("ospo_set_gemm_variant", v)
                 o = outs[v]
                 times.setdefault(v, []).append(timeit(lambda: ops.gemm_nt(a, b, o, a2=a2, b2=b2, **ex)))
         call("ospo_set_gemm_variant", 0)
-        same = bool(torch.equal(outs[0], outs[31]))
-        finite = bool(torch.isfinite(outs[0].float()).all())
+        same = bool(torch.equal(outs[32], outs[0]))
+        finite = bool(torch.isfinite(outs[32].float()).all())
         bad += (not same) or (not finite)
         fl = 2.0 * m * n * k
         line = {"case": name, "M": m, "N": n, "K": k, "K2": k2, "epi": epi, "bit_equal_v5": same, "finite": finite}
         if not same:
-            d = (outs[0].float() - outs[31].float()).abs()
+            d = (outs[32].float() - outs[0].float()).abs()
             idx = torch.nonzero(d > 0)
             line["n_diff"] = int(idx.shape[0])
             line["first_diff"] = idx[:4].tolist()
-        for v, lab in ((31, "v5"), (0, "v6")):
+        for v, lab in ((0, "v5"), (32, "v6")):
             t = sorted(times[v])[len(times[v]) // 2]
             line[lab] = {"ms": round(t, 4), "tflops": round(fl / t / 1e9, 1)}
         print(json.dumps(line), flush=True)
