@@ -124,6 +124,17 @@ int ospo_gemm_nt_tile(int M, int N);
  * drop_p > 0 (mode 0): X is masked as ospo_lora_skinny masked it in the forward (index k * N + n). */
 int ospo_lora_wgrad(const void* X, int ldx, int N, const void* S, int lds, int s_cols, int K, int mode, int nmod,
                     int r, float* C, int ldc, int splits, uint32_t drop_seed, float drop_p, hipStream_t stream);
+/* dA of one adapter group (peft lora_A.weight.grad of the q|k|v, o, gate|up or down adapters reached from
+ * ospo/wrapper/train.py:352; replaces the K-major ospo_gemm_f32acc(_bdrop) product):
+ *   C[j * ldc + n] += sum_k S[k][j] . dropout(X)[k][n]      j < s_cols <= 64, n < N
+ * X [K][N] bf16 (ldx), S [K][lds] bf16 (lds 64 or 128; rows past the real tokens zero), K % 64 == 0,
+ * N % 128 == 0, K * ldx * 2 < 2^31.  One stream over X: a workgroup per 128-column stripe and K range
+ * (splits = K ranges per stripe, 1 .. K / 64), fp32 atomics.  drop_p > 0: X masked as ospo_lora_skinny
+ * masked it in the forward (element index k * N + n, drop_keep): from keep_bits when non-NULL (the
+ * forward's ospo_lora_skinny keep-bit output for this X, K * N / 8 bytes; rows it did not write may hold
+ * anything when S is zero there), else by re-hashing. */
+int ospo_lora_da(const void* X, int ldx, int N, const void* S, int lds, int s_cols, int K, float* C, int ldc,
+                 int splits, uint32_t drop_seed, float drop_p, const void* keep_bits, hipStream_t stream);
 int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
                      int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
                      int diag_nblk, int diag_r, hipStream_t stream);
@@ -296,12 +307,15 @@ int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int
  * drop_p > 0 (dense mode only): peft lora_dropout on A -- element (m, k) is kept
  * iff drop_hash(m*K + k, drop_seed) >= drop_p * 2^32 (common.h) and becomes
  * bf16(A / (1 - drop_p)); the masked A is also written to xd [M, ld_xd] when xd
- * is non-NULL (the dA = g^T . dropout(x) operand of the backward). */
+ * is non-NULL (the dA = g^T . dropout(x) operand of the backward).  keep_bits (non-NULL only with
+ * drop_p > 0, lda % 8 == 0 and K % 64 == 0, xd NULL): the keep decision of every element of rows < M as
+ * bits, row-major, 8 per byte -- byte (m*K + k) / 8, bit k % 8 -- which ospo_lora_da reads instead of
+ * re-hashing (M*K/8 bytes). */
 size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles);
 int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out,
                      int K, int n_tiles, int a_koff, int module_tiles, float scale, void* out, int ldo,
                      int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed, float drop_p,
-                     void* xd, int ld_xd, hipStream_t stream);
+                     void* xd, int ld_xd, void* keep_bits, hipStream_t stream);
 
 /* Fused LoRA backward over one stream of dy, LoRA rank 16 (replaces ospo_lora_skinny's g plus the
  * dB = dy^T u ospo_gemm_f32acc of the same group; ospo/wrapper/train.py:352 through peft lora.Linear's

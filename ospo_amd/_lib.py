@@ -32,6 +32,7 @@ SIGNATURES = {
     "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],
     "ospo_gemm_f32acc_bdrop": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, U, F, P],
     "ospo_lora_wgrad": [P, I, I, P, I, I, I, I, I, I, P, I, I, U, F, P],
+    "ospo_lora_da": [P, I, I, P, I, I, I, P, I, I, U, F, P, P],
     "ospo_f32_to_bf16": [P, P, L, F, P],
     "ospo_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "ospo_rmsnorm_bwd": [P, P, P, P, P, P, I, I, P],
@@ -63,7 +64,7 @@ SIGNATURES = {
     "ospo_lora_pack": [P, P, I, I, I, I, I, P, P, P, P, I, L, P],
     "ospo_lora_gdb": [P, I, P, I, P, I, I, I, I, I, F, P, I, I, P, P, Z, P],
     "ospo_lora_gdb_ws_bytes": [I, I, I],
-    "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, U, F, P, I, P],
+    "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, U, F, P, I, P, P],
     "ospo_lora_skinny_ws_bytes": [I, I, I],
     "ospo_decode_gemv_ws_bytes": [I, I, I],
     "ospo_decode_gemv_fusable": [I, I, I],

@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
                                                       int M, int M_out, int K, int kper, int a_koff, int tiles_total,
                                                       float scale, bf16* __restrict__ out, int ldo, int out_cols,
                                                       float* __restrict__ ws, int M_pad, uint32_t dseed,
-                                                      uint32_t dthresh, float dscale) {
+                                                      uint32_t dthresh, float dscale, uint8_t* __restrict__ kbits) {
   using C = Sk3Cfg<NT>;
   __shared__ __attribute__((aligned(16))) char smem[C::NS * C::STAGE];
   const int lane = threadIdx.x & 63;
@@ -401,6 +401,12 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
         drop_keep_pairs<4>(drow + k0, dseed, dthresh, keep);
 #pragma unroll
         for (int e = 0; e < 8; ++e) av[e] = keep[e] ? f2bf(bf2f(av[e]) * dscale) : f2bf(0.f);
+        if (kbits && m0 + arow_l < M) {  // the keep bits, one byte per 8 columns (bit e = column k0 + e)
+          uint32_t byte = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) byte |= (keep[e] ? 1u : 0u) << e;
+          kbits[(drow + k0) >> 3] = (uint8_t)byte;
+        }
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[j] = MFMA(bok[j] ? b[s][j] : bf16x8{}, av, acc[j]);  // D[16j+4g+q][m]
@@ -582,6 +588,190 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// dA of one adapter group as ONE stream over its input (round 3; replaces the 64 x 64 f32-atomic tiles):
+//   dA[j][n] += sum_m g_s[m][j] * dropout(x)[m][n]        j < s_cols (the used rank rows), n < N
+// (peft lora_A.weight.grad; the backward of train.py:352's adapters).  A workgroup owns a 128-column
+// stripe of x and a range of 64-row K-tiles (tokens); x [64 x 128] and g_s [64 x 64] tiles stream through
+// an NS-stage LDS ring by LDS-DMA from launch-constant per-lane offsets (the K advance in soffset, counted
+// vmcnt, raw s_barrier: nothing drains the ring -- the f32-atomic tile kernel's transposed-read builtin made
+// hipcc wait vmcnt(0) before every read, serialising its loads).  Both MFMA operands are transposed reads
+// (the contraction runs over rows), inline asm with tied waits.  With dropout the x fragments are masked in
+// registers by the forward's hash, one hash per two elements: partner lanes (columns n, n ^ 1 share a hash)
+// each hash half of the fragment's 8 rows and swap halves by DPP.  Split partials meet in fp32 atomics,
+// 64-B segments (D[j][n] with n along the lanes).
+constexpr int DA_TN = 128;                 // x columns per workgroup (32 per wave)
+constexpr int DA_XB = 64 * DA_TN * 2;      // x tile bytes (64 rows of 256 B)
+constexpr int DA_SB = 64 * 128;            // g_s tile bytes (64 rows x 64 rank columns)
+constexpr int DA_STG = DA_XB + DA_SB;
+constexpr int DA_NS = 3;                   // ring stages (72 KiB: two workgroups per CU)
+constexpr int DA_PW = (DA_STG / 1024) / 4; // LDS-DMA pieces per wave per stage (6)
+
+// x image row r (256 B = 16 chunks): logical chunk c at physical c ^ da_swz(r); the 16 rows one
+// transposed read touches (8g + q, q < 4) get 16 distinct values
+__device__ __forceinline__ int da_swz(int r) { return (r & 3) | (((r >> 3) & 3) << 2); }
+
+__device__ __forceinline__ void da_lds16(__amdgpu_buffer_rsrc_t rs, char* dst, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ void da_lds4(__amdgpu_buffer_rsrc_t rs, char* dst, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 4, voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ void tr2_wait(i16x4& a, i16x4& b) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)::"memory");
+}
+
+// the keep bits of a lane's x fragment: column n (even lanes n even), rows m0 .. m0 + 7
+__device__ __forceinline__ void da_keep8(uint32_t m0, uint32_t n, uint32_t ld, uint32_t seed, uint32_t thr, bool odd,
+                                         bool (&keep)[8]) {
+  uint32_t mine[4], other[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {  // even lane: rows 0..3, odd lane: rows 4..7 (the pair's shared hashes)
+    const uint32_t idx = (m0 + (uint32_t)q + (odd ? 4u : 0u)) * ld + n;
+    mine[q] = drop_hash(idx >> 1, seed);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) other[q] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine[q], 0xB1, 0xF, 0xF, false);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t h = (e < 4) ? (odd ? other[e] : mine[e]) : (odd ? mine[e - 4] : other[e - 4]);
+    keep[e] = (odd ? (h >> 16) : (h & 0xffffu)) >= thr;
+  }
+}
+
+// DM: 0 no dropout, 1 mask re-hashed, 2 mask from the forward's keep bits (staged with the tile: 64 rows x
+// 16 B, one 4-B LDS-DMA per wave)
+template <int NJ, int DM>
+__global__ __launch_bounds__(256) void lora_da_kernel(const bf16* __restrict__ X, int ldx, int x_bytes,
+                                                      const bf16* __restrict__ S, int lds, int s_bytes, int s_cols,
+                                                      int nt, float* __restrict__ C, int ldc, uint32_t dseed,
+                                                      uint32_t dthresh, float dscale, int drop_ld,
+                                                      const uint8_t* __restrict__ kbits, int k_bytes) {
+  constexpr bool DROP = DM > 0;
+  constexpr int STG = DA_STG + (DM == 2 ? 1024 : 0);
+  constexpr int PW = DA_PW + (DM == 2 ? 1 : 0);
+  __shared__ __attribute__((aligned(16))) char smem[DA_NS * STG];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4, q4 = l16 >> 2, p4 = l16 & 3;
+  const int n0 = blockIdx.x * DA_TN;
+  const int t0 = (int)((long)nt * blockIdx.y / gridDim.y), t1 = (int)((long)nt * (blockIdx.y + 1) / gridDim.y);
+  const int n_my = t1 - t0;
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc((void*)S, 0, s_bytes, 0x00020000);
+  // per-lane byte offsets of this wave's pieces at K-tile 0: x pieces = 4 rows x 256 B (4 per wave),
+  // g_s pieces = 8 rows x 128 B (2 per wave); the K-tile's 64 rows advance in soffset
+  uint32_t vx[4], vs[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 4 + (lane >> 4), pc = lane & 15;
+    vx[i] = ((uint32_t)row * (uint32_t)ldx + (uint32_t)n0 + (uint32_t)((pc ^ da_swz(row)) * 8)) * 2u;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3), pc = lane & 7;
+    vs[i] = ((uint32_t)row * (uint32_t)lds + (uint32_t)((pc ^ (row & 7)) * 8)) * 2u;
+  }
+  const int xstep = 64 * ldx * 2, sstep = 64 * lds * 2;  // bytes per K-tile (host: < 2^31 in total)
+  // keep bits: row 16 wave + lane / 4, dword lane % 4 of the stripe's 16 bytes
+  const __amdgpu_buffer_rsrc_t rsK =
+      __builtin_amdgcn_make_buffer_rsrc((void*)kbits, 0, DM == 2 ? k_bytes : 0, 0x00020000);
+  const uint32_t vk = (uint32_t)(16 * wave + (lane >> 2)) * (uint32_t)(drop_ld >> 3) + (uint32_t)(n0 >> 3) +
+                      (uint32_t)((lane & 3) * 4);
+  const int kstep = 64 * (drop_ld >> 3);
+  auto stage = [&](int t, int slot) __attribute__((always_inline)) {
+    char* st = smem + slot * STG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) da_lds16(rsX, st + (wave * 4 + i) * 1024, vx[i], t * xstep);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) da_lds16(rsS, st + DA_XB + (wave * 2 + i) * 1024, vs[i], t * sstep);
+    if constexpr (DM == 2) da_lds4(rsK, st + DA_STG + wave * 256, vk, t * kstep);
+  };
+  f32x4 acc[NJ][2];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int f = 0; f < 2; ++f) acc[j][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < DA_NS - 1; ++i)
+    if (i < n_my) stage(t0 + i, i);
+  const bool odd = (l16 & 1) != 0;
+  for (int i = 0; i < n_my; ++i) {
+    // this wave's pieces of stage i landed (NS - 2 newer stages may stay in flight)
+    if (i + 1 < n_my) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (DA_NS - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of stage i; every wave done reading stage i - 1
+    asm volatile("" ::: "memory");
+    if (i + DA_NS - 1 < n_my) stage(t0 + i + DA_NS - 1, (i + DA_NS - 1) % DA_NS);
+    const char* xs = smem + (i % DA_NS) * STG;
+    const char* ss = xs + DA_XB;
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const int r1 = 32 * sk + 8 * g + q4, r2 = r1 + 4;
+      bf16x8 bx[2], as[NJ];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {  // x columns n0 + 32 wave + 16 f + (0..15): chunks 4 wave + 2 f + (0, 1)
+        const int x = 4 * wave + 2 * f + (p4 >> 1), h = (p4 & 1) << 3;
+        i16x4 lo, hi;
+        tr4_issue(xs + r1 * 256 + ((x ^ da_swz(r1)) << 4) + h, lo);
+        tr4_issue(xs + r2 * 256 + ((x ^ da_swz(r2)) << 4) + h, hi);
+        tr2_wait(lo, hi);
+        const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bx[f] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {  // rank columns 16 j + (0..15): chunks 2 j + (0, 1)
+        const int x = 2 * j + (p4 >> 1), h = (p4 & 1) << 3;
+        i16x4 lo, hi;
+        tr4_issue(ss + r1 * 128 + ((x ^ (r1 & 7)) << 4) + h, lo);
+        tr4_issue(ss + r2 * 128 + ((x ^ (r2 & 7)) << 4) + h, hi);
+        tr2_wait(lo, hi);
+        const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        as[j] = __builtin_bit_cast(bf16x8, v);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DM == 1) {  // lane: column n, rows m .. m + 7 of x
+        const uint32_t m = (uint32_t)((t0 + i) * 64 + 32 * sk + 8 * g);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const uint32_t n = (uint32_t)(n0 + 32 * wave + 16 * f + l16);
+          bool keep[8];
+          da_keep8(m, n, (uint32_t)drop_ld, dseed, dthresh, odd, keep);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bx[f][e] = keep[e] ? f2bf(bf2f(bx[f][e]) * dscale) : f2bf(0.f);
+        }
+      } else if constexpr (DM == 2) {  // the bits of rows 32 sk + 8 g + e, columns 32 wave .. + 31
+        const char* kb = xs + DA_STG + (32 * sk + 8 * g) * 16 + wave * 4;
+        uint32_t w[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[e] = *reinterpret_cast<const uint32_t*>(kb + e * 16);
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            bx[f][e] = ((w[e] >> (16 * f + l16)) & 1u) ? f2bf(bf2f(bx[f][e]) * dscale) : f2bf(0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[j][f] = MFMA(as[j], bx[f], acc[j][f]);  // D[16 j + 4 g + q][n = l16]
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int n = n0 + 32 * wave + 16 * f + l16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int jr = 16 * j + 4 * g + q;
+        if (jr < s_cols) atomicAdd(C + (long)jr * ldc + n, acc[j][f][q]);
+      }
+    }
+}
+
 // out[m][16 mod + c] = bf16(scale * sum_sp ws[mod][sp][m][c]) (m < M; 0 for M <= m < M_out), pad columns 0
 __global__ void gdb_reduce_kernel(const float* __restrict__ ws, int nmods, int nsplit, int Mw, int M, int M_out,
                                   float scale, bf16* __restrict__ out, int ldo, int out_cols) {
@@ -623,6 +813,7 @@ struct SkDropArgs {
   float scale = 0.f;  // > 0: dropout on
   bf16* xd = nullptr;
   int ldxd = 0;
+  uint8_t* bits = nullptr;  // v3 only: the keep bits of every element (row-major, 8 per byte)
 };
 
 #ifdef OSPO_ABLATION
@@ -739,11 +930,11 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   if (dr.scale > 0.f)
     hipLaunchKernelGGL((skinny3_kernel<NT, true>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb, b_rows,
                        (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad,
-                       dr.seed, dr.thresh, dr.scale);
+                       dr.seed, dr.thresh, dr.scale, dr.bits);
   else
     hipLaunchKernelGGL((skinny3_kernel<NT, false>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb, b_rows,
                        (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad, 0u,
-                       0u, 0.f);
+                       0u, 0.f, nullptr);
   OSPO_CHECK_LAUNCH();
   if (splits > 1) {
     const long n = (long)M_out * (out_cols / 4);
@@ -788,7 +979,7 @@ static int launch_skinny(const bf16* a, int lda, const bf16* b, int ldb, int b_r
 extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows, int M, int M_out, int K,
                                 int n_tiles, int a_koff, int module_tiles, float scale, void* out, int ldo,
                                 int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed, float drop_p, void* xd,
-                                int ld_xd, hipStream_t stream) {
+                                int ld_xd, void* keep_bits, hipStream_t stream) {
   if (!A || !Bt || !out || !ws) return OSPO_ERR_ARG;
   if (drop_p < 0.f || drop_p >= 1.f) return OSPO_ERR_ARG;
   SkDropArgs dr;
@@ -802,6 +993,9 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
     dr.scale = 1.f / (1.f - drop_p);
     dr.xd = (bf16*)xd;
     dr.ldxd = ld_xd;
+    dr.bits = (uint8_t*)keep_bits;
+  } else if (keep_bits) {
+    return OSPO_ERR_ARG;  // keep bits are a dropout output
   }
   if (M <= 0 || M_out < M || K <= 0 || n_tiles < 1 || n_tiles > 16 || b_rows <= 0 || a_koff < 0 || module_tiles < 1)
     return OSPO_ERR_SHAPE;
@@ -819,6 +1013,8 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
   const bool sk3_ok = K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
                       (long)(M - 1) * lda * 2 + (long)(nmods * (a_koff > 0 ? a_koff : 0) + K) * 2 < (1L << 31) &&
                       (long)b_rows * ldb * 2 < (1L << 31);
+  if (dr.bits && !(g_skinny_variant == 4 && sk3_ok && out_cols % 4 == 0 && !dr.xd))
+    return OSPO_ERR_UNSUPPORTED;  // the keep-bit output is v3's
   if (g_skinny_variant == 4 && sk3_ok && out_cols % 4 == 0 && !dr.xd) {  // (the masked-copy output is v2's)
     const int nz = a_koff > 0 ? nmods : 1;
     const int nt = a_koff > 0 ? module_tiles : n_tiles;
@@ -919,6 +1115,54 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
   hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)ws,
                      nmods, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+// dA of one adapter group (lora_da_kernel): C [s_cols][N] fp32 += S^T . dropout(X) over K = nt * 64 rows.
+// X [K][N] bf16 (ldx), S [K][lds] bf16 with lds in {64, 128} (the packed g_s; rows the caller zero-padded
+// are zero), splits = K-tile ranges per 128-column stripe (1 .. nt).
+extern "C" int ospo_lora_da(const void* X, int ldx, int N, const void* S, int lds, int s_cols, int K, float* C,
+                            int ldc, int splits, unsigned drop_seed, float drop_p, const void* keep_bits,
+                            hipStream_t stream) {
+  if (!X || !S || !C) return OSPO_ERR_ARG;
+  if (N <= 0 || K <= 0 || K % 64 || N % DA_TN || s_cols <= 0 || s_cols > 64) return OSPO_ERR_SHAPE;
+  if (splits < 1 || splits > K / 64) return OSPO_ERR_SHAPE;
+  if (ldx < N || ldx % 8 || (lds != 64 && lds != 128) || ldc < N) return OSPO_ERR_SHAPE;
+  if ((long)K * ldx * 2 >= (1L << 31) || (long)K * lds * 2 >= (1L << 31)) return OSPO_ERR_SHAPE;  // 32-bit offsets
+  if (!aligned16(X) || !aligned16(S)) return OSPO_ERR_ALIGN;
+  if (drop_p < 0.f || drop_p >= 1.f) return OSPO_ERR_ARG;
+  const bool drop = drop_p > 0.f;
+  if (drop && (N & 1)) return OSPO_ERR_SHAPE;  // mask pairs start at even indices
+  if (drop && (long)K * N > 0xFFFFFFFFL) return OSPO_ERR_SHAPE;  // 32-bit mask index
+  const uint32_t thr = drop_threshold(drop_p);
+  const float dscale = drop ? 1.f / (1.f - drop_p) : 0.f;
+  const int nt = K / 64;
+  const int x_bytes = (int)((long)(K - 1) * ldx * 2 + (long)N * 2);
+  const int s_bytes = (int)((long)K * lds * 2);
+  if (keep_bits && (!drop || (long)K * N / 8 >= (1L << 31))) return OSPO_ERR_ARG;
+  const int k_bytes = keep_bits ? (int)((long)K * N / 8) : 0;
+  const uint8_t* kb = (const uint8_t*)keep_bits;
+  const dim3 grid(N / DA_TN, splits);
+#define DA_LAUNCH(NJV)                                                                                            \
+  do {                                                                                                            \
+    if (drop && kb)                                                                                               \
+      hipLaunchKernelGGL((lora_da_kernel<NJV, 2>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes,      \
+                         (const bf16*)S, lds, s_bytes, s_cols, nt, C, ldc, 0u, 0u, dscale, N, kb, k_bytes);       \
+    else if (drop)                                                                                                \
+      hipLaunchKernelGGL((lora_da_kernel<NJV, 1>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes,      \
+                         (const bf16*)S, lds, s_bytes, s_cols, nt, C, ldc, drop_seed, thr, dscale, N, nullptr, 0); \
+    else                                                                                                          \
+      hipLaunchKernelGGL((lora_da_kernel<NJV, 0>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes,      \
+                         (const bf16*)S, lds, s_bytes, s_cols, nt, C, ldc, 0u, 0u, 0.f, N, nullptr, 0);          \
+  } while (0)
+  switch ((s_cols + 15) / 16) {
+    case 1: DA_LAUNCH(1); break;
+    case 2: DA_LAUNCH(2); break;
+    case 3: DA_LAUNCH(3); break;
+    default: DA_LAUNCH(4); break;
+  }
+#undef DA_LAUNCH
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

@@ -293,6 +293,36 @@ def lora_wgrad(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor, *, mode: int
     return out
 
 
+def lora_da(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor, *, s_cols: int, splits: int = 0,
+            dropout: Optional[tuple] = None, keep_bits: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dA of one adapter group as one stream over x [K, N] (ospo_lora_da): out[j, n] += sum_m s[m, j]
+    dropout(x)[m, n] for j < s_cols, fp32 atomics into out [s_cols, >= N] (s [K, Rp], Rp = 64 or 128,
+    K % 64 == 0, N % 128 == 0).  dropout=(seed, p): x is masked with the adapter input's forward mask as it
+    is read -- from keep_bits (lora_skinny's keep-bit output of this x) when given, else re-hashed.
+    splits: K-tile ranges per 128-column stripe (0: ~2 workgroups per CU)."""
+    if keep_bits is not None and (keep_bits.dtype != torch.uint8 or keep_bits.numel() * 8 < x.shape[0] * x.shape[1]):
+        raise ValueError("lora_da: keep_bits must be uint8 with >= K*N/8 elements")
+    _chk(x, BF16, "x")
+    _chk(s, BF16, "s")
+    _chk(out, torch.float32, "out")
+    K, N = x.shape
+    if s.shape[0] != K:
+        raise ValueError(f"lora_da: {s.shape[0]} rows of s, {K} of x")
+    if splits <= 0:
+        splits = lora_da_splits(K, N, x.device)
+    seed, p = dropout if dropout is not None else (0, 0.0)
+    call("ospo_lora_da", _p(x), _ld(x), N, _p(s), _ld(s), int(s_cols), K, _p(out), _ld(out), int(splits),
+         int(seed) & 0xFFFFFFFF, float(p), _p(keep_bits) if p > 0 else None, _s())
+    return out
+
+
+def lora_da_splits(K: int, N: int, device=None) -> int:
+    """K-tile ranges per 128-column stripe of lora_da: ~2 workgroups per CU, >= 4 K-tiles each."""
+    cus = torch.cuda.get_device_properties(device).multi_processor_count if torch.cuda.is_available() else 256
+    stripes = max(1, N // 128)
+    return int(max(1, min(K // 64 // 4, round(2 * cus / stripes))))
+
+
 def f32_to_bf16(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     _chk(src, torch.float32, "src")
     _chk(dst, BF16, "dst")
@@ -521,16 +551,19 @@ def lora_skinny_ws(M_out, K, n_tiles=4, device="cuda") -> torch.Tensor:
 
 
 def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=None, ws=None, module_tiles=1,
-                dropout=None, xd=None):
+                dropout=None, xd=None, keep_bits=None):
     """out[:M_out, :] (bf16) = scale * a . bt^T per 16-column n-tile (see ospo_lora_skinny).
-    dropout=(seed, p): LoRA dropout on a (dense mode); the masked a is written to xd if given."""
+    dropout=(seed, p): LoRA dropout on a (dense mode); the masked a is written to xd if given, the keep
+    decisions as bits (uint8 [>= M * K / 8], row-major) to keep_bits if given."""
     if ws is None:
         ws = lora_skinny_ws(M_out, K, n_tiles, a.device)
     seed, p = dropout if dropout is not None else (0, 0.0)
+    if keep_bits is not None and (keep_bits.dtype != torch.uint8 or keep_bits.numel() * 8 < M * K):
+        raise ValueError("lora_skinny: keep_bits must be uint8 with >= M*K/8 elements")
     call("ospo_lora_skinny", _p(a), _ld(a), _p(bt), _ld(bt), bt.shape[0] if b_rows is None else b_rows, M, M_out,
          K, n_tiles, a_koff, module_tiles, float(scale), _p(out), _ld(out), out.shape[1], _p(ws),
          ws.numel() * ws.element_size(), int(seed) & 0xFFFFFFFF, float(p), _p(xd), _ld(xd) if xd is not None else 0,
-         _s())
+         _p(keep_bits), _s())
 
 
 def query_gdb_ws(M, nmods, Nmod) -> int:

@@ -573,12 +573,18 @@ def test_lora_skinny_dropout_streamed(M, K, used):
     Acat[:used] = rnd(used, K, s=0.05)
     M_out = (M + 63) // 64 * 64
     out = torch.full((M_out, Rp), 7.0, device=DEV, dtype=torch.bfloat16)
-    ops().lora_skinny(x, Acat, out, M, M_out, K, (used + 15) // 16, 0, 2.0, b_rows=used, dropout=(seed, p))
+    bits = torch.full((M_out * K // 8,), 0x5A, device=DEV, dtype=torch.uint8)
+    ops().lora_skinny(x, Acat, out, M, M_out, K, (used + 15) // 16, 0, 2.0, b_rows=used, dropout=(seed, p),
+                      keep_bits=bits)
     keep = torch.from_numpy(Dm.keep_mask(M, K, seed, p)).to(DEV)
     xd = torch.where(keep, (x.float() / (1 - p)).to(torch.bfloat16), torch.zeros((), dtype=torch.bfloat16, device=DEV))
     ref = 2.0 * (xd.float() @ Acat.float().T)
     assert relerr(out[:M].float(), ref) < 8e-3
     assert torch.all(out[M:] == 0) and torch.all(out[:M, 16 * ((used + 15) // 16):] == 0)
+    # the keep-bit output: bit k % 8 of byte (m K + k) / 8 == the mask, rows >= M untouched
+    got = ((bits[: M * K // 8].view(M, K // 8).to(torch.int32).unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1)
+    assert torch.equal(got.view(M, K).bool(), keep)
+    assert torch.all(bits[M * K // 8:] == 0x5A)
 
 
 @pytest.mark.parametrize("M,N,K,K2", [(300, 512, 256, 64), (4800, 4096, 4096, 64), (600, 1024, 512, 128)])
@@ -759,6 +765,84 @@ def test_lora_wgrad_db_blockdiag_exact_integers(nm, nmod, r, Rp, splits):
     full = dy.float().T @ u.float()
     ref = torch.cat([full[i * nmod:(i + 1) * nmod, i * r:(i + 1) * r] for i in range(nm)], 0)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("K,N,used,Rp,splits", [(4800, 4096, 48, 64, 8), (4800, 11008, 16, 64, 4),
+                                                (4800, 4096, 32, 64, 0), (640, 4096, 64, 128, 3),
+                                                (192, 256, 33, 64, 1), (64, 128, 1, 64, 1)])
+def test_lora_da_exact_integers(K, N, used, Rp, splits):
+    """dA = g^T x as one stream over x (ospo_lora_da): exact on integer operands (every product and partial
+    sum an integer below 2^24), all used rank rows and only those, any split, the step's group shapes."""
+    x = ints(K, N)
+    g = ints(K, Rp)
+    out = torch.full((used + 1, N), 7.0, device=DEV, dtype=torch.float32)
+    ops().lora_da(x, g, out, s_cols=used, splits=splits)
+    ref = 7.0 + g[:, :used].float().T @ x.float()
+    assert torch.equal(out[:used], ref)
+    assert torch.all(out[used] == 7.0)
+
+
+@pytest.mark.parametrize("K,N,used", [(640, 4096, 48), (4800, 11008, 16), (4800, 4096, 32)])
+def test_lora_da_dropout_recompute_equals_stored_mask(K, N, used):
+    """ospo_lora_da with dropout (x masked in registers by the forward's hash, one hash per pair of
+    columns shared across partner lanes by DPP) == dA on the masked copy the forward skinny product writes:
+    bit-exact with one split, fp32-reassociation close with atomics over several."""
+    p, seed = 0.05, 4242
+    x = rnd(K, N)
+    g = rnd(K, 64)
+    xd = torch.empty_like(x)
+    u = torch.empty(K, 64, device=DEV, dtype=torch.bfloat16)
+    A = torch.zeros(64, N, device=DEV, dtype=torch.bfloat16)
+    ops().lora_skinny(x, A, u, K, K, N, 1, 0, 1.0, b_rows=16, dropout=(seed, p), xd=xd)
+    ref = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().lora_da(xd, g, ref, s_cols=used, splits=1)
+    out = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().lora_da(x, g, out, s_cols=used, splits=1, dropout=(seed, p))
+    assert torch.equal(out, ref)
+    out2 = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().lora_da(x, g, out2, s_cols=used, dropout=(seed, p))
+    assert relerr(out2, ref) < 1e-6
+    assert relerr(out, (g[:, :used].float().T @ xd.float())) < 1e-5
+
+
+@pytest.mark.parametrize("K,N,used,M", [(4800, 4096, 48, 4800), (4800, 11008, 16, 4744), (640, 4096, 32, 600)])
+def test_lora_da_keep_bits_equal_rehash(K, N, used, M):
+    """dA masked by the forward's keep bits == dA re-hashing the mask: bit-exact with one split; rows >= M
+    (no bits written, zero g) contribute nothing whatever their bits hold."""
+    p, seed = 0.05, 777
+    x = rnd(K, N)
+    g = rnd(K, 64)
+    g[M:] = 0
+    A = torch.zeros(64, N, device=DEV, dtype=torch.bfloat16)
+    u = torch.empty(K, 64, device=DEV, dtype=torch.bfloat16)
+    bits = torch.full((K * N // 8,), 0xFF, device=DEV, dtype=torch.uint8)
+    ops().lora_skinny(x, A, u, M, K, N, 1, 0, 1.0, b_rows=16, dropout=(seed, p), keep_bits=bits)
+    ref = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().lora_da(x, g, ref, s_cols=used, splits=1, dropout=(seed, p))
+    out = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().lora_da(x, g, out, s_cols=used, splits=1, dropout=(seed, p), keep_bits=bits)
+    assert torch.equal(out, ref)
+    out2 = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+    ops().lora_da(x, g, out2, s_cols=used, dropout=(seed, p), keep_bits=bits)
+    assert relerr(out2, ref) < 1e-6
+
+
+def test_lora_da_rejects_bad_shapes():
+    from ospo_amd._lib import call
+    x = torch.zeros(64, 256, device=DEV, dtype=torch.bfloat16)
+    g = torch.zeros(64, 64, device=DEV, dtype=torch.bfloat16)
+    out = torch.zeros(16, 256, device=DEV, dtype=torch.float32)
+    P = lambda t: t.data_ptr()  # noqa: E731
+    for args in [(256, 200, 64, 16, 64, 1),   # N % 128
+                 (256, 256, 64, 16, 96, 1),   # K % 64
+                 (256, 256, 48, 16, 64, 1),   # lds not 64 / 128
+                 (256, 256, 64, 65, 64, 1),   # s_cols > 64
+                 (256, 256, 64, 16, 64, 2)]:  # splits > K / 64
+        ldx, N, lds, s_cols, K, splits = args
+        with pytest.raises(ValueError):
+            call("ospo_lora_da", P(x), ldx, N, P(g), lds, s_cols, K, P(out), 256, splits, 0, 0.0, None, None)
+    with pytest.raises(ValueError):  # keep bits without dropout
+        call("ospo_lora_da", P(x), 256, 256, P(g), 64, 16, 64, P(out), 256, 1, 0, 0.0, P(x), None)
 
 
 def test_lora_wgrad_dropout_recompute_equals_stored_mask():
