@@ -79,11 +79,13 @@ int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M
  * dropout before lora_A): C = A.B^T + mask (.) (A2.B2^T) / (1 - drop_p), with
  * the forward's mask over the [M, N] input of the adapter (element (m, n) kept
  * iff drop_hash(m*N + n, drop_seed) >= drop_p * 2^32, common.h), i.e.
- * dX = dy.W + dropout'(g . A_cat).  N % 256 == 0, K2 > 0, no bias / residual. */
+ * dX = dy.W + dropout'(g . A_cat).  N % 256 == 0, K2 > 0, no bias / residual.
+ * keep_bits (optional, 16-B aligned): that mask as the forward's ospo_lora_skinny keep-bit output
+ * ([M][N / 8] bytes) -- read instead of re-hashed (same result). */
 int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                               const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
-                              unsigned drop_seed, float drop_p, int tail_split, void* ws, size_t ws_bytes,
-                              hipStream_t stream);
+                              unsigned drop_seed, float drop_p, const void* keep_bits, int tail_split, void* ws,
+                              size_t ws_bytes, hipStream_t stream);
 
 /* down_proj backward fused with the SwiGLU backward (replaces ospo_gemm_nt_dropout_bf16 into dh +
  * ospo_swiglu_bwd; the autograd of `down_proj(act_fn(gate_proj(x)) * up_proj(x))` in HF

@@ -23,7 +23,7 @@ SIGNATURES = {
     "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, I, P, Z, P],
     "ospo_gemm_nt_ws_bytes": [I, I, I, I, I, I],
     "ospo_gemm_nt_tile": [I, I],
-    "ospo_gemm_nt_dropout_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, U, F, I, P, Z, P],
+    "ospo_gemm_nt_dropout_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, U, F, P, I, P, Z, P],
     "ospo_gemm_nt_swiglu_bwd_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, I, U, F, I, P, Z, P],
     "ospo_gemm_nt_rope_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, P, I, P, P, I, I, I, P, Z, P],
     "ospo_mx8_scale_bytes": [I, I],

@@ -140,6 +140,9 @@ struct GemmArgs {
   bf16* swg_dgu = nullptr;
   int ld_gu = 0, ld_dgu = 0;
   uint32_t* dbg = nullptr;  // ablation build, DBG 4: per-wave s_memtime stamps of one K-tile
+  // LoRA dropout backward with the forward's keep bits (ospo_lora_skinny keep_bits, [M][drop_ld / 8] bytes)
+  // instead of re-hashing the mask: the v5 kernel stages the tile's 256 x 32-B block into LDS with tile 0
+  const uint8_t* drop_bits = nullptr;
 };
 
 // the SwiGLU-backward store of 8 product columns (row m, columns n..n+7 of F = args.N)
@@ -1067,7 +1070,9 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   constexpr int SC_BASE = 2 * SLOT;
   constexpr int CPITCH = BN * 2 + 16;
   constexpr int MAIN_BYTES = 2 * SLOT + (MX ? 2 * SC_SLOT : 0);
-  constexpr int LDS_BYTES = (MAIN_BYTES > BM * CPITCH) ? MAIN_BYTES : BM * CPITCH;
+  constexpr int BITS_BASE = MAIN_BYTES;                      // DROP: the tile's keep bits, 256 rows x 32 B
+  constexpr int RING_BYTES = MAIN_BYTES + (DROP ? 8192 : 0);
+  constexpr int LDS_BYTES = (RING_BYTES > BM * CPITCH) ? RING_BYTES : BM * CPITCH;
   static_assert(LDS_BYTES <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   // DBG 5 (ablation): s_memrealtime (100 MHz) stamps of the workgroup's phases, wave 0
@@ -1207,6 +1212,14 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   i32x8 a8[4], b8[2];  // MX tiles: both k-halves of a fragment in one 8-register operand
   i32x8 b8sp[2][2];    // SP + MX: [B half][n]
 
+  // dropout with keep bits: the tile's mask block (rows clamped) goes in first, so every wait below covers it
+  if constexpr (DROP) {
+    if (args.drop_bits && tb == 0 && nt2 > 0) {
+      const int p = wave * 64 + lane, row = p >> 1;
+      glds16(args.drop_bits + (long)min(m0 + row, Mlast) * (args.drop_ld >> 3) + (n0 >> 3) + 16 * (p & 1),
+             smem + BITS_BASE + wave * 1024);
+    }
+  }
   // prologue: tile 0 complete, A0 of tile 1 in flight (SP: tile 0 only)
   if constexpr (BAL) {  // tile 0 complete; B0 B1 (+ scales) of tile 1 in flight (its A0 A1 are staged in R(0,0))
     if (nt > 0) { stage_scales(0); stage_any(0, 2); stage_any(0, 3); stage_any(0, 0); stage_any(0, 1); }
@@ -1654,24 +1667,43 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
   for (int t = 0; t < pre; ++t) run_tile(t, BFT{});
   if (pre > 0) {
     if constexpr (DROP) {
-      {  // accumulators hold exactly A2.B2^T: apply the dropout mask
+      {  // accumulators hold exactly A2.B2^T: apply the dropout mask.  Per (row, B half) the keep bits of the
+         // 32 tile columns ib*128 + wn*32 + 0..31 this wave's lanes hold: from the forward's keep bits (staged in
+         // the prologue; landed -- every wait since covers them) or re-hashed (this lane's 8 bits only); one
+         // multiply pass either way (two alternative passes over the 128 accumulators spilled)
         const int gq = lane >> 4, lq = lane & 15;
+        const bool from_bits = args.drop_bits != nullptr;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int ia = (j >= 2) ? 1 : 0;
-          const int ib = (j == 1 || j == 2) ? 1 : 0;
+        for (int ia = 0; ia < 2; ++ia)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int ib = 0; ib < 2; ++ib) {
+            const int j = ia ? (ib ? 2 : 3) : (ib ? 1 : 0);
 #pragma unroll
-            for (int n = 0; n < 2; ++n) {
-              const uint32_t m = (uint32_t)(m0 + ia * 128 + wm * 64 + i * 16 + lq);
-              const uint32_t c = (uint32_t)(n0 + ib * 128 + wn * 32 + n * 16 + 4 * gq);
-              bool keep[4];
-              drop_keep_pairs<2>(m * (uint32_t)args.drop_ld + c, args.drop_seed, args.drop_thresh, keep);  // c % 4 == 0
+            for (int i = 0; i < 4; ++i) {
+              const int rl = ia * 128 + wm * 64 + i * 16 + lq;
+              uint32_t w;
+              if (from_bits) {
+                w = *reinterpret_cast<const uint32_t*>(smem + BITS_BASE + rl * 32 + ib * 16 + wn * 4);
+              } else {
+                w = 0;
+                const uint32_t m = (uint32_t)(m0 + rl);
 #pragma unroll
-              for (int e = 0; e < 4; ++e) acc[j][i][n][e] *= keep[e] ? args.drop_scale : 0.f;
+                for (int n = 0; n < 2; ++n) {
+                  const uint32_t c = (uint32_t)(n0 + ib * 128 + wn * 32 + n * 16 + 4 * gq);
+                  bool keep[4];
+                  drop_keep_pairs<2>(m * (uint32_t)args.drop_ld + c, args.drop_seed, args.drop_thresh, keep);  // c % 4 == 0
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) w |= (keep[e] ? 1u : 0u) << (n * 16 + 4 * gq + e);
+                }
+              }
+#pragma unroll
+              for (int n = 0; n < 2; ++n) {
+                const uint32_t nib = w >> (n * 16 + 4 * gq);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[j][i][n][e] *= ((nib >> e) & 1u) ? args.drop_scale : 0.f;
+              }
             }
-        }
+          }
       }
     }
   }
@@ -2541,8 +2573,8 @@ extern "C" int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int
 
 extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                                          const void* A2, int lda2, const void* B2, int ldb2, int K2, void* C, int ldc,
-                                         unsigned drop_seed, float drop_p, int tail_split, void* ws, size_t ws_bytes,
-                                         hipStream_t stream) {
+                                         unsigned drop_seed, float drop_p, const void* keep_bits, int tail_split,
+                                         void* ws, size_t ws_bytes, hipStream_t stream) {
   if (!A || !B || !C || !A2 || !B2) return OSPO_ERR_ARG;
   if (tail_split < 0 || tail_split > 8 || (ws && !aligned16(ws))) return OSPO_ERR_ARG;
   const SplitOpts so{tail_split, (float*)ws, ws ? ws_bytes : 0};
@@ -2562,6 +2594,10 @@ extern "C" int ospo_gemm_nt_dropout_bf16(const void* A, int lda, const void* B, 
   a.drop_thresh = drop_threshold(drop_p);
   a.drop_scale = 1.f / (1.f - drop_p);
   a.drop_ld = N;
+  if (keep_bits) {
+    if (!aligned16(keep_bits) || N % 128) return OSPO_ERR_ALIGN;  // 16-B rows of the bit block
+    a.drop_bits = (const uint8_t*)keep_bits;
+  }
   return launch_default<true>(a, stream, so);
 }
 

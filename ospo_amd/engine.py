@@ -78,7 +78,7 @@ class SimPOEngine:
                  max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
                  dropout_seed: int = 42, linear_dtype: str = "bf16", fuse_swiglu_bwd: bool = False,
                  dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0, fuse_gdb: bool = True,
-                 da_stream: bool = True):
+                 da_stream: bool = True, keep_bits: bool = True):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
         if linear_dtype not in ("bf16", "mx8"):
@@ -171,6 +171,9 @@ class SimPOEngine:
         # da_stream: dA as one stream over the adapter input (ops.lora_da, round 3) with the forward's dropout
         # keep bits; off: the 64 x 64 f32-atomic tiles re-hashing the mask (ops.gemm_f32acc(b_dropout=...))
         self.da_stream = bool(da_stream)
+        # keep_bits: the forward's u products store each dropout mask as bits, which the dX GEMMs and dA read
+        # instead of re-hashing it (round 3); off: every consumer re-hashes
+        self.use_keep_bits = bool(keep_bits)
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
             raise ValueError("dadb_splits must be four positive split counts")
         self._side = torch.cuda.Stream(device=self.device, priority=int(side_priority))
@@ -273,6 +276,7 @@ class SimPOEngine:
                 ops.quant_mx8(x, a)
             elif a.m != x.shape[0]:
                 raise RuntimeError(f"pre-quantized operand holds {a.m} rows, the Linear needs {x.shape[0]}")
+            kw.pop("keep_bits", None)  # (the MXFP8 GEMM re-hashes the dropout mask)
             return ops.gemm_nt_mx8(a, w, out, **kw)
         return ops.gemm_nt(x, w, out, **kw)
 
@@ -299,8 +303,16 @@ class SimPOEngine:
             ws = self._sk_ws = ops.lora_skinny_ws(self.Mk, K, max(n_tiles, 8), self.device)
         return ws
 
+    def _bits_bwd(self, layer: int, group: str, drop, K: int):
+        """The keep bits the forward wrote for this adapter input (None: the consumer re-hashes)."""
+        if drop is None or not self.use_keep_bits or (layer, group) not in self._kbits:
+            return None
+        return self._keep_bits(layer, group, K)
+
     def _bits_fwd(self, layer: int, group: str, K: int):
-        return self._keep_bits(layer, group, K) if self._drop(layer, group) is not None else None
+        if not self.use_keep_bits or self._drop(layer, group) is None:
+            return None
+        return self._keep_bits(layer, group, K)
 
     def _drop(self, layer: int, group: str):
         """(seed, p) of one adapter input's dropout mask in the current step, or None."""
@@ -535,7 +547,7 @@ class SimPOEngine:
             ev = torch.cuda.Event()
             ev.record(main)
             side.wait_event(ev)
-            bits = self._keep_bits(i, name, x_in.shape[1]) if drop is not None else None
+            bits = self._bits_bwd(i, name, drop, x_in.shape[1])
             with torch.cuda.stream(side):
                 self._lora_grads(gs, x_in, dy, u, lay.groups[name], gbase, drop, skip_db, bits)
             ev2 = torch.cuda.Event()
@@ -558,7 +570,8 @@ class SimPOEngine:
                 ops.gemm_nt_swiglu_bwd(dx[:M], lw["downT"], a["gu"][:M], dgu[:M], a2=gs[:M], b2=AcatT, dropout=dr)
                 lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr, fdb)
             else:
-                self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
+                self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
+                          keep_bits=self._bits_bwd(i, "down", dr, Fd))
                 lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr, fdb)
                 guard("gu", q)  # dgu / g copy q
                 ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
@@ -566,7 +579,8 @@ class SimPOEngine:
             Acat, AcatT, Bcat, BT = pk["gu"]
             gs, fdb = self._lora_g_db(dgu, lay.groups["gu"], Bcat, BT, M, q, a["u_gu"], gbase)
             dr = self._drop(i, "gu")
-            self._lin(dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
+                      keep_bits=self._bits_bwd(i, "gu", dr, D))
             lora_grads_async("gu", q, gs, a["xn2"], dgu, a["u_gu"], gbase, dr, fdb)
             guard("o", q)  # dxmid / g copy q
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], dxmid[:M],
@@ -575,7 +589,8 @@ class SimPOEngine:
             Acat, AcatT, Bcat, BT = pk["o"]
             gs, fdb = self._lora_g_db(dxmid, lay.groups["o"], Bcat, BT, M, q, a["u_o"], gbase)
             dr = self._drop(i, "o")
-            self._lin(dxmid[:M], lw["oT"], self.dattn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
+            self._lin(dxmid[:M], lw["oT"], self.dattn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
+                      keep_bits=self._bits_bwd(i, "o", dr, D))
             lora_grads_async("o", q, gs, a["attn"], dxmid, a["u_o"], gbase, dr, fdb)
             # ---- attention + RoPE
             guard("qkv", q)  # dqkv / g copy q
@@ -587,7 +602,8 @@ class SimPOEngine:
             gs, fdb = self._lora_g_db(dqkv, lay.groups["qkv"], Bcat, BT, M, q, a["u_qkv"], gbase)
             dr = self._drop(i, "qkv")
             if i > 0:
-                self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr)
+                self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
+                          keep_bits=self._bits_bwd(i, "qkv", dr, D))
             lora_grads_async("qkv", q, gs, a["xn1"], dqkv, a["u_qkv"], gbase, dr, fdb)
             if i > 0:
                 guard("down", 1 - q)  # dx copy 1-q: layer i+1's down products read it

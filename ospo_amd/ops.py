@@ -107,10 +107,12 @@ def _ws_args(ws: Optional[torch.Tensor], device, stream):
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0,
-            bias=None, residual=None, rope=None, dropout=None, split: int = 0, ws=None) -> torch.Tensor:
+            bias=None, residual=None, rope=None, dropout=None, split: int = 0, ws=None,
+            keep_bits=None) -> torch.Tensor:
     """out[M,N] = bf16(alpha*(a.b^T + a2.b2^T) + bias) [+ residual]  (nn.Linear layout b=[N,K]).
     rope=(cos, sin, T, ncols): RoPE forward fused on output columns < ncols (ospo_gemm_nt_rope_bf16).
-    dropout=(seed, p): the a2.b2^T term is masked like the adapter input's dropout (ospo_gemm_nt_dropout_bf16).
+    dropout=(seed, p): the a2.b2^T term is masked like the adapter input's dropout (ospo_gemm_nt_dropout_bf16);
+    keep_bits: that mask as the forward's lora_skinny keep-bit output (uint8 [M * N / 8]) instead of re-hashed.
     split: the tail round's split-K (0 = the library's cost model, 1 = none, 2..8 pinned); ws: the fp32
     split-K workspace (default: gemm_workspace of the current stream)."""
     for t, n in ((a, "a"), (b, "b"), (out, "out")):
@@ -130,9 +132,11 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=
     if dropout is not None and dropout[1] > 0:
         if bias is not None or residual is not None or alpha != 1.0 or rope is not None or a2 is None:
             raise ValueError("gemm_nt: dropout needs a2/b2 and excludes bias / residual / alpha / rope")
+        if keep_bits is not None and (keep_bits.dtype != torch.uint8 or keep_bits.numel() * 8 < M * N):
+            raise ValueError("gemm_nt: keep_bits must be uint8 with >= M*N/8 elements")
         call("ospo_gemm_nt_dropout_bf16", _p(a), _ld(a), _p(b), _ld(b), M, N, K, _p(a2), _ld(a2), _p(b2), _ld(b2),
-             K2, _p(out), _ld(out), int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]), int(split), wsp, wsb,
-             st.cuda_stream)
+             K2, _p(out), _ld(out), int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]), _p(keep_bits), int(split), wsp,
+             wsb, st.cuda_stream)
     elif rope is not None:
         if bias is not None or residual is not None or alpha != 1.0:
             raise ValueError("gemm_nt: rope excludes bias / residual / alpha")

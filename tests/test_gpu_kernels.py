@@ -601,6 +601,27 @@ def test_gemm_dropout_backward(M, N, K, K2):
     assert relerr(out.float(), ref) < 4e-3
 
 
+@pytest.mark.parametrize("M,N,K,K2,split", [(4800, 4096, 4096, 64, 0), (4800, 11008, 4096, 64, 0),
+                                             (1280, 3840, 4096, 64, 2), (300, 512, 256, 64, 1), (600, 1024, 512, 128, 0)])
+def test_gemm_dropout_keep_bits_equal_rehash(M, N, K, K2, split):
+    """The dX GEMM's dropout mask from the forward's keep bits (lora_skinny keep_bits, staged with tile 0)
+    == the re-hashed mask: bit-identical outputs, split-K tails included (N % 128 == 0 shapes)."""
+    p, seed = 0.05, 55221
+    a, b = rnd(M, K), rnd(N, K, s=0.05)
+    a2, b2 = rnd(M, K2), rnd(N, K2, s=0.05)
+    # the keep bits of the [M, N] adapter input, as the forward's u product writes them
+    x = rnd(M, N)
+    bits = torch.zeros(M * N // 8, device=DEV, dtype=torch.uint8)
+    u = torch.empty(M, 64, device=DEV, dtype=torch.bfloat16)
+    ops().lora_skinny(x, torch.zeros(64, N, device=DEV, dtype=torch.bfloat16), u, M, M, N, 1, 0, 1.0, b_rows=16,
+                      dropout=(seed, p), keep_bits=bits)
+    ref = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(a, b, ref, a2=a2, b2=b2, dropout=(seed, p), split=split)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops().gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(seed, p), split=split, keep_bits=bits)
+    assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("M,M_out,nm,Nmod", [(4800, 4800, 3, 4096), (4800, 4864, 2, 11008), (777, 832, 1, 4096),
                                             (100, 128, 1, 1024), (1000, 1024, 4, 512)])
 def test_lora_gdb_exact_integers(M, M_out, nm, Nmod):
