@@ -66,7 +66,7 @@ def simpo_setup(layers=30, lora_r=16, pairs=4, text_len=24, img_tokens=576, lora
     weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)
     eng = SimPOEngine(dims, weights, device=dev, max_pairs=pairs, max_text_len=text_len, n_img_tokens=img_tokens,
                       lora_dropout=lora_dropout, dropout_seed=42, linear_dtype=linear_dtype, wgrad_wgs=wgrad_wgs,
-                      da_stream=not round2_lora, keep_bits=not round2_lora)
+                      da_stream=not round2_lora, keep_bits=not round2_lora, fuse_swiglu_u=not round2_lora)
     # each rank draws its own pairs (the DistributedSampler shard of the global batch)
     batches = [synthetic_batch(pairs, text_len, img_tokens, dims.vocab, dims.img_vocab, seed=1000 * rank + i,
                                device=dev) for i in range(4)]
@@ -460,7 +460,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--wgrad-wgs", type=int, default=0)  # A/B: LoRA weight grads as ospo_lora_wgrad streams
-    ap.add_argument("--round2-lora", action="store_true")  # A/B: dA tiles + re-hashed dropout masks (round 2)
+    ap.add_argument("--round2-lora", action="store_true")  # A/B: round 2's LoRA kernels (dA tiles, re-hashed masks, unfused u_d)
     # process-group backend for N > 1: RCCL ("nccl", default on GPUs); "gloo" lets N ranks share one GPU
     # (the multi-rank rehearsal of tests/test_gpu_dp_overlap.py on a one-GPU box)
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None)

@@ -319,6 +319,17 @@ int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb, int b_rows
                      int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed, float drop_p,
                      void* xd, int ld_xd, void* keep_bits, hipStream_t stream);
 
+/* The MLP's SwiGLU forward fused with the down adapter's u product (HF LlamaMLP.forward's
+ * down_proj(act_fn(gate) * up) with peft lora_A on its input; ospo/wrapper/train.py:352):
+ *   h[m][k]   = bf16(bf16(silu(gu[m][k])) * gu[m][F + k])      (= ospo_swiglu_fwd, rows < M)
+ *   out[m][c] = scale * sum_k dropout(h)[m][k] * Bt[c][k]      (= ospo_lora_skinny on h, dense, n_tiles <= 4)
+ * in one stream over gu (h is written, never re-read).  F % 64 == 0; ws, out padding, dropout and keep_bits
+ * as ospo_lora_skinny (K = F). */
+int ospo_swiglu_fwd_lora_down(const void* gu, int ld_gu, void* h, int ld_h, int M, int M_out, int F,
+                              const void* Bt, int ldb, int b_rows, int n_tiles, float scale, void* out, int ldo,
+                              int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed, float drop_p,
+                              void* keep_bits, hipStream_t stream);
+
 /* Fused LoRA backward over one stream of dy, LoRA rank 16 (replaces ospo_lora_skinny's g plus the
  * dB = dy^T u ospo_gemm_f32acc of the same group; ospo/wrapper/train.py:352 through peft lora.Linear's
  * backward):

@@ -33,6 +33,7 @@ SIGNATURES = {
     "ospo_gemm_f32acc_bdrop": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, U, F, P],
     "ospo_lora_wgrad": [P, I, I, P, I, I, I, I, I, I, P, I, I, U, F, P],
     "ospo_lora_da": [P, I, I, P, I, I, I, P, I, I, U, F, P, P],
+    "ospo_swiglu_fwd_lora_down": [P, I, P, I, I, I, I, P, I, I, I, F, P, I, I, P, Z, U, F, P, P],
     "ospo_f32_to_bf16": [P, P, L, F, P],
     "ospo_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "ospo_rmsnorm_bwd": [P, P, P, P, P, P, I, I, P],

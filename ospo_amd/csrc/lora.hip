@@ -315,19 +315,35 @@ __device__ __forceinline__ void sk3_wait(int n) {
     case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
     case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;  // (more in flight: waiting longer is safe)
   }
 }
 
-template <int NT, bool DROP>
+// SWG (round 3): the down-projection's u product fused with the SwiGLU forward that makes its input: A is gu
+// [M][>= 2F] (gate | up); each chunk stages the gate and the up tile, the fragment's h = bf16(silu(g)) * u is
+// formed in registers (swiglu_fwd_kernel's rounding), stored to hout [M][F] (the down GEMM's operand) and
+// fed to the MFMAs -- h is never re-read.  K = F, up_off = F * 2 bytes.
+template <int NT, bool DROP, bool SWG = false>
 __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A, int lda, int a_bytes,
                                                       const bf16* __restrict__ Bt, int ldb, int b_rows, int b_bytes,
                                                       int M, int M_out, int K, int kper, int a_koff, int tiles_total,
                                                       float scale, bf16* __restrict__ out, int ldo, int out_cols,
                                                       float* __restrict__ ws, int M_pad, uint32_t dseed,
-                                                      uint32_t dthresh, float dscale, uint8_t* __restrict__ kbits) {
+                                                      uint32_t dthresh, float dscale, uint8_t* __restrict__ kbits,
+                                                      bf16* __restrict__ hout = nullptr, int ldh = 0, int up_off = 0) {
   using C = Sk3Cfg<NT>;
-  __shared__ __attribute__((aligned(16))) char smem[C::NS * C::STAGE];
+  constexpr int ABYTES = SWG ? 16384 : 8192;        // A image(s): gate and up under SWG
+  constexpr int STAGE = C::STAGE + ABYTES - 8192;
+  constexpr int PW = C::PW + (SWG ? 2 : 0);
+  __shared__ __attribute__((aligned(16))) char smem[C::NS * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, g = lane >> 4, r8 = lane >> 3, c8 = lane & 7;
@@ -355,17 +371,22 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
   }
 #define SK3_STAGE(cc)                                                                                            \
   {                                                                                                              \
-    char* st_ = smem + ((cc) % C::NS) * C::STAGE;                                                               \
+    char* st_ = smem + ((cc) % C::NS) * STAGE;                                                                  \
     const int kb_ = (cc) * 128;                                                                                  \
     _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                                \
         sk3_lds16(rsA, st_ + (wave * 2 + i) * 1024, va[i], kb_);                                                 \
+    if constexpr (SWG) {                                                                                         \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                              \
+          sk3_lds16(rsA, st_ + 8192 + (wave * 2 + i) * 1024, va[i], kb_ + up_off);                               \
+    }                                                                                                            \
     _Pragma("unroll") for (int i = 0; i < C::BPW; ++i)                                                           \
-        sk3_lds16(rsB, st_ + 8192 + (wave * C::BPW + i) * 1024, vb[i], kb_);                                     \
+        sk3_lds16(rsB, st_ + ABYTES + (wave * C::BPW + i) * 1024, vb[i], kb_);                                   \
   }
 
   f32x4 acc[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int spi = (SWG ? 2 : 0) + (DROP && kbits ? 2 : 0);  // global stores per chunk per lane
   const int arow_l = wave * 16 + l16;  // this lane's fragment row in the 64-row block
   const uint32_t drow = (uint32_t)min(m0 + arow_l, M - 1) * (uint32_t)K;
   bool bok[NT];
@@ -376,20 +397,32 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
   for (int j = 0; j < C::NS - 1; ++j)
     if (j < nch) SK3_STAGE(j);
   for (int c = 0; c < nch; ++c) {
-    sk3_wait(C::PW * min(C::NS - 2, nch - 1 - c));  // this wave's pieces of chunk c landed
+    // this wave's pieces of chunk c landed: newer are the pieces of up to NS - 2 later chunks and the stores
+    // (h, keep bits; unconditional, so the count is exact) of the up to NS - 1 chunks computed since
+    sk3_wait(PW * min(C::NS - 2, nch - 1 - c) + spi * min(c, C::NS - 1));
     __builtin_amdgcn_s_barrier();                    // everyone's; and chunk c-1's slot is free
     asm volatile("" ::: "memory");
     if (c + C::NS - 1 < nch) SK3_STAGE(c + C::NS - 1);
-    const char* st = smem + (c % C::NS) * C::STAGE;
+    const char* st = smem + (c % C::NS) * STAGE;
     bf16x8 a[2], b[2][NT];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int q = 4 * s + g;  // 16-B chunk of the 128-B line
       a[s] = *reinterpret_cast<const bf16x8*>(st + arow_l * 128 + ((q ^ (arow_l & 7)) << 4));
+      if constexpr (SWG) {  // h = bf16(silu(gate)) * up of the fragment's 8 elements, rounded; stored once
+        const bf16x8 up = *reinterpret_cast<const bf16x8*>(st + 8192 + arow_l * 128 + ((q ^ (arow_l & 7)) << 4));
+        float hv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[e] = round_bf(silu(bf2f(a[s][e]))) * bf2f(up[e]);
+        const u32x4 pk = pack8(hv);
+        a[s] = __builtin_bit_cast(bf16x8, pk);
+        // rows >= M hold row M - 1 (clamped staging) and rewrite its h: the store is unconditional
+        *reinterpret_cast<u32x4*>(hout + (long)min(m0 + arow_l, M - 1) * ldh + k_begin + 64 * c + 32 * s + 8 * g) = pk;
+      }
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int br = 16 * j + l16;
-        b[s][j] = *reinterpret_cast<const bf16x8*>(st + 8192 + br * 128 + ((q ^ (br & 7)) << 4));
+        b[s][j] = *reinterpret_cast<const bf16x8*>(st + ABYTES + br * 128 + ((q ^ (br & 7)) << 4));
       }
     }
 #pragma unroll
@@ -401,7 +434,7 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
         drop_keep_pairs<4>(drow + k0, dseed, dthresh, keep);
 #pragma unroll
         for (int e = 0; e < 8; ++e) av[e] = keep[e] ? f2bf(bf2f(av[e]) * dscale) : f2bf(0.f);
-        if (kbits && m0 + arow_l < M) {  // the keep bits, one byte per 8 columns (bit e = column k0 + e)
+        if (kbits) {  // the keep bits, one byte per 8 columns (bit e = column k0 + e); rows >= M rewrite row M - 1's
           uint32_t byte = 0;
 #pragma unroll
           for (int e = 0; e < 8; ++e) byte |= (keep[e] ? 1u : 0u) << e;
@@ -910,11 +943,13 @@ static int launch_skinny2(const bf16* a, int lda, const bf16* b, int ldb, int b_
 }
 
 
-// v3 split: ~2 workgroups per CU over (64-row blocks x modules), whole 64-k chunks per split
-template <int NT>
+// v3 split: ~2 workgroups per CU over (64-row blocks x modules), whole 64-k chunks per split.
+// SWG: a = gu (gate | up, up at column K), the SwiGLU product h written to hout on the way
+template <int NT, bool SWG = false>
 static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_rows, int M, int M_out, int K,
                           int a_koff, int nz, int tiles_total, float scale, bf16* o, int ldo, int out_cols, float* part,
-                          size_t ws_bytes, hipStream_t stream, const SkDropArgs& dr) {
+                          size_t ws_bytes, hipStream_t stream, const SkDropArgs& dr, bf16* hout = nullptr,
+                          int ldh = 0) {
   const int blocks = (M_out + 63) / 64 * nz;
   const int chunks = K / 64;
   int splits = (g_sk3_wgs + blocks - 1) / blocks;
@@ -924,17 +959,18 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   splits = (K + kper - 1) / kper;
   const int M_pad = (M_out + 63) / 64 * 64;
   if (splits > 1 && ws_bytes < (size_t)splits * M_pad * 16 * tiles_total * 4) return OSPO_ERR_SHAPE;
-  const long a_bytes = (long)(M - 1) * lda * 2 + (long)((nz - 1) * a_koff + K) * 2;
+  const long a_bytes = (long)(M - 1) * lda * 2 + (long)((nz - 1) * a_koff + K * (SWG ? 2 : 1)) * 2;
   const long b_bytes = (long)(b_rows - 1) * ldb * 2 + (long)K * 2;
+  if (a_bytes >= (1L << 31)) return OSPO_ERR_SHAPE;  // 32-bit buffer offsets
   const dim3 grid(M_pad / 64, splits, nz);
   if (dr.scale > 0.f)
-    hipLaunchKernelGGL((skinny3_kernel<NT, true>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb, b_rows,
-                       (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad,
-                       dr.seed, dr.thresh, dr.scale, dr.bits);
+    hipLaunchKernelGGL((skinny3_kernel<NT, true, SWG>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb,
+                       b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part,
+                       M_pad, dr.seed, dr.thresh, dr.scale, dr.bits, hout, ldh, K * 2);
   else
-    hipLaunchKernelGGL((skinny3_kernel<NT, false>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb, b_rows,
-                       (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part, M_pad, 0u,
-                       0u, 0.f, nullptr);
+    hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb,
+                       b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part,
+                       M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2);
   OSPO_CHECK_LAUNCH();
   if (splits > 1) {
     const long n = (long)M_out * (out_cols / 4);
@@ -1165,4 +1201,45 @@ extern "C" int ospo_lora_da(const void* X, int ldx, int N, const void* S, int ld
 #undef DA_LAUNCH
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
+}
+
+// The MLP's SwiGLU forward fused with the down adapter's u product (ospo/wrapper/train.py:352 through HF
+// LlamaMLP.forward: down_proj(act_fn(gate_proj(x)) * up_proj(x)) with peft's lora_A on the down input):
+//   h[m][k]   = bf16(bf16(silu(gu[m][k])) * gu[m][F + k])                 (= ospo_swiglu_fwd, rows < M)
+//   out[m][c] = scale * sum_k dropout(h)[m][k] * Bt[c][k]                 (= ospo_lora_skinny on h, dense)
+// one stream over gu: h is stored and consumed in registers, never re-read.  K = F % 64 == 0; ws and
+// the zero-fill of out rows M..M_out-1 / columns 16 n_tiles.. as ospo_lora_skinny; keep_bits as there.
+extern "C" int ospo_swiglu_fwd_lora_down(const void* gu, int ld_gu, void* h, int ld_h, int M, int M_out, int F,
+                                         const void* Bt, int ldb, int b_rows, int n_tiles, float scale, void* out,
+                                         int ldo, int out_cols, void* ws, size_t ws_bytes, unsigned drop_seed,
+                                         float drop_p, void* keep_bits, hipStream_t stream) {
+  if (!gu || !h || !Bt || !out || !ws) return OSPO_ERR_ARG;
+  if (drop_p < 0.f || drop_p >= 1.f || (keep_bits && drop_p == 0.f)) return OSPO_ERR_ARG;
+  if (M <= 0 || M_out < M || F <= 0 || F % 64 || b_rows <= 0 || n_tiles < 1 || n_tiles > 8) return OSPO_ERR_SHAPE;
+  if (ld_gu < 2 * F || ld_gu % 8 || ld_h < F || ld_h % 8 || ldb < F || ldb % 8 || ldo % 4 || out_cols % 4 ||
+      out_cols < 16 * n_tiles || ldo < out_cols)
+    return OSPO_ERR_SHAPE;
+  if ((long)b_rows * ldb * 2 >= (1L << 31)) return OSPO_ERR_SHAPE;
+  if (drop_p > 0.f && (long)M * F > 0xFFFFFFFFL) return OSPO_ERR_SHAPE;  // 32-bit mask index
+  if (ws_bytes < ospo_lora_skinny_ws_bytes(M_out, F, n_tiles)) return OSPO_ERR_SHAPE;
+  if (!aligned16(gu) || !aligned16(h) || !aligned16(Bt) || !aligned16(ws) || ((uintptr_t)out & 7)) return OSPO_ERR_ALIGN;
+  SkDropArgs dr;
+  if (drop_p > 0.f) {
+    dr.seed = drop_seed;
+    dr.thresh = drop_threshold(drop_p);
+    dr.scale = 1.f / (1.f - drop_p);
+    dr.bits = (uint8_t*)keep_bits;
+  }
+  const bf16* a = (const bf16*)gu;
+  const bf16* b = (const bf16*)Bt;
+  bf16* o = (bf16*)out;
+  float* p2 = (float*)ws;
+  bf16* ho = (bf16*)h;
+  switch (n_tiles) {
+    case 1: return launch_skinny3<1, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 1, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h);
+    case 2: return launch_skinny3<2, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 2, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h);
+    case 3: return launch_skinny3<3, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 3, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h);
+    case 4: return launch_skinny3<4, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 4, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h);
+    default: return OSPO_ERR_UNSUPPORTED;
+  }
 }

@@ -78,7 +78,7 @@ class SimPOEngine:
                  max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
                  dropout_seed: int = 42, linear_dtype: str = "bf16", fuse_swiglu_bwd: bool = False,
                  dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0, fuse_gdb: bool = True,
-                 da_stream: bool = True, keep_bits: bool = True):
+                 da_stream: bool = True, keep_bits: bool = True, fuse_swiglu_u: bool = True):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
         if linear_dtype not in ("bf16", "mx8"):
@@ -174,6 +174,8 @@ class SimPOEngine:
         # keep_bits: the forward's u products store each dropout mask as bits, which the dX GEMMs and dA read
         # instead of re-hashing it (round 3); off: every consumer re-hashes
         self.use_keep_bits = bool(keep_bits)
+        # fuse_swiglu_u: the SwiGLU forward and the down adapter's u product in one stream over gu (round 3)
+        self.fuse_swiglu_u = bool(fuse_swiglu_u)
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
             raise ValueError("dadb_splits must be four positive split counts")
         self._side = torch.cuda.Stream(device=self.device, priority=int(side_priority))
@@ -438,10 +440,18 @@ class SimPOEngine:
             self._lora_down(a["xn2"], Acat, a["u_gu"], M, lay.groups["gu"].nmods, self._drop(i, "gu"),
                             bits=self._bits_fwd(i, "gu", D))
             self._lin(a["xn2"][:M], lw["gu"], a["gu"][:M], pre=True, a2=a["u_gu"][:M], b2=Bcat)
-            ops.swiglu_fwd(a["gu"][:M], a["h"][:M], mx=self._mxo(Fd))
             Acat, _, Bcat, _ = pk["down"]
-            self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods, self._drop(i, "down"),
-                            bits=self._bits_fwd(i, "down", Fd))
+            used_d = lay.groups["down"].nmods * lay.r
+            if self.fuse_swiglu_u and self._mxo(Fd) is None and Fd % 64 == 0 and used_d <= 64:
+                # SwiGLU fused with the down adapter's u product: one stream over gu, h never re-read
+                nt = (used_d + 15) // 16
+                ops.swiglu_fwd_lora_down(a["gu"], a["h"], Acat, a["u_d"], M, self.Mk, Fd, nt, self.scale,
+                                         b_rows=used_d, ws=self._skinny_ws(Fd, nt), dropout=self._drop(i, "down"),
+                                         keep_bits=self._bits_fwd(i, "down", Fd))
+            else:
+                ops.swiglu_fwd(a["gu"][:M], a["h"][:M], mx=self._mxo(Fd))
+                self._lora_down(a["h"], Acat, a["u_d"], M, lay.groups["down"].nmods, self._drop(i, "down"),
+                                bits=self._bits_fwd(i, "down", Fd))
             xn = self.acts[i + 1]["x"] if i + 1 < dims.n_layers else self.x_final
             self._lin(a["h"][:M], lw["down"], xn[:M], pre=True, a2=a["u_d"][:M], b2=Bcat, residual=a["xmid"][:M])
         ops.rmsnorm_fwd(self.x_final[:M], self.norm, self.hf[:M], self.rstd_f[:M], dims.rms_eps)

@@ -570,6 +570,22 @@ def lora_skinny(a, bt, out, M, M_out, K, n_tiles, a_koff=0, scale=1.0, b_rows=No
          _p(keep_bits), _s())
 
 
+def swiglu_fwd_lora_down(gu, h, bt, out, M, M_out, F, n_tiles, scale=1.0, b_rows=None, ws=None, dropout=None,
+                         keep_bits=None):
+    """h[:M] = SwiGLU(gu) (as swiglu_fwd) and out[:M_out] = scale * dropout(h) . bt^T (as lora_skinny on h) in
+    one stream over gu (ospo_swiglu_fwd_lora_down); keep_bits as lora_skinny's."""
+    _chk(gu, BF16, "gu")
+    _chk(h, BF16, "h")
+    if ws is None:
+        ws = lora_skinny_ws(M_out, F, n_tiles, gu.device)
+    seed, p = dropout if dropout is not None else (0, 0.0)
+    if keep_bits is not None and (keep_bits.dtype != torch.uint8 or keep_bits.numel() * 8 < M * F):
+        raise ValueError("swiglu_fwd_lora_down: keep_bits must be uint8 with >= M*F/8 elements")
+    call("ospo_swiglu_fwd_lora_down", _p(gu), _ld(gu), _p(h), _ld(h), M, M_out, F, _p(bt), _ld(bt),
+         bt.shape[0] if b_rows is None else b_rows, n_tiles, float(scale), _p(out), _ld(out), out.shape[1], _p(ws),
+         ws.numel() * ws.element_size(), int(seed) & 0xFFFFFFFF, float(p), _p(keep_bits), _s())
+
+
 def query_gdb_ws(M, nmods, Nmod) -> int:
     return int(query("ospo_lora_gdb_ws_bytes", M, nmods, Nmod))
 

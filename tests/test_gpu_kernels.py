@@ -587,6 +587,33 @@ def test_lora_skinny_dropout_streamed(M, K, used):
     assert torch.all(bits[M * K // 8:] == 0x5A)
 
 
+@pytest.mark.parametrize("M,M_out,F,used,drop", [(4800, 4800, 11008, 16, True), (4744, 4800, 11008, 16, True),
+                                                   (600, 640, 1024, 32, False), (130, 192, 512, 48, True)])
+def test_swiglu_fwd_lora_down_equals_two_launches(M, M_out, F, used, drop):
+    """SwiGLU forward fused with the down adapter's u product == swiglu_fwd then lora_skinny on h: h, u and
+    the keep bits bit-identical (the same roundings, the same split-K partials and sums)."""
+    p, seed = 0.05, 8642
+    gu = rnd(M_out, 2 * F)
+    A = torch.zeros(64, F, device=DEV, dtype=torch.bfloat16)
+    A[:used] = rnd(used, F, s=0.05)
+    nt = (used + 15) // 16
+    dr = (seed, p) if drop else None
+    h_ref = torch.zeros(M_out, F, device=DEV, dtype=torch.bfloat16)
+    ops().swiglu_fwd(gu[:M], h_ref[:M])
+    u_ref = torch.full((M_out, 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    bits_ref = torch.zeros(M_out * F // 8, device=DEV, dtype=torch.uint8)
+    ops().lora_skinny(h_ref, A, u_ref, M, M_out, F, nt, 0, 2.0, b_rows=used, dropout=dr,
+                      keep_bits=bits_ref if drop else None)
+    h = torch.zeros(M_out, F, device=DEV, dtype=torch.bfloat16)
+    u = torch.full((M_out, 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    bits = torch.zeros_like(bits_ref)
+    ops().swiglu_fwd_lora_down(gu, h, A, u, M, M_out, F, nt, 2.0, b_rows=used, dropout=dr,
+                               keep_bits=bits if drop else None)
+    assert torch.equal(h, h_ref)
+    assert torch.equal(u, u_ref)
+    assert torch.equal(bits, bits_ref)
+
+
 @pytest.mark.parametrize("M,N,K,K2", [(300, 512, 256, 64), (4800, 4096, 4096, 64), (600, 1024, 512, 128)])
 def test_gemm_dropout_backward(M, N, K, K2):
     """dX = dy.W + mask (.) (g.A) / (1-p): the K-extension is masked like the adapter input."""
