@@ -54,7 +54,7 @@ def synthetic_batch(B, Lt, N, vocab, img_vocab, seed, device):
 
 
 def simpo_setup(layers=30, lora_r=16, pairs=4, text_len=24, img_tokens=576, lora_dropout=0.05,
-                linear_dtype="bf16", rank=0, device="cuda", wgrad_wgs=0, round2_lora=False):
+                linear_dtype="bf16", rank=0, device="cuda", wgrad_wgs=0, round2_lora=False, lora_variant=""):
     """The bench's SimPO workload: Janus-Pro-7B-shaped synthetic weights (seed 0, LoRA seed 1, identical
     on every rank), the engine, and rank's 4 synthetic batches (seeds 1000 * rank + i).  Returns
     (dims, engine, batches, weights); tests/test_gpu_step.py builds the same workload to check the
@@ -66,7 +66,8 @@ def simpo_setup(layers=30, lora_r=16, pairs=4, text_len=24, img_tokens=576, lora
     weights = synthetic_weights(dims, dev, seed=0, lora_seed=1)
     eng = SimPOEngine(dims, weights, device=dev, max_pairs=pairs, max_text_len=text_len, n_img_tokens=img_tokens,
                       lora_dropout=lora_dropout, dropout_seed=42, linear_dtype=linear_dtype, wgrad_wgs=wgrad_wgs,
-                      da_stream=not round2_lora, keep_bits=not round2_lora, fuse_swiglu_u=not round2_lora)
+                      da_stream=not (round2_lora or "da_tiles" in lora_variant), keep_bits=not round2_lora,
+                      fuse_swiglu_u=not (round2_lora or "swiglu_unfused" in lora_variant))
     # each rank draws its own pairs (the DistributedSampler shard of the global batch)
     batches = [synthetic_batch(pairs, text_len, img_tokens, dims.vocab, dims.img_vocab, seed=1000 * rank + i,
                                device=dev) for i in range(4)]
@@ -461,6 +462,7 @@ def main():
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--wgrad-wgs", type=int, default=0)  # A/B: LoRA weight grads as ospo_lora_wgrad streams
     ap.add_argument("--round2-lora", action="store_true")  # A/B: round 2's LoRA kernels (dA tiles, re-hashed masks, unfused u_d)
+    ap.add_argument("--lora-variant", default="")  # A/B: "da_tiles", "swiglu_unfused" (comma list): one round-3 change off
     # process-group backend for N > 1: RCCL ("nccl", default on GPUs); "gloo" lets N ranks share one GPU
     # (the multi-rank rehearsal of tests/test_gpu_dp_overlap.py on a one-GPU box)
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None)
@@ -490,7 +492,8 @@ def main():
     dims, eng, batches, weights = simpo_setup(layers=args.layers, lora_r=args.lora_r, pairs=B, text_len=Lt,
                                               img_tokens=N, lora_dropout=args.lora_dropout,
                                               linear_dtype=args.linear_dtype, rank=rank, device=dev,
-                                              wgrad_wgs=args.wgrad_wgs, round2_lora=args.round2_lora)
+                                              wgrad_wgs=args.wgrad_wgs, round2_lora=args.round2_lora,
+                                              lora_variant=args.lora_variant)
     del weights
     torch.cuda.empty_cache()
     cfg = SimPOConfig()

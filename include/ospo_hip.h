@@ -143,10 +143,13 @@ int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ld
 /* As ospo_gemm_f32acc with LoRA dropout recomputed on a K-major B [K][N] (the dA product's
  * activations): element (m, n) enters as bf16(B[m][n] / (1 - p)) when drop_hash(m * N + n, seed)
  * >= p * 2^32, else 0 -- the values ospo_lora_skinny's dropout multiplied in the forward, so the
- * forward need not store the masked copy.  Requires b_kmajor = 1 and 0 < p < 1. */
+ * forward need not store the masked copy.  Requires b_kmajor = 1 and 0 < p < 1.  keep_bits (optional):
+ * the mask as ospo_lora_skinny's keep-bit output for B ([K][N / 8] bytes, N % 8 == 0), read instead of
+ * re-hashed (same result). */
 int ospo_gemm_f32acc_bdrop(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
                            int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
-                           int diag_nblk, int diag_r, uint32_t drop_seed, float drop_p, hipStream_t stream);
+                           int diag_nblk, int diag_r, uint32_t drop_seed, float drop_p, const void* keep_bits,
+                           hipStream_t stream);
 
 /* dst[i] (bf16) = round(scale * src[i]) for i < n (fp32 -> bf16 with scale). */
 int ospo_f32_to_bf16(const float* src, void* dst, long n, float scale, hipStream_t stream);

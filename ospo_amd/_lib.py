@@ -30,7 +30,7 @@ SIGNATURES = {
     "ospo_quant_mx8": [P, I, I, I, P, I, P, P],
     "ospo_gemm_nt_mx8": [P, I, P, P, I, P, I, I, I, P, I, P, I, I, F, P, P, I, P, I, P, P, I, I, U, F, I, P, Z, P],
     "ospo_gemm_f32acc": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, P],
-    "ospo_gemm_f32acc_bdrop": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, U, F, P],
+    "ospo_gemm_f32acc_bdrop": [P, I, I, P, I, I, I, I, I, I, F, P, I, I, I, U, F, P, P],
     "ospo_lora_wgrad": [P, I, I, P, I, I, I, I, I, I, P, I, I, U, F, P],
     "ospo_lora_da": [P, I, I, P, I, I, I, P, I, I, U, F, P, P],
     "ospo_swiglu_fwd_lora_down": [P, I, P, I, I, I, I, P, I, I, I, F, P, I, I, P, Z, U, F, P, P],

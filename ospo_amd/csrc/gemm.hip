@@ -226,7 +226,13 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const GemmArgs args) 
           const uint32_t base = (uint32_t)(t * BK + row) * (uint32_t)args.drop_ld + (uint32_t)(n0 + x * 8);
           bf16x8 v = *reinterpret_cast<const bf16x8*>(lb + c * 16);
           bool keep[8];
-          drop_keep_pairs<4>(base, args.drop_seed, args.drop_thresh, keep);  // base even (drop_ld even)
+          if (args.drop_bits) {  // the forward's keep bits: one byte = these 8 columns (base % 8 == 0)
+            const uint32_t kb = args.drop_bits[base >> 3];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) keep[e] = (kb >> e) & 1u;
+          } else {
+            drop_keep_pairs<4>(base, args.drop_seed, args.drop_thresh, keep);  // base even (drop_ld even)
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = keep[e] ? f2bf(bf2f(v[e]) * args.drop_scale) : f2bf(0.f);
           *reinterpret_cast<bf16x8*>(lb + c * 16) = v;
@@ -2711,7 +2717,8 @@ extern "C" int ospo_gemm_nt_tile(int M, int N) { return pick_nt_tile(M, N); }
 
 static int gemm_f32acc_impl(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor, int M, int N,
                             int K, int k_splits, float alpha, float* C, int ldc, int diag_nblk, int diag_r,
-                            uint32_t drop_seed, float drop_p, hipStream_t stream);
+                            uint32_t drop_seed, float drop_p, hipStream_t stream,
+                            const uint8_t* keep_bits = nullptr);
 
 extern "C" int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
                                 int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
@@ -2722,15 +2729,17 @@ extern "C" int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void
 
 extern "C" int ospo_gemm_f32acc_bdrop(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor,
                                       int M, int N, int K, int k_splits, float alpha, float* C, int ldc, int diag_nblk,
-                                      int diag_r, uint32_t drop_seed, float drop_p, hipStream_t stream) {
+                                      int diag_r, uint32_t drop_seed, float drop_p, const void* keep_bits,
+                                      hipStream_t stream) {
   if (!b_kmajor || !(drop_p > 0.f && drop_p < 1.f)) return OSPO_ERR_ARG;
+  if (keep_bits && N % 8) return OSPO_ERR_SHAPE;  // whole bytes per 8 columns
   return gemm_f32acc_impl(A, lda, a_kmajor, B, ldb, b_kmajor, M, N, K, k_splits, alpha, C, ldc, diag_nblk, diag_r,
-                          drop_seed, drop_p, stream);
+                          drop_seed, drop_p, stream, (const uint8_t*)keep_bits);
 }
 
 static int gemm_f32acc_impl(const void* A, int lda, int a_kmajor, const void* B, int ldb, int b_kmajor, int M, int N,
                             int K, int k_splits, float alpha, float* C, int ldc, int diag_nblk, int diag_r,
-                            uint32_t drop_seed, float drop_p, hipStream_t stream) {
+                            uint32_t drop_seed, float drop_p, hipStream_t stream, const uint8_t* keep_bits) {
   if (!A || !B || !C) return OSPO_ERR_ARG;
   if (M <= 0 || N <= 0 || K <= 0 || K % BK || N % 64) return OSPO_ERR_SHAPE;
   if (k_splits < 1) k_splits = 1;
@@ -2749,6 +2758,7 @@ static int gemm_f32acc_impl(const void* A, int lda, int a_kmajor, const void* B,
     a.drop_thresh = drop_threshold(drop_p);
     a.drop_scale = 1.f / (1.f - drop_p);
     a.drop_ld = N;
+    a.drop_bits = keep_bits;
   }
   const bool wideN = (N % 256 == 0);
   const bool tallM = a_kmajor ? (M % 256 == 0 && lda >= M) : (M >= 1024);

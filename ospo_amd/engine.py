@@ -168,13 +168,16 @@ class SimPOEngine:
         # fuse_gdb (LoRA r = 16): g = s dy.B and dB += dy^T u of a group in one stream over dy on the main stream
         # (ospo_lora_gdb); the side stream then runs only dA.  Off: g on the main stream, dB with dA on the side.
         self.fuse_gdb = bool(fuse_gdb) and dims.lora_r == 16
-        # da_stream: dA as one stream over the adapter input (ops.lora_da, round 3) with the forward's dropout
-        # keep bits; off: the 64 x 64 f32-atomic tiles re-hashing the mask (ops.gemm_f32acc(b_dropout=...))
+        # da_stream: dA as one stream over the adapter input with the forward's keep bits (ops.lora_da, round 3:
+        # 5.2 ms of side-stream kernel time per step against 5.6 for the 64 x 64 f32-atomic tiles re-hashing the
+        # mask, profiles/r03/step_lora_variants_breakdown_v2.txt); off: those tiles (ops.gemm_f32acc(b_dropout=...)),
+        # which re-hash (their byte-wise keep-bit reads cost more than the hashes: 66.7 vs 47 us per launch)
         self.da_stream = bool(da_stream)
         # keep_bits: the forward's u products store each dropout mask as bits, which the dX GEMMs and dA read
         # instead of re-hashing it (round 3); off: every consumer re-hashes
         self.use_keep_bits = bool(keep_bits)
-        # fuse_swiglu_u: the SwiGLU forward and the down adapter's u product in one stream over gu (round 3)
+        # fuse_swiglu_u: the SwiGLU forward and the down adapter's u product in one stream over gu (round 3;
+        # bit-identical; 95.7 us against 50.4 + ~44 + 5 us unfused once silu uses the hardware reciprocal)
         self.fuse_swiglu_u = bool(fuse_swiglu_u)
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
             raise ValueError("dadb_splits must be four positive split counts")
@@ -628,10 +631,10 @@ class SimPOEngine:
         main.wait_stream(side)
 
     def _lora_grads(self, gs, x_in, dy, u, g, gbase, drop=None, skip_db=False, bits=None):
-        """dA = g_s^T . dropout(x_in)  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal).  dA is one
-        stream over x_in (ops.lora_da) with the dropout mask from the forward's keep bits (or re-hashed on
-        x_in: the forward keeps no masked copy); dB, when not fused into ospo_lora_gdb, is the f32-atomic
-        tile product."""
+        """dA = g_s^T . dropout(x_in)  -> rows [nmods*r, Kin];  dB = dy^T . u_s (block diagonal).  dA: the
+        f32-atomic tile product (or, da_stream, one stream over x_in: ops.lora_da), its dropout mask from the
+        forward's keep bits (else re-hashed on x_in: the forward keeps no masked copy); dB, when not fused into
+        ospo_lora_gdb, is the f32-atomic tile product."""
         r = self.layout.r
         Mk = self.Mk
         used = g.nmods * r

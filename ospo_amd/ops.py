@@ -254,11 +254,12 @@ def gemm_nt_mx8(a: MX8, b: MX8, out: torch.Tensor, *, a2=None, b2=None, alpha: f
 
 def gemm_f32acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a_kmajor: bool, b_kmajor: bool,
                 k_splits: int = 1, alpha: float = 1.0, diag: Optional[tuple] = None,
-                b_dropout: Optional[tuple] = None) -> torch.Tensor:
+                b_dropout: Optional[tuple] = None, keep_bits: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[M,N] (fp32) += alpha * op(a) . op(b)^T.
     a_kmajor: a is [K, M] else [M, K];  b_kmajor: b is [K, N] else [N, K].
     diag=(nblk, r): block-diagonal scatter (see include/ospo_hip.h).
-    b_dropout=(seed, p): LoRA dropout recomputed on the K-major b (lora_skinny's mask and scaling)."""
+    b_dropout=(seed, p): LoRA dropout recomputed on the K-major b (lora_skinny's mask and scaling), or read from
+    keep_bits (lora_skinny's keep-bit output of b, uint8 [K * N / 8]) when given."""
     _chk(a, BF16, "a")
     _chk(b, BF16, "b")
     _chk(out, torch.float32, "out")
@@ -270,8 +271,10 @@ def gemm_f32acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a_kmajor
     ldc = _ld(out) if not diag else 0
     if b_dropout is not None:
         seed, p = b_dropout
+        if keep_bits is not None and (keep_bits.dtype != torch.uint8 or keep_bits.numel() * 8 < K * N):
+            raise ValueError("gemm_f32acc: keep_bits must be uint8 with >= K*N/8 elements")
         call("ospo_gemm_f32acc_bdrop", _p(a), _ld(a), int(a_kmajor), _p(b), _ld(b), int(b_kmajor), M, N, K,
-             int(k_splits), float(alpha), _p(out), ldc, nblk, r, int(seed) & 0xFFFFFFFF, float(p), _s())
+             int(k_splits), float(alpha), _p(out), ldc, nblk, r, int(seed) & 0xFFFFFFFF, float(p), _p(keep_bits), _s())
         return out
     call("ospo_gemm_f32acc", _p(a), _ld(a), int(a_kmajor), _p(b), _ld(b), int(b_kmajor), M, N, K, int(k_splits),
          float(alpha), _p(out), ldc, nblk, r, _s())

@@ -158,6 +158,31 @@ def test_gemm_f32acc_dropout_recompute_equals_stored_mask(K, N, used, splits):
         assert relerr(out, ref) < 1e-6
 
 
+@pytest.mark.parametrize("K,N,used,splits,M", [(4800, 4096, 48, 8, 4800), (4800, 11008, 16, 4, 4744),
+                                                (640, 256, 32, 1, 600)])
+def test_gemm_f32acc_dropout_keep_bits_equal_rehash(K, N, used, splits, M):
+    """dA's tile product with the mask read from the forward's keep bits == re-hashed: bit-exact with one
+    split, reassociation-close with atomics; rows >= M (zero g) contribute nothing whatever their bits."""
+    p, seed = 0.05, 24680
+    x = rnd(K, N)
+    g = rnd(K, 64)
+    g[M:] = 0
+    bits = torch.full((K * N // 8,), 0xFF, device=DEV, dtype=torch.uint8)
+    ops().lora_skinny(x, torch.zeros(64, N, device=DEV, dtype=torch.bfloat16),
+                      torch.empty(K, 64, device=DEV, dtype=torch.bfloat16), M, K, N, 1, 0, 1.0, b_rows=16,
+                      dropout=(seed, p), keep_bits=bits)
+    for sp in (1, splits):
+        ref = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+        ops().gemm_f32acc(g[:, :used], x, ref, a_kmajor=True, b_kmajor=True, k_splits=sp, b_dropout=(seed, p))
+        out = torch.zeros(used, N, device=DEV, dtype=torch.float32)
+        ops().gemm_f32acc(g[:, :used], x, out, a_kmajor=True, b_kmajor=True, k_splits=sp, b_dropout=(seed, p),
+                          keep_bits=bits)
+        if sp == 1:
+            assert torch.equal(out, ref)
+        else:
+            assert relerr(out, ref) < 1e-6
+
+
 def test_gemm_f32acc_blockdiag_scatter():
     """dB of a packed q|k|v LoRA: keep only the diagonal blocks, peft layout."""
     r, nblk, nm = 16, 256, 3
