@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r3p2}
+TAG=${TAG:-r3p3}
 timeout -k 10 300 python -u -m pytest tests/test_gpu_mx8.py -q -p no:cacheprovider --timeout 200 --timeout-method thread -k rejects > gpurun_out/${TAG}_t.log 2>&1 || { echo "TEST FAILED"; tail -20 gpurun_out/${TAG}_t.log; exit 1; }
 tail -1 gpurun_out/${TAG}_t.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "SMOKE FAILED"; tail gpurun_out/${TAG}_smoke.log; exit 1; }

@@ -25,7 +25,7 @@ def short(k):
 
 
 def load(tag):
-    f = glob.glob(os.path.join(src, tag, "**", "*counter_collection.csv"), recursive=True)[0]
+    f = max(glob.glob(os.path.join(src, tag, "**", "*counter_collection.csv"), recursive=True), key=os.path.getmtime)
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(dict)
     for r in csv.DictReader(open(f)):

@@ -16,7 +16,7 @@ src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pm
 
 
 def load(tag):
-    f = glob.glob(os.path.join(src, tag, "**", "*counter_collection.csv"), recursive=True)[0]
+    f = max(glob.glob(os.path.join(src, tag, "**", "*counter_collection.csv"), recursive=True), key=os.path.getmtime)
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     n = collections.Counter()
     for r in csv.DictReader(open(f)):
