@@ -544,58 +544,47 @@ class SimPOEngine:
                         mx=self._mxo(D))
         scale_attn = 1.0 / math.sqrt(hd)
         lay = self.layout
-        # LoRA weight grads (dA = g^T x, dB = dy^T u) of each group run on a side stream,
-        # under the dX GEMMs; events guard every buffer the side stream reads before the
-        # main stream rewrites it (g buffer per group, dy buffers, next layer).
+        # LoRA weight grads (dA = g^T x, dB = dy^T u) of a layer run on a side stream, enqueued once the
+        # layer's backward is on the main stream (one event each way per layer: an event record costs the
+        # recording stream ~3.5 us and a wait ~1.4 us, tools/event_cost_probe.py; per-group events cost
+        # ~0.4 ms per step).  Main waits before rewriting what pending side work reads: the g / dy copies of
+        # parity q (layer i+2's) at the start of layer i, dx copy 1-q (layer i+1's) before the input-norm
+        # backward that rewrites it.
         main, side = torch.cuda.current_stream(self.device), self._side
         side.wait_stream(main)
-        done = {}  # (group, layer parity) -> event after its dA/dB were enqueued on the side stream
+        done = {}  # layer parity -> event after that layer's side work was enqueued
 
-        def guard(name, par):  # main must not rewrite what group `name`'s pending dA/dB of parity `par` read
-            ev = done.pop((name, par), None)
+        def wait_done(par):
+            ev = done.pop(par, None)
             if ev is not None:
                 main.wait_event(ev)
-
-        def lora_grads_async(name, par, gs, x_in, dy, u, gbase, drop, skip_db=False):
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            bits = self._bits_bwd(i, name, drop, x_in.shape[1])
-            with torch.cuda.stream(side):
-                self._lora_grads(gs, x_in, dy, u, lay.groups[name], gbase, drop, skip_db, bits)
-            ev2 = torch.cuda.Event()
-            ev2.record(side)
-            done[(name, par)] = ev2
 
         for i in reversed(range(dims.n_layers)):
             a, lw, pk = self.acts[i], self.layers[i], self.packed[i]
             gbase = lay.layer_off(i)
             q = i % 2  # copy of every side-stream operand this layer writes
+            wait_done(q)  # layer i+2's side work read the copies this layer rewrites
             dx = self.dx2[q]  # gradient w.r.t. this layer's output (bf16)
             dgu, dxmid, dqkv = self.dgu2[q], self.dxmid2[q], self.dqkv2[q]
+            pending = []  # (group, g_s, x_in, dy, u, dropout, dB done on main)
             # ---- down_proj: out = xmid + h W_d^T + s (h A_d^T) B_d^T
             Acat, AcatT, Bcat, BT = pk["down"]
-            guard("down", q)  # g buffer copy q (layer i+2's down products read it)
             gs, fdb = self._lora_g_db(dx, lay.groups["down"], Bcat, BT, M, q, a["u_d"], gbase)
             dr = self._drop(i, "down")
             if self.fuse_swiglu_bwd:
-                guard("gu", q)  # dgu / g copy q
                 ops.gemm_nt_swiglu_bwd(dx[:M], lw["downT"], a["gu"][:M], dgu[:M], a2=gs[:M], b2=AcatT, dropout=dr)
-                lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr, fdb)
             else:
                 self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
                           keep_bits=self._bits_bwd(i, "down", dr, Fd))
-                lora_grads_async("down", q, gs, a["h"], dx, a["u_d"], gbase, dr, fdb)
-                guard("gu", q)  # dgu / g copy q
                 ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
+            pending.append(("down", gs, a["h"], dx, a["u_d"], dr, fdb))
             # ---- gate/up
             Acat, AcatT, Bcat, BT = pk["gu"]
             gs, fdb = self._lora_g_db(dgu, lay.groups["gu"], Bcat, BT, M, q, a["u_gu"], gbase)
             dr = self._drop(i, "gu")
             self._lin(dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
                       keep_bits=self._bits_bwd(i, "gu", dr, D))
-            lora_grads_async("gu", q, gs, a["xn2"], dgu, a["u_gu"], gbase, dr, fdb)
-            guard("o", q)  # dxmid / g copy q
+            pending.append(("gu", gs, a["xn2"], dgu, a["u_gu"], dr, fdb))
             ops.rmsnorm_bwd(self.dxn[:M], a["xmid"][:M], lw["ln_post"], a["rstd2"][:M], dxmid[:M],
                             dres=dx[:M], mx=self._mxo(D))
             # ---- o_proj
@@ -604,9 +593,8 @@ class SimPOEngine:
             dr = self._drop(i, "o")
             self._lin(dxmid[:M], lw["oT"], self.dattn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
                       keep_bits=self._bits_bwd(i, "o", dr, D))
-            lora_grads_async("o", q, gs, a["attn"], dxmid, a["u_o"], gbase, dr, fdb)
+            pending.append(("o", gs, a["attn"], dxmid, a["u_o"], dr, fdb))
             # ---- attention + RoPE
-            guard("qkv", q)  # dqkv / g copy q
             ops.flash_attn_bwd(a["qkv"], 0, D, 2 * D, a["attn"], self.dattn, a["lse"], self.delta_ws, self.ds_ws,
                                dqkv, S, T, H, hd, scale_attn, rope_cos=self.cos, rope_sin=self.sin,
                                mx=self._mxo(3 * D) if i > 0 else None)  # layer 0 runs no q|k|v dX GEMM
@@ -617,17 +605,27 @@ class SimPOEngine:
             if i > 0:
                 self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
                           keep_bits=self._bits_bwd(i, "qkv", dr, D))
-            lora_grads_async("qkv", q, gs, a["xn1"], dqkv, a["u_qkv"], gbase, dr, fdb)
+            pending.append(("qkv", gs, a["xn1"], dqkv, a["u_qkv"], dr, fdb))
+            # this layer's LoRA weight grads on the side stream (one event from main)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                for name, gs_, x_in, dy, u, dr_, fdb_ in pending:
+                    self._lora_grads(gs_, x_in, dy, u, lay.groups[name], gbase, dr_, fdb_,
+                                     self._bits_bwd(i, name, dr_, x_in.shape[1]))
+                if on_layer_grads is not None:  # this layer's dA/dB are the last side-stream work so far
+                    on_layer_grads(gbase, gbase + lay.per_layer)
+            ev2 = torch.cuda.Event()
+            ev2.record(side)
+            done[q] = ev2
             if i > 0:
-                guard("down", 1 - q)  # dx copy 1-q: layer i+1's down products read it
+                wait_done(1 - q)  # dx copy 1-q: layer i+1's side work read it
                 ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[1 - q][:M],
                                 dres=dxmid[:M], mx=self._mxo(D))
             # layer 0: the gradient w.r.t. its input (the text / image embeddings) feeds nothing that
             # trains -- the embedding tables and gen_aligner are frozen (train.py:148-216) -- so its q|k|v dX
             # GEMM and the input RMSNorm backward are not run
-            if on_layer_grads is not None:
-                with torch.cuda.stream(side):  # this layer's dA/dB are the last side-stream work so far
-                    on_layer_grads(gbase, gbase + lay.per_layer)
         main.wait_stream(side)
 
     def _lora_grads(self, gs, x_in, dy, u, g, gbase, drop=None, skip_db=False, bits=None):
