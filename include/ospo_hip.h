@@ -307,8 +307,12 @@ int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int
  *   g = s dy B      : A = dy [M, nmods*Nmod], Bt = BT [nmods*r, Nmod],
  *                     K = a_koff = Nmod, module_tiles = r / 16
  * K is split across workgroups; ws (>= ospo_lora_skinny_ws_bytes(M_out, K,
- * n_tiles) bytes, 16-B aligned) holds the fp32 partials that a second launch
- * sums.  Calls sharing a ws must be ordered (same stream).
+ * n_tiles) bytes, 16-B aligned) holds, after a 4 KiB head of per-row-block
+ * arrival counters, the fp32 partials; the last workgroup to arrive at a row
+ * block sums them in order (deterministic) and resets its counter.  The first
+ * 4 KiB of ws must be ZERO the first time it is used (hipMemset once at
+ * allocation); every call leaves them zero again.  Calls sharing a ws must be
+ * ordered (same stream).
  * drop_p > 0 (dense mode only): peft lora_dropout on A -- element (m, k) is kept
  * iff drop_hash(m*K + k, drop_seed) >= drop_p * 2^32 (common.h) and becomes
  * bf16(A / (1 - drop_p)); the masked A is also written to xd [M, ld_xd] when xd

@@ -20,6 +20,8 @@
 
 namespace {
 
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));  // the buffer intrinsics' 16-B operand
+
 // out[m][16j + c] = scale * sum_k A[m][j*a_koff + k] * Bt[16j + c][k]
 // grid (row blocks of 16, K splits).  Each workgroup reduces its K range; with
 // splits > 1 the fp32 partial tile goes to ws and skinny_reduce_kernel sums the
@@ -338,7 +340,8 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
                                                       float scale, bf16* __restrict__ out, int ldo, int out_cols,
                                                       float* __restrict__ ws, int M_pad, uint32_t dseed,
                                                       uint32_t dthresh, float dscale, uint8_t* __restrict__ kbits,
-                                                      bf16* __restrict__ hout = nullptr, int ldh = 0, int up_off = 0) {
+                                                      bf16* __restrict__ hout = nullptr, int ldh = 0, int up_off = 0,
+                                                      unsigned* __restrict__ cnt = nullptr) {
   using C = Sk3Cfg<NT>;
   constexpr int ABYTES = SWG ? 16384 : 8192;        // A image(s): gate and up under SWG
   constexpr int STAGE = C::STAGE + ABYTES - 8192;
@@ -447,12 +450,65 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
   }
   const int m = m0 + arow_l;
   const int ctot = 16 * tiles_total;
-  if (splits > 1) {
+  if (splits > 1 && !cnt) {  // fp32 partials; skinny2_reduce_kernel sums them
     if (m < M_pad) {
 #pragma unroll
       for (int j = 0; j < NT; ++j)
         *reinterpret_cast<f32x4*>(ws + ((long)z * M_pad + m) * ctot + 16 * (tbase + j) + 4 * g) = acc[j];
     }
+    return;
+  }
+  if (splits > 1) {
+    // The split sum in this launch (round 3; it was a separate reduce launch, ~5.7 us each): every workgroup
+    // stores its fp32 partial write-through (sc1) and takes a ticket on its row block's counter; the last of
+    // the row block's splits x modules workgroups reads all partials back (sc1 loads), sums them in split order
+    // (as skinny2_reduce_kernel, bit-identical), writes the bf16 rows and zeroes the counter for the next call.
+    // No release / acquire fence: sc1 stores are visible device-wide once acknowledged (vmcnt(0)), and sc1
+    // loads do not hit a stale line (cdna_hip_programming.md, the in-launch split-K hand-off).
+    const __amdgpu_buffer_rsrc_t rsW =
+        __builtin_amdgcn_make_buffer_rsrc((void*)ws, 0, (int)((long)splits * M_pad * ctot * 4), 0x00020000);
+    if (m < M_pad) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc[j]), rsW,
+                                               (uint32_t)((((long)z * M_pad + m) * ctot + 16 * (tbase + j) + 4 * g) * 4),
+                                               0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's partial acknowledged; every wave done with the ring (the flag reuses it)
+    unsigned* flag = reinterpret_cast<unsigned*>(smem);
+    if (threadIdx.x == 0) {
+      const unsigned total = gridDim.y * gridDim.z;
+      const unsigned t = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (t == total - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (*flag == 0u) return;
+    const int cq = out_cols / 4;
+    for (int it = threadIdx.x; it < 64 * cq; it += blockDim.x) {
+      const int r = it / cq, c = (it % cq) * 4;
+      const int mm = m0 + r;
+      if (mm >= M_out) continue;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (mm < M && c < ctot) {
+        for (int z0 = 0; z0 < splits; z0 += 8) {  // 8 partials in flight, summed in split order
+          u32x4v pv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (z0 + u < splits)
+              pv[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                  rsW, (uint32_t)((((long)(z0 + u) * M_pad + mm) * ctot + c) * 4), 0, 16);
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (z0 + u < splits) v += __builtin_bit_cast(f32x4, pv[u]);
+        }
+      }
+      uint2 pk;
+      pk.x = pack2(v[0] * scale, v[1] * scale);
+      pk.y = pack2(v[2] * scale, v[3] * scale);
+      *reinterpret_cast<uint2*>(out + (long)mm * ldo + c) = pk;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   if (m < M_out) {
@@ -841,6 +897,14 @@ static int skinny_splits(int M_out, int K) {
   return s;
 }
 
+// skinny workspace head: one counter per 64-row block for the in-launch split sum (M_out <= 65536)
+constexpr int SK_CNT_BYTES = 4096;
+#ifdef OSPO_ABLATION
+static bool g_sk_reduce_launch = getenv("OSPO_SK_REDUCE_LAUNCH") != nullptr;  // A/B: the separate reduce kernel
+#else
+constexpr bool g_sk_reduce_launch = false;
+#endif
+
 struct SkDropArgs {
   uint32_t seed = 0, thresh = 0;
   float scale = 0.f;  // > 0: dropout on
@@ -899,7 +963,7 @@ extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
     const size_t b = sp3 > 1 ? (size_t)sp3 * (size_t)((M_out + 63) / 64 * 64) * 16 * n_tiles * 4 : 0;
     v2 = b > v2 ? b : v2;
   }
-  return (v1 > v2 ? v1 : v2) + 16;
+  return (v1 > v2 ? v1 : v2) + 16 + SK_CNT_BYTES;  // + the row-block counters at the head
 }
 
 #ifdef OSPO_ABLATION
@@ -945,11 +1009,12 @@ static int launch_skinny2(const bf16* a, int lda, const bf16* b, int ldb, int b_
 
 // v3 split: ~2 workgroups per CU over (64-row blocks x modules), whole 64-k chunks per split.
 // SWG: a = gu (gate | up, up at column K), the SwiGLU product h written to hout on the way
+// ws: [row-block counters: SK_CNT_BYTES][fp32 partials] (the counters are zero between calls)
 template <int NT, bool SWG = false>
 static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_rows, int M, int M_out, int K,
                           int a_koff, int nz, int tiles_total, float scale, bf16* o, int ldo, int out_cols, float* part,
                           size_t ws_bytes, hipStream_t stream, const SkDropArgs& dr, bf16* hout = nullptr,
-                          int ldh = 0) {
+                          int ldh = 0, unsigned* cnt = nullptr) {
   const int blocks = (M_out + 63) / 64 * nz;
   const int chunks = K / 64;
   int splits = (g_sk3_wgs + blocks - 1) / blocks;
@@ -963,16 +1028,18 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   const long b_bytes = (long)(b_rows - 1) * ldb * 2 + (long)K * 2;
   if (a_bytes >= (1L << 31)) return OSPO_ERR_SHAPE;  // 32-bit buffer offsets
   const dim3 grid(M_pad / 64, splits, nz);
+  // the split sum in the launch (last arriver per row block) unless the ablation build asks for the reduce kernel
+  unsigned* c = (splits > 1 && M_pad / 64 <= SK_CNT_BYTES / 4 && !g_sk_reduce_launch) ? cnt : nullptr;
   if (dr.scale > 0.f)
     hipLaunchKernelGGL((skinny3_kernel<NT, true, SWG>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb,
                        b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part,
-                       M_pad, dr.seed, dr.thresh, dr.scale, dr.bits, hout, ldh, K * 2);
+                       M_pad, dr.seed, dr.thresh, dr.scale, dr.bits, hout, ldh, K * 2, c);
   else
     hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb,
                        b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part,
-                       M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2);
+                       M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2, c);
   OSPO_CHECK_LAUNCH();
-  if (splits > 1) {
+  if (splits > 1 && !c) {
     const long n = (long)M_out * (out_cols / 4);
     if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
     hipLaunchKernelGGL(skinny2_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, part, splits,
@@ -1045,7 +1112,10 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)Bt;
   bf16* o = (bf16*)out;
-  f32x4* part = (f32x4*)ws;
+  // ws head: the skinny kernel's row-block counters (zero between calls); partials after it
+  unsigned* cnt = (unsigned*)ws;
+  f32x4* part = (f32x4*)((char*)ws + SK_CNT_BYTES);
+  ws_bytes -= SK_CNT_BYTES;
   const bool sk3_ok = K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
                       (long)(M - 1) * lda * 2 + (long)(nmods * (a_koff > 0 ? a_koff : 0) + K) * 2 < (1L << 31) &&
                       (long)b_rows * ldb * 2 < (1L << 31);
@@ -1054,14 +1124,14 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
   if (g_skinny_variant == 4 && sk3_ok && out_cols % 4 == 0 && !dr.xd) {  // (the masked-copy output is v2's)
     const int nz = a_koff > 0 ? nmods : 1;
     const int nt = a_koff > 0 ? module_tiles : n_tiles;
-    float* p2 = (float*)ws;
+    float* p2 = (float*)part;
     switch (nt) {
-      case 1: return launch_skinny3<1>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
-      case 2: return launch_skinny3<2>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
-      case 3: return launch_skinny3<3>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
-      case 4: return launch_skinny3<4>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
-      case 6: return launch_skinny3<6>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
-      case 8: return launch_skinny3<8>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
+      case 1: return launch_skinny3<1>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, nullptr, 0, cnt);
+      case 2: return launch_skinny3<2>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, nullptr, 0, cnt);
+      case 3: return launch_skinny3<3>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, nullptr, 0, cnt);
+      case 4: return launch_skinny3<4>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, nullptr, 0, cnt);
+      case 6: return launch_skinny3<6>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, nullptr, 0, cnt);
+      case 8: return launch_skinny3<8>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, nullptr, 0, cnt);
       default: break;
     }
   }
@@ -1069,7 +1139,7 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
     // dense: one workgroup column over all n-tiles; block-diagonal: grid z = module
     const int nz = a_koff > 0 ? nmods : 1;
     const int nt = a_koff > 0 ? module_tiles : n_tiles;
-    float* p2 = (float*)ws;
+    float* p2 = (float*)part;
     switch (nt) {
       case 1: return launch_skinny2<1>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
       case 2: return launch_skinny2<2>(a, lda, b, ldb, b_rows, M, M_out, K, a_koff, nz, n_tiles, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr);
@@ -1233,13 +1303,15 @@ extern "C" int ospo_swiglu_fwd_lora_down(const void* gu, int ld_gu, void* h, int
   const bf16* a = (const bf16*)gu;
   const bf16* b = (const bf16*)Bt;
   bf16* o = (bf16*)out;
-  float* p2 = (float*)ws;
+  unsigned* cnt = (unsigned*)ws;  // ws head: the row-block counters (see ospo_lora_skinny)
+  float* p2 = (float*)((char*)ws + SK_CNT_BYTES);
+  ws_bytes -= SK_CNT_BYTES;
   bf16* ho = (bf16*)h;
   switch (n_tiles) {
-    case 1: return launch_skinny3<1, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 1, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h);
-    case 2: return launch_skinny3<2, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 2, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h);
-    case 3: return launch_skinny3<3, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 3, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h);
-    case 4: return launch_skinny3<4, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 4, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h);
+    case 1: return launch_skinny3<1, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 1, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h, cnt);
+    case 2: return launch_skinny3<2, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 2, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h, cnt);
+    case 3: return launch_skinny3<3, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 3, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h, cnt);
+    case 4: return launch_skinny3<4, true>(a, ld_gu, b, ldb, b_rows, M, M_out, F, 0, 1, 4, scale, o, ldo, out_cols, p2, ws_bytes, stream, dr, ho, ld_h, cnt);
     default: return OSPO_ERR_UNSUPPORTED;
   }
 }

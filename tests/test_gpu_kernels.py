@@ -587,6 +587,29 @@ def test_lora_skinny_dropout(M, K, used):
     assert relerr(out.float(), ref) < 8e-3
 
 
+def test_lora_skinny_split_sum_in_launch_leaves_counters_zero():
+    """The u product's split sum runs in the launch (last arriver per row block, write-through partials): the
+    same ws serves calls of different shapes back to back, results are deterministic, and the row-block
+    counters at the ws head are zero after every call (the next call's precondition)."""
+    ws = ops().lora_skinny_ws(4864, 11008, 8, DEV)
+    outs = []
+    for M, K, used in [(4800, 4096, 48), (4800, 11008, 16), (4800, 4096, 48), (600, 4096, 32), (4800, 4096, 48)]:
+        torch.manual_seed(K + used)
+        x = rnd(M, K)
+        A = torch.zeros(64, K, device=DEV, dtype=torch.bfloat16)
+        A[:used] = rnd(used, K, s=0.05)
+        M_out = (M + 63) // 64 * 64
+        out = torch.full((M_out, 64), 7.0, device=DEV, dtype=torch.bfloat16)
+        ops().lora_skinny(x, A, out, M, M_out, K, (used + 15) // 16, 0, 2.0, b_rows=used, ws=ws)
+        torch.cuda.synchronize()
+        assert torch.all(ws[:1024] == 0), "row-block counters not reset"
+        ref = 2.0 * (x.float() @ A[:used].float().T)
+        assert relerr(out[:M, :used].float(), ref) < 8e-3
+        assert torch.all(out[M:] == 0) and torch.all(out[:M, 16 * ((used + 15) // 16):] == 0)
+        outs.append(out.clone())
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[0], outs[4])
+
+
 @pytest.mark.parametrize("M,K,used", [(4800, 4096, 48), (4800, 11008, 16), (130, 4096, 32), (600, 4096, 96)])
 def test_lora_skinny_dropout_streamed(M, K, used):
     """The step's form (no masked copy requested): the LDS-line streaming kernel masks x in registers."""
