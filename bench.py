@@ -155,7 +155,7 @@ def bench_t2i(args):
     w = synthetic_weights(dims, dev, seed=0, lora_seed=1)
     vw = {**synthetic_vq_weights(0), **synthetic_vq_decoder_weights(1)}  # gen_vision_model (pixel decoder)
     gen = T2IGenerator(dims, w, device=dev, max_batch=B, max_prompt_len=Lp, n_img_tokens=N, cfg_weight=5.0,
-                       temperature=1.0, vq_weights=vw)
+                       temperature=1.0, vq_weights=vw, fused_layers=not args.t2i_unfused)
     del w
     torch.cuda.empty_cache()
     g = torch.Generator().manual_seed(0)
@@ -206,7 +206,10 @@ def bench_t2i(args):
                    "vq_decode_ms_per_batch": round(decode_ms, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                      "frac": round(achieved / 8000.0, 4), "traffic": None,
-                     "kernel": "decode step (hipGraph: 30 x (4 decode_gemv + attn_cache + norms) + gen_head + sampler)",
+                     "kernel": ("decode step (hipGraph: 30 x (4 decode_linear + attn_cache) + gen_head + sampler)"
+                                if gen.fused else
+                                "decode step (hipGraph: 30 x (4 decode_gemv + split sums + attn_cache + norms) + gen_head"
+                                " + sampler)"),
                      "algorithmic_bytes_per_step": round(nbytes), "avg_step_us": round(step_ms * 1e3, 1)},
         "tokens_checksum": int(tok.long().sum().item()),
         "pixels_checksum": int(imgs.long().sum().item()),
@@ -458,6 +461,7 @@ def main():
     ap.add_argument("--vq-batch", type=int, default=16)
     ap.add_argument("--t2i-batch", type=int, default=16)       # parallel_size: prompts (x2 rows with CFG)
     ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
+    ap.add_argument("--t2i-unfused", action="store_true")      # A/B: the round-2 decode step (GEMV + split-sum + norm launches)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--wgrad-wgs", type=int, default=0)  # A/B: LoRA weight grads as ospo_lora_wgrad streams

@@ -419,6 +419,27 @@ int ospo_decode_gemv_kv(const void* W, int ldw, const void* X, int ldx, int R, i
 int ospo_decode_gemv_swiglu(const void* W, int ldw, const void* X, int ldx, int R, int F, int K, void* ws,
                             size_t ws_bytes, void* h, int ldh, hipStream_t stream);
 
+/* One Linear of the decode step in ONE launch (round 3; image_generation.py:132-171 through HF
+ * LlamaDecoderLayer): W tiled (ospo_decode_gemv with ldw = 0), R <= 32, N % 128 == 0, K % 32 == 0.
+ *   input: X, or with ss_in the RMSNorm of X folded in: xn = bf16(ln_w * bf16(X * rsqrt(ss / K + eps)))
+ *     as ospo_rmsnorm_fwd, ss[r] = sum over g < ss_groups of ss_in[g * 32 + r] (the row sums of squares
+ *     a DL_PLAIN producer wrote, one per 128-column group, ss_groups <= 32; summed in group order);
+ *   epi 0 (plain):  out[r][n] = act(X . W^T + bias) (+ residual) as ospo_decode_gemv; with ss_out also
+ *     ss_out[n/128 * 32 + r] = sum over the group's 128 columns of out^2 (the next RMSNorm's input);
+ *   epi 1 (kv):     N = 3 H 128: q (to out, ldo >= H 128) and the k / v cache rows at *pos_dev, RoPE as
+ *     ospo_kv_store (== ospo_decode_gemv_kv);
+ *   epi 2 (swiglu): W's 128-row group g = gate rows 64g .. 64g + 63, then up rows F + 64g .. (F = N / 2;
+ *     ospo_amd.ops.interleave_gate_up); out[r][64g + c] = bf16(bf16(silu(gate)) * up) (== ospo_swiglu_fwd).
+ * The K split is summed inside the launch (the last workgroup per 128-row group, in split order).
+ * ws >= ospo_decode_linear_ws_bytes(R, N, K): a 4 KiB head of counters that must be ZERO the first time
+ * it is used (every call leaves them zero), then the fp32 partials.  Calls sharing a ws are ordered. */
+size_t ospo_decode_linear_ws_bytes(int R, int N, int K);
+int ospo_decode_linear(const void* W, const void* X, int ldx, int R, int N, int K, const float* ss_in,
+                       int ss_groups, const void* ln_w, float eps, int epi, const void* bias, int gelu,
+                       const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* pos_dev,
+                       const void* rope_cos, const void* rope_sin, void* k_cache, void* v_cache, int n_heads,
+                       int Tmax, void* ws, size_t ws_bytes, hipStream_t stream);
+
 /* ------------------------------------------------------- VQ image tokenizer ---
  * janus/models/vq_model.py Encoder (:46-124) + quant_conv + VectorQuantizer
  * (:236-282) = gen_vision_model.encode, called per image at ospo/wrapper/train.py:246-264.  fp32

@@ -72,6 +72,8 @@ SIGNATURES = {
     "ospo_decode_gemv_kv": [P, I, P, I, I, I, I, I, P, Z, P, P, P, P, P, I, P, I, P],
     "ospo_decode_gemv_swiglu": [P, I, P, I, I, I, I, P, Z, P, I, P],
     "ospo_decode_gemv": [P, I, P, I, I, I, I, P, I, P, I, P, I, P, Z, P],
+    "ospo_decode_linear_ws_bytes": [I, I, I],
+    "ospo_decode_linear": [P, P, I, I, I, I, P, I, P, F, I, P, I, P, I, P, I, P, P, P, P, P, P, I, I, P, Z, P],
     "ospo_kv_store": [P, I, I, I, P, I, P, P, P, P, I, I, I, P, I, P],
     "ospo_attn_cache": [P, I, P, P, I, I, I, I, I, P, P, F, P, I, P],
     "ospo_cfg_sample": [P, I, I, I, F, F, P, P, I, P, P, P, P],
@@ -97,7 +99,7 @@ ABLATION_SIGNATURES = {"ospo_set_gemm_variant": [I], "ospo_set_gemv_variant": [I
                        "ospo_set_skinny_variant": [I], "ospo_gemm_set_debug_buffer": [P],
                        "ospo_attn_set_stamps": [P]}
 
-RESTYPES = {"ospo_gemm_nt_ws_bytes": c_size_t, "ospo_row_dot_sum_ws_bytes": c_size_t, "ospo_lora_gdb_ws_bytes": c_size_t, "ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
+RESTYPES = {"ospo_gemm_nt_ws_bytes": c_size_t, "ospo_row_dot_sum_ws_bytes": c_size_t, "ospo_lora_gdb_ws_bytes": c_size_t, "ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_decode_linear_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 

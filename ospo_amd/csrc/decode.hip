@@ -602,6 +602,238 @@ __global__ __launch_bounds__(256) void attn_cache2_kernel(const bf16* __restrict
   }
 }
 
+// ------------------------------------------------ fused decode Linear (round 3)
+// ospo_decode_linear: one launch per Linear of the decode step (the round-2 step ran each as a GEMV, a
+// split-sum launch and, before q|k|v and gate|up, an RMSNorm launch: ~10 launches of 5-13 us per layer,
+// most of them ramp).  gemv3's weight stream (tiled layout, 128 rows per workgroup, K split over
+// gridDim.y), plus:
+//  * NORM: the RMSNorm of the input folded into the x staging.  X is the PRE-norm residual stream; its
+//    row sums of squares come from the producer's epilogue (ss_in [ss_groups][32]: one partial per
+//    128-column group), summed here in group order; xn = bf16(w * bf16(x * rsqrt(ss / K + eps))) is
+//    formed in LDS once per 512-k chunk, rounded as rmsnorm_fwd rounds it.
+//  * the split sum in the launch: every workgroup stores its fp32 partial write-through (sc1) and takes a
+//    ticket on its row group's counter (workspace head, zero at allocation); the last arriver sums the
+//    partials in split order (gemv2_reduce_kernel's order) and runs the consumer:
+//      DL_PLAIN   out = act(v + bias) (+ residual) as gemv_store, and, with ss_out, the row sums of
+//                 squares of out over the group's 128 columns (ss_out [N/128][32]) for the next RMSNorm;
+//      DL_KV      RoPE + KV-cache store of one head slice (row group = head slice; as gemv_reduce_kv);
+//      DL_SWIGLU  h = bf16(bf16(silu(gate)) * up) from a gate|up weight whose row group g holds gate rows
+//                 64g .. 64g+63 then up rows F + 64g .. (ops.interleave_gate_up); out cols 64g .. +63.
+//    The last arriver zeroes its counter again.  No fence: sc1 stores are visible device-wide once
+//    acknowledged (vmcnt(0) before the ticket) and sc1 loads do not hit a stale line.
+enum { DL_PLAIN = 0, DL_KV = 1, DL_SWIGLU = 2 };
+constexpr int DL_CNT_BYTES = 4096;  // workspace head: one counter per 128-row group (N <= 131072)
+struct DlArgs {
+  const bf16* W;
+  const bf16* X;
+  int ldx, R, K, kper;
+  const float* ss_in;
+  int ss_groups;
+  const bf16* ln_w;
+  float eps;
+  const bf16* bias;
+  int gelu;
+  const bf16* res;
+  int ldr;
+  bf16* out;
+  int ldo;
+  float* ss_out;
+  const int* pos;
+  const bf16* cs;
+  const bf16* sn;
+  bf16* kc;
+  bf16* vc;
+  int H, Tmax;
+  float* part;
+  unsigned* cnt;
+  int part_bytes;
+};
+
+template <int NT, int EPI, bool NORM>
+__global__ __launch_bounds__(64 * G3_WAVES) void dlin_kernel(const DlArgs a) {
+  static_assert(16 * NT * G2_PITCH >= 16 * NT * 129 * 4, "epilogue tile fits the x staging");
+  __shared__ __attribute__((aligned(16))) char xs[16 * NT * G2_PITCH];
+  __shared__ float rs[32];
+  __shared__ float sst[NORM ? 1024 : 1];
+  __shared__ float ssr[G3_WAVES][32];
+  __shared__ unsigned flag;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int n = blockIdx.x * G3_ROWS + wave * 16 + l16;
+  const int z = blockIdx.y, splits = gridDim.y;
+  const int K = a.K, R = a.R;
+  const int k_begin = z * a.kper, k_end = min(K, k_begin + a.kper);
+  const bf16* wrow = a.W + ((long)(n >> 4) * (K >> 5) * 64 + lane) * 8;
+  // NORM: the producer's ss partials (<= 32 groups x 32 rows) are loaded here, two per thread, and only
+  // used after the first chunk's wait: a serial per-group load chain in one wave cost ~20 us per launch
+  float ssv[2] = {0.f, 0.f};
+  if constexpr (NORM) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = threadIdx.x + 512 * u;
+      if (i < a.ss_groups * 32) ssv[u] = a.ss_in[i];
+    }
+  }
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6;  // NORM: 8 columns x rows tr, tr + 8, ...
+  for (int kc = k_begin; kc < k_end; kc += G2_KC) {
+    const int nsteps = min(G2_KC, k_end - kc) >> 5;
+    for (int r = wave; r < 16 * NT; r += G3_WAVES) {
+      const int rr = r < R ? r : R - 1;
+      const int col = min(kc + 8 * lane, K - 8);
+      __builtin_amdgcn_global_load_lds(a.X + (long)rr * a.ldx + col, (LDS_AS void*)(xs + r * G2_PITCH), 16, 0, 0);
+    }
+    u32x4 lw = u32x4{0u, 0u, 0u, 0u};
+    if constexpr (NORM) lw = *reinterpret_cast<const u32x4*>(a.ln_w + min(kc + 8 * tc, K - 8));
+    asm volatile("" ::: "memory");  // x DMA (+ the norm weights) before the weight loads: vmcnt(16) covers them
+    bf16x8 wv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) wv[s] = *reinterpret_cast<const bf16x8*>(wrow + (long)((kc >> 5) + min(s, nsteps - 1)) * 512);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __syncthreads();
+    if constexpr (NORM) {
+      if (kc == k_begin) {  // rstd of the 32 rows: the partials summed in group order
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (threadIdx.x + 512 * u < 1024) sst[threadIdx.x + 512 * u] = ssv[u];
+        __syncthreads();
+        if (threadIdx.x < 32) {
+          float s = 0.f;
+          for (int q = 0; q < a.ss_groups; ++q) s += sst[q * 32 + threadIdx.x];
+          rs[threadIdx.x] = rsqrtf(s / (float)K + a.eps);
+        }
+        __syncthreads();
+      }
+      float wf[8];
+      unpack8(lw, wf);
+#pragma unroll
+      for (int i = 0; i < 2 * NT; ++i) {
+        const int r = tr + 8 * i;
+        u32x4* p = reinterpret_cast<u32x4*>(xs + r * G2_PITCH + tc * 16);
+        float f[8];
+        unpack8(*p, f);
+        const float rr = rs[r < R ? r : R - 1];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) f[q] = wf[q] * round_bf(f[q] * rr);
+        *p = pack8(f);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < nsteps) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          bf16x8 xf = *reinterpret_cast<const bf16x8*>(xs + (16 * j + l16) * G2_PITCH + (32 * s + 8 * g) * 2);
+          if (16 * j + l16 >= R) xf = bf16x8{};
+          acc[j] = MFMA(xf, wv[s], acc[j]);  // D[x row 4g+q][w row l16]
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int nb = n >> 4, NB = gridDim.x * G3_WAVES;
+  if (splits > 1) {
+    const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, a.part_bytes, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j]), rsP,
+                                             (uint32_t)((((z * NB + nb) * NT + j) * 64 + lane) * 16), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(a.cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag = (t == (unsigned)splits - 1u) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (flag == 0u) return;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int z0 = 0; z0 < splits; z0 += 8) {  // 8 partials in flight, summed in split order
+        u32x4 pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (z0 + u < splits)
+            pv[u] = __builtin_amdgcn_raw_buffer_load_b128(rsP, (uint32_t)(((((z0 + u) * NB + nb) * NT + j) * 64 + lane) * 16),
+                                                          0, 16);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (z0 + u < splits) v += __builtin_bit_cast(f32x4, pv[u]);
+      }
+      acc[j] = v;
+    }
+  }
+  if constexpr (EPI == DL_PLAIN) {
+    float ssq[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * j + 4 * g + q;
+        float y = acc[j][q] + (a.bias ? bf2f(a.bias[n]) : 0.f);
+        if (a.gelu) y = gelu_erf(round_bf(y));
+        if (a.res) y = round_bf(y) + bf2f(a.res[(long)(r < R ? r : 0) * a.ldr + n]);
+        y = round_bf(y);
+        if (r < R) a.out[(long)r * a.ldo + n] = f2bf(y);
+        ssq[j][q] = dpp_sum16(y * y);  // over the wave's 16 columns
+      }
+    if (a.ss_out) {
+      if (l16 == 0) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ssr[wave][16 * j + 4 * g + q] = ssq[j][q];
+      }
+      __syncthreads();
+      if (threadIdx.x < 16 * NT) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < G3_WAVES; ++w) s += ssr[w][threadIdx.x];
+        a.ss_out[blockIdx.x * 32 + threadIdx.x] = s;
+      }
+    }
+  } else {
+    // the group's 128 columns x 16 NT rows, bf16-rounded sums, through LDS (the x staging is free)
+    float* ep = reinterpret_cast<float*>(xs);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ep[(16 * j + 4 * g + q) * 129 + wave * 16 + l16] = round_bf(acc[j][q]);
+    __syncthreads();
+    if constexpr (EPI == DL_KV) {
+      const int hs = blockIdx.x, which = hs / a.H, h = hs % a.H;
+      const int p = *a.pos;
+      if (p < a.Tmax) {
+        for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
+          const int r = it >> 6, d = it & 63;
+          const float x1 = ep[r * 129 + d], x2 = ep[r * 129 + d + 64];
+          float o1 = x1, o2 = x2;
+          if (which < 2) {  // rotate-half RoPE, rounded per op as kv_store_kernel
+            const float c = bf2f(a.cs[(long)p * 64 + d]), sv = bf2f(a.sn[(long)p * 64 + d]);
+            o1 = round_bf(x1 * c) + round_bf(-x2 * sv);
+            o2 = round_bf(x2 * c) + round_bf(x1 * sv);
+          }
+          bf16* dst = which == 0 ? a.out + (long)r * a.ldo + h * HD
+                                 : (which == 1 ? a.kc : a.vc) + (((long)r * a.H + h) * a.Tmax + p) * HD;
+          dst[d] = f2bf(o1);
+          dst[d + 64] = f2bf(o2);
+        }
+      }
+    } else {
+      for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
+        const int r = it >> 6, c = it & 63;
+        const float gt = ep[r * 129 + c], up = ep[r * 129 + 64 + c];
+        a.out[(long)r * a.ldo + 64 * blockIdx.x + c] = f2bf(round_bf(silu(gt)) * up);
+      }
+    }
+  }
+  if (splits > 1 && threadIdx.x == 0) __hip_atomic_store(a.cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // --------------------------------------------------------- CFG + sampling
 // one workgroup per image b: logits rows 2b (cond) and 2b+1 (uncond) [V] bf16 (train.py-style
 // interleaving of image_generation.py:132-141, 156-157).  l = bf16(lu + bf16(w * bf16(lc - lu))),
@@ -853,6 +1085,65 @@ extern "C" int ospo_decode_gemv_swiglu(const void* W, int ldw, const void* X, in
   else
     hipLaunchKernelGGL((gemv_reduce_swiglu_kernel<2>), grid, dim3(256), 0, stream, (const f32x4*)ws, splits, R, F,
                        (bf16*)h, ldh);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" size_t ospo_decode_linear_ws_bytes(int R, int N, int K) {
+  if (R <= 0 || R > 32 || N <= 0 || N % G3_ROWS || N / G3_ROWS > DL_CNT_BYTES / 4 || K < 32 || K % 32) return 0;
+  const int kp = gemv3_kper(N, K), splits = (K + kp - 1) / kp;
+  return DL_CNT_BYTES + (size_t)splits * (N / 16) * ((R + 15) / 16) * 64 * sizeof(f32x4);
+}
+
+extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, int N, int K, const float* ss_in,
+                                  int ss_groups, const void* ln_w, float eps, int epi, const void* bias, int gelu,
+                                  const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* pos_dev,
+                                  const void* rope_cos, const void* rope_sin, void* k_cache, void* v_cache, int n_heads,
+                                  int Tmax, void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (!W || !X || !out || !ws) return OSPO_ERR_ARG;
+  const size_t need = ospo_decode_linear_ws_bytes(R, N, K);
+  if (need == 0 || ldx < K || ldx % 8) return OSPO_ERR_SHAPE;
+  if (ws_bytes < need) return OSPO_ERR_ARG;
+  if (!aligned16(W) || !aligned16(X) || !aligned16(ws)) return OSPO_ERR_ALIGN;
+  if (ss_in && (ss_groups <= 0 || !ln_w || !aligned16(ln_w) || !(eps >= 0.f))) return OSPO_ERR_ARG;
+  if (ss_in && ss_groups > 32) return OSPO_ERR_UNSUPPORTED;  // rows of <= 4096 columns (32 groups of 128)
+  if (epi == DL_PLAIN) {
+    if (ldo < N || (residual && ldr < N)) return OSPO_ERR_SHAPE;
+  } else if (epi == DL_KV) {
+    if (bias || gelu || residual || ss_out) return OSPO_ERR_UNSUPPORTED;
+    if (!pos_dev || !rope_cos || !rope_sin || !k_cache || !v_cache) return OSPO_ERR_ARG;
+    if (n_heads <= 0 || N != 3 * n_heads * HD || ldo < n_heads * HD || Tmax <= 0) return OSPO_ERR_SHAPE;
+  } else if (epi == DL_SWIGLU) {
+    if (bias || gelu || residual || ss_out) return OSPO_ERR_UNSUPPORTED;
+    if (ldo < N / 2) return OSPO_ERR_SHAPE;
+  } else {
+    return OSPO_ERR_ARG;
+  }
+  const int kper = gemv3_kper(N, K), splits = (K + kper - 1) / kper;
+  DlArgs a;
+  a.W = (const bf16*)W; a.X = (const bf16*)X; a.ldx = ldx; a.R = R; a.K = K; a.kper = kper;
+  a.ss_in = ss_in; a.ss_groups = ss_groups; a.ln_w = (const bf16*)ln_w; a.eps = eps;
+  a.bias = (const bf16*)bias; a.gelu = gelu; a.res = (const bf16*)residual; a.ldr = ldr;
+  a.out = (bf16*)out; a.ldo = ldo; a.ss_out = ss_out;
+  a.pos = pos_dev; a.cs = (const bf16*)rope_cos; a.sn = (const bf16*)rope_sin; a.kc = (bf16*)k_cache;
+  a.vc = (bf16*)v_cache; a.H = n_heads; a.Tmax = Tmax;
+  a.cnt = (unsigned*)ws; a.part = (float*)((char*)ws + DL_CNT_BYTES); a.part_bytes = (int)(need - DL_CNT_BYTES);
+  const dim3 grid(N / G3_ROWS, splits);
+  const bool norm = ss_in != nullptr;
+#define DLIN(NT_, EPI_)                                                                                             \
+  hipLaunchKernelGGL((norm ? dlin_kernel<NT_, EPI_, true> : dlin_kernel<NT_, EPI_, false>), grid, dim3(64 * G3_WAVES), \
+                     0, stream, a)
+#define DLIN_NT(EPI_) \
+  if (R <= 16) DLIN(1, EPI_); else DLIN(2, EPI_);
+  if (epi == DL_PLAIN) {
+    DLIN_NT(DL_PLAIN)
+  } else if (epi == DL_KV) {
+    DLIN_NT(DL_KV)
+  } else {
+    DLIN_NT(DL_SWIGLU)
+  }
+#undef DLIN_NT
+#undef DLIN
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

@@ -48,7 +48,7 @@ class T2IGenerator:
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_batch: int = 16,
                  max_prompt_len: int = 64, n_img_tokens: int = 576, cfg_weight: float = 5.0,
                  temperature: float = 1.0, pad_id: int = PAD_ID, vq_weights: Optional[Dict[str, torch.Tensor]] = None,
-                 tiled_weights: bool = True):
+                 tiled_weights: bool = True, fused_layers: bool = True):
         if dims.head_dim != 128:
             raise ValueError("head_dim must be 128 (Janus-Pro)")
         if 2 * max_batch > 64:
@@ -94,9 +94,15 @@ class T2IGenerator:
         def dw(t):
             return ops.tile_decode_weight(t) if self.tiled and t.shape[0] % 128 == 0 and t.shape[1] % 32 == 0 else t
 
+        # one launch per Linear (ops.decode_linear, round 3): the RMSNorms folded into the q|k|v and gate|up
+        # stagings, split sums and consumers in the launch; needs every decode weight tiled (N % 128)
+        Dg, Fa = dims.gen_head_dim, self.al_w2.shape[1]
+        self.fused = (bool(fused_layers) and self.tiled and all(n % 128 == 0 for n in (D, 3 * D, 2 * Fd, Dg))
+                      and dims.img_vocab % 128 == 0 and all(k % 32 == 0 for k in (D, Fd, Dg, Fa)))
         for lw in self.layers:
             for k in ("qkv", "o", "gu", "down"):
-                lw[k + "_d"] = dw(lw[k])
+                src = ops.interleave_gate_up(lw[k]) if (k == "gu" and self.fused) else lw[k]
+                lw[k + "_d"] = dw(src)
         self.gh_w1_d, self.gh_w2_d, self.al_w2_d = dw(self.gh_w1), dw(self.gh_w2), dw(self.al_w2)
         # ---- KV cache and decode-step buffers (R = 2 * max_batch rows)
         self.max_batch, self.max_prompt = max_batch, max_prompt_len
@@ -121,6 +127,13 @@ class T2IGenerator:
         self.gws = torch.zeros(max(ops.query("ospo_decode_gemv_ws_bytes", R, n, k) for n, k in shapes) // 4 + 4,
                                dtype=torch.float32, device=dev)
         self.cos, self.sin = ops.rope_tables(self.Tmax, 128, dims.rope_theta, dev)
+        if self.fused:
+            self.lws = torch.zeros(max(ops.query("ospo_decode_linear_ws_bytes", R, n, k) for n, k in shapes) // 4 + 4,
+                                   dtype=torch.float32, device=dev)
+            # row sums of squares of the residual stream for the folded RMSNorms: [D / 128, 32] per buffer
+            # (x, xo: the layer stack ping-pongs them; xmid)
+            self.ss_x, self.ss_xo, self.ss_mid = (torch.zeros(D // 128, 32, dtype=torch.float32, device=dev)
+                                                  for _ in range(3))
         self._graph = None
         self._graph_B = None
         self.probs = None  # [n, B, V] fp32 when record_probs
@@ -176,12 +189,20 @@ class T2IGenerator:
         self._head_and_sample(last, R)
 
     # ---------------------------------------------------------------- one step
-    def _head_and_sample(self, last: torch.Tensor, R: int):
-        """gen_head on the last position, CFG + sampling, next input embeds (aligner)."""
+    def _head_and_sample(self, last: torch.Tensor, R: int, ss: Optional[torch.Tensor] = None):
+        """gen_head on the last position, CFG + sampling, next input embeds (aligner).  ss: the row sums of
+        squares of ``last`` (fused path), so the final RMSNorm folds into gen_head's first Linear."""
         dims = self.dims
-        ops.rmsnorm_fwd(last, self.norm, self.hf[:R], self.rstd[:R], dims.rms_eps)
-        ops.decode_gemv(self.hf[:R], self.gh_w1_d, self.zg[:R], bias=self.gh_b1, gelu=True, ws=self.gws)
-        ops.decode_gemv(self.zg[:R], self.gh_w2_d, self.logits[:R], bias=self.gh_b2, ws=self.gws)
+        if self.fused and ss is not None:
+            ops.decode_linear(last, self.gh_w1_d, self.zg[:R], self.lws, norm=(ss, self.norm, dims.rms_eps),
+                              bias=self.gh_b1, gelu=True)
+        else:
+            ops.rmsnorm_fwd(last, self.norm, self.hf[:R], self.rstd[:R], dims.rms_eps)
+            ops.decode_gemv(self.hf[:R], self.gh_w1_d, self.zg[:R], bias=self.gh_b1, gelu=True, ws=self.gws)
+        if self.fused:
+            ops.decode_linear(self.zg[:R], self.gh_w2_d, self.logits[:R], self.lws, bias=self.gh_b2)
+        else:
+            ops.decode_gemv(self.zg[:R], self.gh_w2_d, self.logits[:R], bias=self.gh_b2, ws=self.gws)
         B = R // 2
         probs = None
         if self.probs is not None:
@@ -189,7 +210,10 @@ class T2IGenerator:
         ops.cfg_sample(self.logits[:R], B, self.cfg_weight, self.temperature, self.u, self.step, self.n_img,
                        self.tokens[:B], self.next_ids[:R], probs)
         ops.gen_aligner_in(self.next_ids[:R], self.gen_embed, self.al_w1, self.al_b1, self.e1[:R])
-        ops.decode_gemv(self.e1[:R], self.al_w2_d, self.x[:R], bias=self.al_b2, ws=self.gws)
+        if self.fused:  # the next step's input and its row sums of squares (layer 0's folded RMSNorm)
+            ops.decode_linear(self.e1[:R], self.al_w2_d, self.x[:R], self.lws, bias=self.al_b2, ss_out=self.ss_x)
+        else:
+            ops.decode_gemv(self.e1[:R], self.al_w2_d, self.x[:R], bias=self.al_b2, ws=self.gws)
         ops.decode_advance(self.pos, self.step)
 
     def _decode_step(self, R: int):
@@ -201,6 +225,9 @@ class T2IGenerator:
         g = self.gws
         x, xo = self.x[:R], self.xo[:R]
         D, Fd = dims.d_model, dims.d_ff
+        if self.fused:
+            self._decode_step_fused(R)
+            return
         fuse_qkv = ops.decode_gemv_fusable(R, 3 * D, D)  # split sum + RoPE/KV store in one kernel
         fuse_gu = ops.decode_gemv_fusable(R, 2 * Fd, D)  # split sum + SwiGLU in one kernel
         for i, lw in enumerate(self.layers):
@@ -224,6 +251,29 @@ class T2IGenerator:
             ops.decode_gemv(self.h[:R], lw["down_d"], xo, residual=self.xmid[:R], ws=g)
             x, xo = xo, x
         self._head_and_sample(x, R)
+
+    def _decode_step_fused(self, R: int):
+        """_decode_step in 5 launches per layer (ops.decode_linear): q|k|v with the input RMSNorm folded in
+        + RoPE / KV store, cached attention, o + residual (+ its row sums of squares), gate|up with the
+        post-attention RMSNorm folded in + SwiGLU, down + residual (+ row sums of squares)."""
+        dims = self.dims
+        H, eps = dims.n_heads, dims.rms_eps
+        scale = 1.0 / math.sqrt(128)
+        ws = self.lws
+        x, xo = self.x[:R], self.xo[:R]
+        ss, sso = self.ss_x, self.ss_xo
+        for i, lw in enumerate(self.layers):
+            ops.decode_linear(x, lw["qkv_d"], self.q[:R], ws, epi="kv", norm=(ss, lw["ln_in"], eps),
+                              kv=(self.pos, (self.cos, self.sin), self.kc[i], self.vc[i], H, self.Tmax))
+            ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos, scale,
+                           self.attn[:R])
+            ops.decode_linear(self.attn[:R], lw["o_d"], self.xmid[:R], ws, residual=x, ss_out=self.ss_mid)
+            ops.decode_linear(self.xmid[:R], lw["gu_d"], self.h[:R], ws, epi="swiglu",
+                              norm=(self.ss_mid, lw["ln_post"], eps))
+            ops.decode_linear(self.h[:R], lw["down_d"], xo, ws, residual=self.xmid[:R], ss_out=sso)
+            x, xo = xo, x
+            ss, sso = sso, ss
+        self._head_and_sample(x, R, ss)
 
     # ----------------------------------------------------------------- generate
     @torch.inference_mode()

@@ -662,6 +662,56 @@ def decode_gemv(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=Non
     return out
 
 
+DL_EPI = {"plain": 0, "kv": 1, "swiglu": 2}
+
+
+def decode_linear_ws(R: int, N: int, K: int, device) -> torch.Tensor:
+    """Workspace of ospo_decode_linear: zeroed (its 4 KiB counter head must start at zero; every call
+    leaves it zero)."""
+    nbytes = int(query("ospo_decode_linear_ws_bytes", R, N, K))
+    if nbytes == 0:
+        raise ValueError(f"decode_linear: unsupported shape R={R} N={N} K={K}")
+    return torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=device)
+
+
+def interleave_gate_up(gu: torch.Tensor) -> torch.Tensor:
+    """[gate; up] rows [2F, K] -> the order ospo_decode_linear's swiglu epilogue reads: 128-row group g =
+    gate rows 64g .. 64g+63, then up rows F + 64g .. (F % 64 == 0)."""
+    N, K = gu.shape
+    F = N // 2
+    if N % 128:
+        raise ValueError(f"interleave_gate_up: 2F = {N} must be a multiple of 128")
+    return gu.view(2, F // 64, 64, K).permute(1, 0, 2, 3).reshape(N, K).contiguous()
+
+
+def decode_linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, ws: torch.Tensor, *, epi: str = "plain",
+                  norm=None, bias=None, gelu: bool = False, residual=None, ss_out=None, kv=None) -> torch.Tensor:
+    """One decode-step Linear in one launch (ospo_decode_linear): w tiled (tile_decode_weight);
+    norm = (ss_in [G, 32] fp32, ln_w, eps) folds the RMSNorm of x into the staging; epi "plain" (bias,
+    gelu, residual, ss_out [N/128, 32]), "kv" (kv = (pos_dev, (cos, sin), k_cache, v_cache, n_heads,
+    Tmax); out = q) or "swiglu" (w from interleave_gate_up; out = h [R, N/2])."""
+    for t, nme in ((x, "x"), (w, "w"), (out, "out")):
+        _chk(t, BF16, nme)
+    R, K = x.shape
+    N, Kw, ldw = _decode_w(w)
+    if ldw != 0 or Kw != K:
+        raise ValueError(f"decode_linear needs a tiled weight with K = {K}, got {tuple(w.shape)}")
+    ss_in, ln_w, eps = norm if norm is not None else (None, None, 0.0)
+    if ss_in is not None and (ss_in.dtype != torch.float32 or not ss_in.is_contiguous()):
+        raise ValueError("decode_linear: ss_in must be contiguous fp32 [groups, 32]")
+    if ss_out is not None and (ss_out.dtype != torch.float32 or ss_out.numel() < N // 128 * 32):
+        raise ValueError("decode_linear: ss_out must be fp32 with N/128 x 32 entries")
+    pos = cs = sn = kc = vc = None
+    H = Tmax = 0
+    if kv is not None:
+        pos, (cs, sn), kc, vc, H, Tmax = kv
+    call("ospo_decode_linear", _p(w), _p(x), _ld(x), R, N, K, _p(ss_in), 0 if ss_in is None else ss_in.numel() // 32,
+         _p(ln_w), float(eps), DL_EPI[epi], _p(bias), int(gelu), _p(residual),
+         _ld(residual) if residual is not None else 0, _p(out), _ld(out), _p(ss_out), _p(pos), _p(cs), _p(sn), _p(kc),
+         _p(vc), H, Tmax, _p(ws), ws.numel() * 4, _s())
+    return out
+
+
 def decode_gemv_fusable(R: int, N: int, K: int) -> bool:
     return bool(query("ospo_decode_gemv_fusable", R, N, K))
 

@@ -381,10 +381,129 @@ def test_generate_tiled_weights_same_tokens():
     toks = []
     for tiled in (True, False):
         gen = T2IGenerator(ModelDims.from_any(dims), w, device=DEV, max_batch=4, max_prompt_len=16, n_img_tokens=24,
-                           cfg_weight=5.0, temperature=1.0, pad_id=7, tiled_weights=tiled)
-        assert gen.tiled == tiled
+                           cfg_weight=5.0, temperature=1.0, pad_id=7, tiled_weights=tiled, fused_layers=False)
+        assert gen.tiled == tiled and not gen.fused
         if tiled:
             assert any(lw["gu_d"].dim() == 3 for lw in gen.layers)
         toks.append(gen.generate(prompts, seed=5, use_graph=False).cpu().clone())
         toks.append(gen.generate(prompts, seed=5, use_graph=True).cpu().clone())
     assert all(torch.equal(t, toks[0]) for t in toks[1:])
+
+
+@pytest.mark.parametrize("R", [32, 12])
+def test_decode_linear_equals_unfused(R):
+    """ops.decode_linear (one launch per Linear: split sum + consumer in the launch) writes exactly what
+    the GEMV + split-sum launches write -- plain with bias / residual, q|k|v + RoPE / KV store, gate|up
+    (interleaved rows) + SwiGLU; its row sums of squares equal the output's; the folded RMSNorm matches
+    rmsnorm_fwd + GEMV (the sum of squares runs in another order: rstd may move by an ulp); the counter
+    head of the workspace is zero after every call."""
+    H, D, F, Tmax, p, eps = 32, 4096, 11008, 96, 37, 1e-6
+    torch.manual_seed(R)
+    x = torch.randn(R, D, device=DEV).bfloat16()
+    xr = torch.randn(R, D, device=DEV).bfloat16()
+    wo = (torch.randn(D, D, device=DEV) * 0.02).bfloat16()
+    wq = (torch.randn(3 * D, D, device=DEV) * 0.02).bfloat16()
+    wg = (torch.randn(2 * F, D, device=DEV) * 0.02).bfloat16()
+    wd = (torch.randn(D, F, device=DEV) * 0.02).bfloat16()
+    b = torch.randn(D, device=DEV).bfloat16()
+    lnw = (1 + 0.1 * torch.randn(D, device=DEV)).bfloat16()
+    T = ops().tile_decode_weight
+    wo_t, wq_t, wd_t = T(wo), T(wq), T(wd)
+    wg_t, wgi_t = T(wg), T(ops().interleave_gate_up(wg))
+    gws = torch.zeros(max(ops().decode_gemv_ws(R, n, k, DEV).numel() for n, k in ((2 * F, D), (3 * D, D), (D, F))),
+                      device=DEV)
+    lws = torch.zeros(max(ops().decode_linear_ws(R, n, k, DEV).numel() for n, k in ((2 * F, D), (3 * D, D), (D, F))),
+                      device=DEV)
+    z = lambda *sh: torch.zeros(*sh, dtype=torch.bfloat16, device=DEV)  # noqa: E731
+
+    def heads_zero():
+        assert torch.all(lws[:1024] == 0)
+
+    # plain: o + residual (+ ss), down + residual, bias + gelu
+    for w_, wt_, xin, kw in ((wo, wo_t, x, {"residual": xr}), (wd, wd_t, torch.randn(R, F, device=DEV).bfloat16(),
+                                                               {"residual": xr}),
+                             (wo, wo_t, x, {"bias": b, "gelu": True})):
+        o1, o2 = z(R, D), z(R, D)
+        ss = torch.full((D // 128, 32), float("nan"), device=DEV)
+        ops().decode_gemv(xin, wt_, o1, ws=gws, **kw)
+        ops().decode_linear(xin, wt_, o2, lws, ss_out=ss, **kw)
+        heads_zero()
+        assert torch.equal(o1, o2), kw.keys()
+        ref_ss = (o2.float() ** 2).view(R, D // 128, 128).sum(-1).T  # [groups, R]
+        torch.testing.assert_close(ss[:, :R], ref_ss, rtol=1e-5, atol=1e-5)
+    # kv
+    pos = torch.tensor([p], dtype=torch.int32, device=DEV)
+    cos, sin = ops().rope_tables(Tmax, 128, 1e4, DEV)
+    kc1, vc1, q1 = z(R, H, Tmax, 128), z(R, H, Tmax, 128), z(R, D)
+    kc2, vc2, q2 = z(R, H, Tmax, 128), z(R, H, Tmax, 128), z(R, D)
+    ops().decode_gemv_kv(x, wq_t, gws, pos, (cos, sin), kc1, vc1, H, Tmax, q1)
+    ops().decode_linear(x, wq_t, q2, lws, epi="kv", kv=(pos, (cos, sin), kc2, vc2, H, Tmax))
+    heads_zero()
+    assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    assert float(kc2[:, :, p].abs().sum()) > 0 and float(kc2[:, :, p + 1].abs().sum()) == 0
+    # swiglu on the interleaved weight
+    h1, h2 = z(R, F), z(R, F)
+    ops().decode_gemv_swiglu(x, wg_t, gws, h1)
+    ops().decode_linear(x, wgi_t, h2, lws, epi="swiglu")
+    heads_zero()
+    assert torch.equal(h1, h2)
+    # folded RMSNorm: the producer's ss_out feeds the consumer's staging
+    xm, ss = z(R, D), torch.zeros(D // 128, 32, device=DEV)
+    ops().decode_linear(x, wo_t, xm, lws, residual=xr, ss_out=ss)
+    xn, rstd = z(R, D), torch.zeros(R, device=DEV)
+    ops().rmsnorm_fwd(xm, lnw, xn, rstd, eps)
+    h1, h2 = z(R, F), z(R, F)
+    ops().decode_gemv_swiglu(xn, wg_t, gws, h1)
+    ops().decode_linear(xm, wgi_t, h2, lws, epi="swiglu", norm=(ss, lnw, eps))
+    heads_zero()
+    same = float((h1 == h2).float().mean())
+    print(f"\nfolded RMSNorm: {same:.4f} of h bit-equal to rmsnorm_fwd + GEMV, relerr {relerr(h2.float(), h1.float()):.2e}")
+    assert same > 0.5 and relerr(h2.float(), h1.float()) < 5e-3
+    q3, kc3, vc3 = z(R, D), z(R, H, Tmax, 128), z(R, H, Tmax, 128)
+    ops().decode_gemv_kv(xn, wq_t, gws, pos, (cos, sin), kc1, vc1, H, Tmax, q1)
+    ops().decode_linear(xm, wq_t, q3, lws, epi="kv", norm=(ss, lnw, eps), kv=(pos, (cos, sin), kc3, vc3, H, Tmax))
+    heads_zero()
+    assert relerr(q3.float(), q1.float()) < 5e-3 and relerr(kc3.float(), kc1.float()) < 5e-3
+
+
+def test_decode_linear_rejects_bad_arguments():
+    """Row-major weights, R > 32, N % 128, a short workspace, and epilogue-incompatible arguments
+    fail loudly."""
+    x = torch.randn(8, 256, device=DEV).bfloat16()
+    w = torch.randn(256, 256, device=DEV).bfloat16()
+    out = torch.empty(8, 256, device=DEV).bfloat16()
+    ws = ops().decode_linear_ws(8, 256, 256, DEV)
+    with pytest.raises(ValueError):
+        ops().decode_linear(x, w, out, ws)  # row-major
+    wt = ops().tile_decode_weight(w)
+    with pytest.raises((RuntimeError, ValueError)):
+        ops().decode_linear(x, wt, out, ws[:4])
+    with pytest.raises((RuntimeError, ValueError)):
+        ops().decode_linear(x, wt, out[:, :128], ws, epi="swiglu", bias=torch.zeros(256, device=DEV).bfloat16())
+    x40 = torch.randn(40, 256, device=DEV).bfloat16()
+    with pytest.raises((RuntimeError, ValueError)):
+        ops().decode_linear(x40, wt, torch.empty(40, 256, device=DEV).bfloat16(), ws)
+    with pytest.raises(ValueError):
+        ops().decode_linear_ws(8, 208, 256, DEV)
+
+
+def test_generate_fused_layers_close_to_unfused():
+    """The 5-launch decode layer (folded RMSNorms, in-launch split sums) against the round-2 step: the
+    per-step probabilities agree to rounding (the folded RMSNorm sums squares in another order), the
+    tokens agree, and the fused graph replay equals its eager loop."""
+    from ospo_amd.engine import ModelDims
+    from ospo_amd.generate import T2IGenerator
+    dims, w, prompts = _small_case()
+    res = {}
+    for fused in (True, False):
+        gen = T2IGenerator(ModelDims.from_any(dims), w, device=DEV, max_batch=4, max_prompt_len=16, n_img_tokens=24,
+                           cfg_weight=5.0, temperature=1.0, pad_id=7, fused_layers=fused)
+        assert gen.fused == fused
+        tok = gen.generate(prompts, seed=5, use_graph=False, record_probs=True).cpu().clone()
+        res[fused] = (tok, gen.probs.cpu().clone())
+        if fused:
+            assert torch.equal(gen.generate(prompts, seed=5, use_graph=True).cpu(), tok)
+    l1 = (res[True][1] - res[False][1]).abs().sum(-1)
+    agree = float((res[True][0] == res[False][0]).float().mean())
+    print(f"\nfused vs unfused decode: per-step L1(probs) max {float(l1.max()):.2e}; tokens agree {agree:.3f}")
+    assert float(l1.max()) < 1e-2 and agree > 0.9
