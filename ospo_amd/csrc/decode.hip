@@ -834,6 +834,273 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_kernel(const DlArgs a) {
   if (splits > 1 && threadIdx.x == 0) __hip_atomic_store(a.cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifdef OSPO_ABLATION
+// ABLATION BUILD ONLY (measured and rejected): ospo_decode_linear v2 (round 3): the same units, partials, summation order and consumers as dlin_kernel
+// (bit-identical outputs), but ~256 long-lived workgroups instead of one workgroup per (row group, split).
+// dlin_kernel's workgroups each load one 128-KiB unit and end after one round trip for the weights and one
+// for the partial store + ticket, at 2-3 resident per CU, so its launches ran at 2.8-4.0 TB/s (T2I profile,
+// profiles/r03/t2i_step_breakdown_v1_decode_linear.txt).  Here workgroup w owns split z = w % splits and the
+// row groups g0 .. g0 + G - 1 of set w / splits:
+//  * the x rows of ALL its chunks (<= DL2_MAXC x 512 k) are staged (and RMSNorm-folded) once;
+//  * it streams units (group, chunk) in group order with the next unit's 16 weight fragments per wave in
+//    flight under the current unit's MFMAs (registers double-buffered by a 2x-unrolled loop);
+//  * a finished group's partial is stored write-through at once; its ticket is taken one unit later, after
+//    the vmcnt(0) that the next unit's weights need anyway and a barrier (every wave's stores acknowledged;
+//    a ticket right after the store would drain the prefetched weights: vmcnt retires in issue order), and
+//    the last arriver sums + runs the consumer there, in an LDS tile of its own (xs still holds the x).
+constexpr int DL2_MAXC = 4;   // 512-k chunks per split: kper <= 2048
+constexpr int DL2_WGS = 256;  // workgroups to aim for: one per CU of an MI355X
+
+template <int NT, int EPI, bool NORM>
+__global__ __launch_bounds__(64 * G3_WAVES) void dlin2_kernel(const DlArgs a, int splits, int G, int ngroups) {
+  __shared__ __attribute__((aligned(16))) char xs[DL2_MAXC * 16 * NT * G2_PITCH];
+  __shared__ __attribute__((aligned(16))) float ep[16 * NT * 129];
+  __shared__ float rs[32];
+  __shared__ float sst[NORM ? 1024 : 1];
+  __shared__ float ssr[G3_WAVES][32];
+  __shared__ unsigned flag;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int z = blockIdx.x % splits, set = blockIdx.x / splits;
+  const int g0 = set * G, ng = min(G, ngroups - g0);
+  const int K = a.K, R = a.R;
+  const int k_begin = z * a.kper, k_end = min(K, k_begin + a.kper);
+  const int nch = (k_end - k_begin + G2_KC - 1) / G2_KC;  // <= DL2_MAXC (host check)
+  const int U = ng * nch;
+  const int NB = ngroups * G3_WAVES;
+  const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, a.part_bytes, 0x00020000);
+
+  float ssv[2] = {0.f, 0.f};
+  if constexpr (NORM) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = threadIdx.x + 512 * u;
+      if (i < a.ss_groups * 32) ssv[u] = a.ss_in[i];
+    }
+  }
+  // x rows of every chunk of the split, once
+  for (int c = 0; c < nch; ++c) {
+    const int kc = k_begin + c * G2_KC;
+    for (int r = wave; r < 16 * NT; r += G3_WAVES) {
+      const int rr = r < R ? r : R - 1;
+      const int col = min(kc + 8 * lane, K - 8);
+      __builtin_amdgcn_global_load_lds(a.X + (long)rr * a.ldx + col,
+                                       (LDS_AS void*)(xs + (c * 16 * NT + r) * G2_PITCH), 16, 0, 0);
+    }
+  }
+  const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6;  // NORM: 8 columns x rows tr, tr + 8, ...
+  u32x4 lw[DL2_MAXC];
+#pragma unroll
+  for (int c = 0; c < DL2_MAXC; ++c) {
+    lw[c] = u32x4{0u, 0u, 0u, 0u};
+    if (NORM && c < nch) lw[c] = *reinterpret_cast<const u32x4*>(a.ln_w + min(k_begin + c * G2_KC + 8 * tc, K - 8));
+  }
+  asm volatile("" ::: "memory");  // x DMA + norm weights before the first unit's weights: vmcnt(16) covers them
+
+  auto load_unit = [&](int u, bf16x8 (&wv)[16]) __attribute__((always_inline)) {
+    const int q = u / nch;
+    const int c = u - q * nch;
+    const int kc = k_begin + c * G2_KC;
+    const int nsteps = min(G2_KC, k_end - kc) >> 5;
+    const bf16* wr = a.W + ((long)((g0 + q) * G3_WAVES + wave) * (K >> 5) * 64 + lane) * 8;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) wv[s] = *reinterpret_cast<const bf16x8*>(wr + (long)((kc >> 5) + min(s, nsteps - 1)) * 512);
+  };
+  bf16x8 wa[16];
+  load_unit(0, wa);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __syncthreads();
+  if constexpr (NORM) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (threadIdx.x + 512 * u < 1024) sst[threadIdx.x + 512 * u] = ssv[u];
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      float s = 0.f;
+      for (int q = 0; q < a.ss_groups; ++q) s += sst[q * 32 + threadIdx.x];
+      rs[threadIdx.x] = rsqrtf(s / (float)K + a.eps);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < DL2_MAXC; ++c) {
+      if (c < nch) {
+        float wf[8];
+        unpack8(lw[c], wf);
+#pragma unroll
+        for (int i = 0; i < 2 * NT; ++i) {
+          const int r = tr + 8 * i;
+          u32x4* p = reinterpret_cast<u32x4*>(xs + (c * 16 * NT + r) * G2_PITCH + tc * 16);
+          float f[8];
+          unpack8(*p, f);
+          const float rr = rs[r < R ? r : R - 1];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = wf[q] * round_bf(f[q] * rr);
+          *p = pack8(f);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // the last arriver of row group gp: the splits' partials in split order, then the consumer
+  auto finish = [&](int gp, const f32x4 (&own)[NT], bool load) __attribute__((always_inline)) {
+    const int n = gp * G3_ROWS + wave * 16 + l16, nb = gp * G3_WAVES + wave;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      acc[j] = own[j];
+      if (!load) continue;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int z0 = 0; z0 < splits; z0 += 8) {  // 8 partials in flight, summed in split order
+        u32x4 pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (z0 + u < splits)
+            pv[u] = __builtin_amdgcn_raw_buffer_load_b128(rsP, (uint32_t)(((((z0 + u) * NB + nb) * NT + j) * 64 + lane) * 16),
+                                                          0, 16);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (z0 + u < splits) v += __builtin_bit_cast(f32x4, pv[u]);
+      }
+      acc[j] = v;
+    }
+    if constexpr (EPI == DL_PLAIN) {
+      float ssq[NT][4];
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * j + 4 * g + q;
+          float y = acc[j][q] + (a.bias ? bf2f(a.bias[n]) : 0.f);
+          if (a.gelu) y = gelu_erf(round_bf(y));
+          if (a.res) y = round_bf(y) + bf2f(a.res[(long)(r < R ? r : 0) * a.ldr + n]);
+          y = round_bf(y);
+          if (r < R) a.out[(long)r * a.ldo + n] = f2bf(y);
+          ssq[j][q] = dpp_sum16(y * y);  // over the wave's 16 columns
+        }
+      if (a.ss_out) {
+        if (l16 == 0) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ssr[wave][16 * j + 4 * g + q] = ssq[j][q];
+        }
+        __syncthreads();
+        if (threadIdx.x < 16 * NT) {
+          float s = 0.f;
+#pragma unroll
+          for (int w = 0; w < G3_WAVES; ++w) s += ssr[w][threadIdx.x];
+          a.ss_out[gp * 32 + threadIdx.x] = s;
+        }
+      }
+    } else {
+      // the group's 128 columns x 16 NT rows, bf16-rounded sums, through LDS
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ep[(16 * j + 4 * g + q) * 129 + wave * 16 + l16] = round_bf(acc[j][q]);
+      __syncthreads();
+      if constexpr (EPI == DL_KV) {
+        const int which = gp / a.H, h = gp % a.H;
+        const int p = *a.pos;
+        if (p < a.Tmax) {
+          for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
+            const int r = it >> 6, d = it & 63;
+            const float x1 = ep[r * 129 + d], x2 = ep[r * 129 + d + 64];
+            float o1 = x1, o2 = x2;
+            if (which < 2) {  // rotate-half RoPE, rounded per op as kv_store_kernel
+              const float cv = bf2f(a.cs[(long)p * 64 + d]), sv = bf2f(a.sn[(long)p * 64 + d]);
+              o1 = round_bf(x1 * cv) + round_bf(-x2 * sv);
+              o2 = round_bf(x2 * cv) + round_bf(x1 * sv);
+            }
+            bf16* dst = which == 0 ? a.out + (long)r * a.ldo + h * HD
+                                   : (which == 1 ? a.kc : a.vc) + (((long)r * a.H + h) * a.Tmax + p) * HD;
+            dst[d] = f2bf(o1);
+            dst[d + 64] = f2bf(o2);
+          }
+        }
+      } else {
+        for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
+          const int r = it >> 6, cc = it & 63;
+          const float gt = ep[r * 129 + cc], up = ep[r * 129 + 64 + cc];
+          a.out[(long)r * a.ldo + 64 * gp + cc] = f2bf(round_bf(silu(gt)) * up);
+        }
+      }
+      __syncthreads();  // ep is reused by the next finished group
+    }
+    if (splits > 1 && threadIdx.x == 0) __hip_atomic_store(a.cnt + gp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int pend = -1;  // a group whose partial is stored and not yet ticketed
+  // (no lambda calls another lambda here: hipcc's host pass then dropped the kernel's launch stub)
+  for (int u = 0; u < U; ++u) {
+    const int q = u / nch;
+    const int c = u - q * nch;
+    const int kc = k_begin + c * G2_KC;
+    const int nsteps = min(G2_KC, k_end - kc) >> 5;
+    if (pend >= 0) {  // its stores (every wave's) and this unit's weights (issued before them) have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // all waves' partial stores acknowledged before the ticket
+      if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(a.cnt + pend, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag = (t == (unsigned)splits - 1u) ? 1u : 0u;
+      }
+    }
+    bf16x8 cur[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) cur[s] = wa[s];  // waits for this unit's weights, then frees wa for the next
+    if (u + 1 < U) load_unit(u + 1, wa);
+    const char* xc = xs + c * 16 * NT * G2_PITCH;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < nsteps) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          bf16x8 xf = *reinterpret_cast<const bf16x8*>(xc + (16 * j + l16) * G2_PITCH + (32 * s + 8 * g) * 2);
+          if (16 * j + l16 >= R) xf = bf16x8{};
+          acc[j] = MFMA(xf, cur[s], acc[j]);  // D[x row 4g+q][w row l16]
+        }
+      }
+    }
+    if (pend >= 0) {
+      __syncthreads();  // flag
+      const bool last = flag != 0u;
+      __syncthreads();  // every wave has read it before the next ticket overwrites it
+      if (last) finish(pend, acc, true);
+      pend = -1;
+    }
+    if (c == nch - 1) {  // group g0 + q complete
+      const int gi = g0 + q;
+      if (splits > 1) {  // its partial, write-through; the ticket comes one unit later
+        const int nb = gi * G3_WAVES + wave;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j]), rsP,
+                                                 (uint32_t)((((z * NB + nb) * NT + j) * 64 + lane) * 16), 0, 16);
+        pend = gi;
+      } else {
+        finish(gi, acc, false);  // unsplit: one workgroup per group, the consumer on the registers
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if (pend >= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(a.cnt + pend, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag = (t == (unsigned)splits - 1u) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (flag != 0u) finish(pend, acc, true);
+  }
+}
+#endif  // OSPO_ABLATION
+
 // --------------------------------------------------------- CFG + sampling
 // one workgroup per image b: logits rows 2b (cond) and 2b+1 (uncond) [V] bf16 (train.py-style
 // interleaving of image_generation.py:132-141, 156-157).  l = bf16(lu + bf16(w * bf16(lc - lu))),
@@ -1128,13 +1395,30 @@ extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, 
   a.pos = pos_dev; a.cs = (const bf16*)rope_cos; a.sn = (const bf16*)rope_sin; a.kc = (bf16*)k_cache;
   a.vc = (bf16*)v_cache; a.H = n_heads; a.Tmax = Tmax;
   a.cnt = (unsigned*)ws; a.part = (float*)((char*)ws + DL_CNT_BYTES); a.part_bytes = (int)(need - DL_CNT_BYTES);
-  const dim3 grid(N / G3_ROWS, splits);
   const bool norm = ss_in != nullptr;
+  // one workgroup per (row group, split); the ablation build's OSPO_DLIN_V2 selects the streaming form
+  // (~256 long-lived workgroups, bit-identical, 7 % slower per decode step: DESIGN.md section 9)
+  const int ngroups = N / G3_ROWS;
+#ifdef OSPO_ABLATION
+  static const bool want_v2 = getenv("OSPO_DLIN_V2") != nullptr;
+  const bool v2 = want_v2 && (kper + G2_KC - 1) / G2_KC <= DL2_MAXC;
+  const int G = std::max(1, (ngroups * splits + DL2_WGS - 1) / DL2_WGS), nsets = (ngroups + G - 1) / G;
+  const dim3 grid = v2 ? dim3(splits * nsets) : dim3(ngroups, splits);
+#define DLIN(NT_, EPI_)                                                                                              \
+  if (v2)                                                                                                            \
+    hipLaunchKernelGGL((norm ? dlin2_kernel<NT_, EPI_, true> : dlin2_kernel<NT_, EPI_, false>), grid,                \
+                       dim3(64 * G3_WAVES), 0, stream, a, splits, G, ngroups);                                       \
+  else                                                                                                               \
+    hipLaunchKernelGGL((norm ? dlin_kernel<NT_, EPI_, true> : dlin_kernel<NT_, EPI_, false>), grid,                  \
+                       dim3(64 * G3_WAVES), 0, stream, a)
+#else
+  const dim3 grid(ngroups, splits);
 #define DLIN(NT_, EPI_)                                                                                             \
   hipLaunchKernelGGL((norm ? dlin_kernel<NT_, EPI_, true> : dlin_kernel<NT_, EPI_, false>), grid, dim3(64 * G3_WAVES), \
                      0, stream, a)
+#endif
 #define DLIN_NT(EPI_) \
-  if (R <= 16) DLIN(1, EPI_); else DLIN(2, EPI_);
+  if (R <= 16) { DLIN(1, EPI_); } else { DLIN(2, EPI_); }
   if (epi == DL_PLAIN) {
     DLIN_NT(DL_PLAIN)
   } else if (epi == DL_KV) {

@@ -390,7 +390,7 @@ def test_generate_tiled_weights_same_tokens():
     assert all(torch.equal(t, toks[0]) for t in toks[1:])
 
 
-@pytest.mark.parametrize("R", [32, 12])
+@pytest.mark.parametrize("R", [32, 12, 4])
 def test_decode_linear_equals_unfused(R):
     """ops.decode_linear (one launch per Linear: split sum + consumer in the launch) writes exactly what
     the GEMV + split-sum launches write -- plain with bias / residual, q|k|v + RoPE / KV store, gate|up
