@@ -742,16 +742,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc((void*)obase, 0, T * ldd * 2, 0x00020000);
   const int srow = 4 * wave + (lane >> 4);                       // + 16 i: the row of piece wave + 4 i
   const uint32_t chb = (uint32_t)(((lane & 15) ^ aswz(srow)) << 4);  // aswz(srow + 16 i) == aswz(srow)
-  auto stage = [&](int qt, int b) {
+  // part i of a tile's staging: this wave's Q and dO pieces i (+ the lse / delta row with part 0).  The loop
+  // issues the next tile's parts one per half sub-phase, in the shadow of that sub-phase's MFMAs (issued
+  // together at the tile start they took ~830 of a tile's ~6100 cycles, profiles/r02/attn/variants_stamps_v2.txt)
+  auto stage_part = [&](int qt, int b, int i) __attribute__((always_inline)) {
     char* Qs = smem + b * 2 * TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 16 / NW; ++i) {
-      int r = qt * QB + 16 * i + srow;
-      r = r < T ? r : T - 1;
-      dk_lds16(rsQ, Qs + (wave + NW * i) * 1024, (uint32_t)r * (uint32_t)(ldq * 2) + chb);
-      dk_lds16(rsO, Qs + TILE_BYTES + (wave + NW * i) * 1024, (uint32_t)r * (uint32_t)(ldd * 2) + chb);
-    }
-    if (wave < 2) {
+    int r = qt * QB + 16 * i + srow;
+    r = r < T ? r : T - 1;
+    dk_lds16(rsQ, Qs + (wave + NW * i) * 1024, (uint32_t)r * (uint32_t)(ldq * 2) + chb);
+    dk_lds16(rsO, Qs + TILE_BYTES + (wave + NW * i) * 1024, (uint32_t)r * (uint32_t)(ldd * 2) + chb);
+    if (i == 0 && wave < 2) {
       int q = qt * QB + lane;
       q = q < T ? q : T - 1;
       const float* src = (wave == 0 ? lse_sh : del_sh) + q;
@@ -814,7 +814,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     *reinterpret_cast<uint4*>(dsrow + (qt0 - 1) * QB + 16 * g) = z;
     *reinterpret_cast<uint4*>(dsrow + (qt0 - 1) * QB + 16 * g + 8) = z;
   }
-  stage(qt0, 0);
+#pragma unroll
+  for (int i = 0; i < 16 / NW; ++i) stage_part(qt0, 0, i);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const unsigned long long mt_loop = stamp();
@@ -828,7 +829,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     constexpr bool LAST = decltype(last_c)::value;
     constexpr int b = decltype(b_c)::value;
     const unsigned long long cs0 = stamp();
-    if (qt + 1 < nq) stage(qt + 1, b ^ 1);
+    const bool nxt = qt + 1 < nq;
+    // the next tile's staging, part i after the MFMAs of half sub-phase i (all before this tile's first
+    // dS^T store, so the tile end's vmcnt(4) still leaves exactly those stores in flight)
+    auto stage_next = [&](int i) __attribute__((always_inline)) {
+      if (i < 16 / NW && nxt) {
+        __builtin_amdgcn_sched_barrier(0);
+        stage_part(qt + 1, b ^ 1, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
     const int lo = key_l - (qt * QB + 4 * g), hi = T - (qt * QB + 4 * g);
     f32x4 sv[4], dp[4];
     bf16x8 pb[2], sb[2];
@@ -916,18 +926,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     const unsigned long long c1 = stamp();
     issue_half(b_c, I0{}, IO{}, h1);
     s_only(I0{}, h0);
+    stage_next(0);
     h1.x = f32x4{0.f, 0.f, 0.f, 0.f};
     wait_half(h1);                                     // sp0b
     issue_half(b_c, I1{}, IQ{}, h0);
     dp_only(I0{}, h1);
+    stage_next(1);
     wait_half(h0);                                     // sp1a
     const f32x4 l0 = h0.x;
     issue_half(b_c, I1{}, IO{}, h1);
     s_only(I1{}, h0);
+    stage_next(2);
     wait_half(h1);                                     // sp1b
     const f32x4 d0 = h1.x;
     issue_half(b_c, I2{}, IQ{}, h0);
     dp_only(I1{}, h1);
+    stage_next(3);
     softmax(I0{}, l0, d0);
     wait_half(h0);                                     // sp2a
     const f32x4 l1 = h0.x;
