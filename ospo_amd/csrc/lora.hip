@@ -293,7 +293,7 @@ struct Sk3Cfg {
   static constexpr int NTP = NT <= 2 ? 2 : (NT <= 4 ? 4 : 8);  // staged Bt tiles
   static constexpr int BPW = NTP / 2;                           // Bt pieces per wave per chunk
   static constexpr int PW = 2 + BPW;                            // pieces per wave per chunk
-  static constexpr int NS = 4;                                  // ring stages
+  static constexpr int NS = 2;                                  // ring stages (the launchers' default)
   static constexpr int STAGE = 8192 + NTP * 2048;               // A 64 x 128 B + Bt 16 NTP x 128 B
 };
 
@@ -304,7 +304,7 @@ __device__ __forceinline__ void sk3_lds16(__amdgpu_buffer_rsrc_t rs, char* dst, 
 }
 
 __device__ __forceinline__ void sk3_wait(int n) {
-  switch (n) {
+  switch (n) {  // vmcnt holds 6 bits on gfx950
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
@@ -325,7 +325,50 @@ __device__ __forceinline__ void sk3_wait(int n) {
     case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
     case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
     case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;  // (more in flight: waiting longer is safe)
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
+    case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+    case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+    case 27: asm volatile("s_waitcnt vmcnt(27)" ::: "memory"); break;
+    case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 29: asm volatile("s_waitcnt vmcnt(29)" ::: "memory"); break;
+    case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+    case 31: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 33: asm volatile("s_waitcnt vmcnt(33)" ::: "memory"); break;
+    case 34: asm volatile("s_waitcnt vmcnt(34)" ::: "memory"); break;
+    case 35: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+    case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    case 37: asm volatile("s_waitcnt vmcnt(37)" ::: "memory"); break;
+    case 38: asm volatile("s_waitcnt vmcnt(38)" ::: "memory"); break;
+    case 39: asm volatile("s_waitcnt vmcnt(39)" ::: "memory"); break;
+    case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 41: asm volatile("s_waitcnt vmcnt(41)" ::: "memory"); break;
+    case 42: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
+    case 43: asm volatile("s_waitcnt vmcnt(43)" ::: "memory"); break;
+    case 44: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+    case 45: asm volatile("s_waitcnt vmcnt(45)" ::: "memory"); break;
+    case 46: asm volatile("s_waitcnt vmcnt(46)" ::: "memory"); break;
+    case 47: asm volatile("s_waitcnt vmcnt(47)" ::: "memory"); break;
+    case 48: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    case 49: asm volatile("s_waitcnt vmcnt(49)" ::: "memory"); break;
+    case 50: asm volatile("s_waitcnt vmcnt(50)" ::: "memory"); break;
+    case 51: asm volatile("s_waitcnt vmcnt(51)" ::: "memory"); break;
+    case 52: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
+    case 53: asm volatile("s_waitcnt vmcnt(53)" ::: "memory"); break;
+    case 54: asm volatile("s_waitcnt vmcnt(54)" ::: "memory"); break;
+    case 55: asm volatile("s_waitcnt vmcnt(55)" ::: "memory"); break;
+    case 56: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+    case 57: asm volatile("s_waitcnt vmcnt(57)" ::: "memory"); break;
+    case 58: asm volatile("s_waitcnt vmcnt(58)" ::: "memory"); break;
+    case 59: asm volatile("s_waitcnt vmcnt(59)" ::: "memory"); break;
+    case 60: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+    case 61: asm volatile("s_waitcnt vmcnt(61)" ::: "memory"); break;
+    case 62: asm volatile("s_waitcnt vmcnt(62)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;  // (more in flight: waiting longer is safe)
   }
 }
 
@@ -333,7 +376,7 @@ __device__ __forceinline__ void sk3_wait(int n) {
 // [M][>= 2F] (gate | up); each chunk stages the gate and the up tile, the fragment's h = bf16(silu(g)) * u is
 // formed in registers (swiglu_fwd_kernel's rounding), stored to hout [M][F] (the down GEMM's operand) and
 // fed to the MFMAs -- h is never re-read.  K = F, up_off = F * 2 bytes.
-template <int NT, bool DROP, bool SWG = false>
+template <int NT, bool DROP, bool SWG = false, int NSREQ = 4>
 __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A, int lda, int a_bytes,
                                                       const bf16* __restrict__ Bt, int ldb, int b_rows, int b_bytes,
                                                       int M, int M_out, int K, int kper, int a_koff, int tiles_total,
@@ -346,7 +389,8 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
   constexpr int ABYTES = SWG ? 16384 : 8192;        // A image(s): gate and up under SWG
   constexpr int STAGE = C::STAGE + ABYTES - 8192;
   constexpr int PW = C::PW + (SWG ? 2 : 0);
-  __shared__ __attribute__((aligned(16))) char smem[C::NS * STAGE];
+  constexpr int NS = NSREQ * STAGE <= 163840 ? NSREQ : 163840 / STAGE;  // ring stages (the LDS caps deep rings)
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, g = lane >> 4, r8 = lane >> 3, c8 = lane & 7;
@@ -374,7 +418,7 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
   }
 #define SK3_STAGE(cc)                                                                                            \
   {                                                                                                              \
-    char* st_ = smem + ((cc) % C::NS) * STAGE;                                                                  \
+    char* st_ = smem + ((cc) % NS) * STAGE;                                                                  \
     const int kb_ = (cc) * 128;                                                                                  \
     _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                                \
         sk3_lds16(rsA, st_ + (wave * 2 + i) * 1024, va[i], kb_);                                                 \
@@ -397,16 +441,16 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
   for (int j = 0; j < NT; ++j) bok[j] = 16 * (tbase + j) + l16 < b_rows;
 
 #pragma unroll
-  for (int j = 0; j < C::NS - 1; ++j)
+  for (int j = 0; j < NS - 1; ++j)
     if (j < nch) SK3_STAGE(j);
   for (int c = 0; c < nch; ++c) {
     // this wave's pieces of chunk c landed: newer are the pieces of up to NS - 2 later chunks and the stores
     // (h, keep bits; unconditional, so the count is exact) of the up to NS - 1 chunks computed since
-    sk3_wait(PW * min(C::NS - 2, nch - 1 - c) + spi * min(c, C::NS - 1));
+    sk3_wait(PW * min(NS - 2, nch - 1 - c) + spi * min(c, NS - 1));
     __builtin_amdgcn_s_barrier();                    // everyone's; and chunk c-1's slot is free
     asm volatile("" ::: "memory");
-    if (c + C::NS - 1 < nch) SK3_STAGE(c + C::NS - 1);
-    const char* st = smem + (c % C::NS) * STAGE;
+    if (c + NS - 1 < nch) SK3_STAGE(c + NS - 1);
+    const char* st = smem + (c % NS) * STAGE;
     bf16x8 a[2], b[2][NT];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1030,14 +1074,43 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   const dim3 grid(M_pad / 64, splits, nz);
   // the split sum in the launch (last arriver per row block) unless the ablation build asks for the reduce kernel
   unsigned* c = (splits > 1 && M_pad / 64 <= SK_CNT_BYTES / 4 && !g_sk_reduce_launch) ? cnt : nullptr;
-  if (dr.scale > 0.f)
-    hipLaunchKernelGGL((skinny3_kernel<NT, true, SWG>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb,
-                       b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part,
-                       M_pad, dr.seed, dr.thresh, dr.scale, dr.bits, hout, ldh, K * 2, c);
-  else
-    hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, ldb,
-                       b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols, part,
-                       M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2, c);
+  // LDS ring stages: 2 (one chunk in flight beside the one computed).  The loop is issue-bound (per 64-k chunk
+  // and wave: the LDS-DMA issue, a barrier, the dropout hash's quarter-rate multiplies), so residency beats
+  // depth: per call 19.3 / 17.5 / 93.7 us at 2 stages against 20.3 / 18.7 / 97.1 at 4 and 29.0 / 25.1 / 121.4
+  // at 8 (u_qkv / u_o / SwiGLU + u_d, profiles/r03/skinny_ring_depth.jsonl).  Ablation: OSPO_SK3_NS.
+  int ns = 2;
+#ifdef OSPO_ABLATION
+  static const int ns_env = [] {
+    const char* e = getenv("OSPO_SK3_NS");
+    return e ? atoi(e) : 2;
+  }();
+  ns = ns_env;
+#endif
+#define SK3_LAUNCH(NS_)                                                                                          \
+  if (dr.scale > 0.f)                                                                                            \
+    hipLaunchKernelGGL((skinny3_kernel<NT, true, SWG, NS_>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b,  \
+                       ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols,  \
+                       part, M_pad, dr.seed, dr.thresh, dr.scale, dr.bits, hout, ldh, K * 2, c);                  \
+  else                                                                                                           \
+    hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG, NS_>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, \
+                       ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols,  \
+                       part, M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2, c);
+#ifdef OSPO_ABLATION
+  if (ns == 2) {
+    SK3_LAUNCH(2)
+  } else if (ns == 3) {
+    SK3_LAUNCH(3)
+  } else if (ns == 6) {
+    SK3_LAUNCH(6)
+  } else if (ns == 8) {
+    SK3_LAUNCH(8)
+  } else {
+    SK3_LAUNCH(4)
+  }
+#else
+  SK3_LAUNCH(2)
+#endif
+#undef SK3_LAUNCH
   OSPO_CHECK_LAUNCH();
   if (splits > 1 && !c) {
     const long n = (long)M_out * (out_cols / 4);
