@@ -372,11 +372,19 @@ __device__ __forceinline__ void sk3_wait(int n) {
   }
 }
 
+// one 16-B Bt fragment into registers (a device function for the same reason as sk3_lds16)
+__device__ __forceinline__ bf16x8 sk3_ldb(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
 // SWG (round 3): the down-projection's u product fused with the SwiGLU forward that makes its input: A is gu
 // [M][>= 2F] (gate | up); each chunk stages the gate and the up tile, the fragment's h = bf16(silu(g)) * u is
 // formed in registers (swiglu_fwd_kernel's rounding), stored to hout [M][F] (the down GEMM's operand) and
 // fed to the MFMAs -- h is never re-read.  K = F, up_off = F * 2 bytes.
-template <int NT, bool DROP, bool SWG = false, int NSREQ = 4>
+// BTR (ablation build, OSPO_SK3_BTREG; 2-stage ring only): the adapter rows' fragments come straight from L2 into
+// registers (one chunk ahead, issued before the chunk's LDS-DMA pieces so the counted wait is unchanged) instead
+// of being staged with every 64-k chunk: 2 DMA pieces + 2 NT LDS reads fewer per chunk and wave.
+template <int NT, bool DROP, bool SWG = false, int NSREQ = 4, bool BTR = false>
 __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A, int lda, int a_bytes,
                                                       const bf16* __restrict__ Bt, int ldb, int b_rows, int b_bytes,
                                                       int M, int M_out, int K, int kper, int a_koff, int tiles_total,
@@ -387,9 +395,10 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
                                                       unsigned* __restrict__ cnt = nullptr) {
   using C = Sk3Cfg<NT>;
   constexpr int ABYTES = SWG ? 16384 : 8192;        // A image(s): gate and up under SWG
-  constexpr int STAGE = C::STAGE + ABYTES - 8192;
-  constexpr int PW = C::PW + (SWG ? 2 : 0);
+  constexpr int STAGE = BTR ? ABYTES : C::STAGE + ABYTES - 8192;
+  constexpr int PW = (BTR ? 2 : C::PW) + (SWG ? 2 : 0);
   constexpr int NS = NSREQ * STAGE <= 163840 ? NSREQ : 163840 / STAGE;  // ring stages (the LDS caps deep rings)
+  static_assert(!BTR || NS == 2, "register Bt fragments: the 2-stage ring's counted waits only");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -426,8 +435,10 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
       _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                              \
           sk3_lds16(rsA, st_ + 8192 + (wave * 2 + i) * 1024, va[i], kb_ + up_off);                               \
     }                                                                                                            \
-    _Pragma("unroll") for (int i = 0; i < C::BPW; ++i)                                                           \
-        sk3_lds16(rsB, st_ + ABYTES + (wave * C::BPW + i) * 1024, vb[i], kb_);                                   \
+    if constexpr (!BTR) {                                                                                        \
+      _Pragma("unroll") for (int i = 0; i < C::BPW; ++i)                                                         \
+          sk3_lds16(rsB, st_ + ABYTES + (wave * C::BPW + i) * 1024, vb[i], kb_);                                 \
+    }                                                                                                            \
   }
 
   f32x4 acc[NT];
@@ -440,6 +451,20 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
 #pragma unroll
   for (int j = 0; j < NT; ++j) bok[j] = 16 * (tbase + j) + l16 < b_rows;
 
+  // BTR: this lane's Bt fragment offsets (row 16 (tbase + j) + l16 clamped, k group g), + 64 B per k step s
+  uint32_t vbr[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int br = min(16 * (tbase + j) + l16, b_rows - 1);
+    vbr[j] = ((uint32_t)br * (uint32_t)ldb + (uint32_t)k_begin + 8u * (uint32_t)g) * 2u;
+  }
+  bf16x8 bcur[2][NT], bnxt[2][NT];
+  if constexpr (BTR) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bcur[s2][j] = sk3_ldb(rsB, vbr[j] + 64u * s2, 0);
+  }
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j)
     if (j < nch) SK3_STAGE(j);
@@ -447,8 +472,24 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
     // this wave's pieces of chunk c landed: newer are the pieces of up to NS - 2 later chunks and the stores
     // (h, keep bits; unconditional, so the count is exact) of the up to NS - 1 chunks computed since
     sk3_wait(PW * min(NS - 2, nch - 1 - c) + spi * min(c, NS - 1));
+    if constexpr (BTR) {  // chunk c's Bt fragments were issued before its pieces: landed too
+      if (c > 0) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) bcur[s2][j] = bnxt[s2][j];
+      }
+    }
     __builtin_amdgcn_s_barrier();                    // everyone's; and chunk c-1's slot is free
     asm volatile("" ::: "memory");
+    if constexpr (BTR) {
+      if (c + 1 < nch) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) bnxt[s2][j] = sk3_ldb(rsB, vbr[j] + 64u * s2, (c + 1) * 128);
+      }
+    }
     if (c + NS - 1 < nch) SK3_STAGE(c + NS - 1);
     const char* st = smem + (c % NS) * STAGE;
     bf16x8 a[2], b[2][NT];
@@ -468,8 +509,12 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const int br = 16 * j + l16;
-        b[s][j] = *reinterpret_cast<const bf16x8*>(st + ABYTES + br * 128 + ((q ^ (br & 7)) << 4));
+        if constexpr (BTR) {
+          b[s][j] = bcur[s][j];
+        } else {
+          const int br = 16 * j + l16;
+          b[s][j] = *reinterpret_cast<const bf16x8*>(st + ABYTES + br * 128 + ((q ^ (br & 7)) << 4));
+        }
       }
     }
 #pragma unroll
@@ -1086,17 +1131,21 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   }();
   ns = ns_env;
 #endif
-#define SK3_LAUNCH(NS_)                                                                                          \
+#define SK3_LAUNCH2(NS_, BTR_)                                                                                   \
   if (dr.scale > 0.f)                                                                                            \
-    hipLaunchKernelGGL((skinny3_kernel<NT, true, SWG, NS_>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b,  \
-                       ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols,  \
-                       part, M_pad, dr.seed, dr.thresh, dr.scale, dr.bits, hout, ldh, K * 2, c);                  \
+    hipLaunchKernelGGL((skinny3_kernel<NT, true, SWG, NS_, BTR_>), grid, dim3(256), 0, stream, a, lda,             \
+                       (int)a_bytes, b, ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, \
+                       ldo, out_cols, part, M_pad, dr.seed, dr.thresh, dr.scale, dr.bits, hout, ldh, K * 2, c);     \
   else                                                                                                           \
-    hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG, NS_>), grid, dim3(256), 0, stream, a, lda, (int)a_bytes, b, \
-                       ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, ldo, out_cols,  \
-                       part, M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2, c);
+    hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG, NS_, BTR_>), grid, dim3(256), 0, stream, a, lda,            \
+                       (int)a_bytes, b, ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, \
+                       ldo, out_cols, part, M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2, c);
+#define SK3_LAUNCH(NS_) SK3_LAUNCH2(NS_, false)
 #ifdef OSPO_ABLATION
-  if (ns == 2) {
+  static const bool btreg = getenv("OSPO_SK3_BTREG") != nullptr;
+  if (ns == 2 && btreg) {
+    SK3_LAUNCH2(2, true)
+  } else if (ns == 2) {
     SK3_LAUNCH(2)
   } else if (ns == 3) {
     SK3_LAUNCH(3)
@@ -1111,6 +1160,7 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   SK3_LAUNCH(2)
 #endif
 #undef SK3_LAUNCH
+#undef SK3_LAUNCH2
   OSPO_CHECK_LAUNCH();
   if (splits > 1 && !c) {
     const long n = (long)M_out * (out_cols / 4);

@@ -1,0 +1,20 @@
+# SQ counters of the skinny LoRA products (issue vs wait), one pass per counter set
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/skpmc
+i=0
+for SET in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM" "SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $SET --output-format csv -d gpurun_out/skpmc/p$i -o p -- python tools/skinny_pmc_probe.py > gpurun_out/skpmc/p$i.log 2>&1 || { echo "PMC pass $i FAILED"; tail -5 gpurun_out/skpmc/p$i.log; exit 1; }
+done
+python - <<'PY'
+import csv, glob, collections
+agg = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
+for f in glob.glob("gpurun_out/skpmc/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:40]
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"]); n[(k, r["Counter_Name"])] += 1
+for k, d in agg.items():
+    if "skinny" not in k and "swiglu" not in k: continue
+    print(k, {c: round(v / max(1, n[(k, c)]), 1) for c, v in sorted(d.items())})
+PY
