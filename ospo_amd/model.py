@@ -17,6 +17,7 @@ from __future__ import annotations
 import glob
 import json
 import os
+import sys
 from typing import Dict, Optional
 
 import torch
@@ -187,7 +188,7 @@ def get_model(mode: str = "train", dtype=torch.bfloat16, config=None, device=Non
             raise ValueError(f"unknown model.arch {arch}")
         over = get(config, "model.override", {}) or {}
         dims = ModelDims(**{**base.__dict__, **over, "lora_r": r, "lora_alpha": alpha})
-        print(f"[ospo_amd] model.synthetic: random-init {dims.n_layers}-layer d={dims.d_model} weights")
+        print(f"[ospo_amd] model.synthetic: random-init {dims.n_layers}-layer d={dims.d_model} weights", file=sys.stderr)
         w = synthetic_weights(dims, device, seed=seed, lora_seed=seed + 1)
     else:
         if not model_path or not os.path.isdir(model_path):
