@@ -1336,6 +1336,8 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   auto kfn = lora_gdb_kernel<8, 4>;
 #ifdef OSPO_ABLATION
   if (getenv("OSPO_GDB_NS6")) kfn = lora_gdb_kernel<8, 6>;  // A/B: a 6-stage ring
+  if (getenv("OSPO_GDB_NS2")) kfn = lora_gdb_kernel<8, 2>;  // A/B: 2- and 3-stage rings (more residency)
+  if (getenv("OSPO_GDB_NS3")) kfn = lora_gdb_kernel<8, 3>;
 #endif
   hipLaunchKernelGGL(kfn, grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
                      (const bf16*)u, ldu, M, Nmod, nch, (float*)ws, Mw, dB);
