@@ -11,4 +11,4 @@ for run in v2a v1 v2b; do
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['roofline']['avg_step_us'], d['roofline']['frac'], d.get('tokens_checksum'))" gpurun_out/${TAG}_t2i_$run.json $run
 done
 unset OSPO_HIP_LIB OSPO_DLIN_V1
-TAG=${TAG}p bash tools/gpu_r03_t2i_prof.sh
+TAG=${TAG}p bash tools/gpu/gpu_r03_t2i_prof.sh

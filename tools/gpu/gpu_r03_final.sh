@@ -4,7 +4,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 TAG=${TAG:-fin}
-NO_BENCH=1 TAG=$TAG bash tools/gpu_r03_suite.sh || exit 1
+NO_BENCH=1 TAG=$TAG bash tools/gpu/gpu_r03_suite.sh || exit 1
 if [ -f ospo_amd/libospo_hip_base.so ]; then
   for r in 1 2; do
     for lib in base new; do
