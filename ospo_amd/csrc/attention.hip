@@ -255,7 +255,8 @@ __device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf1
 }
 
 // ============================================================== forward ====
-template <int NW, int DBG = 0, bool MXO = false>  // MXO: also the MXFP8 copy of O (config 5)
+// SPR (ablation): the next tile's K pieces issued after this tile's S MFMAs, its V pieces after the softmax
+template <int NW, int DBG = 0, bool MXO = false, bool SPR = false>  // MXO: also the MXFP8 copy of O (config 5)
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
                                                        bf16* __restrict__ out, int ldo, float* __restrict__ lse,
                                                        int T, int H, float scale,
@@ -304,10 +305,10 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
   for (int kt = 0; kt < n_kv; ++kt) {
     const bool diag = (kt * KB + KB - 1 > qb * RB) || ((kt + 1) * KB > T);
     const int buf = kt & 1;
-    if (DBG == 0 && kt + 1 < n_kv) {
-      char* nb = smem + (buf ^ 1) * 2 * TILE_BYTES;
-      stage64<NW>(kbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nb, wave, lane);
-      stage64<NW>(vbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nb + TILE_BYTES, wave, lane);
+    char* const nbuf = smem + (buf ^ 1) * 2 * TILE_BYTES;
+    if (!SPR && DBG == 0 && kt + 1 < n_kv) {
+      stage64<NW>(kbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nbuf, wave, lane);
+      stage64<NW>(vbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nbuf + TILE_BYTES, wave, lane);
     }
     const char* Ks = smem + buf * 2 * TILE_BYTES;
     const char* Vs = Ks + TILE_BYTES;
@@ -319,6 +320,11 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
       st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int d = 0; d < 4; ++d) st[t] = MFMA(frag_row(Ks, 16 * t, d, lane), qf[d], st[t]);
+    }
+    if (SPR && DBG == 0 && kt + 1 < n_kv) {
+      __builtin_amdgcn_sched_barrier(0);
+      stage64<NW>(kbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nbuf, wave, lane);
+      __builtin_amdgcn_sched_barrier(0);
     }
     // element (t, j) is key kt*KB + 4g + 16t + j; off the diagonal no element is masked
     const int rel = diag ? lim - (kt * KB + 4 * g) : 64;
@@ -353,6 +359,11 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
     m_run = m_new;
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] *= alpha;
+    if (SPR && DBG == 0 && kt + 1 < n_kv) {
+      __builtin_amdgcn_sched_barrier(0);
+      stage64<NW>(vbase, ldq, (kt + 1) * KB, rows_lim_seq, 0, nbuf + TILE_BYTES, wave, lane);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 
     // O^T[d][q] += V^T[d][key] . P^T[key][q]: V^T fragments in batches of 4 (asm reads: no
     // vmcnt drain of the in-flight next tile, 4 LDS waits per tile instead of 16)
@@ -1498,6 +1509,8 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
 #ifdef OSPO_ABLATION
   static const bool dbg = getenv("OSPO_ATTN_DBG") != nullptr;  // ablation only (results invalid)
   auto kfn = dbg ? attn_fwd_kernel<8, 1> : (nw == 8 ? attn_fwd_kernel<8, 0> : attn_fwd_kernel<4, 0>);
+  static const bool spr = getenv("OSPO_ATTN_FWD_SPREAD") != nullptr;
+  if (spr && !dbg && nw == 8) kfn = attn_fwd_kernel<8, 0, false, true>;
 #else
   auto kfn = attn_fwd_kernel<8, 0>;
 #endif
@@ -1591,6 +1604,7 @@ static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
     int order_dkdv = 0, order_dq = 0;
 #ifdef OSPO_ABLATION
     if (const char* e = getenv("OSPO_ATTN_ORDER")) order_dkdv = order_dq = atoi(e);  // A/B: 0 block-, 1 group-major
+    if (const char* e = getenv("OSPO_ATTN_ORDER_DQ")) order_dq = atoi(e);             // A/B: the dQ kernel alone
 #endif
     using DkdvFn = decltype(&attn_bwd_dkdv3_kernel<4>);
     DkdvFn dkdv3 = attn_bwd_dkdv3_kernel<4>;
