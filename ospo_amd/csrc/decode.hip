@@ -1253,7 +1253,8 @@ int gemv3_kper(int N, int K) {
   const int groups = N / G3_ROWS;
   int splits = 1;
   while (splits * 2 <= std::min(8, K / G2_KC) && groups * splits * 2 <= 1024) splits *= 2;
-  if (g_gemv_splits > 0) splits = std::max(1, std::min(std::min(g_gemv_splits, K / G2_KC), G2_MAX_SPLITS));
+  // A/B knob: down to 256-k splits (half a staged chunk)
+  if (g_gemv_splits > 0) splits = std::max(1, std::min(std::min(g_gemv_splits, K / 256), G2_MAX_SPLITS));
   int kper = (K + splits - 1) / splits;
   return (kper + 31) / 32 * 32;
 }
