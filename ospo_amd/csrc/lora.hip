@@ -1004,11 +1004,15 @@ struct SkDropArgs {
 
 #ifdef OSPO_ABLATION
 static int g_skinny_variant = 4;  // 1 = 16-row skinny loop, 2 = 64-row LDS-shared, 3 = 2 with whole-chunk splits, 4 = v3 (default)
-static int g_sk3_wgs = 512;       // v3: target workgroups per launch
+static int g_sk3_wgs = 0;         // v3: target workgroups per launch (0: sk3_target's rule; A/B knob 100 + W)
 #else
 constexpr int g_skinny_variant = 4;  // the product library runs v3 (v2 where v3's 32-bit buffer offsets do not reach)
-constexpr int g_sk3_wgs = 512;
+constexpr int g_sk3_wgs = 0;
 #endif
+// v3 workgroup target: 512 (two per CU) for the 4096-long adapter inputs; 1024 for the 11008-long down input,
+// whose 25-chunk workgroups at 512 left the loop latency-bound (SwiGLU + u_d 100.8 / 93.9 / 86.4 / 92.0 us at
+// 512 / 768 / 1024 / 1536, profiles/r03/skinny_swg_wgs.json).  At most 1024 (the workspace rule below).
+static inline int sk3_target(int K) { return g_sk3_wgs > 0 ? g_sk3_wgs : (K >= 8192 ? 1024 : 512); }
 
 // v2 K split: ~1024 workgroups over (64-row blocks x modules), each split >= one chunk.
 // Variant 3: splits own whole KC chunks (kper = a multiple of KC), so no workgroup runs a short
@@ -1046,7 +1050,7 @@ extern "C" size_t ospo_lora_skinny_ws_bytes(int M_out, int K, int n_tiles) {
   // v3: at most max(g_sk3_wgs, 1024) workgroups' worth of splits over one module's row blocks
   {
     const long blocks = (M_out + 63) / 64;
-    const long wgs = g_sk3_wgs > 1024 ? g_sk3_wgs : 1024;
+    const long wgs = sk3_target(K) > 1024 ? sk3_target(K) : 1024;
     long sp3 = (wgs + blocks - 1) / blocks;
     sp3 = sp3 > K / 64 ? K / 64 : sp3;
     const size_t b = sp3 > 1 ? (size_t)sp3 * (size_t)((M_out + 63) / 64 * 64) * 16 * n_tiles * 4 : 0;
@@ -1064,6 +1068,7 @@ extern "C" int ospo_set_skinny_variant(int v) {
   }
   if (v < 1 || v > 4) return OSPO_ERR_ARG;
   g_skinny_variant = v;
+  g_sk3_wgs = 0;  // back to sk3_target's rule
   return OSPO_OK;
 }
 #endif
@@ -1106,7 +1111,7 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
                           int ldh = 0, unsigned* cnt = nullptr) {
   const int blocks = (M_out + 63) / 64 * nz;
   const int chunks = K / 64;
-  int splits = (g_sk3_wgs + blocks - 1) / blocks;
+  int splits = (sk3_target(K) + blocks - 1) / blocks;
   splits = splits < 1 ? 1 : (splits > chunks ? chunks : splits);
   const int cps = (chunks + splits - 1) / splits;
   const int kper = cps * 64;
