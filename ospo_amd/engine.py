@@ -78,7 +78,8 @@ class SimPOEngine:
                  max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
                  dropout_seed: int = 42, linear_dtype: str = "bf16", fuse_swiglu_bwd: bool = False,
                  dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0, fuse_gdb: bool = True,
-                 da_stream: bool = True, keep_bits: bool = True, fuse_swiglu_u: bool = True):
+                 da_stream: bool = True, keep_bits: bool = True, fuse_swiglu_u: bool = True,
+                 side_after_norm: bool = True):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
         if linear_dtype not in ("bf16", "mx8"):
@@ -179,6 +180,10 @@ class SimPOEngine:
         # fuse_swiglu_u: the SwiGLU forward and the down adapter's u product in one stream over gu (round 3;
         # bit-identical; 95.7 us against 50.4 + ~44 + 5 us unfused once silu uses the hardware reciprocal)
         self.fuse_swiglu_u = bool(fuse_swiglu_u)
+        # side_after_norm: a layer's dA work is enqueued after its input-norm backward, so it overlaps the next
+        # layer's down dX GEMM instead of that memory-bound norm (+0.4 % at the step, 3 of 3 alternating rounds,
+        # profiles/r03/step_side_order_ab.jsonl); off: enqueued right after the q|k|v dX GEMM
+        self.side_after_norm = bool(side_after_norm)
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
             raise ValueError("dadb_splits must be four positive split counts")
         self._side = torch.cuda.Stream(device=self.device, priority=int(side_priority))
@@ -606,23 +611,31 @@ class SimPOEngine:
                 self._lin(dqkv[:M], lw["qkvT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
                           keep_bits=self._bits_bwd(i, "qkv", dr, D))
             pending.append(("qkv", gs, a["xn1"], dqkv, a["u_qkv"], dr, fdb))
-            # this layer's LoRA weight grads on the side stream (one event from main)
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                for name, gs_, x_in, dy, u, dr_, fdb_ in pending:
-                    self._lora_grads(gs_, x_in, dy, u, lay.groups[name], gbase, dr_, fdb_,
-                                     self._bits_bwd(i, name, dr_, x_in.shape[1]))
-                if on_layer_grads is not None:  # this layer's dA/dB are the last side-stream work so far
-                    on_layer_grads(gbase, gbase + lay.per_layer)
-            ev2 = torch.cuda.Event()
-            ev2.record(side)
-            done[q] = ev2
+            def enqueue_side():
+                # this layer's LoRA weight grads on the side stream (one event from main)
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    for name, gs_, x_in, dy, u, dr_, fdb_ in pending:
+                        self._lora_grads(gs_, x_in, dy, u, lay.groups[name], gbase, dr_, fdb_,
+                                         self._bits_bwd(i, name, dr_, x_in.shape[1]))
+                    if on_layer_grads is not None:  # this layer's dA/dB are the last side-stream work so far
+                        on_layer_grads(gbase, gbase + lay.per_layer)
+                ev2 = torch.cuda.Event()
+                ev2.record(side)
+                done[q] = ev2
+
+            late = self.side_after_norm and i > 0
+            if not late:
+                enqueue_side()
             if i > 0:
                 wait_done(1 - q)  # dx copy 1-q: layer i+1's side work read it
+                # (writes dxn and dx copy 1-q: neither is read by this layer's side work)
                 ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[1 - q][:M],
                                 dres=dxmid[:M], mx=self._mxo(D))
+            if late:
+                enqueue_side()
             # layer 0: the gradient w.r.t. its input (the text / image embeddings) feeds nothing that
             # trains -- the embedding tables and gen_aligner are frozen (train.py:148-216) -- so its q|k|v dX
             # GEMM and the input RMSNorm backward are not run

@@ -418,6 +418,30 @@ def test_step_lora_dropout_vs_oracle_with_replayed_masks():
     assert max(rel(grads[k], plain.lora_grads[k]) for k in plain.lora_grads) > 0.05
 
 
+def test_step_side_after_norm_same_grads():
+    """side_after_norm only moves where a layer's dA work joins the side stream (after the input-norm
+    backward instead of after the q|k|v dX GEMM); with dropout and 4 layers (both operand copies in use)
+    the log-probs are bit-equal and the grads equal up to the dA kernel's fp32-atomic summation order."""
+    dims = O.JanusDims(n_layers=4, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=2048,
+                       gen_head_dim=256, lora_r=16, lora_alpha=32, lora_dropout=0.05)
+    w = O.init_weights(dims, seed=41, dtype=torch.bfloat16, lora_b_std=1e-2)
+    g = torch.Generator().manual_seed(42)
+    B, Lt, N = 2, 8, 64
+    text = [torch.randint(0, dims.vocab, (1, Lt - i), generator=g, dtype=torch.int32) for i in range(B)]
+    chosen = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    rejected = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    algo = {"beta": 10.0, "gamma_beta_ratio": 0.5, "label_smoothing": 0.0, "loss_type": "sigmoid"}
+    from ospo_amd.engine import ModelDims, SimPOEngine
+    out = []
+    for late in (False, True):
+        eng = SimPOEngine(ModelDims.from_any(dims), w, device="cuda", max_pairs=B, max_text_len=Lt,
+                          n_img_tokens=N, lora_dropout=0.05, dropout_seed=7, side_after_norm=late)
+        out.append(run_hip_step(eng, text, chosen, rejected, algo))
+    (l0, s0, g0), (l1, s1, g1) = out
+    assert torch.equal(l0, l1) and s0 == s1
+    assert max(rel(g1[k], g0[k]) for k in g0) < 1e-5
+
+
 def _mx8_case(dims, seed, B, Lt, N):
     w = O.init_weights(dims, seed=seed, dtype=torch.bfloat16, lora_b_std=1e-2)
     g = torch.Generator().manual_seed(seed + 1)
