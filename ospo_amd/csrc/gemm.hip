@@ -1930,6 +1930,41 @@ SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus
   return pl;
 }
 
+#include "gemm_w4.h"
+
+// The 4-wave hand-scheduled kernel (gemm_w4.h) when the shape fits it: bf16, <= 2 LoRA extension tiles,
+// 32-bit buffer offsets, and every work unit with enough main K-tiles for its program (plain: 4; the
+// dropout unit that carries the extension tiles: 3).  Returns OSPO_ERR_UNSUPPORTED otherwise (the caller
+// then runs the v5 kernel).  DBG 1 (ablation): no loads after the prologue.
+template <bool DROP, int DBG = 0, int V = 0>
+int launch_w4(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
+  if (a.N % 256 || a.K % 64 || a.K2 % 64 || a.K2 > 128) return OSPO_ERR_UNSUPPORTED;
+  if ((long)a.M * a.lda * 2 >= (1L << 31) || (long)a.N * a.ldb * 2 >= (1L << 31)) return OSPO_ERR_UNSUPPORTED;
+  if (a.K2 > 0 && ((long)a.M * a.lda2 * 2 >= (1L << 31) || (long)a.N * a.ldb2 * 2 >= (1L << 31)))
+    return OSPO_ERR_UNSUPPORTED;
+  const int tm = (a.M + 255) / 256, tn = a.N / 256;
+  const int nt1 = a.K / 64, nt2 = a.K2 / 64, ntot = nt1 + nt2;
+  const SplitPlan pl = plan_split(a.M, a.N, ntot, a.K2, false, DROP, device_cus(), so.split, so.ws ? so.ws_bytes : 0);
+  for (int z = 0; z < (pl.tail ? pl.split : 1); ++z) {  // every unit's program must fit (z = 0: the whole range)
+    const int tb = pl.tail ? (int)((long)ntot * z / pl.split) : 0;
+    const int tc = pl.tail ? (int)((long)ntot * (z + 1) / pl.split) - tb : ntot;
+    const W4Range r = w4_range(DROP, nt1, nt2, tb, tc);
+    const bool drop_unit = DROP && r.ne > 0;
+    if (r.ne > 2 || r.nm < (drop_unit ? 3 : 4) || (!DROP && r.ne > 0 && tb + r.nm != nt1)) return OSPO_ERR_UNSUPPORTED;
+  }
+  if (pl.tail && ntot < 4) return OSPO_ERR_UNSUPPORTED;
+  const int grid = pl.dp + pl.tail * pl.split;
+  hipLaunchKernelGGL((gemm_nt_w4_kernel<DROP, DBG, V>), dim3(grid), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split, so.ws,
+                     g_v5_gm);
+  OSPO_CHECK_LAUNCH();
+  if (pl.tail) {
+    hipLaunchKernelGGL(splitk_fixup_kernel, dim3(pl.tail * 32), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split,
+                       (const float*)so.ws, g_v5_gm);
+    OSPO_CHECK_LAUNCH();
+  }
+  return OSPO_OK;
+}
+
 template <int DBG = 0, bool DROP = false, bool MX = false, int SP = 0>
 int launch_v5(const GemmArgs& a, hipStream_t s, const SplitOpts& so, bool allow_split = true) {
   if (a.N % 256) return OSPO_ERR_SHAPE;
@@ -2476,6 +2511,29 @@ int launch_default(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
   if (g_gemm_variant == 27) return launch_v5<0, DROP, false, 8>(a, s, so);
   if (g_gemm_variant == 28) return launch_v5<0, DROP, false, 9>(a, s, so);
   if (g_gemm_variant == 32) return launch_v6<DROP>(a, s, so);  // persistent SP8 (rejected)
+  if (g_gemm_variant == 40) {
+    const int r = launch_w4<DROP>(a, s, so);
+    if (r != OSPO_ERR_UNSUPPORTED) return r;
+  }
+  if (g_gemm_variant == 41) {
+    const int r = launch_w4<DROP, 1>(a, s, so);
+    if (r != OSPO_ERR_UNSUPPORTED) return r;
+  }
+  if (g_gemm_variant == 42) {  // w4 with workgroup stamps (tools/w4_stamps.py)
+    GemmArgs d = a;
+    d.dbg = g_dbg_buf;
+    const int r = launch_w4<DROP, 2>(d, s, so);
+    if (r != OSPO_ERR_UNSUPPORTED) return r;
+  }
+  if constexpr (!DROP) {  // schedule variants 43.. = gen_gemm_w4.py ABL_VARIANTS 1..
+    int r = OSPO_ERR_UNSUPPORTED;
+    if (g_gemm_variant == 43) r = launch_w4<false, 0, 1>(a, s, so);
+    if (g_gemm_variant == 44) r = launch_w4<false, 0, 2>(a, s, so);
+    if (g_gemm_variant == 45) r = launch_w4<false, 0, 3>(a, s, so);
+    if (g_gemm_variant == 46) r = launch_w4<false, 0, 4>(a, s, so);
+    if (g_gemm_variant == 47) r = launch_w4<false, 0, 5>(a, s, so);
+    if (r != OSPO_ERR_UNSUPPORTED) return r;
+  }
 #endif
   return launch_v5<0, DROP, false, 8>(a, s, so);
 }
@@ -2547,6 +2605,8 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 30: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<5, false, false, 8>(d, stream, so, false); }  // SP8 + phase stamps
     case 17: return launch_v5<0>(a, stream, so, true);                                   // 8-phase + split-K tail
     case 32: return launch_v6<false>(a, stream, so);                                  // persistent SP8 (v6, rejected)
+    case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47:
+      return launch_default<false>(a, stream, so);                                   // 4-wave hand-scheduled (w4)
     default: return launch_v5<0, false, false, 8>(a, stream, so, true);               // SP8 + split-K tail
   }
 #endif
@@ -2706,7 +2766,8 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || v > 32 || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23) return OSPO_ERR_ARG;
+  if (v < 0 || (v > 32 && (v < 40 || v > 47)) || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23)
+    return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;
   return OSPO_OK;

@@ -1,0 +1,305 @@
+#!/usr/bin/env python3
+"""Generates gemm_w4_asm.inc: the hand-placed K-loop programs of the 4-wave 256x256 bf16 GEMM
+(gemm_nt_w4_kernel in gemm_w4.h).  Build-time only (the Makefile runs it); the output is committed.
+
+Structure (one wave per SIMD, each wave a 128 x 128 quadrant of the 256 x 256 tile, 8 x 8 blocks of
+v_mfma_f32_16x16x32_bf16, 256 accumulators in a[0:255]):
+
+  * a K-tile (64 deep) is 128 MFMAs: substep 0 (k 0..31) for all 64 blocks, then substep 1 (k 32..63);
+    block (i, j) = B fragment i (srcA, 16 output columns) x A fragment j (srcB, 16 output rows).
+  * every fragment of a K-tile lives in registers (2 substeps x 16 fragments x 4 VGPRs = v[128:255]):
+    substep-0 fragments of tile t+1 are read in the last MFMA gaps of tile t, substep-1 fragments of tile
+    t in its first 16 gaps.  After the first 16 gaps the wave holds tile t whole, so one barrier
+    (barrier 1) frees tile t's LDS stage and tile t+2's 16 LDS-DMA pieces go into it, spread over the
+    following MFMAs (A pieces in substep 0, B pieces in substep 1).
+  * barrier 2 (near the end of the tile) is preceded by a counted vmcnt that leaves tile t+2's pieces in
+    flight and retires tile t+1's, whose substep-0 fragments are then read.
+  * LDS: 2 stages x 64 KiB ([A 256 rows][B 256 rows] x 128 B, chunk XOR row&7 swizzle applied on the
+    DMA source address), so each piece has ~1-1.5 K-tiles of load latency.
+
+Every MFMA gap holds at most one ds_read or one LDS-DMA issue plus SALU, so the MFMA pipe stays fed
+(MI355X_MICROARCH.md: 16x16x32 holds the SIMD's issue for 8 of its 16 cycles).  Accumulation order per
+output element is that of gemm_nt_v5_kernel (K-tiles in order, substep 0 then 1; LoRA extension tiles
+last, or first with dropout), so results are bit-identical to it.
+
+Programs (runtime-selected by the kernel; each one asm statement):
+  plain_E (E = 0, 1, 2 extension tiles at the end): prologue, tile 0, loop over main tiles 1..nm-3,
+      tail tiles nm-2 .. nm-1+E.  Needs nm >= 4 main tiles.
+  drop_E (E = 1, 2 extension tiles first, dropout mask applied to the accumulators after them):
+      prologue, the E extension tiles, mask pass, loop over main tiles E..nt-3, the last two tiles.
+      Needs nm >= 3.
+"""
+import sys
+
+MFMA = "v_mfma_f32_16x16x32_bf16"
+RD_ORDER = [("X", 0)] + [("Y", j) for j in range(8)] + [("X", i) for i in range(1, 8)]
+
+
+def X(s, i):
+    b = 128 + 64 * s + 4 * i
+    return f"v[{b}:{b + 3}]"
+
+
+def Y(s, j):
+    b = 160 + 64 * s + 4 * j
+    return f"v[{b}:{b + 3}]"
+
+
+def ACC(i, j):
+    b = 4 * (8 * i + j)
+    return f"a[{b}:{b + 3}]"
+
+
+DEFAULT = dict(m0_early=False, nop=True, sc1=True, a_slots=[24 + 4 * k for k in range(8)],
+               b_slots=[64 + 5 * k for k in range(8)], bar2=108)
+
+
+class Prog:
+    def __init__(self, noload=False, opt=None):
+        self.opt = dict(DEFAULT, **(opt or {}))
+        self.lines = []
+        self.lgkm = []        # outstanding LDS reads (dest register names), in issue order
+        self.done = 0         # reads [0, done) of self.lgkm known complete
+        self.noload = noload  # ablation: no LDS-DMA after the prologue (results invalid)
+
+    def emit(self, s):
+        self.lines.append(s)
+
+    def read(self, kind, s, idx):
+        reg = X(s, idx) if kind == "X" else Y(s, idx)
+        base = ("%[rB" if kind == "X" else "%[rA") + f"{s}]"
+        off = 2048 * idx
+        self.emit(f"ds_read_b128 {reg}, {base}" + (f" offset:{off}" if off else ""))
+        self.lgkm.append(reg)
+
+    def need(self, regs):
+        last = -1
+        for n, r in enumerate(self.lgkm):
+            if r in regs:
+                last = n
+        if last < self.done:
+            return
+        after = len(self.lgkm) - 1 - last
+        n = min(after, 15)
+        self.emit(f"s_waitcnt lgkmcnt({n})")
+        self.done = len(self.lgkm) - n
+
+    def wait_all_lgkm(self):
+        self.emit("s_waitcnt lgkmcnt(0)")
+        self.done = len(self.lgkm)
+
+    def set_m0(self, op, k):
+        off = (32768 if op == "B" else 0) + 4096 * k
+        self.emit(f"s_add_u32 m0, %[sM], {off}")
+
+    def piece(self, op, k, src, m0=True):
+        """LDS-DMA piece k (0..7) of operand op ('A'/'B') of a K-tile into the current load stage (m0 base
+        %[sM]); src 'm' (main operand, k offset %[sK]) or 'e0' / 'e1' (LoRA extension tile 0 / 1).
+        m0=False: M0 was set one MFMA gap earlier (set_m0), which also covers the M0 -> LDS-DMA wait state."""
+        if m0:
+            self.set_m0(op, k)
+            self.emit("s_nop 0")
+        c = " sc1" if self.opt["sc1"] else ""
+        if src == "m":
+            self.emit(f"buffer_load_dwordx4 %[o{op}{k}], %[rs{op}], %[sK] offen{c} lds")
+        else:
+            so = "0" if src == "e0" else "%[sE1]"
+            self.emit(f"buffer_load_dwordx4 %[e{op}{k}], %[rs{op}2], {so} offen{c} lds")
+
+    def tile(self, first=False, load=None, has_next=True, vm_next=None, loop=None):
+        """One K-tile.  load: the source of the tile two ahead ('m', 'e0', 'e1') or None.  vm_next: the
+        vmcnt that retires the next tile's pieces (pieces issued after them).  loop: label to branch back
+        to while --%[cnt] != 0."""
+        if self.noload and not first:
+            load = None
+            vm_next = 0
+        post = {k: [] for k in range(128)}
+        pre = {k: [] for k in range(128)}
+        # substep-1 fragments of this tile (stage t): gaps 0..15
+        for n, (kind, idx) in enumerate(RD_ORDER):
+            post[n].append(("read", kind, 1, idx))
+        # read-base toggles: rA0/rB0 (substep 0, next tile) and rA1/rB1 (substep 1, next tile)
+        post[18].append(("v_xor_b32 %[rA0], %[tA0], %[rA0]",))
+        post[19].append(("v_xor_b32 %[rB0], %[tB0], %[rB0]",))
+        post[20].append(("v_xor_b32 %[rA1], %[tA1], %[rA1]",))
+        post[21].append(("v_xor_b32 %[rB1], %[tB1], %[rB1]",))
+        if load is not None:
+            pre[24].append(("lgkm0",))
+            pre[24].append(("s_barrier",))
+            early = self.opt["m0_early"]
+            for op, slots in (("A", self.opt["a_slots"]), ("B", self.opt["b_slots"])):
+                for k, sl in enumerate(slots):
+                    if early:
+                        post[sl - 1].append(("m0", op, k))
+                    post[sl].append(("piece", op, k, load, not early))
+            if load == "m":
+                post[103].append(("s_add_u32 %[sK], %[sK], 128",))
+        post[102].append(("s_xor_b32 %[sM], %[sM], %[sMT]",))
+        if has_next:
+            b2 = self.opt["bar2"]
+            pre[b2].append((f"s_waitcnt vmcnt({vm_next})",))
+            pre[b2].append(("s_barrier",))
+            for n, (kind, idx) in enumerate(RD_ORDER):
+                post[min(b2 + n, 127)].append(("read", kind, 0, idx))
+        for k in range(128):
+            for it in pre[k]:
+                self._item(it)
+            s, r = divmod(k, 64)
+            i, j = divmod(r, 8)
+            if j == 0:  # one wait per row of 8 blocks: fragment X(s, i) and every Y(s, *)
+                self.need({X(s, i)} | {Y(s, jj) for jj in range(8)})
+            self.need({X(s, i), Y(s, j)})
+            c = "0" if (first and s == 0) else ACC(i, j)
+            self.emit(f"{MFMA} {ACC(i, j)}, {X(s, i)}, {Y(s, j)}, {c}")
+            for it in post[k]:
+                self._item(it)
+        if loop is not None:
+            self.emit("s_sub_u32 %[cnt], %[cnt], 1")
+            self.emit("s_cmp_lg_u32 %[cnt], 0")
+            self.emit(f"s_cbranch_scc1 {loop}")
+
+    def _item(self, it):
+        if it[0] == "read":
+            self.read(it[1], it[2], it[3])
+        elif it[0] == "lgkm0":
+            self.wait_all_lgkm()
+        elif it[0] == "piece":
+            self.piece(it[1], it[2], it[3], it[4] if len(it) > 4 else True)
+        elif it[0] == "m0":
+            self.set_m0(it[1], it[2])
+        else:
+            self.emit(it[0])
+
+    def prologue(self, src0, src1):
+        self.emit("s_mov_b32 %[sSave], m0")
+        self.emit("s_nop 4")
+        for t, src in ((0, src0), (1, src1)):
+            for op in "AB":
+                for k in range(8):
+                    self.piece(op, k, src)
+            if src == "m":
+                self.emit("s_add_u32 %[sK], %[sK], 128")
+            self.emit("s_xor_b32 %[sM], %[sM], %[sMT]")
+        self.emit("s_waitcnt vmcnt(16)")
+        self.emit("s_barrier")
+        for kind, idx in RD_ORDER:
+            self.read(kind, 0, idx)
+
+    def mask_pass(self):
+        """Dropout on the extension product held in the accumulators: acc *= keep ? scale : 0.
+        Mask word %[mk<j>] bit 4i+e keeps element e of block (i, j)."""
+        self.emit("s_nop 15")
+        self.emit("s_nop 15")
+        for i in range(8):
+            for j in range(8):
+                for e in range(4):
+                    a = f"a{4 * (8 * i + j) + e}"
+                    self.emit(f"v_accvgpr_read_b32 v120, {a}")
+                    self.emit(f"v_bfe_i32 v121, %[mk{j}], {4 * i + e}, 1")
+                    self.emit("v_mul_f32 v120, %[dsc], v120")
+                    self.emit("v_and_b32 v120, v121, v120")
+                    self.emit(f"v_accvgpr_write_b32 {a}, v120")
+        self.emit("s_nop 7")
+
+    def epilogue(self):
+        self.emit("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.emit("s_nop 15")
+        self.emit("s_nop 15")
+        self.emit("s_barrier")
+        self.emit("s_mov_b32 m0, %[sSave]")
+
+
+def prog_plain(E, noload=False, opt=None):
+    p = Prog(noload, opt)
+    p.prologue("m", "m")
+    p.tile(first=True, load="m", vm_next=16)
+    p.emit("L_w4loop_%=:")
+    p.tile(load="m", vm_next=16, loop="L_w4loop_%=")
+    # tail: main tiles nm-2, nm-1, then the E extension tiles; loads of the tile two ahead
+    seq = ["m", "m"] + ["e0", "e1"][:E]
+    for n in range(len(seq)):
+        ld = seq[n + 2] if n + 2 < len(seq) else None
+        nxt = n + 1 < len(seq)
+        p.tile(load=ld, has_next=nxt, vm_next=(16 if ld else 0))
+    p.epilogue()
+    return p
+
+
+def prog_drop(E, noload=False):
+    p = Prog(noload)
+    seq0 = ["e0", "e1"][:E] + ["m", "m"]
+    p.prologue(seq0[0], seq0[1])
+    for n in range(E):
+        p.tile(first=(n == 0), load=seq0[n + 2], vm_next=16)
+    p.mask_pass()
+    p.emit("L_w4loop_%=:")
+    p.tile(load="m", vm_next=16, loop="L_w4loop_%=")
+    p.tile(load=None, has_next=True, vm_next=0)
+    p.tile(load=None, has_next=False)
+    p.epilogue()
+    return p
+
+
+HEADER = """// GENERATED by gen_gemm_w4.py -- do not edit.  The hand-placed K-loop programs of gemm_nt_w4_kernel
+// (gemm_w4.h): see the generator's docstring for the schedule.
+"""
+
+
+def asm_fn(name, prog, drop):
+    outs = ['[sSave] "=&s"(o.save)', '[cnt] "+s"(o.cnt)', '[sK] "+s"(o.sK)', '[sM] "+s"(o.sM)',
+            '[rA0] "+v"(o.rA0)', '[rA1] "+v"(o.rA1)', '[rB0] "+v"(o.rB0)', '[rB1] "+v"(o.rB1)']
+    ins = ['[rsA] "s"(o.rsA)', '[rsB] "s"(o.rsB)', '[rsA2] "s"(o.rsA2)', '[rsB2] "s"(o.rsB2)',
+           '[sE1] "s"(o.sE1)', '[sMT] "s"(o.sMT)',
+           '[tA0] "v"(o.tA0)', '[tA1] "v"(o.tA1)', '[tB0] "v"(o.tB0)', '[tB1] "v"(o.tB1)']
+    ins += [f'[oA{k}] "v"(o.oA[{k}])' for k in range(8)] + [f'[oB{k}] "v"(o.oB[{k}])' for k in range(8)]
+    ins += [f'[eA{k}] "v"(o.eA[{k}])' for k in range(8)] + [f'[eB{k}] "v"(o.eB[{k}])' for k in range(8)]
+    if drop:
+        ins += [f'[mk{j}] "v"(o.mk[{j}])' for j in range(8)] + ['[dsc] "s"(o.dsc)']
+    clob = ['"memory"', '"scc"'] + [f'"v{r}"' for r in (120, 121)] + [f'"v{r}"' for r in range(128, 256)] + \
+        [f'"a{r}"' for r in range(256)]
+    body = "\n".join(f'      "{l}\\n"' for l in prog.lines)
+    return (f"__device__ __forceinline__ void {name}(W4Ops& o) {{\n  asm volatile(\n{body}\n"
+            f"      : {', '.join(outs)}\n      : {', '.join(ins)}\n      : {', '.join(clob)});\n}}\n")
+
+
+# ablation schedule variants (gemm_nt_w4_kernel<false, DBG, V>, library variants 42..)
+ABL_VARIANTS = {
+    1: dict(m0_early=True),
+    2: dict(m0_early=True, sc1=False),
+    3: dict(m0_early=True, a_slots=[25 + 3 * k for k in range(8)], b_slots=[49 + 3 * k for k in range(8)]),
+    4: dict(m0_early=True, a_slots=[25 + 3 * k for k in range(8)], b_slots=[49 + 3 * k for k in range(8)], bar2=112),
+    5: dict(a_slots=[26, 26, 34, 34, 42, 42, 50, 50], b_slots=[66, 66, 74, 74, 82, 82, 90, 90]),
+}
+
+
+def acc_reader():
+    """w4_acc(N): accumulator block N (= 8 i + j) of a[0:255] as f32x4; N folds to a constant."""
+    cases = []
+    for n in range(64):
+        b = 4 * n
+        cases.append(f'    case {n}: asm volatile("v_accvgpr_read_b32 %0, a{b}\\n\\tv_accvgpr_read_b32 %1, a{b + 1}\\n\\t'
+                     f'v_accvgpr_read_b32 %2, a{b + 2}\\n\\tv_accvgpr_read_b32 %3, a{b + 3}" '
+                     f': "=v"(x), "=v"(y), "=v"(z), "=v"(w)); break;')
+    return ("__device__ __forceinline__ f32x4 w4_acc(int n) {\n  float x = 0.f, y = 0.f, z = 0.f, w = 0.f;\n"
+            "  switch (n) {\n" + "\n".join(cases) + "\n    default: break;\n  }\n  return f32x4{x, y, z, w};\n}\n")
+
+
+def main(out):
+    parts = [HEADER, acc_reader()]
+    for E in (0, 1, 2):
+        parts.append(asm_fn(f"w4_plain{E}", prog_plain(E), False))
+    for E in (1, 2):
+        parts.append(asm_fn(f"w4_drop{E}", prog_drop(E), True))
+    parts.append("#ifdef OSPO_ABLATION\n// decomposition (results invalid): no LDS-DMA after the prologue\n")
+    parts.append(asm_fn("w4_plain0_noload", prog_plain(0, noload=True), False))
+    parts.append("// schedule variants for A/B (w4v<V>_plain<E>, bf16 without dropout)\n")
+    for v, opt in ABL_VARIANTS.items():
+        for E in (0, 1, 2):
+            parts.append(asm_fn(f"w4v{v}_plain{E}", prog_plain(E, opt=opt), False))
+    parts.append("#endif\n")
+    with open(out, "w") as f:
+        f.write("".join(parts))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gemm_w4_asm.inc")

@@ -1,0 +1,182 @@
+"""The 4-wave hand-scheduled GEMM (gemm_w4.h, ablation variant 40) against the default SP8 kernel
+(variant 0): bit-equality on every epilogue / extension / dropout / split-K form, then interleaved
+timing on the step shapes (variant 41 = w4 with no loads after the prologue: the loop's own rate).
+Run on the GPU box: python tools/w4_check.py [--no-time]"""
+import os as _os
+_os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
+                                                     "ospo_amd", "libospo_hip_ablation.so"))
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
+from ospo_amd import ops  # noqa: E402
+from ospo_amd._lib import call  # noqa: E402
+
+dev = "cuda"
+
+
+def rnd(*s, scale=1.0):
+    return ((torch.rand(*s, device=dev) * 2 - 1) * scale).bfloat16()
+
+
+def ints(*s):
+    return torch.randint(-3, 4, s, device=dev).bfloat16()
+
+
+def run(v, fn):
+    call("ospo_set_gemm_variant", v)
+    out = fn()
+    torch.cuda.synchronize()
+    call("ospo_set_gemm_variant", 0)
+    return out
+
+
+def check(name, fn, ref_fn=None):
+    o0 = run(0, fn)
+    o1 = run(40, fn)
+    line = {"case": name, "bit_equal": bool(torch.equal(o0, o1)),
+            "max_abs_diff": float((o0.float() - o1.float()).abs().max())}
+    if ref_fn is not None:
+        ref = ref_fn()
+        line["w4_exact_vs_fp32"] = bool(torch.equal(o1.float(), ref))
+    print(json.dumps(line), flush=True)
+    return line["bit_equal"]
+
+
+def correctness():
+    ok = True
+    torch.manual_seed(1)
+    for (M, N, K, K2) in [(1000, 512, 512, 0), (1000, 512, 512, 64), (777, 768, 1024, 128), (4800, 4096, 4096, 64),
+                          (300, 256, 256, 64), (4608, 4096, 2048, 0)]:
+        a, b = ints(M, K), ints(N, K)
+        a2 = ints(M, K2) if K2 else None
+        b2 = ints(N, K2) if K2 else None
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+        def f(a=a, b=b, a2=a2, b2=b2, out=out):
+            out.fill_(7)
+            ops.gemm_nt(a, b, out, a2=a2, b2=b2)
+            return out.clone()
+
+        def ref(a=a, b=b, a2=a2, b2=b2):
+            r = a.float() @ b.float().t()
+            if a2 is not None:
+                r = r + a2.float() @ b2.float().t()
+            return r.bfloat16().float()
+        ok &= check(f"int M{M} N{N} K{K} K2{K2}", f, ref)
+        # random data, bias + residual + alpha
+        a, b = rnd(M, K), rnd(N, K)
+        a2 = rnd(M, K2) if K2 else None
+        b2 = rnd(N, K2) if K2 else None
+        bias, res = rnd(N, scale=0.5), rnd(M, N, scale=0.5)
+
+        def g(a=a, b=b, a2=a2, b2=b2, out=out, bias=bias, res=res):
+            out.fill_(7)
+            ops.gemm_nt(a, b, out, a2=a2, b2=b2, alpha=0.75, bias=bias, residual=res)
+            return out.clone()
+        ok &= check(f"rnd+bias+res M{M} N{N} K{K} K2{K2}", g)
+        for sp in (2, 3, 5):
+            def h(a=a, b=b, a2=a2, b2=b2, out=out, sp=sp):
+                out.fill_(7)
+                ops.gemm_nt(a, b, out, a2=a2, b2=b2, split=sp)
+                return out.clone()
+            ok &= check(f"split{sp} M{M} N{N} K{K} K2{K2}", h)
+        if K2:
+            for p in (0.05, 0.3):
+                def d(a=a, b=b, a2=a2, b2=b2, out=out, p=p):
+                    out.fill_(7)
+                    ops.gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(1234, p))
+                    return out.clone()
+                ok &= check(f"dropout{p} M{M} N{N} K{K} K2{K2}", d)
+            if N % 128 == 0:
+                bits = torch.randint(0, 256, (M * N // 8,), device=dev, dtype=torch.uint8)
+
+                def kb(a=a, b=b, a2=a2, b2=b2, out=out, bits=bits):
+                    out.fill_(7)
+                    ops.gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(99, 0.05), keep_bits=bits)
+                    return out.clone()
+                ok &= check(f"keepbits M{M} N{N} K{K} K2{K2}", kb)
+                for sp in (2, 4):
+                    def kbs(a=a, b=b, a2=a2, b2=b2, out=out, bits=bits, sp=sp):
+                        out.fill_(7)
+                        ops.gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(99, 0.05), keep_bits=bits, split=sp)
+                        return out.clone()
+                    ok &= check(f"keepbits split{sp} M{M} N{N} K{K} K2{K2}", kbs)
+    # RoPE epilogue on the q|k|v shape
+    M, N, K = 1200, 12288, 4096
+    a, b, a2, b2 = rnd(M, K), rnd(N, K), rnd(M, 64), rnd(N, 64)
+    cos, sin = ops.rope_tables(600, 128, 1e4, dev)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+    def r(out=out):
+        out.fill_(7)
+        ops.gemm_nt(a, b, out, a2=a2, b2=b2, rope=(cos, sin, 600, 8192))
+        return out.clone()
+    ok &= check("rope qkv M1200", r)
+    print(json.dumps({"all_bit_equal": bool(ok)}), flush=True)
+    return ok
+
+
+def timing():
+    M = 4800
+    shapes = [("qkv_fwd", M, 12288, 4096, 64), ("o_fwd", M, 4096, 4096, 64), ("gu_fwd", M, 22016, 4096, 64),
+              ("down_fwd", M, 4096, 11008, 64), ("down_dx", M, 11008, 4096, 64), ("gu_dx", M, 4096, 22016, 64),
+              ("qkv_dx", M, 4096, 12288, 64), ("gh2_fwd", 4608, 16384, 4096, 0), ("gh2_dx", 4608, 4096, 16384, 0),
+              ("sq4096", 4096, 4096, 4096, 0)]
+    variants = [int(v) for v in os.environ.get("W4_VARIANTS", "0,40,41").split(",")]
+    tot = {v: 0.0 for v in variants}
+    for name, m, n, k, k2 in shapes:
+        a, b = rnd(m, k), rnd(n, k)
+        a2 = rnd(m, k2) if k2 else None
+        b2 = rnd(n, k2) if k2 else None
+        out = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+        drop = (name.endswith("_dx") and k2) and os.environ.get("W4_DROP", "1") == "1"
+        bits = torch.randint(0, 256, (m * n // 8,), device=dev, dtype=torch.uint8) if drop else None
+        res = {v: [] for v in variants}
+        res["hipblaslt"] = []
+
+        def fn():
+            if drop:
+                ops.gemm_nt(a, b, out, a2=a2, b2=b2, dropout=(5, 0.05), keep_bits=bits)
+            else:
+                ops.gemm_nt(a, b, out, a2=a2, b2=b2)
+        for _ in range(5):
+            for v in variants:
+                call("ospo_set_gemm_variant", v)
+                fn()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(10):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                res[v].append(e0.elapsed_time(e1) / 10)
+            call("ospo_set_gemm_variant", 0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.matmul(a, b.t(), out=out)
+            e0.record()
+            for _ in range(10):
+                torch.matmul(a, b.t(), out=out)
+            e1.record()
+            torch.cuda.synchronize()
+            res["hipblaslt"].append(e0.elapsed_time(e1) / 10)
+        fl = 2.0 * m * n * k
+        line = {"shape": name, "drop": bool(drop)}
+        for kk, ts in res.items():
+            t = sorted(ts)[len(ts) // 2]
+            line[str(kk)] = {"us": round(t * 1e3, 1), "tflops": round(fl / t / 1e9, 1)}
+            if kk in tot and name != "sq4096":
+                tot[kk] += t
+        print(json.dumps(line), flush=True)
+    print(json.dumps({"step_shapes_total_ms": {str(k): round(v, 3) for k, v in tot.items()}}), flush=True)
+
+
+import os  # noqa: E402
+
+if __name__ == "__main__":
+    ok = correctness()
+    if "--no-time" not in sys.argv:
+        timing()
+    sys.exit(0 if ok else 1)
