@@ -2511,10 +2511,6 @@ int launch_default(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
   if (g_gemm_variant == 27) return launch_v5<0, DROP, false, 8>(a, s, so);
   if (g_gemm_variant == 28) return launch_v5<0, DROP, false, 9>(a, s, so);
   if (g_gemm_variant == 32) return launch_v6<DROP>(a, s, so);  // persistent SP8 (rejected)
-  if (g_gemm_variant == 40) {
-    const int r = launch_w4<DROP>(a, s, so);
-    if (r != OSPO_ERR_UNSUPPORTED) return r;
-  }
   if (g_gemm_variant == 41) {
     const int r = launch_w4<DROP, 1>(a, s, so);
     if (r != OSPO_ERR_UNSUPPORTED) return r;
@@ -2534,7 +2530,11 @@ int launch_default(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
     if (g_gemm_variant == 47) r = launch_w4<false, 0, 5>(a, s, so);
     if (r != OSPO_ERR_UNSUPPORTED) return r;
   }
+  if (g_gemm_variant == 27) return launch_v5<0, DROP, false, 8>(a, s, so);  // the round-3 default (SP8)
 #endif
+  // the 4-wave hand-scheduled kernel where it applies (gemm_w4.h), else SP8
+  const int r = launch_w4<DROP>(a, s, so);
+  if (r != OSPO_ERR_UNSUPPORTED) return r;
   return launch_v5<0, DROP, false, 8>(a, s, so);
 }
 
@@ -2576,7 +2576,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
   const int tile = pick_nt_tile(M, N);
   if (tile == 64) return launch<2, 2, 2, 2, false, false, EPI_BF16>(a, stream);
 #ifndef OSPO_ABLATION
-  return launch_v5<0, false, false, 8>(a, stream, so);  // SP8 (4 + 4 refills, buffer-offset staging) + split-K tail
+  return launch_default<false>(a, stream, so);  // w4 (gemm_w4.h), else SP8; + split-K tail
 #else
   switch (g_gemm_variant) {
     // A/B alternatives (tools/gemm_bench.py); results identical, schedules differ
@@ -2599,7 +2599,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 24: return launch_v5<0, false, false, 5>(a, stream, so, true);  // SP5: 4 + 4 refills, buffer-offset staging
     case 25: return launch_v5<0, false, false, 6>(a, stream, so, true);  // SP, 4 + 4 refills, generic staging
     case 26: return launch_v5<0, false, false, 7>(a, stream, so, true);  // SP, 2 + 6 refills, buffer-offset staging
-    case 27: return launch_v5<0, false, false, 8>(a, stream, so, true);  // SP5 unrolled by 2
+    case 27: return launch_v5<0, false, false, 8>(a, stream, so, true);  // SP8 (SP5 unrolled by 2): the round-3 default
     case 28: return launch_v5<0, false, false, 9>(a, stream, so, true);  // SP8 + B0 of the next tile read early
     case 29: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<4, false, false, 8>(d, stream, so, false); }  // SP8 + stamps
     case 30: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<5, false, false, 8>(d, stream, so, false); }  // SP8 + phase stamps
@@ -2607,7 +2607,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 32: return launch_v6<false>(a, stream, so);                                  // persistent SP8 (v6, rejected)
     case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47:
       return launch_default<false>(a, stream, so);                                   // 4-wave hand-scheduled (w4)
-    default: return launch_v5<0, false, false, 8>(a, stream, so, true);               // SP8 + split-K tail
+    default: return launch_default<false>(a, stream, so);                            // w4 / SP8 + split-K tail
   }
 #endif
 }

@@ -1263,6 +1263,7 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
       default: break;
     }
   }
+  if (dr.bits) return OSPO_ERR_UNSUPPORTED;  // keep bits are written by the v3 cases above only (tile counts 1-4, 6, 8)
   if (g_skinny_variant >= 2 && out_cols % 4 == 0 && K >= 128) {
     // dense: one workgroup column over all n-tiles; block-diagonal: grid z = module
     const int nz = a_koff > 0 ? nmods : 1;

@@ -154,6 +154,9 @@ class SimPOEngine:
                     torch.zeros(max(L, 1), g.nmods * r, g.Nmod, dtype=BF16, device=dev))
             for gname, g in self.layout.groups.items()}
         self.packed = [{gname: tuple(t[i] for t in ts) for gname, ts in self._packed_all.items()} for i in range(L)]
+        # fuse_gdb (LoRA r = 16): g = s dy.B and dB += dy^T u of a group in one stream over dy on the main stream
+        # (ospo_lora_gdb); the side stream then runs only dA.  Off: g on the main stream, dB with dA on the side.
+        self.fuse_gdb = bool(fuse_gdb) and dims.lora_r == 16
         self.pack_lora()
         self._alloc(max_pairs, max_text_len, n_img_tokens)
         self._rope_T = -1
@@ -166,9 +169,6 @@ class SimPOEngine:
         # > 0: the LoRA weight gradients as ospo_lora_wgrad streams of ~wgrad_wgs workgroups; 0: the 64 x 64
         # f32-atomic tiles (faster in isolation, 180.8 vs 198.8 us per layer, tools/lora_grads_bench.py)
         self.wgrad_wgs = int(wgrad_wgs)
-        # fuse_gdb (LoRA r = 16): g = s dy.B and dB += dy^T u of a group in one stream over dy on the main stream
-        # (ospo_lora_gdb); the side stream then runs only dA.  Off: g on the main stream, dB with dA on the side.
-        self.fuse_gdb = bool(fuse_gdb) and dims.lora_r == 16
         # da_stream: dA as one stream over the adapter input with the forward's keep bits (ops.lora_da, round 3:
         # 5.2 ms of side-stream kernel time per step against 5.6 for the 64 x 64 f32-atomic tiles re-hashing the
         # mask, profiles/r03/step_lora_variants_breakdown_v2.txt); off: those tiles (ops.gemm_f32acc(b_dropout=...)),
@@ -251,10 +251,11 @@ class SimPOEngine:
         # fp32 g partials of the fused g / dB stream (ospo_lora_gdb, r = 16), sized once for the capacity
         # (the size grows with the rows); every group's call fits
         self._gdb_ws = None
-        if self.layout.r == 16:
-            nb = max(int(ops.query_gdb_ws(Mc, g.nmods, g.Nmod)) for g in self.layout.groups.values()
-                     if g.Nmod % 128 == 0)
-            self._gdb_ws = torch.empty((nb + 15) // 16 * 4, dtype=F32, device=dev)
+        if self.fuse_gdb:
+            nb = max((int(ops.query_gdb_ws(Mc, g.nmods, g.Nmod)) for g in self.layout.groups.values()
+                      if g.Nmod % 128 == 0 and g.nmods <= 4), default=0)
+            if nb > 0:
+                self._gdb_ws = torch.empty((nb + 15) // 16 * 4, dtype=F32, device=dev)
         # MXFP8 activation operands, one per contraction size (main-stream GEMMs only, reused in order)
         self._mx = {K: ops.MX8(Mc, K, dev) for K in {D, Fd, 2 * Fd, 3 * D}} if self.linear_dtype == "mx8" else {}
 
@@ -319,9 +320,15 @@ class SimPOEngine:
             return None
         return self._keep_bits(layer, group, K)
 
+    # u-product tile counts whose streaming kernel writes keep bits (ospo_lora_skinny refuses the others)
+    _BITS_TILES = (1, 2, 3, 4, 6, 8)
+
     def _bits_fwd(self, layer: int, group: str, K: int):
         if not self.use_keep_bits or self._drop(layer, group) is None:
             return None
+        nt = (self.layout.groups[group].nmods * self.layout.r + 15) // 16
+        if nt not in self._BITS_TILES:
+            return None  # (no bits written: the backward's consumers re-hash the mask)
         return self._keep_bits(layer, group, K)
 
     def _drop(self, layer: int, group: str):
@@ -356,7 +363,7 @@ class SimPOEngine:
         """(g_s, dB done): with fuse_gdb, g_s = bf16(scale * dy . Bcat) and dB += dy^T . u in one stream over dy
         (ospo_lora_gdb); else _lora_g and the side stream computes dB."""
         r = self.layout.r
-        if not (self.fuse_gdb and r == 16 and g.Nmod % 128 == 0 and g.nmods <= 4):
+        if not (self.fuse_gdb and self._gdb_ws is not None and r == 16 and g.Nmod % 128 == 0 and g.nmods <= 4):
             return self._lora_g(dy, g, Bcat, BT, M, par), False
         out = self.gsc2[g.name][par]
         b_off = gbase + g.b_off

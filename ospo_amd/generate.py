@@ -97,8 +97,12 @@ class T2IGenerator:
         # one launch per Linear (ops.decode_linear, round 3): the RMSNorms folded into the q|k|v and gate|up
         # stagings, split sums and consumers in the launch; needs every decode weight tiled (N % 128)
         Dg, Fa = dims.gen_head_dim, self.al_w2.shape[1]
+        # (the folded RMSNorm reads one sum-of-squares partial per 128 input columns, <= 32 of them: D, Dg <= 4096;
+        # the in-launch split sums keep one counter per 128 output rows, <= 1024 of them)
         self.fused = (bool(fused_layers) and self.tiled and all(n % 128 == 0 for n in (D, 3 * D, 2 * Fd, Dg))
-                      and dims.img_vocab % 128 == 0 and all(k % 32 == 0 for k in (D, Fd, Dg, Fa)))
+                      and dims.img_vocab % 128 == 0 and all(k % 32 == 0 for k in (D, Fd, Dg, Fa))
+                      and D // 128 <= 32 and Dg // 128 <= 32
+                      and all(n // 128 <= 1024 for n in (3 * D, 2 * Fd, D, Dg, dims.img_vocab)))
         for lw in self.layers:
             for k in ("qkv", "o", "gu", "down"):
                 src = ops.interleave_gate_up(lw[k]) if (k == "gu" and self.fused) else lw[k]

@@ -126,12 +126,17 @@ class ConstantLR:
 
 
 class CosineDecayWarmUpRestarts:
-    """ospo/utils/train.py:119-148 (linear warm-up, cosine decay to eta_min)."""
+    """ospo/utils/train.py:119-148 (linear warm-up, cosine decay to eta_min).  As there, construction
+    takes the first step: torch's _LRScheduler.__init__ calls the overridden step() once, so the first
+    optimizer step already runs at iteration 1 (lr = eta_max / warmup_iter, not 0) -- pinned by
+    tests/golden/sched_golden.json (make_golden_sched.py runs the reference's class)."""
 
     def __init__(self, optimizer, warmup_iter, max_iter, eta_min=0.0, eta_max=1.5e-4):
         self.optimizer, self.warmup_iter, self.max_iter = optimizer, warmup_iter, max_iter
         self.eta_min, self.eta_max, self.iteration = eta_min, eta_max, 0
-        self._apply()
+        for g in optimizer.param_groups:
+            g.setdefault("initial_lr", g["lr"])
+        self.step()
 
     def get_lr(self):
         import math

@@ -423,3 +423,129 @@ def test_image_processor_equals_reference_processor_bytes():
         assert x.dtype == np.float32 and x.shape == (1, 3, 384, 384), name
         np.testing.assert_array_equal(x.reshape(-1)[::331], z[f"px{i}_sample"], err_msg=name)
         assert hashlib.sha256(x.tobytes()).hexdigest() == str(z[f"px{i}_sha256"]), name
+
+
+def _golden_sched():
+    with open(os.path.join(ROOT, "tests", "golden", "sched_golden.json")) as f:
+        return json.load(f)
+
+
+class _Opt:
+    """The optimizer surface the schedules touch (param_groups)."""
+
+    def __init__(self, lr, lr_scale=None):
+        g = {"lr": float(lr)}
+        if lr_scale is not None:
+            g["lr_scale"] = lr_scale
+        self.param_groups = [g]
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_cosine_schedule_equals_reference_golden(case):
+    """CosineDecayWarmUpRestarts (ospo_amd/wrapper/train.py) against the reference's own class
+    (ospo/utils/train.py:119-148, run by tests/golden/make_golden_sched.py): the lr of every optimizer step,
+    including the construction step torch's _LRScheduler takes (the first step runs at iteration 1)."""
+    from ospo_amd.wrapper.train import CosineDecayWarmUpRestarts
+    c = _golden_sched()["cosine"][case]
+    opt = _Opt(c["init_lr"], c["lr_scale"])
+    s = CosineDecayWarmUpRestarts(opt, warmup_iter=c["max_training_steps"] * c["warmup_ratio"],
+                                  max_iter=c["max_training_steps"], eta_min=c["min_lr"], eta_max=c["init_lr"])
+    got = [opt.param_groups[0]["lr"]]
+    for _ in range(len(c["lrs"]) - 1):
+        s.step()
+        got.append(opt.param_groups[0]["lr"])
+    assert got == pytest.approx(c["lrs"], rel=1e-12, abs=1e-18)
+    # a resumed schedule continues where the checkpoint left it
+    s2 = CosineDecayWarmUpRestarts(_Opt(c["init_lr"], c["lr_scale"]), warmup_iter=c["max_training_steps"] * c["warmup_ratio"],
+                                   max_iter=c["max_training_steps"], eta_min=c["min_lr"], eta_max=c["init_lr"])
+    s2.load_state_dict(s.state_dict())
+    assert s2.optimizer.param_groups[0]["lr"] == pytest.approx(got[-1], rel=1e-12, abs=1e-18)
+
+
+def test_constant_schedule_equals_reference_golden():
+    from ospo_amd.wrapper.train import ConstantLR
+    c = _golden_sched()["constant"][0]
+    opt = _Opt(c["init_lr"])
+    s = ConstantLR(opt, factor=1.0, total_iters=c["total_iters"])
+    got = [opt.param_groups[0]["lr"]]
+    for _ in range(len(c["lrs"]) - 1):
+        s.step()
+        got.append(opt.param_groups[0]["lr"])
+    assert got == pytest.approx(c["lrs"], rel=1e-12)
+
+
+def test_configure_optimizers_builds_reference_schedules():
+    """configure_optimizers (ospo/wrapper/train.py:107-130): 'cosine' -> warm-up max_steps * warmup_ratio,
+    eta_min = optimizer.min_lr, eta_max = optimizer.init_lr, interval 'step'; 'constant' -> ConstantLR."""
+    from ospo_amd.wrapper.train import ConstantLR, CosineDecayWarmUpRestarts, JanusProTrainWrapper
+    import inspect
+    src = inspect.getsource(JanusProTrainWrapper.configure_optimizers)
+    assert "warmup_ratio" in src and "min_lr" in src and "init_lr" in src and '"interval": "step"' in src
+    assert issubclass(ConstantLR, object) and issubclass(CosineDecayWarmUpRestarts, object)
+
+
+class _AccumWrapper:
+    """A wrapper with the SimPO wrapper's trainer-facing surface over one CPU parameter, so the fit loop's
+    gradient accumulation can be checked against PL 1.9's (loss / accumulate_grad_batches, one optimizer step,
+    clip and scheduler step per accumulate_grad_batches micro-batches; ospo/utils/train.py:32)."""
+
+    def __init__(self):
+        self.w = torch.zeros(3, requires_grad=True)
+        self.engine = types.SimpleNamespace(grads=torch.zeros(3))
+        self.steps = []  # (the .grad seen by each optimizer step)
+        self.global_step = 0
+        outer = self
+
+        class Opt:
+            param_groups = [{"lr": 1.0}]
+
+            def step(self_):
+                outer.steps.append(outer.w.grad.clone())
+                with torch.no_grad():
+                    outer.w -= outer.w.grad
+
+            def zero_grad(self_):
+                outer.w.grad = None
+        self.opt = Opt()
+
+    def setup(self, stage, log_dir=None):
+        if log_dir:
+            os.makedirs(log_dir, exist_ok=True)  # (the real wrapper writes its config there)
+
+    def configure_optimizers(self):
+        sched = types.SimpleNamespace(n=0)
+        sched.step = lambda: setattr(sched, "n", sched.n + 1)
+        self.sched = sched
+        return [self.opt], [{"scheduler": sched, "interval": "step"}]
+
+    def training_step(self, batch, idx):
+        return (self.w * batch).sum() ** 2 / 2
+
+    def on_before_optimizer_step(self):
+        pass
+
+    @property
+    def logged(self):
+        return {}
+
+
+@pytest.mark.parametrize("accum", [1, 2, 3])
+def test_trainer_gradient_accumulation_matches_pl(accum, tmp_path):
+    from ospo_amd.trainer import Trainer
+    cfg = {"base": {"save_path": str(tmp_path), "exp_name": "acc"},
+           "experiment": {"max_training_steps": 2, "gradient_accumulation_steps": accum, "log_steps": 1,
+                          "enable_checkpointing": False}}
+    batches = [torch.tensor([1.0, 2.0, 3.0]) * (i + 1) for i in range(2 * accum)]
+    wr = _AccumWrapper()
+    Trainer(cfg).fit(wr, batches)
+    assert len(wr.steps) == 2 and wr.sched.n == 2
+    # PL: each micro-batch's loss / accum, grads summed over the window, one step per window
+    w = torch.zeros(3, requires_grad=True)
+    for s in range(2):
+        g = torch.zeros(3)
+        for b in batches[s * accum:(s + 1) * accum]:
+            w_ = w.detach().clone().requires_grad_(True)
+            ((w_ * b).sum() ** 2 / 2 / accum).backward()
+            g += w_.grad
+        assert torch.allclose(wr.steps[s], g, rtol=1e-6), (s, wr.steps[s], g)
+        w = (w.detach() - g).requires_grad_(True)
