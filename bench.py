@@ -470,7 +470,13 @@ def main():
     # process-group backend for N > 1: RCCL ("nccl", default on GPUs); "gloo" lets N ranks share one GPU
     # (the multi-rank rehearsal of tests/test_gpu_dp_overlap.py on a one-GPU box)
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None)
+    # A/B only: a GEMM schedule of the ablation library (OSPO_HIP_LIB=ospo_amd/libospo_hip_ablation.so), e.g.
+    # 27 = the round-3 SP8 kernel; the product library has no such knob and refuses the flag
+    ap.add_argument("--gemm-variant", type=int, default=None)
     args = ap.parse_args()
+    if args.gemm_variant is not None:
+        from ospo_amd._lib import call
+        call("ospo_set_gemm_variant", int(args.gemm_variant))
     if launch_ranks(args):
         sys.exit(args.child_rc)
     if args.workload == "stub":
@@ -555,7 +561,8 @@ def main():
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_note": "HBM+Infinity-Cache bytes per launch (2*FETCH_SIZE+WRITE_SIZE, profiles/gemm_pmc.json)",
                 "algorithmic_bytes_per_launch": round(d["bytes"] / d["count"]),
-                "kernel": f"{dom} (gemm_nt_v5_kernel SP-schedule MFMA {'MXFP8 e4m3' if mx else 'bf16'} + split-K fixup)",
+                "kernel": (f"{dom} (gemm_nt_v5_kernel SP-schedule MFMA MXFP8 e4m3 + split-K fixup)" if mx else
+                           f"{dom} (gemm_nt_w4_kernel: 4 waves, hand-placed asm K loop, MFMA bf16; + split-K fixup)"),
                 "launches": d["count"],
                 "avg_launch_us": round(d["ms"] * 1e3 / d["count"], 2),
                 "step_mfma_frac": round(flops_pair * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)}

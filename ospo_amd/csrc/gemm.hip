@@ -2528,6 +2528,10 @@ int launch_default(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
     if (g_gemm_variant == 45) r = launch_w4<false, 0, 3>(a, s, so);
     if (g_gemm_variant == 46) r = launch_w4<false, 0, 4>(a, s, so);
     if (g_gemm_variant == 47) r = launch_w4<false, 0, 5>(a, s, so);
+    if (g_gemm_variant == 48) r = launch_w4<false, 0, 6>(a, s, so);
+    if (g_gemm_variant == 49) r = launch_w4<false, 0, 7>(a, s, so);
+    if (g_gemm_variant == 50) r = launch_w4<false, 0, 8>(a, s, so);
+    if (g_gemm_variant == 51) r = launch_w4<false, 0, 9>(a, s, so);
     if (r != OSPO_ERR_UNSUPPORTED) return r;
   }
   if (g_gemm_variant == 27) return launch_v5<0, DROP, false, 8>(a, s, so);  // the round-3 default (SP8)
@@ -2605,7 +2609,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 30: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<5, false, false, 8>(d, stream, so, false); }  // SP8 + phase stamps
     case 17: return launch_v5<0>(a, stream, so, true);                                   // 8-phase + split-K tail
     case 32: return launch_v6<false>(a, stream, so);                                  // persistent SP8 (v6, rejected)
-    case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47:
+    case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48: case 49: case 50: case 51:
       return launch_default<false>(a, stream, so);                                   // 4-wave hand-scheduled (w4)
     default: return launch_default<false>(a, stream, so);                            // w4 / SP8 + split-K tail
   }
@@ -2766,7 +2770,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || (v > 32 && (v < 40 || v > 47)) || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23)
+  if (v < 0 || (v > 32 && (v < 40 || v > 51)) || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23)
     return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;

@@ -53,7 +53,10 @@ def ACC(i, j):
 # m0_early: each piece's M0 is set one MFMA gap before its LDS-DMA (that gap also covers the M0 -> DMA wait
 # state); 1.3 % faster over the step shapes than M0 + s_nop + DMA in one gap (profiles/r04/w4_variants_v1.log)
 DEFAULT = dict(m0_early=True, sc1=True, a_slots=[24 + 4 * k for k in range(8)],
-               b_slots=[64 + 5 * k for k in range(8)], bar2=108)
+               b_slots=[64 + 5 * k for k in range(8)], bar2=108,
+               # decompositions (ablation only, results invalid): vm_wait overrides barrier 2's vmcnt,
+               # no_bar1 / no_bar2 drop those barriers (and bar1's lgkmcnt(0)), no_reads drops the fragment reads
+               vm_wait=None, no_bar1=False, no_bar2=False, no_reads=False)
 
 
 class Prog:
@@ -68,6 +71,8 @@ class Prog:
         self.lines.append(s)
 
     def read(self, kind, s, idx):
+        if self.opt["no_reads"]:
+            return
         reg = X(s, idx) if kind == "X" else Y(s, idx)
         base = ("%[rB" if kind == "X" else "%[rA") + f"{s}]"
         off = 2048 * idx
@@ -125,9 +130,10 @@ class Prog:
         post[19].append(("v_xor_b32 %[rB0], %[tB0], %[rB0]",))
         post[20].append(("v_xor_b32 %[rA1], %[tA1], %[rA1]",))
         post[21].append(("v_xor_b32 %[rB1], %[tB1], %[rB1]",))
-        if load is not None:
+        if load is not None and not self.opt["no_bar1"]:
             pre[24].append(("lgkm0",))
             pre[24].append(("s_barrier",))
+        if load is not None:
             early = self.opt["m0_early"]
             for op, slots in (("A", self.opt["a_slots"]), ("B", self.opt["b_slots"])):
                 for k, sl in enumerate(slots):
@@ -139,8 +145,10 @@ class Prog:
         post[102].append(("s_xor_b32 %[sM], %[sM], %[sMT]",))
         if has_next:
             b2 = self.opt["bar2"]
-            pre[b2].append((f"s_waitcnt vmcnt({vm_next})",))
-            pre[b2].append(("s_barrier",))
+            vw = vm_next if self.opt["vm_wait"] is None else self.opt["vm_wait"]
+            pre[b2].append((f"s_waitcnt vmcnt({vw})",))
+            if not self.opt["no_bar2"]:
+                pre[b2].append(("s_barrier",))
             for n, (kind, idx) in enumerate(RD_ORDER):
                 post[min(b2 + n, 127)].append(("read", kind, 0, idx))
         for k in range(128):
@@ -271,6 +279,10 @@ ABL_VARIANTS = {
     3: dict(m0_early=True, a_slots=[25 + 3 * k for k in range(8)], b_slots=[49 + 3 * k for k in range(8)]),
     4: dict(m0_early=True, a_slots=[25 + 3 * k for k in range(8)], b_slots=[49 + 3 * k for k in range(8)], bar2=112),
     5: dict(a_slots=[26, 26, 34, 34, 42, 42, 50, 50], b_slots=[66, 66, 74, 74, 82, 82, 90, 90]),
+    6: dict(vm_wait=63),      # decomposition: no wait for the next tile's pieces
+    7: dict(no_bar1=True),    # decomposition: no barrier 1
+    8: dict(no_bar2=True),    # decomposition: no barrier 2
+    9: dict(no_reads=True),   # decomposition: no fragment reads
 }
 
 
@@ -286,8 +298,29 @@ def acc_reader():
             "  switch (n) {\n" + "\n".join(cases) + "\n    default: break;\n  }\n  return f32x4{x, y, z, w};\n}\n")
 
 
+def stage_fn():
+    """w4_stage_bf16: every accumulator block rounded to bf16 (v_cvt_pk_bf16_f32, RNE, as the C++ epilogue's
+    pack2) and written to the epilogue's LDS staging rows (ml * 528 + nl * 2; %[sb] = this lane's block-(0,0)
+    address, block (i, j) at +8448 j + 32 i).  The plain epilogue (alpha 1, no bias): 7 instructions per block
+    instead of the compiler's ~16 (one wave per SIMD: every VALU instruction costs its full issue)."""
+    lines = []
+    for n in range(64):
+        i, j = divmod(n, 8)
+        b = 120 + 4 * (n % 2)
+        for e in range(4):
+            lines.append(f"v_accvgpr_read_b32 v{b + e}, a{4 * n + e}")
+        lines.append(f"v_cvt_pk_bf16_f32 v{b}, v{b}, v{b + 1}")
+        lines.append(f"v_cvt_pk_bf16_f32 v{b + 1}, v{b + 2}, v{b + 3}")
+        off = 8448 * j + 32 * i
+        lines.append(f"ds_write_b64 %[sb], v[{b}:{b + 1}]" + (f" offset:{off}" if off else ""))
+    body = "\n".join(f'      "{l}\\n"' for l in lines)
+    clob = ", ".join(['"memory"'] + [f'"v{r}"' for r in range(120, 128)])
+    return ("__device__ __forceinline__ void w4_stage_bf16(uint32_t sb) {\n  asm volatile(\n" + body +
+            f"\n      :\n      : [sb] \"v\"(sb)\n      : {clob});\n}}\n")
+
+
 def main(out):
-    parts = [HEADER, acc_reader()]
+    parts = [HEADER, acc_reader(), stage_fn()]
     for E in (0, 1, 2):
         parts.append(asm_fn(f"w4_plain{E}", prog_plain(E), False))
     for E in (1, 2):

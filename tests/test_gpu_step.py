@@ -29,8 +29,10 @@ pytestmark = pytest.mark.gpu
 # 7B-shape 2-layer 3.14e-2, r = 32 1.01e-2, r = 8 1.13e-2.  Each test also holds the HIP error to 1.25x
 # the oracle's own bf16-autograd error against fp32 (GRAD_FLOOR_RATIO; measured ratios 0.87-0.97): the
 # fp32-accumulated HIP backward is at least as close to the fp32 gradients as a bf16 autograd is.
+# At 30 layers there is no fixed cap: the bound is 1.25x the oracle's own spread (0.12 / 0.14 / 0.16 for layers
+# 0 / 15 / 29; measured HIP 0.11 / 0.12 / 0.14, profiles/r03/parity_suite_v4_final.jsonl).
 GRAD_FP32_TOL = {"step_tiny_bf16.npz": 2.5e-2, "step_1b2l_bf16.npz": 4e-2, "tiny_fp32_ref": 2.5e-2, "7b_2l": 6.5e-2,
-                 "r32": 2.5e-2, "r8": 2.5e-2, "7b_30l": 1.5e-1}
+                 "r32": 2.5e-2, "r8": 2.5e-2}
 GRAD_FLOOR_RATIO = 1.25
 
 
@@ -253,7 +255,9 @@ def test_step_full_depth_7b_30_layers():
     assert el32 < max(1e-3, floor_l), (el32, floor_l)
     worst = max(ge, key=lambda k: ge[k] / fl[k])
     assert ge[worst] < GRAD_FLOOR_RATIO * fl[worst], (worst, ge[worst], fl[worst])
-    assert max(ge.values()) < GRAD_FP32_TOL["7b_30l"], max(ge.values())
+    # (no fixed absolute cap at 30 layers: the oracle's own bf16 autograd sits 0.12-0.16 from fp32 there
+    # (layer 29 above any fixed 0.15), so the bound is that spread, per tensor above and over all here)
+    assert max(ge.values()) < GRAD_FLOOR_RATIO * max(fl.values()), (max(ge.values()), max(fl.values()))
 
 
 def test_bench_config_first_step_vs_oracle():
@@ -334,6 +338,78 @@ def test_step_7b_shapes_8_pairs_two_layers():
     assert g32 < GRAD_FLOOR_RATIO * floor, (g32, floor)
 
 
+def test_trajectory_five_steps_7b_shapes_two_layers_vs_oracle():
+    """Training past step 1: five optimizer steps of the bench workload (bench.simpo_setup: 4 ragged pairs,
+    T = 600, LoRA r = 16, dropout 0.05) at Janus-Pro-7B widths with 2 decoder layers -- HIP forward, SimPO
+    loss, backward, clip 1.0 + AdamW each step (simpo.train_step, the bench's step) -- against the oracle's
+    own trajectory (oracle.simpo_step + clip_and_adamw: PL clip -> torch AdamW on the bf16 LoRA tensors,
+    ospo/utils/train.py:30, ospo/wrapper/train.py:107-115), the HIP dropout masks of every step replayed.
+    Run in bf16 (the reference's path) and in fp32 (the value both approximate).
+    Bounds: every step's loss within max(1e-3, 1.25x the bf16 oracle's own gap) of the fp32 trajectory;
+    the LoRA update after 5 steps (params - init, all tensors) at most 1.25x as far from the fp32
+    trajectory's update as the bf16 oracle's update is."""
+    import bench
+    from ospo_amd.simpo import SimPOConfig, SimPOLossBuffers, train_step
+    dims, eng, batches, w = bench.simpo_setup(layers=2)
+    cfg = SimPOConfig()
+    B = batches[0][1].shape[0]
+    buf = SimPOLossBuffers(B, "cuda")
+    steps = 5
+    hip_loss, calls, rows = [], [], []
+    for s in range(steps):
+        text, ch, rj = batches[s % len(batches)]
+        out = train_step(eng, text, ch, rj, cfg, buf)
+        hip_loss.append(float(out["loss"].item()))
+        calls.append(eng._drop_call)
+        rows.append(eng.M)
+    torch.cuda.synchronize()
+    hip_p = {k: v.float().cpu() for k, v in eng.lora_tensors().items()}
+    p = eng.lora_dropout
+    wc = {k: v.cpu() for k, v in w.items()}
+    del w, eng
+    torch.cuda.empty_cache()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    odims = O.JanusDims(**{**_oracle_dims(dims).__dict__, "lora_dropout": p})
+    kin = {"qkv": dims.d_model, "o": dims.d_model, "gu": dims.d_model, "down": dims.d_ff}
+    init = {k: v.float() for k, v in wc.items() if ".lora_" in k}
+
+    def trajectory(dt):
+        ww = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in wc.items()}
+        params = {k: ww[k] for k in ww if ".lora_" in k}
+        state, losses = {}, []
+        for s in range(steps):
+            text, ch, rj = batches[s % len(batches)]
+            masks = _LazyMasks(rows[s], kin, 42, calls[s], p)
+            o = O.simpo_step(_unpad(text), ch.cpu().long(), rj.cpu().long(), ww, odims, dtype=dt, dropout_masks=masks)
+            losses.append(float(o.loss))
+            O.clip_and_adamw(params, o.lora_grads, state, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps,
+                             weight_decay=cfg.weight_decay, max_norm=cfg.max_norm)
+        return losses, {k: v.float() for k, v in params.items()}
+
+    l16, p16 = trajectory(torch.bfloat16)
+    l32, p32 = trajectory(torch.float32)
+    names = sorted(init)
+    cat = lambda d: torch.cat([(d[k] - init[k]).flatten() for k in names])  # noqa: E731
+    d_hip, d16, d32 = cat(hip_p), cat(p16), cat(p32)
+    e_upd32, floor_upd, e_upd16 = rel(d_hip, d32), rel(d16, d32), rel(d_hip, d16)
+    e_loss = [abs(a - b) / abs(b) for a, b in zip(hip_loss, l32)]
+    gap = [abs(a - b) / abs(b) for a, b in zip(l16, l32)]
+    record_parity("trajectory_5steps_7b_2l", hip_loss=hip_loss, oracle_bf16_loss=l16, oracle_fp32_loss=l32,
+                  loss_rel_vs_fp32=e_loss, oracle_bf16_loss_gap=gap, update_rel_vs_fp32=e_upd32,
+                  update_rel_vs_bf16=e_upd16, oracle_bf16_update_vs_fp32=floor_upd,
+                  update_norm_rel=float(d_hip.norm() / d32.norm()))
+    e16 = [abs(a - b) / abs(b) for a, b in zip(hip_loss, l16)]
+    for s in range(steps):
+        assert e_loss[s] < max(1e-3, GRAD_FLOOR_RATIO * gap[s]), (s, e_loss[s], gap[s])
+        # and the HIP path follows the reference's own bf16 trajectory far more closely than bf16 and fp32
+        # differ (measured 4.8e-4 .. 2.9e-3 against gaps of 2-11 %)
+        assert e16[s] < max(1e-3, 0.25 * gap[s]), (s, e16[s], gap[s])
+    assert hip_loss[-1] != hip_loss[0]  # the adapters did train
+    assert e_upd32 < GRAD_FLOOR_RATIO * floor_upd, (e_upd32, floor_upd)
+    # the update itself: 0.09 from the bf16 oracle's, against 0.57 between the bf16 and fp32 oracles
+    assert e_upd16 < 0.5 * floor_upd, (e_upd16, floor_upd)
+
+
 def test_engine_optimizer_step_matches_torch_adamw():
     """clip(1.0) + AdamW on the flat LoRA buffer vs torch.optim.AdamW on the oracle's tensors."""
     z = FX.load("step_tiny_bf16.npz")
@@ -383,14 +459,16 @@ def test_step_lora_rank_variants_vs_oracle(r):
     assert g32 < GRAD_FLOOR_RATIO * floor, (g32, floor)
 
 
-def test_step_lora_dropout_vs_oracle_with_replayed_masks():
-    """configs/peft/lora.yaml: lora_dropout 0.05.  The HIP path's counter-based masks
-    (ospo_amd/dropout.py) are replayed into the oracle, which then computes peft's
+@pytest.mark.parametrize("r", [16, 32, 24])
+def test_step_lora_dropout_vs_oracle_with_replayed_masks(r):
+    """configs/peft/lora.yaml: lora_dropout 0.05 (at its r = 32 and the bench's r = 16; r = 24 gives q|k|v a
+    5-tile u product, which writes no keep bits, so its consumers re-hash the mask).  The HIP path's
+    counter-based masks (ospo_amd/dropout.py) are replayed into the oracle, which then computes peft's
     dropout(x) exactly: forward log-probs, loss and every LoRA grad must match."""
     from ospo_amd import dropout as Dm
     p = 0.05
     dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=2048,
-                       gen_head_dim=256, lora_r=16, lora_alpha=32, lora_dropout=p)
+                       gen_head_dim=256, lora_r=r, lora_alpha=2 * r, lora_dropout=p)
     w = O.init_weights(dims, seed=21, dtype=torch.bfloat16, lora_b_std=1e-2)
     g = torch.Generator().manual_seed(22)
     B, N = 2, 64

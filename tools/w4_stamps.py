@@ -45,21 +45,24 @@ def main():
         call("ospo_set_gemm_variant", 0)
         st = dbg.cpu().numpy().reshape(-1, 8)
         st = st[st[:, 1] != 0].astype(np.float64)
-        mt, rt = st[:, 0::2], st[:, 1::2] * 0.01  # memtime ticks, realtime us
-        clk = (mt[:, 2] - mt[:, 1]) / (rt[:, 2] - rt[:, 1]) / 1e3  # GHz over the K loop
+        rt = st[:, [1, 2, 4, 5, 6, 7]] * 0.01  # realtime us: entry, prog start, prog end, staged, issued, drained
+        clk = (st[:, 3] - st[:, 0]) / (rt[:, 2] - rt[:, 1]) / 1e3  # GHz over the program
         ntile = (k + k2) // 64
         loop_us = rt[:, 2] - rt[:, 1]
         r0 = rt[:, 0].min()
+        med = lambda x: round(float(np.median(x)), 2)  # noqa: E731
         line = {"shape": name, "wgs": int(len(st)), "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
-                "span_us": round(rt[:, 3].max() - r0, 1),
+                "span_us": round(rt[:, 5].max() - r0, 1),
                 "clock_ghz_p10_p50_p90": [round(float(np.percentile(clk, q)), 3) for q in (10, 50, 90)],
-                "setup_us_p50": round(float(np.median(rt[:, 1] - rt[:, 0])), 2),
-                "program_us_p50": round(float(np.median(loop_us)), 2),
+                "setup_us_p50": med(rt[:, 1] - rt[:, 0]),
+                "program_us_p50": med(loop_us),
                 "per_ktile_us_p50": round(float(np.median(loop_us)) / ntile, 4),
-                "per_ktile_cycles_p50": round(float(np.median((mt[:, 2] - mt[:, 1]) / ntile)), 1),
-                "epilogue_us_p50": round(float(np.median(rt[:, 3] - rt[:, 2])), 2),
-                "wg_total_us_p50": round(float(np.median(rt[:, 3] - rt[:, 0])), 2),
-                "entry_spread_us": round(float(np.percentile(rt[:, 0] - r0, 90)), 2)}
+                "per_ktile_cycles_p50": round(float(np.median((st[:, 3] - st[:, 0]) / ntile)), 1),
+                "stage_us_p50": med(rt[:, 3] - rt[:, 2]), "store_issue_us_p50": med(rt[:, 4] - rt[:, 3]),
+                "store_drain_us_p50": med(rt[:, 5] - rt[:, 4]),
+                "wg_total_us_p50": med(rt[:, 5] - rt[:, 0]),
+                "entry_spread_us": round(float(np.percentile(rt[:, 0] - r0, 90)), 2),
+                "prog_end_spread_us_p10_p90": [round(float(np.percentile(rt[:, 2] - r0, q)), 2) for q in (10, 90)]}
         print(json.dumps(line), flush=True)
 
 
