@@ -286,30 +286,31 @@ def bench_vq(args):
     print(json.dumps(line), flush=True)
 
 
-def bench_wrapper(args):
-    """The drop-in path timed end to end (VERDICT r1): JanusProTrainWrapper.training_step -> loss.backward()
-    -> Trainer all-reduce -> on_before_optimizer_step (grad-norm log) -> FusedLoraAdamW.step -> scheduler ->
-    the logged metrics read on the host, as ospo_amd.trainer.Trainer runs a step, on batches in the
-    reference's collate format: VQ token ids (a token cache), or with --inline-vq f32 pixel tensors
-    [1, 3, 384, 384] that preprocess_batch VQ-encodes on the GPU (train.py:246-261).  Inputs resident in
-    HBM; synthetic weights and pixels."""
+def wrapper_setup(args, world, rank, dev, engine=None):
+    """The drop-in path's objects: JanusProTrainWrapper over a model (get_model, or around an existing
+    engine), its FusedLoraAdamW + scheduler (configure_optimizers), the Trainer's all-reduce and two batches
+    in the reference's collate format (VQ token ids, or with --inline-vq f32 pixel tensors).  Logging as the
+    reference's Trainer: its step5.yaml leaves experiment.log_steps empty, so PL logs every 50 steps."""
     from ospo_amd import dist as odist
     from ospo_amd.config import build_config
-    from ospo_amd.model import get_model
     from ospo_amd.wrapper.train import JanusProTrainWrapper
-    world, rank, local = odist.init()
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
     B, Lt, N, r = args.pairs_per_gpu or default_pairs_per_gpu(world), args.text_len, args.img_tokens, args.lora_r
     cfg = build_config(os.path.join(ROOT, "configs", "step5.yaml"), argv=[
         "model.synthetic=true", f"model.override={{'n_layers': {args.layers}}}", f"lora.lora_rank={r}",
         f"lora.lora_alpha={2 * r}", f"lora.lora_dropout={args.lora_dropout}", f"dataset.train.batch_size={B}",
-        f"model.linear_dtype={args.linear_dtype}"])
-    model, cp, ip, tok = get_model(mode="train", config=cfg, device=dev, max_text_len=Lt, n_img_tokens=N)
+        f"model.linear_dtype={args.linear_dtype}", "experiment.log_steps=50"])
+    if engine is None:
+        from ospo_amd.model import get_model
+        model, cp, ip, tok = get_model(mode="train", config=cfg, device=dev, max_text_len=Lt, n_img_tokens=N)
+    else:
+        from ospo_amd.data import ChatProcessor, VLMImageProcessor, load_tokenizer
+        from ospo_amd.model import TARGETS, JanusProPolicy
+        model = JanusProPolicy(engine, {"lora_rank": r, "lora_alpha": 2 * r, "lora_dropout": args.lora_dropout,
+                                        "target_modules": TARGETS}, True)
+        tok = load_tokenizer(None, vocab=engine.dims.vocab)
+        cp, ip = ChatProcessor(tok), VLMImageProcessor()
     w = JanusProTrainWrapper(cfg, model, cp, ip, tok)
     (opt,), (sch,) = w.configure_optimizers()
-    sched = sch["scheduler"]
-    allreduce = odist.GradAllReduce(world)
     dims = model.engine.dims
     g = torch.Generator().manual_seed(1000 * rank)
     batches = []
@@ -320,6 +321,15 @@ def bench_wrapper(args):
         else:
             imgs = [torch.randint(0, dims.img_vocab, (1, N), generator=g) for _ in range(2 * B)]
         batches.append(([f"{i}{j:06d}" for j in range(B)], text, imgs[:B], imgs[B:]))
+    log_steps = int(cfg["experiment"].get("log_steps") or 50)
+    return model, w, opt, sch["scheduler"], odist.GradAllReduce(world), batches, log_steps
+
+
+def time_wrapper(model, w, opt, sched, allreduce, batches, log_steps, args, world, dev):
+    """A Trainer step as ospo_amd.trainer.Trainer runs it: training_step -> loss.backward() -> all-reduce ->
+    on_before_optimizer_step (grad-norm log) -> FusedLoraAdamW.step -> scheduler -> zero_grad, the logged
+    metrics read on the host every log_steps optimizer steps."""
+    from ospo_amd import dist as odist
 
     def step(i):
         loss = w.training_step(batches[i % 2], i)
@@ -329,9 +339,26 @@ def bench_wrapper(args):
         opt.step()
         sched.step()
         opt.zero_grad()
-        return w.logged  # the Trainer writes the metrics every log step (host read)
+        return w.logged if (i + 1) % log_steps == 0 else None
 
-    dt, logged = timed_region(step, args.warmup, args.steps, odist.barrier, torch.cuda.synchronize, world, dev)
+    dt, _ = timed_region(step, args.warmup, args.steps, odist.barrier, torch.cuda.synchronize, world, dev)
+    return dt, w.logged
+
+
+def bench_wrapper(args):
+    """The drop-in path timed end to end (VERDICT r1): JanusProTrainWrapper.training_step -> loss.backward()
+    -> Trainer all-reduce -> on_before_optimizer_step (grad-norm log) -> FusedLoraAdamW.step -> scheduler,
+    as ospo_amd.trainer.Trainer runs a step, on batches in the reference's collate format: VQ token ids (a
+    token cache), or with --inline-vq f32 pixel tensors [1, 3, 384, 384] that preprocess_batch VQ-encodes
+    on the GPU (train.py:246-261).  Inputs resident in HBM; synthetic weights and pixels.  (The default
+    simpo bench also times this path, around its own engine: its 'drop_in_wrapper' sub-object.)"""
+    from ospo_amd import dist as odist
+    world, rank, local = odist.init()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B, Lt, N, r = args.pairs_per_gpu or default_pairs_per_gpu(world), args.text_len, args.img_tokens, args.lora_r
+    model, w, opt, sched, allreduce, batches, log_steps = wrapper_setup(args, world, rank, dev)
+    dt, logged = time_wrapper(model, w, opt, sched, allreduce, batches, log_steps, args, world, dev)
     if rank != 0:
         return
     value = B * world * args.steps / dt
@@ -463,6 +490,7 @@ def main():
     ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
     ap.add_argument("--t2i-unfused", action="store_true")      # A/B: the round-2 decode step (GEMV + split-sum + norm launches)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-wrapper", action="store_true")  # skip the drop-in wrapper sub-measurement
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--wgrad-wgs", type=int, default=0)  # A/B: LoRA weight grads as ospo_lora_wgrad streams
     ap.add_argument("--round2-lora", action="store_true")  # A/B: round 2's LoRA kernels (dA tiles, re-hashed masks, unfused u_d)
@@ -529,6 +557,15 @@ def main():
     loss = float(out["loss"].item())
     if not math.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
+    wrap = None
+    if not args.no_wrapper:  # the drop-in path on the same engine and box
+        wm, ww, wopt, wsch, war, wb, wls = wrapper_setup(args, world, rank, dev, engine=eng)
+        wdt, _ = time_wrapper(wm, ww, wopt, wsch, war, wb, wls, args, world, dev)
+        wrap = {"workload": "JanusProTrainWrapper.training_step + loss.backward + Trainer step (all-reduce, "
+                            "grad-norm log, FusedLoraAdamW, scheduler; metrics read every 50 steps as PL), "
+                            "VQ token-id batches in the reference's collate format, same engine",
+                "value": round(B * world * args.steps / wdt, 3), "unit": "pairs/s", "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(wdt / args.steps * 1e3, 2)}
     checks = None
     if world > 1:  # the all-reduced grads and the updated LoRA params must be identical on every rank
         import torch.distributed as tdist
@@ -584,6 +621,9 @@ def main():
         "gemm_kernels": {k: {"count": v["count"], "ms": round(v["ms"], 2),
                              "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)} for k, v in kern.items()},
     }
+    if wrap is not None:
+        wrap["vs_engine_path"] = round(wrap["value"] / value, 4)
+        line["drop_in_wrapper"] = wrap
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(Lt=Lt, N=N)
     print(json.dumps(line), flush=True)

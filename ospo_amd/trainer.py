@@ -28,7 +28,8 @@ class Trainer:
         self.max_steps = int(get(config, "experiment.max_training_steps") or 10)
         self.accum = int(get(config, "experiment.gradient_accumulation_steps") or 1)
         self.save_steps = get(config, "experiment.save_steps")
-        self.log_steps = int(get(config, "experiment.log_steps") or 1)
+        # PL's log_every_n_steps (the reference passes experiment.log_steps, empty in its step5.yaml -> PL's 50)
+        self.log_steps = int(get(config, "experiment.log_steps") or 50)
         self.enable_ckpt = bool(get(config, "experiment.enable_checkpointing", True))
         self.global_step = 0
         self.allreduce = odist.GradAllReduce(world)

@@ -231,9 +231,17 @@ class JanusProTrainWrapper:
         self.log_dict({name: value}, sync_dist=sync_dist)
 
     def log_dict(self, d: Dict[str, Any], sync_dist: bool = True, **kw):
-        names = list(d)
-        vals = torch.stack([(v.detach().float().reshape(()).to(self.device) if torch.is_tensor(v)
-                             else torch.tensor(float(v), device=self.device)) for v in d.values()])
+        # host numbers (lr, global_step) are the same on every rank: they are logged as they are, without a
+        # device round trip (a pageable host->device copy would stall the host until the stream drains)
+        dev = {n: v for n, v in d.items() if torch.is_tensor(v)}
+        for n, v in d.items():
+            if not torch.is_tensor(v):
+                self._logged[n] = float(v)
+                self._pending.pop(n, None)
+        if not dev:
+            return
+        names = list(dev)
+        vals = torch.stack([v.detach().float().reshape(()).to(self.device) for v in dev.values()])
         if sync_dist:
             odist.all_reduce_mean_(vals)  # one fused all-reduce for all scalars
         for i, n in enumerate(names):
@@ -286,21 +294,50 @@ class JanusProTrainWrapper:
             ids = self.model.vq_encode(torch.cat([x.reshape(-1, *x.shape[-3:]) for x in images]))
             if ids.shape != (2 * B, self.engine.N):
                 raise ValueError(f"{ids.shape[1]} VQ tokens per image, the engine expects {self.engine.N}")
+            text_dev = self._upload(text_ids.reshape(-1)).view(B, Lt)
             ch, rj = ids[:B], ids[B:]
         elif not any(pixels):
-            ids = torch.stack([x.reshape(-1).long() for x in images])
+            ids = torch.stack([x.reshape(-1).to(torch.int32) for x in images])
             if int(ids.max()) >= d.img_vocab or int(ids.min()) < 0:
                 raise ValueError(f"VQ token id outside [0, {d.img_vocab})")
-            ch, rj = ids[:B].to(self.device, torch.int32), ids[B:].to(self.device, torch.int32)
+            # text and image ids in ONE asynchronous copy from pinned memory (a pageable copy would hold
+            # the host until the previous step's kernels drain)
+            flat = self._upload(torch.cat([text_ids.reshape(-1), ids.reshape(-1)]))
+            text_dev = flat[: B * Lt].view(B, Lt)
+            ids_dev = flat[B * Lt:].view(2 * B, -1)
+            ch, rj = ids_dev[:B], ids_dev[B:]
         else:
             raise ValueError("a batch mixes pixel tensors and VQ token ids")
         lab_txt = torch.full((B, Lt), self.label_pad_token_id, dtype=torch.long, device=ch.device)
         return {
             "item_ids": list(item_ids),
-            "text_ids": text_ids.to(self.device, non_blocking=True),
+            "text_ids": text_dev,
             "chosen_ids": ch, "rejected_ids": rj,
             "chosen_labels": torch.cat([lab_txt, ch.long()], 1), "rejected_labels": torch.cat([lab_txt, rj.long()], 1),
         }
+
+    def _upload(self, host: torch.Tensor) -> torch.Tensor:
+        """int32 host ids -> a fresh device tensor by a non-blocking copy from one of two pinned staging
+        buffers (each reused only after its previous copy has completed: an event wait, normally already
+        satisfied one step later)."""
+        if self.device.type != "cuda":
+            return host.to(self.device)
+        n = host.numel()
+        st = getattr(self, "_pin", None)
+        if st is None or st[0][0].numel() < n:
+            cap = max(n, 1 << 16)
+            st = self._pin = [[torch.empty(cap, dtype=torch.int32).pin_memory(), None] for _ in range(2)]
+            self._pin_i = 0
+        slot = st[self._pin_i]
+        self._pin_i ^= 1
+        if slot[1] is not None:
+            slot[1].synchronize()
+        slot[0][:n].copy_(host)
+        out = torch.empty(n, dtype=torch.int32, device=self.device)
+        out.copy_(slot[0][:n], non_blocking=True)
+        slot[1] = torch.cuda.Event()
+        slot[1].record()
+        return out
 
     def concatenated_inputs(self, batch: Dict[str, Any]) -> Dict[str, torch.Tensor]:
         """cat chosen | rejected along dim 0 (train.py:282-314; pad_to_length is a no-op here)."""

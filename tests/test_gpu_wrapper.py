@@ -17,7 +17,7 @@ TINY = ["model.synthetic=true", "dataset.train.synthetic_tokens=true",
         "model.override={'n_layers': 2, 'd_model': 256, 'd_ff': 512, 'n_heads': 2, 'vocab': 512, "
         "'img_vocab': 2048, 'gen_head_dim': 256}",
         "lora.lora_rank=16", "lora.lora_alpha=32", "dataset.train.batch_size=2", "experiment.max_training_steps=4",
-        "experiment.save_steps=2"]
+        "experiment.save_steps=2", "lora.lora_dropout=0.0"]  # (these tests compare forwards; step5.yaml trains at 0.05)
 
 
 # images as the reference feeds them: the 2 example pairs' PNGs (tests/golden/step3) -> f32 pixels;
@@ -27,7 +27,7 @@ PIXELS = ["model.synthetic=true", f"dataset.train.data_path={ROOT}/tests/golden/
           "model.arch=janus-pro-1b",
           "model.override={'n_layers': 2, 'd_model': 256, 'd_ff': 512, 'n_heads': 2, 'vocab': 512, "
           "'gen_head_dim': 256}",
-          "lora.lora_rank=16", "lora.lora_alpha=32", "dataset.train.batch_size=2"]
+          "lora.lora_rank=16", "lora.lora_alpha=32", "dataset.train.batch_size=2", "lora.lora_dropout=0.0"]
 
 
 def make(tmp_path, extra=(), base=TINY):
