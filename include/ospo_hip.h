@@ -77,8 +77,8 @@ int ospo_gemm_nt_rope_bf16(const void* A, int lda, const void* B, int ldb, int M
 
 /* LoRA-dropout backward of a frozen Linear with its adapter (peft lora.Linear,
  * dropout before lora_A): C = A.B^T + mask (.) (A2.B2^T) / (1 - drop_p), with
- * the forward's mask over the [M, N] input of the adapter (element (m, n) kept
- * iff drop_hash(m*N + n, drop_seed) >= drop_p * 2^32, common.h), i.e.
+ * the forward's mask over the [M, N] input of the adapter (element idx = m*N + n kept
+ * iff the 16-bit half (idx & 1) of drop_hash(idx >> 1, drop_seed) is >= drop_p * 2^16, common.h), i.e.
  * dX = dy.W + dropout'(g . A_cat).  N % 256 == 0, K2 > 0, no bias / residual.
  * keep_bits (optional, 16-B aligned): that mask as the forward's ospo_lora_skinny keep-bit output
  * ([M][N / 8] bytes) -- read instead of re-hashed (same result). */

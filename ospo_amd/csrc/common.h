@@ -26,20 +26,27 @@ __device__ __forceinline__ float round_bf(float x) { return (float)(bf16)x; }
 // LoRA dropout mask (counter-based; ospo_amd/dropout.py restates it bit for bit):
 // element idx = row * ncols + col of the adapter input, kept iff drop_keep(idx) (below);
 // kept values become bf16(x / (1 - p)).
+// Round 4: three multiply-xorshift rounds on 24-bit multiplies (v_mul_u32_u24, full rate) instead of three
+// 32-bit ones (v_mul_lo_u32, quarter rate): the hash was the issue-bound LoRA u products' largest VALU cost.
+// The first xorshift folds the high half into the low 24 bits the first multiply reads (injective for
+// idx < 2^24 pairs, i.e. M * K < 2^25; beyond it distinct elements may share a hash, still uniform).
+// Statistics on a [4800, 4096] mask at p = 0.05 (tools/hash_stats.py): keep rate, both halves of a hash,
+// rows 1-64 and columns 2-256 apart all uncorrelated to within sampling noise, as the round-3 hash.
 __host__ __device__ __forceinline__ uint32_t drop_hash(uint32_t idx, uint32_t seed) {
-  uint32_t x = idx * 0x9E3779B1u + seed;
+  uint32_t x = idx ^ seed;
   x ^= x >> 16;
-  x *= 0x7FEB352Du;
+  x = (x & 0xFFFFFFu) * 0xED5AD5u;
   x ^= x >> 15;
-  x *= 0x846CA68Bu;
+  x = (x & 0xFFFFFFu) * 0xAC4C1Bu;
+  x ^= x >> 13;
+  x = (x & 0xFFFFFFu) * 0x9E3779u;
   x ^= x >> 16;
   return x;
 }
 
 // Keep decision of mask element idx: the 16-bit half (idx & 1) of drop_hash(idx >> 1), kept iff it is
-// >= thr = p * 2^16 -- one hash per two adjacent elements of a row (the hash's integer multiplies are
-// quarter-rate VALU, and each adapter input's mask is regenerated three times per step: the forward's u
-// product, the dX GEMM's extension, the dA product).  Callers that decide 2n consecutive elements start
+// >= thr = p * 2^16 -- one hash per two adjacent elements of a row (since round 3 the forward's u product
+// hashes each adapter input once per step and writes keep bits that the backward reads).  Callers that decide 2n consecutive elements start
 // at an even index (row widths are even: the launchers check) and hash n times.
 __host__ __device__ __forceinline__ bool drop_keep(uint32_t idx, uint32_t seed, uint32_t thr) {
   const uint32_t h = drop_hash(idx >> 1, seed);

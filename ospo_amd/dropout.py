@@ -23,7 +23,23 @@ _M32 = np.uint32(0xFFFFFFFF)
 
 
 def drop_hash(idx, seed):
-    """uint32 hash of element index idx (array) under seed (int), as on the device."""
+    """uint32 hash of element (pair) index idx (array) under seed (int), as on the device: three
+    multiply-xorshift rounds on 24-bit multiplies (common.h drop_hash, round 4)."""
+    m24 = np.uint32(0xFFFFFF)
+    with np.errstate(over="ignore"):
+        x = np.asarray(idx, dtype=np.uint32) ^ np.uint32(seed & 0xFFFFFFFF)
+        x ^= x >> np.uint32(16)
+        x = (x & m24) * np.uint32(0xED5AD5)
+        x ^= x >> np.uint32(15)
+        x = (x & m24) * np.uint32(0xAC4C1B)
+        x ^= x >> np.uint32(13)
+        x = (x & m24) * np.uint32(0x9E3779)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def _seed_mix(idx, seed):
+    """The host-side seed mixer of layer_seed (32-bit multiply-xorshift; never evaluated on the device)."""
     with np.errstate(over="ignore"):
         x = np.asarray(idx, dtype=np.uint32) * np.uint32(0x9E3779B1) + np.uint32(seed & 0xFFFFFFFF)
         x ^= x >> np.uint32(16)
@@ -49,8 +65,8 @@ def keep_bits(idx, seed, p: float):
 
 def layer_seed(base: int, call: int, layer: int, group: str) -> int:
     """Seed of one adapter input's mask: distinct per (base seed, forward call, layer, group)."""
-    h = drop_hash(np.uint32((call * 131 + layer * 8 + GROUP_IDS[group]) & 0xFFFFFFFF), base & 0xFFFFFFFF)
-    return int(drop_hash(h, 0x5BD1E995))
+    h = _seed_mix(np.uint32((call * 131 + layer * 8 + GROUP_IDS[group]) & 0xFFFFFFFF), base & 0xFFFFFFFF)
+    return int(_seed_mix(h, 0x5BD1E995))
 
 
 def keep_mask(M: int, K: int, seed: int, p: float) -> np.ndarray:
