@@ -351,6 +351,16 @@ int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* 
                   int nmods, int Nmod, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
                   size_t ws_bytes, hipStream_t stream);
 
+/* The SwiGLU backward fused with the gate|up group's g / dB (LoRA rank 16; the backward of
+ * down_proj(act_fn(gate) * up) and of gate|up's peft adapters, ospo/wrapper/train.py:352):
+ *   dgu = [dgate | dup] = ospo_swiglu_bwd(dh, gu)           (rows < M, bf16, stored)
+ *   out, dB             = ospo_lora_gdb(dgu, nmods = 2, Nmod = F, ...)
+ * in one stream over (dh, gu): dgu is written once and not read back.  F % 128 == 0; Bt [32, F] (ldb),
+ * u [M, >= 32]; out / ws / dB as ospo_lora_gdb with nmods = 2.  Same g bits as the two calls. */
+int ospo_swiglu_lora_gdb(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu, const void* Bt,
+                         int ldb, const void* u, int ldu, int M, int M_out, int F, float scale, void* out, int ldo,
+                         int out_cols, float* dB, void* ws, size_t ws_bytes, hipStream_t stream);
+
 /* ------------------------------------------------------------ MXFP8 variant ---
  * BASELINE config 5 / SURVEY §8f rank 1: the frozen Linears of the SimPO step
  * (q|k|v, o, gate|up, down; forward and dX backward -- the products that

@@ -65,6 +65,7 @@ SIGNATURES = {
     "ospo_lora_pack": [P, P, I, I, I, I, I, P, P, P, P, I, L, P],
     "ospo_lora_gdb": [P, I, P, I, P, I, I, I, I, I, F, P, I, I, P, P, Z, P],
     "ospo_lora_gdb_ws_bytes": [I, I, I],
+    "ospo_swiglu_lora_gdb": [P, I, P, I, P, I, P, I, P, I, I, I, I, F, P, I, I, P, P, Z, P],
     "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, U, F, P, I, P, P],
     "ospo_lora_skinny_ws_bytes": [I, I, I],
     "ospo_decode_gemv_ws_bytes": [I, I, I],

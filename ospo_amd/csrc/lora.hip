@@ -640,7 +640,7 @@ __device__ __forceinline__ void tr4_wait(i16x4& a, i16x4& b, i16x4& c, i16x4& d)
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int RSB, int NS = 4>
+template <int RSB, int NS = 4, int YA = 0>  // YA: cache-policy bits of the dy loads
 __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ dy, int ldy, const bf16* __restrict__ Bt,
                                                        int ldb, const bf16* __restrict__ u, int ldu, int M, int Nmod,
                                                        int nch, float* __restrict__ ws, int Mw,
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
       const int p = wave * 2 + i;
       const int row = min(rb0 + rb * 64 + p * 8 + r8, M - 1);
       __builtin_amdgcn_global_load_lds(dy + (long)row * ldy + col0 + cc * 64 + ((c8 ^ r8) << 3),
-                                       (LDS_AS void*)(st + p * 1024), 16, 0, 0);
+                                       (LDS_AS void*)(st + p * 1024), 16, 0, YA);
     }
   };
   const int T = nch * RSB;
@@ -767,6 +767,182 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
+// SwiGLU backward fused with the gate|up group's g / dB stream (round 4): a workgroup computes
+// dgate | dup = swiglu_bwd(dh, gate, up) (swiglu_bwd8, as swiglu_bwd_kernel) over 64*RSB rows x 64*nch
+// columns of BOTH modules -- the two share their inputs -- stores them (the A operand of the gate|up dX
+// GEMM) and feeds the same tiles to lora_gdb_kernel's g / dB MFMAs, so dgu is written once and never read
+// back.  Inputs come to registers by 16-B buffer loads PF sub-tiles ahead (no input ring in LDS); the two
+// output tiles of a sub-tile go through one LDS image each, in lora_gdb_kernel's swizzled dy layout, between
+// two barriers.  Row sub-blocks outer (runtime loop), the NCH column chunks inner (unrolled): g of a row
+// sub-block is complete after its chunks (2 accumulators, stored at once), dB keeps one accumulator per
+// chunk -- the fully unrolled chunk-outer order of lora_gdb_kernel held 8x the live registers here.  Same
+// nch, per-element MFMA order and partials layout as lora_gdb_kernel over dgu: bit-identical g (and dB up
+// to the f32 atomics' order) to ospo_swiglu_bwd + ospo_lora_gdb.
+// LAUX / SAUX: cache-policy bits of the input loads / dgu stores.  DBG (measurement only): 1 no MFMA phase,
+// 2 no dgu stores.
+template <int RSB, int PF, int NCH, int DBG = 0, int LAUX = 2, int SAUX = 16>
+__global__ __launch_bounds__(256) void swiglu_gdb_kernel(const bf16* __restrict__ dh, int lddh,
+                                                         const bf16* __restrict__ gu, int ldg, bf16* __restrict__ dgu,
+                                                         int lddg, const bf16* __restrict__ Bt, int ldb,
+                                                         const bf16* __restrict__ u, int ldu, int M, int F,
+                                                         float* __restrict__ ws, int Mw, float* __restrict__ dB) {
+  static_assert(NCH % PF == 0, "the prefetch slot must be a compile-time index");
+  constexpr int nch = NCH;
+  constexpr int TILE = 8192;  // a 64 x 64 bf16 image; [dgate | dup] at 0 and TILE
+  constexpr int BT_OFF = 2 * TILE, BT_BYTES = 16 * 4 * 128;  // per module, up to nch = 4
+  constexpr int ROWS = 64 * RSB;
+  constexpr int U_OFF = BT_OFF + 2 * BT_BYTES;  // per module ROWS * 32 B
+  __shared__ __attribute__((aligned(16))) char smem[U_OFF + 2 * ROWS * 32];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int rb0 = blockIdx.x * ROWS;
+  const int nsplit = F / (64 * nch);
+  const int sp = blockIdx.y;
+  const int kc0 = sp * 64 * nch;
+  const int btrow = nch * 128;
+
+  // Bt and u images as lora_gdb_kernel's (same swizzle), through registers: no LDS-DMA in this kernel, so
+  // the compiler's vmcnt tracking of the register prefetch below stays exact.  All loads first, then the writes.
+  {
+    const int off = lane * 16, rpp = 1024 / btrow;
+    u32x4 bv[2][2], uv[ROWS / 32 / 2];
+#pragma unroll
+    for (int mod = 0; mod < 2; ++mod)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {  // pieces p = wave + 4k < 2 nch (nch = 2: k = 0 only)
+        const int p = min(wave + 4 * k, 2 * nch - 1);
+        const int j = p * rpp + off / btrow, pc = (off % btrow) >> 4;
+        bv[mod][k] = *reinterpret_cast<const u32x4*>(Bt + (long)(mod * 16 + j) * ldb + kc0 + (pc ^ j) * 8);
+      }
+#pragma unroll
+    for (int k = 0; k < ROWS / 32 / 2; ++k) {  // pieces p = wave + 4k of the two modules' u images
+      const int p = wave + 4 * k, mod = p / (ROWS / 32), pp = p % (ROWS / 32);
+      const int row = min(rb0 + pp * 32 + (lane >> 1), M - 1);
+      uv[k] = *reinterpret_cast<const u32x4*>(u + (long)row * ldu + mod * 16 + (lane & 1) * 8);
+    }
+#pragma unroll
+    for (int mod = 0; mod < 2; ++mod)
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (wave + 4 * k < 2 * nch)
+          *reinterpret_cast<u32x4*>(smem + BT_OFF + mod * BT_BYTES + (wave + 4 * k) * 1024 + off) = bv[mod][k];
+#pragma unroll
+    for (int k = 0; k < ROWS / 32 / 2; ++k) {
+      const int p = wave + 4 * k, mod = p / (ROWS / 32), pp = p % (ROWS / 32);
+      *reinterpret_cast<u32x4*>(smem + U_OFF + mod * ROWS * 32 + pp * 1024 + off) = uv[k];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the images are read after the first barrier
+
+  // this thread's two 16-B chunks of a sub-tile: rows r0, r0 + 32, logical chunk c.  Buffer loads / stores:
+  // rows >= M fall outside the ranges, so their loads return 0 (finite dgate / dup: g partials of rows >= M
+  // are never read) and their stores drop.
+  const int r0 = tid >> 3, c = tid & 7;
+  const __amdgpu_buffer_rsrc_t rsG = __builtin_amdgcn_make_buffer_rsrc((void*)gu, 0, (int)((long)M * ldg * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsH = __builtin_amdgcn_make_buffer_rsrc((void*)dh, 0, (int)((long)M * lddh * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc((void*)dgu, 0, (int)((long)M * lddg * 2), 0x00020000);
+  const uint32_t vg = (uint32_t)((r0 * ldg + c * 8) * 2), vh = (uint32_t)((r0 * lddh + c * 8) * 2);
+  const uint32_t vd = (uint32_t)((r0 * lddg + c * 8) * 2);
+  u32x4 in[PF][6];  // [slot][gate0, gate1, up0, up1, dh0, dh1]
+  auto load = [&](int t, u32x4* v) {  // sub-tile t = (row sub-block t / NCH, chunk t % NCH)
+    const int rb = t / NCH, cc = t % NCH;
+    const int row = rb0 + rb * 64, col = kc0 + cc * 64;
+    // the whole offset in voffset: the range check does not cover soffset
+    const uint32_t og = vg + (uint32_t)((row * ldg + col) * 2), oh = vh + (uint32_t)((row * lddh + col) * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsG, og + i * 64 * ldg, 0, LAUX));
+      v[2 + i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsG, og + i * 64 * ldg + 2 * F, 0, LAUX));
+      v[4 + i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsH, oh + i * 64 * lddh, 0, LAUX));
+    }
+  };
+  constexpr int T = NCH * RSB;
+#pragma unroll
+  for (int s = 0; s < PF - 1; ++s) load(s, in[s]);
+
+  f32x4 accb[2][NCH];
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) accb[0][cc] = accb[1][cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int li = l16, q4 = li >> 2, p4 = li & 3;
+  const int grow = 16 * wave + l16;
+  for (int rb = 0; rb < RSB; ++rb) {
+    f32x4 accg[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int cc = 0; cc < NCH; ++cc) {
+      const int t = rb * NCH + cc;
+      load(min(t + PF - 1, T - 1), in[(cc + PF - 1) % PF]);  // unconditional: exact vmcnt, no join
+      __builtin_amdgcn_s_barrier();  // every wave is done with the previous sub-tile's images
+      asm volatile("" ::: "memory");
+      {
+        const u32x4* v = in[cc % PF];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = r0 + 32 * i;
+          float d[8], gg[8], uu[8], dg[8], du[8];
+          unpack8(v[4 + i], d);
+          unpack8(v[i], gg);
+          unpack8(v[2 + i], uu);
+          swiglu_bwd8(d, gg, uu, dg, du);
+          const u32x4 pg = pack8(dg), pu = pack8(du);
+          const int so = r * 128 + ((c ^ (r & 7)) << 4);
+          *reinterpret_cast<u32x4*>(smem + so) = pg;
+          *reinterpret_cast<u32x4*>(smem + TILE + so) = pu;
+          const uint32_t od = vd + (uint32_t)(((rb0 + rb * 64 + 32 * i) * lddg + kc0 + cc * 64) * 2);
+          if (DBG != 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, pg), rsD, od, 0, SAUX);
+          if (DBG != 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, pu), rsD, od + 2 * F, 0, SAUX);
+        }
+      }
+      if (DBG == 1) continue;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // both images complete
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int mod = 0; mod < 2; ++mod) {
+        const char* st = smem + mod * TILE;
+        const char* bts = smem + BT_OFF + mod * BT_BYTES;
+        const char* us = smem + U_OFF + mod * ROWS * 32;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int qk = cc * 8 + 4 * s2 + g;
+          const bf16x8 bt = *reinterpret_cast<const bf16x8*>(bts + l16 * btrow + ((qk ^ l16) << 4));
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + grow * 128 + (((4 * s2 + g) ^ (grow & 7)) << 4));
+          accg[mod] = MFMA(bt, a, accg[mod]);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int r1 = 32 * s + 8 * g + q4, r2 = r1 + 4;
+          const int x = 2 * wave + (p4 >> 1), h = (p4 & 1) << 3;
+          const int ur = rb * 64 + 32 * s + 8 * g;
+          // the builtin here (no LDS-DMA in flight to drain): immediate offsets, exact lgkmcnt
+          i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(st + r1 * 128 + ((x ^ (r1 & 7)) << 4) + h));
+          i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(st + r2 * 128 + ((x ^ (r2 & 7)) << 4) + h));
+          i16x4 ulo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(us + (ur + q4) * 32 + p4 * 8));
+          i16x4 uhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(us + (ur + 4 + q4) * 32 + p4 * 8));
+          // no row mask on u: the dgate / dup rows >= M are exact zeros (zero inputs), u's clamped rows finite
+          const i16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const i16x8 bv = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+          accb[mod][cc] = MFMA(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), accb[mod][cc]);
+        }
+      }
+    }
+    const int m = rb0 + rb * 64 + grow;  // g partials of this row sub-block: ws [mod][sp][Mw][16]
+#pragma unroll
+    for (int mod = 0; mod < 2; ++mod)
+      if (m < Mw) *reinterpret_cast<f32x4*>(ws + (((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[mod];
+  }
+#pragma unroll
+  for (int mod = 0; mod < 2; ++mod)
+#pragma unroll
+    for (int cc = 0; cc < NCH; ++cc) {  // each chunk's dB over the workgroup's rows
+      const long n0 = (long)mod * F + kc0 + cc * 64 + 16 * wave + 4 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[mod][cc][i]);
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
 // dA of one adapter group as ONE stream over its input (round 3; replaces the 64 x 64 f32-atomic tiles):
 //   dA[j][n] += sum_m g_s[m][j] * dropout(x)[m][n]        j < s_cols (the used rank rows), n < N
 // (peft lora_A.weight.grad; the backward of train.py:352's adapters).  A workgroup owns a 128-column
@@ -789,8 +965,9 @@ constexpr int DA_PW = (DA_STG / 1024) / 4; // LDS-DMA pieces per wave per stage 
 // transposed read touches (8g + q, q < 4) get 16 distinct values
 __device__ __forceinline__ int da_swz(int r) { return (r & 3) | (((r >> 3) & 3) << 2); }
 
+template <int AUX = 0>
 __device__ __forceinline__ void da_lds16(__amdgpu_buffer_rsrc_t rs, char* dst, uint32_t voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, voff, soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, voff, soff, 0, AUX);
 }
 
 __device__ __forceinline__ void da_lds4(__amdgpu_buffer_rsrc_t rs, char* dst, uint32_t voff, int soff) {
@@ -821,7 +998,7 @@ __device__ __forceinline__ void da_keep8(uint32_t m0, uint32_t n, uint32_t ld, u
 
 // DM: 0 no dropout, 1 mask re-hashed, 2 mask from the forward's keep bits (staged with the tile: 64 rows x
 // 16 B, one 4-B LDS-DMA per wave)
-template <int NJ, int DM>
+template <int NJ, int DM, int XA = 0>  // XA: cache-policy bits of the x loads
 __global__ __launch_bounds__(256) void lora_da_kernel(const bf16* __restrict__ X, int ldx, int x_bytes,
                                                       const bf16* __restrict__ S, int lds, int s_bytes, int s_cols,
                                                       int nt, float* __restrict__ C, int ldc, uint32_t dseed,
@@ -862,7 +1039,7 @@ __global__ __launch_bounds__(256) void lora_da_kernel(const bf16* __restrict__ X
   auto stage = [&](int t, int slot) __attribute__((always_inline)) {
     char* st = smem + slot * STG;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) da_lds16(rsX, st + (wave * 4 + i) * 1024, vx[i], t * xstep);
+    for (int i = 0; i < 4; ++i) da_lds16<XA>(rsX, st + (wave * 4 + i) * 1024, vx[i], t * xstep);
 #pragma unroll
     for (int i = 0; i < 2; ++i) da_lds16(rsS, st + DA_XB + (wave * 2 + i) * 1024, vs[i], t * sstep);
     if constexpr (DM == 2) da_lds4(rsK, st + DA_STG + wave * 256, vk, t * kstep);
@@ -1344,6 +1521,7 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   if (getenv("OSPO_GDB_NS6")) kfn = lora_gdb_kernel<8, 6>;  // A/B: a 6-stage ring
   if (getenv("OSPO_GDB_NS2")) kfn = lora_gdb_kernel<8, 2>;  // A/B: 2- and 3-stage rings (more residency)
   if (getenv("OSPO_GDB_NS3")) kfn = lora_gdb_kernel<8, 3>;
+  if (getenv("OSPO_NT_GDB")) kfn = lora_gdb_kernel<8, 4, 2>;  // A/B: non-temporal dy loads
 #endif
   hipLaunchKernelGGL(kfn, grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
                      (const bf16*)u, ldu, M, Nmod, nch, (float*)ws, Mw, dB);
@@ -1352,6 +1530,57 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
   hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)ws,
                      nmods, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_swiglu_lora_gdb(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu,
+                                    const void* Bt, int ldb, const void* u, int ldu, int M, int M_out, int F,
+                                    float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
+                                    size_t ws_bytes, hipStream_t stream) {
+  if (!dh || !gu || !dgu || !Bt || !u || !out || !dB || !ws) return OSPO_ERR_ARG;
+  if (M <= 0 || M_out < M || F <= 0 || F % 128) return OSPO_ERR_SHAPE;
+  if (ld_dh < F || ld_gu < 2 * F || ld_dgu < 2 * F || ldb < F || ldu < 32 || ldo < out_cols || out_cols < 32 ||
+      out_cols % 4 || ld_dh % 8 || ld_gu % 8 || ld_dgu % 8 || ldb % 8 || ldu % 8 || ldo % 4)
+    return OSPO_ERR_SHAPE;
+  if (ws_bytes < ospo_lora_gdb_ws_bytes(M, 2, F)) return OSPO_ERR_SHAPE;
+  if (!aligned16(dh) || !aligned16(gu) || !aligned16(dgu) || !aligned16(Bt) || !aligned16(u) || !aligned16(ws) ||
+      ((uintptr_t)dB & 3) || ((uintptr_t)out & 7))
+    return OSPO_ERR_ALIGN;
+  const long Mr = (long)(M + 511) / 512 * 512;  // rows the grid addresses (clamped by the ranges, not the offsets)
+  if (Mr * ld_dgu * 2 >= (1L << 31) || Mr * ld_gu * 2 >= (1L << 31) || Mr * ld_dh * 2 >= (1L << 31))
+    return OSPO_ERR_UNSUPPORTED;  // the buffer ranges / offsets (32-bit)
+  const int nch = gdb_nch(M, 2, F);  // as ospo_lora_gdb on dgu: the same partials
+  const int nsplit = F / (64 * nch);
+  const int Mw = (M + 63) / 64 * 64;
+  // one sub-tile of prefetch, non-temporal input loads (gu, dh are dead after this pass) and sc1 dgu stores:
+  // 103.6 us at the step shape against 125.0 with default policies and 150 for the two launches
+  // (profiles/r04/swiglu_gdb_variants.log)
+  auto kfn = nch == 4 ? swiglu_gdb_kernel<8, 2, 4> : swiglu_gdb_kernel<8, 2, 2>;
+  const int rows = 512;
+#ifdef OSPO_ABLATION
+  if (const char* e = getenv("OSPO_SWGDB")) {  // A/B: prefetch depth, cache policies, phases removed
+    const int v = atoi(e);
+    if (nch == 4) {
+      if (v == 1) kfn = swiglu_gdb_kernel<8, 2, 4, 0, 0, 0>;
+      if (v == 2) kfn = swiglu_gdb_kernel<8, 4, 4, 0, 0, 0>;
+      if (v == 3) kfn = swiglu_gdb_kernel<8, 2, 4, 0, 2, 0>;
+      if (v == 4) kfn = swiglu_gdb_kernel<8, 2, 4, 0, 2, 2>;
+      if (v == 5) kfn = swiglu_gdb_kernel<8, 2, 4, 0, 0, 2>;
+      if (v == 6) kfn = swiglu_gdb_kernel<8, 4, 4>;
+      if (v == 7) kfn = swiglu_gdb_kernel<8, 2, 4, 1>;
+      if (v == 8) kfn = swiglu_gdb_kernel<8, 2, 4, 2>;
+    }
+  }
+#endif
+  hipLaunchKernelGGL(kfn, dim3((M + rows - 1) / rows, nsplit), dim3(256), 0, stream,
+                     (const bf16*)dh, ld_dh, (const bf16*)gu, ld_gu, (bf16*)dgu, ld_dgu, (const bf16*)Bt, ldb,
+                     (const bf16*)u, ldu, M, F, (float*)ws, Mw, dB);
+  OSPO_CHECK_LAUNCH();
+  const long n = (long)M_out * (out_cols / 4);
+  if (n >= (1L << 31)) return OSPO_ERR_SHAPE;
+  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)ws, 2,
+                     nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
@@ -1381,17 +1610,26 @@ extern "C" int ospo_lora_da(const void* X, int ldx, int N, const void* S, int ld
   const int k_bytes = keep_bits ? (int)((long)K * N / 8) : 0;
   const uint8_t* kb = (const uint8_t*)keep_bits;
   const dim3 grid(N / DA_TN, splits);
-#define DA_LAUNCH(NJV)                                                                                            \
+  int xa = 0;
+#ifdef OSPO_ABLATION
+  if (getenv("OSPO_NT_DA")) xa = 2;  // A/B: non-temporal x loads
+#endif
+#define DA_LAUNCH2(NJV, XAV)                                                                                      \
   do {                                                                                                            \
     if (drop && kb)                                                                                               \
-      hipLaunchKernelGGL((lora_da_kernel<NJV, 2>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes,      \
+      hipLaunchKernelGGL((lora_da_kernel<NJV, 2, XAV>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes, \
                          (const bf16*)S, lds, s_bytes, s_cols, nt, C, ldc, 0u, 0u, dscale, N, kb, k_bytes);       \
     else if (drop)                                                                                                \
-      hipLaunchKernelGGL((lora_da_kernel<NJV, 1>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes,      \
+      hipLaunchKernelGGL((lora_da_kernel<NJV, 1, XAV>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes, \
                          (const bf16*)S, lds, s_bytes, s_cols, nt, C, ldc, drop_seed, thr, dscale, N, nullptr, 0); \
     else                                                                                                          \
-      hipLaunchKernelGGL((lora_da_kernel<NJV, 0>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes,      \
+      hipLaunchKernelGGL((lora_da_kernel<NJV, 0, XAV>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, x_bytes, \
                          (const bf16*)S, lds, s_bytes, s_cols, nt, C, ldc, 0u, 0u, 0.f, N, nullptr, 0);          \
+  } while (0)
+#define DA_LAUNCH(NJV)            \
+  do {                            \
+    if (xa) DA_LAUNCH2(NJV, 2);   \
+    else DA_LAUNCH2(NJV, 0);      \
   } while (0)
   switch ((s_cols + 15) / 16) {
     case 1: DA_LAUNCH(1); break;
@@ -1399,6 +1637,7 @@ extern "C" int ospo_lora_da(const void* X, int ldx, int N, const void* S, int ld
     case 3: DA_LAUNCH(3); break;
     default: DA_LAUNCH(4); break;
   }
+#undef DA_LAUNCH2
 #undef DA_LAUNCH
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;

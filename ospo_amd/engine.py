@@ -78,6 +78,7 @@ class SimPOEngine:
                  max_text_len: int = 64, n_img_tokens: int = 576, lora_dropout: float = 0.0,
                  dropout_seed: int = 42, linear_dtype: str = "bf16", fuse_swiglu_bwd: bool = False,
                  dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0, fuse_gdb: bool = True,
+                 fuse_swiglu_gdb: bool = True,
                  da_stream: bool = True, keep_bits: bool = True, fuse_swiglu_u: bool = True,
                  side_after_norm: bool = True):
         if not 0.0 <= float(lora_dropout) < 1.0:
@@ -157,6 +158,9 @@ class SimPOEngine:
         # fuse_gdb (LoRA r = 16): g = s dy.B and dB += dy^T u of a group in one stream over dy on the main stream
         # (ospo_lora_gdb); the side stream then runs only dA.  Off: g on the main stream, dB with dA on the side.
         self.fuse_gdb = bool(fuse_gdb) and dims.lora_r == 16
+        # fuse_swiglu_gdb (with fuse_gdb, bf16): the SwiGLU backward and the gate|up group's g / dB in one stream
+        # over (dh, gu) -- dgu written once, never read back by a separate g / dB pass (ospo_swiglu_lora_gdb)
+        self.fuse_swiglu_gdb = bool(fuse_swiglu_gdb) and self.fuse_gdb
         self.pack_lora()
         self._alloc(max_pairs, max_text_len, n_img_tokens)
         self._rope_T = -1
@@ -370,6 +374,20 @@ class SimPOEngine:
         dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
         ops.lora_gdb(dy, BT, u, out, dB, M, self.Mk, g.nmods, g.Nmod, self.scale, ws=self._gdb_ws)
         return out, True
+
+    def _swiglu_g_db(self, g, M, par, a, dgu, gbase, BT):
+        """dgu = swiglu_bwd(dh, gu) with the gate|up group's g_s and dB in one stream (ospo_swiglu_lora_gdb);
+        None when the shapes do not fit it (the caller then runs swiglu_bwd and _lora_g_db)."""
+        r = self.layout.r
+        if not (self.fuse_swiglu_gdb and self._gdb_ws is not None and r == 16 and g.nmods == 2
+                and g.Nmod % 128 == 0 and self.dh is not None and self._mxo(2 * g.Nmod) is None
+                and dgu.shape[0] * dgu.stride(0) * 2 < 2 ** 31):
+            return None
+        out = self.gsc2[g.name][par]
+        b_off = gbase + g.b_off
+        dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
+        ops.swiglu_lora_gdb(self.dh, a["gu"], dgu, BT, a["u_gu"], out, dB, M, self.Mk, self.scale, ws=self._gdb_ws)
+        return out
 
     def _lora_g(self, dy, g, Bcat, BT, M, par=0):
         """g_s = bf16(scale * dy . Bcat)  ([Mcap, Rp]; rows M..Mk-1 zero), into g buffer copy `par`."""
@@ -588,11 +606,16 @@ class SimPOEngine:
             else:
                 self._lin(dx[:M], lw["downT"], self.dh[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
                           keep_bits=self._bits_bwd(i, "down", dr, Fd))
-                ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
             pending.append(("down", gs, a["h"], dx, a["u_d"], dr, fdb))
             # ---- gate/up
             Acat, AcatT, Bcat, BT = pk["gu"]
-            gs, fdb = self._lora_g_db(dgu, lay.groups["gu"], Bcat, BT, M, q, a["u_gu"], gbase)
+            gs = None if self.fuse_swiglu_bwd else self._swiglu_g_db(lay.groups["gu"], M, q, a, dgu, gbase, BT)
+            if gs is not None:
+                fdb = True
+            else:
+                if not self.fuse_swiglu_bwd:
+                    ops.swiglu_bwd(self.dh[:M], a["gu"][:M], dgu[:M], mx=self._mxo(2 * Fd))
+                gs, fdb = self._lora_g_db(dgu, lay.groups["gu"], Bcat, BT, M, q, a["u_gu"], gbase)
             dr = self._drop(i, "gu")
             self._lin(dgu[:M], lw["guT"], self.dxn[:M], pre=True, a2=gs[:M], b2=AcatT, dropout=dr,
                       keep_bits=self._bits_bwd(i, "gu", dr, D))

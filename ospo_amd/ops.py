@@ -609,6 +609,20 @@ def lora_gdb(dy, bt, u, out, dB, M, M_out, nmods, Nmod, scale, ws=None):
          _p(out), _ld(out), out.shape[1], _p(dB), _p(ws), ws.numel() * ws.element_size(), _s())
 
 
+def swiglu_lora_gdb(dh, gu, dgu, bt, u, out, dB, M, M_out, scale, ws=None):
+    """dgu[:M] = swiglu_bwd(dh, gu) and lora_gdb(dgu, nmods=2, Nmod=F) in one stream over (dh, gu)
+    (ospo_swiglu_lora_gdb; same bits as swiglu_bwd + lora_gdb)."""
+    _chk(dB, torch.float32, "dB")
+    F = dh.shape[1]
+    if gu.shape[1] < 2 * F or dgu.shape[1] < 2 * F:
+        raise ValueError(f"swiglu_lora_gdb: gu/dgu need 2F = {2 * F} columns")
+    if ws is None:
+        ws = lora_gdb_ws(M, 2, F, dh.device)
+    call("ospo_swiglu_lora_gdb", _p(dh), _ld(dh), _p(gu), _ld(gu), _p(dgu), _ld(dgu), _p(bt), _ld(bt), _p(u), _ld(u),
+         M, M_out, F, float(scale), _p(out), _ld(out), out.shape[1], _p(dB), _p(ws), ws.numel() * ws.element_size(),
+         _s())
+
+
 # -------------------------------------------------------------- optimizer
 def sumsq(g, out):
     call("ospo_sumsq", _p(g), g.numel(), _p(out), _s())

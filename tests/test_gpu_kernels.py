@@ -719,6 +719,34 @@ def test_lora_gdb_exact_integers(M, M_out, nm, Nmod):
     assert torch.equal(dB.double(), dB_ref)
 
 
+@pytest.mark.parametrize("M,M_out,F", [(4800, 4800, 11008), (4800, 4864, 11008), (777, 832, 4096), (100, 128, 1024),
+                                       (1000, 1024, 384), (64, 64, 128), (3001, 3008, 2816)])
+def test_swiglu_lora_gdb_equals_two_launches(M, M_out, F):
+    """ospo_swiglu_lora_gdb == ospo_swiglu_bwd then ospo_lora_gdb (nmods 2, Nmod F): dgu and g bit-equal (rows
+    >= M of dgu untouched), dB equal up to the f32 atomics' order and against fp64."""
+    r = 16
+    dh, gu = rnd(M_out, F), rnd(M_out, 2 * F, s=3.0)
+    BT, u = rnd(2 * r, F), rnd(M_out, 64)
+    dgu_ref = torch.full((M_out, 2 * F), 5.0, device=DEV, dtype=torch.bfloat16)
+    out_ref = torch.full((M_out, 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    dB_ref = torch.zeros(2 * F, r, device=DEV)
+    ops().swiglu_bwd(dh[:M], gu[:M], dgu_ref[:M])
+    ops().lora_gdb(dgu_ref, BT, u, out_ref, dB_ref, M, M_out, 2, F, 0.75)
+    dgu = torch.full((M_out, 2 * F), 5.0, device=DEV, dtype=torch.bfloat16)
+    out = torch.full((M_out, 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    dB = torch.zeros(2 * F, r, device=DEV)
+    ops().swiglu_lora_gdb(dh, gu, dgu, BT, u, out, dB, M, M_out, 0.75)
+    assert torch.equal(dgu, dgu_ref)
+    assert torch.equal(out, out_ref)
+    assert relerr(dB, dB_ref) < 1e-6
+    # dB against fp64 dgu^T u over the kernel's own dgu (silu keeps dgu off the integers)
+    u_i = ints(M_out, 64, lo=-2, hi=3)
+    dB2 = torch.zeros(2 * F, r, device=DEV)
+    ops().swiglu_lora_gdb(dh, gu, dgu, BT, u_i, out, dB2, M, M_out, 1.0)
+    ref2 = torch.cat([dgu[:M, j * F:(j + 1) * F].double().T @ u_i[:M, j * r:(j + 1) * r].double() for j in range(2)])
+    assert relerr(dB2.double(), ref2) < 1e-6
+
+
 @pytest.mark.parametrize("M,nm,Nmod,r", [(4800, 3, 4096, 16), (640, 2, 11008, 16), (100, 1, 4096, 16),
                                          (300, 3, 1024, 32), (200, 2, 2048, 32)])
 def test_lora_skinny_up_blockdiag(M, nm, Nmod, r):
