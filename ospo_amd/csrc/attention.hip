@@ -398,6 +398,260 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
   }
 }
 
+// Forward, round 4 (the default): 4 waves x 32 query rows = the same 128-row blocks, grid and causal
+// tile counts as attn_fwd_kernel<8>, but each wave owns TWO 16-row query groups, so every K fragment
+// (S^T = K.Q^T) and every V^T fragment (O^T += V^T.P^T) read from LDS feeds two MFMAs: half the LDS
+// bytes per flop (the 8-wave form read 32 KiB per 16 rows and tile, as much LDS traffic per CU as its
+// softmax VALU).  V^T reads use per-lane addresses computed once (immediate offsets for the key half and
+// the second row quad), and the causal mask runs only on the diagonal tiles.
+// PIPE (the default): the scores of tile kt+1 are issued before the softmax of tile kt, so the MFMA pipe
+// works on S(kt+1) while the same wave's VALU runs the softmax of kt.  K and V get separate double
+// buffers: after the tile-start barrier K(kt+2) goes into the K buffer S(kt) used and V(kt+1) into the V
+// buffer PV(kt-1) used, both a full tile ahead of their readers (LDS stays 64 KiB, two workgroups per CU).
+// Per query row the MFMA order, the softmax and the PV accumulation are those of attn_fwd_kernel:
+// bit-identical output and lse in both forms.
+template <int OFF>
+__device__ __forceinline__ void fwd_rdtr(uint32_t a, i16x4& v) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+}
+
+// S^T of both query groups against one K tile image.  The k steps d run outermost: consecutive MFMAs on
+// one accumulator are 8 apart (t-inner order put them 2 apart, each waiting for its predecessor's
+// result); per accumulator the order over d is unchanged, so the scores are bit-identical.
+__device__ __forceinline__ void fwd_scores(const char* Ks, const bf16x8 (&qf)[2][4], f32x4 (&st)[2][4], int lane) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) st[0][t] = st[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf16x8 kf = frag_row(Ks, 16 * t, d, lane);
+      st[0][t] = MFMA(kf, qf[0][d], st[0][t]);
+      st[1][t] = MFMA(kf, qf[1][d], st[1][t]);
+    }
+  }
+}
+
+// HF scores, causal mask (diagonal tiles only), online softmax of one tile for both groups -> P^T packs
+__device__ __forceinline__ void fwd_softmax(f32x4 (&st)[2][4], bool diag, int key0, const int (&lim)[2], float scale,
+                                            float (&m_run)[2], float (&l_run)[2], f32x4 (&o)[2][8],
+                                            bf16x8 (&pb)[2][2]) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    float tmax = -INFINITY;
+    if (diag) {
+      const int rel = lim[q] - key0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+          float a = st[q][t][j], b = st[q][t][j + 1];
+          hf_scores2(a, b, scale);
+          a = (16 * t + j > rel) ? -INFINITY : a;
+          b = (16 * t + j + 1 > rel) ? -INFINITY : b;
+          st[q][t][j] = a;
+          st[q][t][j + 1] = b;
+          tmax = fmaxf(tmax, fmaxf(a, b));
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+          float a = st[q][t][j], b = st[q][t][j + 1];
+          hf_scores2(a, b, scale);
+          st[q][t][j] = a;
+          st[q][t][j + 1] = b;
+          tmax = fmaxf(tmax, fmaxf(a, b));
+        }
+    }
+    tmax = grp_max(tmax);
+    const float m_new = fmaxf(m_run[q], tmax);
+    const float alpha = __builtin_amdgcn_exp2f((m_run[q] - m_new) * L2E);
+    const float mb = m_new * L2E;
+    float psum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float pv = __builtin_amdgcn_exp2f(fmaf(st[q][t][j], L2E, -mb));
+        st[q][t][j] = pv;
+        psum += pv;
+      }
+    psum = grp_sum(psum);
+    l_run[q] = l_run[q] * alpha + psum;
+    m_run[q] = m_new;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[q][i] *= alpha;
+    pb[q][0] = pack_perm(st[q][0], st[q][1]);
+    pb[q][1] = pack_perm(st[q][2], st[q][3]);
+  }
+}
+
+// O^T += V^T . P^T for both groups: each V^T fragment (batches of 4) feeds two MFMAs
+__device__ __forceinline__ void fwd_pv(const uint32_t (&va)[8], uint32_t boff, const bf16x8 (&pb)[2][2],
+                                       f32x4 (&o)[2][8]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+#pragma unroll
+    for (int d0 = 0; d0 < 8; d0 += 4) {
+      i16x4 vlo[4], vhi[4];
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {
+        const uint32_t a = va[d0 + dd] + boff;
+        if (u == 0) {
+          fwd_rdtr<0>(a, vlo[dd]);
+          fwd_rdtr<16 * ROWB>(a, vhi[dd]);
+        } else {
+          fwd_rdtr<32 * ROWB>(a, vlo[dd]);
+          fwd_rdtr<48 * ROWB>(a, vhi[dd]);
+        }
+      }
+      trp_wait4(vlo, vhi);
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {
+        const bf16x8 vf = trp_join(vlo[dd], vhi[dd]);
+        o[0][d0 + dd] = MFMA(vf, pb[0][u], o[0][d0 + dd]);
+        o[1][d0 + dd] = MFMA(vf, pb[1][u], o[1][d0 + dd]);
+      }
+    }
+  }
+}
+
+// DBG (ablation build, results invalid): 1 no softmax VALU (P = S), 2 no PV products, 3 no S products,
+// 4 no K/V loads after the first tile
+template <bool MXO = false, bool PIPE = false, int DBG = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd2_kernel(
+    const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, bf16* __restrict__ out, int ldo,
+    float* __restrict__ lse, int T, int H, float scale, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0}) {
+  constexpr int NW = 4, RB = 128;
+  // PIPE: K0 K1 V0 V1; else K0 V0 K1 V1 (a tile's K and V side by side)
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qb = gridDim.z - 1 - blockIdx.z;  // heaviest blocks first (LPT), as attn_fwd_kernel
+  const int h = blockIdx.x, s = blockIdx.y;
+  const int g = lane >> 4, l16 = lane & 15;
+  const long rowbase = (long)s * T;
+
+  int qrow[2], lim[2];
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    qrow[q] = qb * RB + wave * 32 + q * 16 + l16;
+    const int qr_c = qrow[q] < T ? qrow[q] : T - 1;
+    lim[q] = qr_c;  // last key this row attends to (padding rows: T - 1)
+    const bf16* qp = qkv + (rowbase + qr_c) * ldq + qc + h * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) qf[q][d] = *reinterpret_cast<const bf16x8*>(qp + 32 * d + 8 * g);
+  }
+  f32x4 o[2][8];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
+
+  const int last = (qb * RB + RB - 1 < T ? qb * RB + RB - 1 : T - 1);
+  const int n_kv = last / KB + 1;
+  const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
+  const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
+  constexpr int KOFF = PIPE ? TILE_BYTES : 2 * TILE_BYTES;  // K buffer stride
+  constexpr int V0 = PIPE ? 2 * TILE_BYTES : TILE_BYTES;    // first V buffer
+  auto diag_of = [&](int kt) { return (kt * KB + KB - 1 > qb * RB) || ((kt + 1) * KB > T); };
+
+  // V^T read addresses of this lane (V buffer 0), one per 16-column group dt: rows 4g + q4 (+16: offset, +32
+  // for the second key half: offset), chunk (2 dt + p/2) ^ swizzle -- the XOR keeps dt out of the offset
+  uint32_t va[8];
+  {
+    const int q4 = l16 >> 2, p = l16 & 3;
+    const int r1 = 4 * g + q4, hh = (p & 1) << 3;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      va[dt] = lds_u32(smem + V0 + r1 * ROWB + (((2 * dt + (p >> 1)) ^ aswz(r1)) << 4) + hh);
+  }
+
+  bf16x8 pb[2][2];
+  if constexpr (PIPE) {
+    stage64<NW>(kbase, ldq, 0, T, 0, smem, wave, lane);
+    stage64<NW>(vbase, ldq, 0, T, 0, smem + V0, wave, lane);
+    if (n_kv > 1) stage64<NW>(kbase, ldq, KB, T, 0, smem + KOFF, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    f32x4 st[2][4];
+    fwd_scores(smem, qf, st, lane);
+    for (int kt = 0; kt < n_kv; ++kt) {
+      const int buf = kt & 1;
+      // every wave is past S(kt) and PV(kt - 1); K(kt + 1) and V(kt) have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      f32x4 sn[2][4];
+      if (kt + 1 < n_kv) fwd_scores(smem + (buf ^ 1) * KOFF, qf, sn, lane);
+      if (kt + 2 < n_kv) stage64<NW>(kbase, ldq, (kt + 2) * KB, T, 0, smem + buf * KOFF, wave, lane);
+      if (kt + 1 < n_kv) stage64<NW>(vbase, ldq, (kt + 1) * KB, T, 0, smem + V0 + (buf ^ 1) * TILE_BYTES, wave, lane);
+      fwd_softmax(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
+      fwd_pv(va, (uint32_t)(buf * TILE_BYTES), pb, o);
+      if (kt + 1 < n_kv) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) st[q][t] = sn[q][t];
+      }
+    }
+    __syncthreads();  // the K/V buffers become the output scratch
+  } else {
+    stage64<NW>(kbase, ldq, 0, T, 0, smem, wave, lane);
+    stage64<NW>(vbase, ldq, 0, T, 0, smem + V0, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < n_kv; ++kt) {
+      const int buf = kt & 1;
+      if (DBG != 4 && kt + 1 < n_kv) {
+        char* const nbuf = smem + (buf ^ 1) * KOFF;
+        stage64<NW>(kbase, ldq, (kt + 1) * KB, T, 0, nbuf, wave, lane);
+        stage64<NW>(vbase, ldq, (kt + 1) * KB, T, 0, nbuf + TILE_BYTES, wave, lane);
+      }
+      f32x4 st[2][4];
+      if constexpr (DBG == 3) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) st[0][t] = st[1][t] = f32x4{0.01f * t, 0.02f, 0.f, -0.01f};
+      } else {
+        fwd_scores(smem + buf * KOFF, qf, st, lane);
+      }
+      if constexpr (DBG == 1) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          pb[q][0] = pack_perm(st[q][0], st[q][1]);
+          pb[q][1] = pack_perm(st[q][2], st[q][3]);
+        }
+      } else {
+        fwd_softmax(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
+      }
+      if constexpr (DBG != 2) fwd_pv(va, (uint32_t)(buf * KOFF), pb, o);
+      else {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) o[q][0] += __builtin_bit_cast(f32x4, pb[q][0]) + __builtin_bit_cast(f32x4, pb[q][1]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const float inv = 1.f / l_run[q];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[q][dt] *= inv;
+    const int row0 = qb * RB + wave * 32 + q * 16;
+    if constexpr (MXO)
+      store_rows16(o[q], smem + (wave * 2 + q) * SCR_BYTES, out + rowbase * ldo + h * HD, ldo, row0, T, lane, mo,
+                   rowbase, h * (HD / 8));
+    else
+      store_rows16(o[q], smem + (wave * 2 + q) * SCR_BYTES, out + rowbase * ldo + h * HD, ldo, row0, T, lane);
+    if (qrow[q] < T && g == 0) lse[((long)s * H + h) * T + qrow[q]] = m_run[q] + __logf(l_run[q]);
+  }
+}
+
 // ============================================================ backward =====
 // dK / dV: workgroup = 4 waves = 64 keys of one (sequence, head); each wave
 // owns 16 keys (K, V fragments in registers, dK^T dV^T accumulators) and
@@ -1504,22 +1758,33 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
   if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || q_col % 8 || k_col % 8 || v_col % 8)
     return OSPO_ERR_SHAPE;
   if (!aligned16(qkv) || !aligned16(o)) return OSPO_ERR_ALIGN;
-  const int nw = attn_waves();
-  dim3 grid(n_heads, S, (T + 16 * nw - 1) / (16 * nw));
+  int nw = 4;  // attn_fwd2_kernel: 4 waves x 32 query rows
+  auto kfn = mo.q ? attn_fwd2_kernel<true, false> : attn_fwd2_kernel<false, false>;
 #ifdef OSPO_ABLATION
-  static const bool dbg = getenv("OSPO_ATTN_DBG") != nullptr;  // ablation only (results invalid)
-  auto kfn = dbg ? attn_fwd_kernel<8, 1> : (nw == 8 ? attn_fwd_kernel<8, 0> : attn_fwd_kernel<4, 0>);
-  static const bool spr = getenv("OSPO_ATTN_FWD_SPREAD") != nullptr;
-  if (spr && !dbg && nw == 8) kfn = attn_fwd_kernel<8, 0, false, true>;
-#else
-  auto kfn = attn_fwd_kernel<8, 0>;
-#endif
-  if (mo.q) {
-#ifdef OSPO_ABLATION
-    if (dbg || nw != 8) return OSPO_ERR_UNSUPPORTED;  // ablation forms: no MXFP8 copy
-#endif
-    kfn = attn_fwd_kernel<8, 0, true>;
+  if (getenv("OSPO_ATTN_FWD_PIPE")) kfn = mo.q ? attn_fwd2_kernel<true, true> : attn_fwd2_kernel<false, true>;
+  if (const char* e = getenv("OSPO_ATTN_FWD2_DBG")) {  // decomposition (results invalid)
+    const int v = atoi(e);
+    if (v == 1) kfn = attn_fwd2_kernel<false, false, 1>;
+    if (v == 2) kfn = attn_fwd2_kernel<false, false, 2>;
+    if (v == 3) kfn = attn_fwd2_kernel<false, false, 3>;
+    if (v == 4) kfn = attn_fwd2_kernel<false, false, 4>;
   }
+  // A/B: the 8-wave x 16-row kernel (rounds 1-3; OSPO_ATTN_FWD8), its decomposition / spread forms
+  static const bool fwd8 = getenv("OSPO_ATTN_FWD8") != nullptr;
+  static const bool dbg = getenv("OSPO_ATTN_DBG") != nullptr;  // ablation only (results invalid)
+  static const bool spr = getenv("OSPO_ATTN_FWD_SPREAD") != nullptr;
+  if (fwd8 || dbg || spr) {
+    nw = attn_waves();
+    kfn = dbg ? attn_fwd_kernel<8, 1> : (nw == 8 ? attn_fwd_kernel<8, 0> : attn_fwd_kernel<4, 0>);
+    if (spr && !dbg && nw == 8) kfn = attn_fwd_kernel<8, 0, false, true>;
+    if (mo.q) {
+      if (dbg || nw != 8) return OSPO_ERR_UNSUPPORTED;  // ablation forms: no MXFP8 copy
+      kfn = attn_fwd_kernel<8, 0, true>;
+    }
+  }
+#endif
+  const int rb = nw == 4 && kfn != attn_fwd_kernel<4, 0> ? 128 : 16 * nw;
+  dim3 grid(n_heads, S, (T + rb - 1) / rb);
   hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                      (bf16*)o, ld_o, lse, T, n_heads, scale, mo);
   OSPO_CHECK_LAUNCH();

@@ -750,6 +750,9 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_kernel(const DlArgs a) {
     }
     __syncthreads();
     if (flag == 0u) return;
+    // no instruction: keeps the sc1 partial loads below the ticket (sc1 stores drained before it, sc1 loads
+    // after it: the hand-off Valid form of cdna_hip_programming.md, where this replaces the agent-scope acquire)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1069,7 +1072,10 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin2_kernel(const DlArgs a, in
       __syncthreads();  // flag
       const bool last = flag != 0u;
       __syncthreads();  // every wave has read it before the next ticket overwrites it
-      if (last) finish(pend, acc, true);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (as in dlin_kernel's last arriver)
+        finish(pend, acc, true);
+      }
       pend = -1;
     }
     if (c == nch - 1) {  // group g0 + q complete
@@ -1096,7 +1102,10 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin2_kernel(const DlArgs a, in
       flag = (t == (unsigned)splits - 1u) ? 1u : 0u;
     }
     __syncthreads();
-    if (flag != 0u) finish(pend, acc, true);
+    if (flag != 0u) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (as above)
+      finish(pend, acc, true);
+    }
   }
 }
 #endif  // OSPO_ABLATION

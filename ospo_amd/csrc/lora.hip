@@ -299,8 +299,9 @@ struct Sk3Cfg {
 
 // (a device function: hipcc's host pass drops the kernel's launch stub when this builtin sits in the
 // kernel body itself inside a loop)
+template <int AUX = 0>
 __device__ __forceinline__ void sk3_lds16(__amdgpu_buffer_rsrc_t rs, char* dst, uint32_t voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, voff, soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, voff, soff, 0, AUX);
 }
 
 __device__ __forceinline__ void sk3_wait(int n) {
@@ -384,7 +385,7 @@ __device__ __forceinline__ bf16x8 sk3_ldb(__amdgpu_buffer_rsrc_t rs, uint32_t vo
 // BTR (ablation build, OSPO_SK3_BTREG; 2-stage ring only): the adapter rows' fragments come straight from L2 into
 // registers (one chunk ahead, issued before the chunk's LDS-DMA pieces so the counted wait is unchanged) instead
 // of being staged with every 64-k chunk: 2 DMA pieces + 2 NT LDS reads fewer per chunk and wave.
-template <int NT, bool DROP, bool SWG = false, int NSREQ = 4, bool BTR = false>
+template <int NT, bool DROP, bool SWG = false, int NSREQ = 4, bool BTR = false, int AA = 0>  // AA: A-load policy bits
 __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A, int lda, int a_bytes,
                                                       const bf16* __restrict__ Bt, int ldb, int b_rows, int b_bytes,
                                                       int M, int M_out, int K, int kper, int a_koff, int tiles_total,
@@ -430,10 +431,10 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
     char* st_ = smem + ((cc) % NS) * STAGE;                                                                  \
     const int kb_ = (cc) * 128;                                                                                  \
     _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                                \
-        sk3_lds16(rsA, st_ + (wave * 2 + i) * 1024, va[i], kb_);                                                 \
+        sk3_lds16<AA>(rsA, st_ + (wave * 2 + i) * 1024, va[i], kb_);                                             \
     if constexpr (SWG) {                                                                                         \
       _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                              \
-          sk3_lds16(rsA, st_ + 8192 + (wave * 2 + i) * 1024, va[i], kb_ + up_off);                               \
+          sk3_lds16<AA>(rsA, st_ + 8192 + (wave * 2 + i) * 1024, va[i], kb_ + up_off);                           \
     }                                                                                                            \
     if constexpr (!BTR) {                                                                                        \
       _Pragma("unroll") for (int i = 0; i < C::BPW; ++i)                                                         \
@@ -573,6 +574,9 @@ __global__ __launch_bounds__(256) void skinny3_kernel(const bf16* __restrict__ A
     }
     __syncthreads();
     if (*flag == 0u) return;
+    // no instruction: keeps the sc1 partial loads below the ticket (sc1 stores drained before it, sc1 loads
+    // after it: the hand-off Valid form of cdna_hip_programming.md, where this replaces the agent-scope acquire)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int cq = out_cols / 4;
     for (int it = threadIdx.x; it < 64 * cq; it += blockDim.x) {
       const int r = it / cq, c = (it % cq) * 4;
@@ -1313,19 +1317,26 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   }();
   ns = ns_env;
 #endif
-#define SK3_LAUNCH2(NS_, BTR_)                                                                                   \
+#define SK3_LAUNCH3(NS_, BTR_, AA_)                                                                              \
   if (dr.scale > 0.f)                                                                                            \
-    hipLaunchKernelGGL((skinny3_kernel<NT, true, SWG, NS_, BTR_>), grid, dim3(256), 0, stream, a, lda,             \
+    hipLaunchKernelGGL((skinny3_kernel<NT, true, SWG, NS_, BTR_, AA_>), grid, dim3(256), 0, stream, a, lda,        \
                        (int)a_bytes, b, ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, \
                        ldo, out_cols, part, M_pad, dr.seed, dr.thresh, dr.scale, dr.bits, hout, ldh, K * 2, c);     \
   else                                                                                                           \
-    hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG, NS_, BTR_>), grid, dim3(256), 0, stream, a, lda,            \
+    hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG, NS_, BTR_, AA_>), grid, dim3(256), 0, stream, a, lda,       \
                        (int)a_bytes, b, ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, \
                        ldo, out_cols, part, M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2, c);
+#define SK3_LAUNCH2(NS_, BTR_) SK3_LAUNCH3(NS_, BTR_, 0)
 #define SK3_LAUNCH(NS_) SK3_LAUNCH2(NS_, false)
 #ifdef OSPO_ABLATION
   static const bool btreg = getenv("OSPO_SK3_BTREG") != nullptr;
-  if (ns == 2 && btreg) {
+  static const int sk_nt = [] {  // A/B: non-temporal A loads, 1 = the SwiGLU form only, 2 = every form
+    const char* e = getenv("OSPO_SK3_NT");
+    return e ? atoi(e) : 0;
+  }();
+  if (ns == 2 && (sk_nt == 2 || (sk_nt == 1 && SWG))) {
+    SK3_LAUNCH3(2, false, 2)
+  } else if (ns == 2 && btreg) {
     SK3_LAUNCH2(2, true)
   } else if (ns == 2) {
     SK3_LAUNCH(2)
@@ -1343,6 +1354,7 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
 #endif
 #undef SK3_LAUNCH
 #undef SK3_LAUNCH2
+#undef SK3_LAUNCH3
   OSPO_CHECK_LAUNCH();
   if (splits > 1 && !c) {
     const long n = (long)M_out * (out_cols / 4);
