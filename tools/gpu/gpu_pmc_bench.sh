@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out/pmc_bench
 export TMPDIR=/tmp
 ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timer"
-for SET in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+for SET in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES"; do
   tag=$(echo $SET | cut -d' ' -f1)
   timeout -k 10 600 rocprofv3 --pmc $SET --output-format csv -d gpurun_out/pmc_bench/$tag -o p -- python bench.py $ARGS > gpurun_out/pmc_bench/$tag.log 2>&1 || { echo "PMC $tag FAILED"; tail -5 gpurun_out/pmc_bench/$tag.log; exit 1; }
 done

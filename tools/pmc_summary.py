@@ -34,27 +34,28 @@ fetch, nf = load("FETCH_SIZE")
 write, nw = load("WRITE_SIZE")
 sq, ns = load("SQ_VALU_MFMA_BUSY_CYCLES")
 out = {}
-gemm = [k for k in fetch if "gemm_nt_v5_kernel" in k]
+GEMM_NAMES = ("gemm_nt_w4_kernel", "gemm_nt_v5_kernel")  # round 4 default / the SP8 schedule
+gemm = [k for k in fetch if any(g in k for g in GEMM_NAMES)]
 fix = [k for k in fetch if "splitk_fixup" in k]
 launches = sum(nf[(k, "FETCH_SIZE")] for k in gemm)
 kib = sum(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"] for k in gemm + fix)
-busy = sum(sq[k]["SQ_VALU_MFMA_BUSY_CYCLES"] for k in sq if "gemm_nt_v5_kernel" in k)
-gui = sum(sq[k]["GRBM_GUI_ACTIVE"] for k in sq if "gemm_nt_v5_kernel" in k)
+busy = sum(sq[k]["SQ_VALU_MFMA_BUSY_CYCLES"] for k in sq if any(g in k for g in GEMM_NAMES))
 # kernel wall time of the same dispatches (counter rows carry the dispatch timestamps)
 f = glob.glob(os.path.join(src, "SQ_VALU_MFMA_BUSY_CYCLES", "**", "*counter_collection.csv"), recursive=True)[0]
 durs = {}
 for r in csv.DictReader(open(f)):
-    if "gemm_nt_v5_kernel" in r["Kernel_Name"]:
+    if any(g in r["Kernel_Name"] for g in GEMM_NAMES):
         durs[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
 dur_s = sum(durs.values()) * 1e-9
 out["gemm_nt_256x256"] = {
     "hbm_bytes_per_launch": round(kib * 1024 / launches),
     "launches": int(launches),
-    "method": "2*FETCH_SIZE + WRITE_SIZE (KiB), gemm_nt_v5_kernel + splitk_fixup_kernel, averaged over launches",
-    # SQ_VALU_MFMA_BUSY_CYCLES: summed over the 1024 SIMDs (16 cycles per 16x16x32 bf16 MFMA);
-    # GRBM_GUI_ACTIVE: summed over the 8 XCDs (GRBM / wall time = 8 x the shader clock)
-    "effective_clock_ghz": round(gui / 8 / dur_s / 1e9, 3) if dur_s else None,
-    "mfma_busy_frac_of_active_cycles": round(busy / (gui / 8 * 1024), 4) if gui else None,
+    "kernels": sorted({short(k) for k in gemm}),
+    "method": "2*FETCH_SIZE + WRITE_SIZE (KiB), the NT GEMM + splitk_fixup_kernel, averaged over launches",
+    # SQ_VALU_MFMA_BUSY_CYCLES: summed over the 1024 SIMDs (16 cycles per 16x16x32 bf16 MFMA), against
+    # the cycles of the counter pass's kernel durations at the 2.4 GHz peak clock.  (The round-3 clock from
+    # GRBM_GUI_ACTIVE / 8 / duration came out above 2.4 GHz and is no longer reported; in-kernel clocks come
+    # from s_memtime / s_memrealtime stamps, tools/w4_stamps.py.)
     "mfma_busy_frac_at_2p4ghz_peak": round(busy / (dur_s * 2.4e9 * 1024), 4) if dur_s else None,
 }
 for k in sorted(set(fetch) | set(write), key=lambda k: -(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"]))[:15]:
