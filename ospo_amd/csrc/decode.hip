@@ -512,6 +512,20 @@ __device__ __forceinline__ float dpp_sum16(float x) {
   return x;
 }
 
+// non-temporal weight / KV-cache loads (decode streams read once per step); -DOSPO_DLIN_NTW=0 for the A/B
+#ifndef OSPO_DLIN_NTW
+#define OSPO_DLIN_NTW 1
+#endif
+// KV-cache rows: each workgroup reads its own row's cache once per step (5 GB over 30 layers late in an image,
+// far past the 256 MB MALL): non-temporal, like the weight streams (OSPO_DLIN_NTW)
+__device__ __forceinline__ u32x4 kv_load(const bf16* p) {
+#if OSPO_DLIN_NTW
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#else
+  return *reinterpret_cast<const u32x4*>(p);
+#endif
+}
+
 __global__ __launch_bounds__(256) void attn_cache2_kernel(const bf16* __restrict__ q, int ldq,
                                                           const bf16* __restrict__ kc, const bf16* __restrict__ vc,
                                                           int H, int Tmax, const int* __restrict__ start,
@@ -539,7 +553,7 @@ __global__ __launch_bounds__(256) void attn_cache2_kernel(const bf16* __restrict
   for (int k0 = kg; k0 < L; k0 += 64) {
     u32x4 kv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) kv[u] = *reinterpret_cast<const u32x4*>(kb + (long)min(k0 + 16 * u, L - 1) * HD);
+    for (int u = 0; u < 4; ++u) kv[u] = kv_load(kb + (long)min(k0 + 16 * u, L - 1) * HD);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float kf[8];
@@ -576,7 +590,7 @@ __global__ __launch_bounds__(256) void attn_cache2_kernel(const bf16* __restrict
   for (int k0 = kg; k0 < L; k0 += 64) {
     u32x4 vv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) vv[u] = *reinterpret_cast<const u32x4*>(vb + (long)min(k0 + 16 * u, L - 1) * HD);
+    for (int u = 0; u < 4; ++u) vv[u] = kv_load(vb + (long)min(k0 + 16 * u, L - 1) * HD);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const float pk = (k0 + 16 * u < L) ? round_bf(sc[min(k0 + 16 * u, L - 1)] * inv) : 0.f;
@@ -691,7 +705,14 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_kernel(const DlArgs a) {
     asm volatile("" ::: "memory");  // x DMA (+ the norm weights) before the weight loads: vmcnt(16) covers them
     bf16x8 wv[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) wv[s] = *reinterpret_cast<const bf16x8*>(wrow + (long)((kc >> 5) + min(s, nsteps - 1)) * 512);
+    for (int s = 0; s < 16; ++s) {
+      const bf16x8* wp = reinterpret_cast<const bf16x8*>(wrow + (long)((kc >> 5) + min(s, nsteps - 1)) * 512);
+#if OSPO_DLIN_NTW
+      wv[s] = __builtin_nontemporal_load(wp);  // the weight stream is read once per step: no cache allocation
+#else
+      wv[s] = *wp;
+#endif
+    }
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __syncthreads();
     if constexpr (NORM) {

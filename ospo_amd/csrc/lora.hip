@@ -1326,16 +1326,18 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
     hipLaunchKernelGGL((skinny3_kernel<NT, false, SWG, NS_, BTR_, AA_>), grid, dim3(256), 0, stream, a, lda,       \
                        (int)a_bytes, b, ldb, b_rows, (int)b_bytes, M, M_out, K, kper, a_koff, tiles_total, scale, o, \
                        ldo, out_cols, part, M_pad, 0u, 0u, 0.f, nullptr, hout, ldh, K * 2, c);
-#define SK3_LAUNCH2(NS_, BTR_) SK3_LAUNCH3(NS_, BTR_, 0)
+// A loads non-temporal (the activation is not re-read from this CU's caches): same-box step 111.04 / 110.77 ->
+// 110.73 / 110.58 ms (profiles/r04/step_skinny_nt_ab.txt); OSPO_SK3_NT=0 (ablation build) restores the default policy
+#define SK3_LAUNCH2(NS_, BTR_) SK3_LAUNCH3(NS_, BTR_, 2)
 #define SK3_LAUNCH(NS_) SK3_LAUNCH2(NS_, false)
 #ifdef OSPO_ABLATION
   static const bool btreg = getenv("OSPO_SK3_BTREG") != nullptr;
-  static const int sk_nt = [] {  // A/B: non-temporal A loads, 1 = the SwiGLU form only, 2 = every form
+  static const int sk_nt = [] {  // A/B: OSPO_SK3_NT=0 restores the default cache policy of the A loads
     const char* e = getenv("OSPO_SK3_NT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
-  if (ns == 2 && (sk_nt == 2 || (sk_nt == 1 && SWG))) {
-    SK3_LAUNCH3(2, false, 2)
+  if (ns == 2 && sk_nt == 0) {
+    SK3_LAUNCH3(2, false, 0)
   } else if (ns == 2 && btreg) {
     SK3_LAUNCH2(2, true)
   } else if (ns == 2) {
