@@ -1902,19 +1902,25 @@ struct SplitPlan {
 // plus the fp32 partials (256 KiB per piece, written here and read by the fixup: ~0.13 us each at ~4 TB/s).
 // T = one tile's K loop, ~1.9 us per bf16 K-tile (2.3 per MX K-tile) at the measured rate.  At most one
 // round of pieces (tail s <= CUs) and as many as ws_bytes holds.
-SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus, int pinned, size_t ws_bytes) {
+// w4 (the 4-wave bf16 kernel): T = 1.3 us per K-tile and at most ~0.78 x CUs pieces.  Fitted on
+// the step shapes' pinned-split sweep (tools/w4_split_sweep.py, profiles/r04/w4_split_sweep.log): a tail round
+// that leaves CUs idle runs them at a higher clock (the chip is power-limited under this load), so few large
+// pieces beat a full round of small ones (304-tile shapes: 4 pieces per tail tile, not 5; 1152 tiles: no split).
+SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus, int pinned, size_t ws_bytes,
+                     bool w4 = false) {
   const int tiles = ((M + 255) / 256) * (N / 256);
   SplitPlan pl{tiles, 1, 0};
   if (tiles <= cus || pinned == 1) return pl;
   const int tail = tiles % cus;
   if (!tail) return pl;
   const long ws_pieces = (long)(ws_bytes / (65536 * sizeof(float)));
-  const int sp_max = (int)std::min<long>(std::min(std::min(8, ntot / 4), cus / tail), ws_pieces / tail);
+  const int piece_cap = w4 ? cus * 25 / 32 : cus;
+  const int sp_max = (int)std::min<long>(std::min(std::min(8, ntot / 4), piece_cap / tail), ws_pieces / tail);
   int split = 1;
   if (pinned > 1) {
     split = std::max(1, std::min(pinned, sp_max));
   } else {
-    const double T = ntot * (mx ? 2.3 : 1.9);
+    const double T = ntot * (w4 ? 1.3 : (mx ? 2.3 : 1.9));
     double best = T;
     for (int sp = 2; sp <= sp_max; ++sp) {
       const double cost = (double)((tail * sp + cus - 1) / cus) / sp * T + 0.13 * tail * sp;
@@ -1944,7 +1950,8 @@ int launch_w4(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
     return OSPO_ERR_UNSUPPORTED;
   const int tm = (a.M + 255) / 256, tn = a.N / 256;
   const int nt1 = a.K / 64, nt2 = a.K2 / 64, ntot = nt1 + nt2;
-  const SplitPlan pl = plan_split(a.M, a.N, ntot, a.K2, false, DROP, device_cus(), so.split, so.ws ? so.ws_bytes : 0);
+  const SplitPlan pl = plan_split(a.M, a.N, ntot, a.K2, false, DROP, device_cus(), so.split, so.ws ? so.ws_bytes : 0,
+                                  true);
   for (int z = 0; z < (pl.tail ? pl.split : 1); ++z) {  // every unit's program must fit (z = 0: the whole range)
     const int tb = pl.tail ? (int)((long)ntot * z / pl.split) : 0;
     const int tc = pl.tail ? (int)((long)ntot * (z + 1) / pl.split) - tb : ntot;
@@ -2754,7 +2761,9 @@ extern "C" size_t ospo_gemm_nt_ws_bytes(int M, int N, int K, int K2, int mx, int
   const int ntot = (mx ? K / 128 : K / BK) + K2 / BK;
   // with dropout the plan can only shrink (drop_ok), so the plan without it bounds the bytes
   const SplitPlan pl = plan_split(M, N, ntot, K2, mx != 0, false, device_cus(), tail_split, SIZE_MAX);
-  return (size_t)pl.tail * pl.split * 65536 * sizeof(float);
+  const SplitPlan p4 = plan_split(M, N, ntot, K2, false, false, device_cus(), tail_split, SIZE_MAX, true);  // w4
+  const size_t pieces = std::max((size_t)pl.tail * pl.split, mx ? (size_t)0 : (size_t)p4.tail * p4.split);
+  return pieces * 65536 * sizeof(float);
 }
 
 #ifdef OSPO_ABLATION
