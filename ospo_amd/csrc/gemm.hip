@@ -1806,6 +1806,32 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
 }
 
 // sum the split partials of each tail tile, apply alpha / bias / residual, write bf16
+// The split partials of 8 columns (row r of a tile), summed in split order: every load issued before the first
+// add (a split-long load->add chain cost ~2 us per partial), non-temporal (each partial is read once).  Loads are
+// unconditional (index clamped: no branch, one counted wait), W = 4 or 8 at a time.
+template <int W>
+__device__ __forceinline__ void fixup_sum_w(const float* p, int split, f32x4& lo, f32x4& hi) {
+  for (int z0 = 0; z0 < split; z0 += W) {
+    f32x4 pl[W], ph[W];
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+      const long zz = min(z0 + u, split - 1);
+      pl[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + zz * 65536));
+      ph[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + zz * 65536 + 4));
+    }
+#pragma unroll
+    for (int u = 0; u < W; ++u)
+      if (z0 + u < split) {
+        lo += pl[u];
+        hi += ph[u];
+      }
+  }
+}
+__device__ __forceinline__ void fixup_sum(const float* p, int split, f32x4& lo, f32x4& hi) {
+  if (split <= 4) fixup_sum_w<4>(p, split, lo, hi);
+  else fixup_sum_w<8>(p, split, lo, hi);
+}
+
 __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, int tiles_m, int tiles_n, int dp,
                                                            int split, const float* __restrict__ ws, int GM) {
   const int tile = blockIdx.x >> 5, rblk = blockIdx.x & 31;
@@ -1815,11 +1841,7 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
   const int m = m0 + r;
   if (m >= args.M) return;
   f32x4 lo = f32x4{0.f, 0.f, 0.f, 0.f}, hi = lo;
-  for (int z = 0; z < split; ++z) {
-    const float* p = ws + (long)(tile * split + z) * 65536 + r * 256 + c;
-    lo += *reinterpret_cast<const f32x4*>(p);
-    hi += *reinterpret_cast<const f32x4*>(p + 4);
-  }
+  fixup_sum(ws + (long)tile * split * 65536 + r * 256 + c, split, lo, hi);
   float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -1836,11 +1858,7 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
     const bool lo_half = d < 64;
     const int pc = lo_half ? c + 64 : c - 64, dd = lo_half ? d : d - 64;
     f32x4 plo = f32x4{0.f, 0.f, 0.f, 0.f}, phi = plo;
-    for (int z = 0; z < split; ++z) {
-      const float* pp = ws + (long)(tile * split + z) * 65536 + r * 256 + pc;
-      plo += *reinterpret_cast<const f32x4*>(pp);
-      phi += *reinterpret_cast<const f32x4*>(pp + 4);
-    }
+    fixup_sum(ws + (long)tile * split * 65536 + r * 256 + pc, split, plo, phi);
     const float pv[8] = {plo[0], plo[1], plo[2], plo[3], phi[0], phi[1], phi[2], phi[3]};
     const int t = m % args.rope_T;
     const u32x4 cw = *reinterpret_cast<const u32x4*>(args.rope_cs + (long)t * 64 + dd);

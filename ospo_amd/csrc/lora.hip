@@ -1145,7 +1145,9 @@ __global__ void gdb_reduce_kernel(const float* __restrict__ ws, int nmods, int n
       f32x4 p[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if (s0 + k < nsplit) p[k] = *reinterpret_cast<const f32x4*>(ws + (((long)mod * nsplit + s0 + k) * Mw + m) * 16 + (c & 15));
+        if (s0 + k < nsplit)  // (non-temporal: each partial is read once)
+          p[k] = __builtin_nontemporal_load(
+              reinterpret_cast<const f32x4*>(ws + (((long)mod * nsplit + s0 + k) * Mw + m) * 16 + (c & 15)));
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         if (s0 + k < nsplit) v += p[k];

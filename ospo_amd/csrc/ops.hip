@@ -200,8 +200,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
   for (int it = 0; it < IT; ++it) {
     const int c = it * 64 + lane;
     if (FULL || c < nch) {
-      xv[it] = xr[c];
-      dv[it] = dr[c];
+      xv[it] = __builtin_nontemporal_load(xr + c);  // (read once: non-temporal)
+      dv[it] = __builtin_nontemporal_load(dr + c);
     }
   }
   float dot = 0.f;
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int c = it * 64 + lane;
-      if (FULL || c < nch) rv[it] = rr[c];
+      if (FULL || c < nch) rv[it] = __builtin_nontemporal_load(rr + c);
     }
   }
 #pragma unroll
