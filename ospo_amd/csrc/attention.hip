@@ -1596,7 +1596,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ds_kernel(const bf16* __r
 }
 
 // Stage 32 rows x 128 bf16 (clamped to [0, row_lim)): 8 pieces of 1 KiB (4 rows each) over the NW waves.
-template <int NW>
+// AUX: cache-policy bits of the loads (2 = non-temporal: the dS^T workspace, read once).
+template <int NW, int AUX = 0>
 __device__ __forceinline__ void stage32(const bf16* base, int ld, int row0, int row_lim, int col0, char* lds,
                                         int wave, int lane) {
 #pragma unroll
@@ -1605,7 +1606,7 @@ __device__ __forceinline__ void stage32(const bf16* base, int ld, int row0, int 
     const int ch = (lane & 15) ^ aswz(row);
     int gr = row0 + row;
     gr = gr < row_lim ? gr : row_lim - 1;
-    glds16(base + (long)gr * ld + col0 + ch * 8, lds + p * 1024);
+    __builtin_amdgcn_global_load_lds(base + (long)gr * ld + col0 + ch * 8, (LDS_AS void*)(lds + p * 1024), 16, 0, AUX);
   }
 }
 
@@ -1658,7 +1659,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ring_kernel(const bf16* _
   auto stage = [&](int st) {
     char* Ks = smem + (st % NSLOT) * SLOT;
     stage32<NW>(kbase, ldq, st * 32, T, 0, Ks, wave, lane);
-    stage32<NW>(dbase, ds_ld, st * 32, ds_ld, qb * RB, Ks + 32 * ROWB, wave, lane);
+    stage32<NW, 2>(dbase, ds_ld, st * 32, ds_ld, qb * RB, Ks + 32 * ROWB, wave, lane);
   };
 #pragma unroll
   for (int st = 0; st < NSLOT - 1; ++st)

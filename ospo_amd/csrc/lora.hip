@@ -1626,9 +1626,10 @@ extern "C" int ospo_lora_da(const void* X, int ldx, int N, const void* S, int ld
   const int k_bytes = keep_bits ? (int)((long)K * N / 8) : 0;
   const uint8_t* kb = (const uint8_t*)keep_bits;
   const dim3 grid(N / DA_TN, splits);
-  int xa = 0;
+  int xa = 2;  // x non-temporal: the saved activation is read once here (same-box step 111.74 / 111.33 -> 111.48 /
+               // 111.31 ms, profiles/r04/step_swiglu_gdb_nt_ab.txt)
 #ifdef OSPO_ABLATION
-  if (getenv("OSPO_NT_DA")) xa = 2;  // A/B: non-temporal x loads
+  if (getenv("OSPO_DA_DEFAULT_POLICY")) xa = 0;  // A/B: the default cache policy
 #endif
 #define DA_LAUNCH2(NJV, XAV)                                                                                      \
   do {                                                                                                            \
