@@ -558,6 +558,19 @@ def main():
     loss = float(out["loss"].item())
     if not math.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
+    def rank_checks(vals):  # gathered from every rank: equal lists = ranks in sync
+        if world <= 1:
+            return None
+        import torch.distributed as tdist
+        c = torch.stack(vals)
+        c = c.cpu() if backend == "gloo" else c
+        every = [torch.zeros_like(c) for _ in range(world)]
+        tdist.all_gather(every, c)
+        return [[float(v) for v in e.cpu()] for e in every]
+
+    # the engine path's all-reduced grads and updated LoRA params must be identical on every rank (taken before
+    # the wrapper sub-measurement, which steps the same engine and zeroes its grads)
+    checks = rank_checks([eng.grads.double().sum(), eng.grads.double().abs().sum(), eng.lora.double().sum()])
     wrap = None
     if not args.no_wrapper:  # the drop-in path on the same engine and box
         wm, ww, wopt, wsch, war, wb, wls = wrapper_setup(args, world, rank, dev, engine=eng)
@@ -566,15 +579,8 @@ def main():
                             "grad-norm log, FusedLoraAdamW, scheduler; metrics read every 50 steps as PL), "
                             "VQ token-id batches in the reference's collate format, same engine",
                 "value": round(B * world * args.steps / wdt, 3), "unit": "pairs/s", "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": round(wdt / args.steps * 1e3, 2)}
-    checks = None
-    if world > 1:  # the all-reduced grads and the updated LoRA params must be identical on every rank
-        import torch.distributed as tdist
-        c = torch.stack([eng.grads.double().sum(), eng.grads.double().abs().sum(), eng.lora.double().sum()])
-        c = c.cpu() if backend == "gloo" else c
-        every = [torch.zeros_like(c) for _ in range(world)]
-        tdist.all_gather(every, c)
-        checks = [[float(v) for v in e.cpu()] for e in every]
+                "warmup": args.warmup, "ms_per_step": round(wdt / args.steps * 1e3, 2),
+                "rank_checksums": rank_checks([eng.lora.double().sum(), eng.lora.double().abs().sum()])}
     if rank != 0:
         return
     global_batch = B * world

@@ -120,6 +120,8 @@ def test_bench_two_ranks_gloo_share_one_gpu():
     assert ln["n_gpus"] == 2 and ln["config"]["backend"] == "gloo" and ln["config"]["parallelism"] == "dp2"
     assert ln["config"]["pairs_per_gpu"] == 8 and ln["config"]["global_batch"] == 16
     assert ln["value"] > 0 and ln["loss"] == ln["loss"]
-    c0, c1 = ln["rank_checksums"]
+    c0, c1 = ln["rank_checksums"]  # after the engine path's timed steps
     assert c0 == c1, (c0, c1)
     assert c0[1] > 0  # the grads are live
+    w0, w1 = ln["drop_in_wrapper"]["rank_checksums"]  # LoRA params after the wrapper path's steps too
+    assert w0 == w1, (w0, w1)
