@@ -1960,15 +1960,17 @@ SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus
 // 32-bit buffer offsets, and every work unit with enough main K-tiles for its program (plain: 4; the
 // dropout unit that carries the extension tiles: 3).  Returns OSPO_ERR_UNSUPPORTED otherwise (the caller
 // then runs the v5 kernel).  DBG 1 (ablation): no loads after the prologue.
-template <bool DROP, int DBG = 0, int V = 0>
+template <bool DROP, int DBG = 0, int V = 0, bool MX = false>
 int launch_w4(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
-  if (a.N % 256 || a.K % 64 || a.K2 % 64 || a.K2 > 128) return OSPO_ERR_UNSUPPORTED;
-  if ((long)a.M * a.lda * 2 >= (1L << 31) || (long)a.N * a.ldb * 2 >= (1L << 31)) return OSPO_ERR_UNSUPPORTED;
+  constexpr int EB = MX ? 1 : 2;
+  if (a.N % 256 || a.K % (MX ? 128 : 64) || a.K2 % 64 || a.K2 > 128) return OSPO_ERR_UNSUPPORTED;
+  if ((long)a.M * a.lda * EB >= (1L << 31) || (long)a.N * a.ldb * EB >= (1L << 31)) return OSPO_ERR_UNSUPPORTED;
   if (a.K2 > 0 && ((long)a.M * a.lda2 * 2 >= (1L << 31) || (long)a.N * a.ldb2 * 2 >= (1L << 31)))
     return OSPO_ERR_UNSUPPORTED;
+  if (MX && (!a.sa || !a.sb)) return OSPO_ERR_UNSUPPORTED;
   const int tm = (a.M + 255) / 256, tn = a.N / 256;
-  const int nt1 = a.K / 64, nt2 = a.K2 / 64, ntot = nt1 + nt2;
-  const SplitPlan pl = plan_split(a.M, a.N, ntot, a.K2, false, DROP, device_cus(), so.split, so.ws ? so.ws_bytes : 0,
+  const int nt1 = MX ? a.K / 128 : a.K / 64, nt2 = a.K2 / 64, ntot = nt1 + nt2;
+  const SplitPlan pl = plan_split(a.M, a.N, ntot, a.K2, MX, DROP, device_cus(), so.split, so.ws ? so.ws_bytes : 0,
                                   true);
   for (int z = 0; z < (pl.tail ? pl.split : 1); ++z) {  // every unit's program must fit (z = 0: the whole range)
     const int tb = pl.tail ? (int)((long)ntot * z / pl.split) : 0;
@@ -1979,8 +1981,8 @@ int launch_w4(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
   }
   if (pl.tail && ntot < 4) return OSPO_ERR_UNSUPPORTED;
   const int grid = pl.dp + pl.tail * pl.split;
-  hipLaunchKernelGGL((gemm_nt_w4_kernel<DROP, DBG, V>), dim3(grid), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split, so.ws,
-                     g_v5_gm);
+  hipLaunchKernelGGL((gemm_nt_w4_kernel<DROP, DBG, V, MX>), dim3(grid), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split,
+                     so.ws, g_v5_gm);
   OSPO_CHECK_LAUNCH();
   if (pl.tail) {
     hipLaunchKernelGGL(splitk_fixup_kernel, dim3(pl.tail * 32), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split,
@@ -2573,6 +2575,15 @@ int launch_mx(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
 #ifdef OSPO_ABLATION
   if (g_gemm_variant == 17) return launch_v5<0, DROP, true>(a, s, so);
   if (g_gemm_variant == 14) return launch_v5<0, DROP, true, 1>(a, s, so);
+  if constexpr (!DROP) {
+    // variant 52: the 4-wave hand-scheduled loop (w4_mx programs).  Bit-identical to SP8 under the same split
+    // (tools/w4mx_check.py) and within 1 % per shape alone, but the config-5 step ran 1.1 % slower with it
+    // (profiles/r04/w4mx_check.log, step_mx8_w4_ab.txt): not the default.
+    if (g_gemm_variant == 52) {
+      const int r = launch_w4<false, 0, 0, true>(a, s, so);
+      if (r != OSPO_ERR_UNSUPPORTED) return r;
+    }
+  }
 #endif
   return launch_v5<0, DROP, true, 8>(a, s, so);
 }
@@ -2634,7 +2645,7 @@ extern "C" int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb,
     case 30: { GemmArgs d = a; d.dbg = g_dbg_buf; return launch_v5<5, false, false, 8>(d, stream, so, false); }  // SP8 + phase stamps
     case 17: return launch_v5<0>(a, stream, so, true);                                   // 8-phase + split-K tail
     case 32: return launch_v6<false>(a, stream, so);                                  // persistent SP8 (v6, rejected)
-    case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48: case 49: case 50: case 51:
+    case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48: case 49: case 50: case 51: case 52:
       return launch_default<false>(a, stream, so);                                   // 4-wave hand-scheduled (w4)
     default: return launch_default<false>(a, stream, so);                            // w4 / SP8 + split-K tail
   }
@@ -2797,7 +2808,7 @@ extern "C" int ospo_set_gemm_variant(int v) {
     g_gemm_variant = 0;
     return OSPO_OK;
   }
-  if (v < 0 || (v > 32 && (v < 40 || v > 51)) || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23)
+  if (v < 0 || (v > 32 && (v < 40 || v > 52)) || (v > 5 && v < 10) || v == 20 || v == 21 || v == 22 || v == 23)
     return OSPO_ERR_ARG;
   g_v5_gm = 4;
   g_gemm_variant = v;

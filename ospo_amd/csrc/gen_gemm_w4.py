@@ -250,6 +250,211 @@ def prog_drop(E, noload=False):
     return p
 
 
+# ------------------------------------------------------------------------------------------------------
+# MXFP8 programs (gemm_nt_w4_kernel<.., MX = true>): main K-tiles of 128 e4m3 per row (the same 128-B LDS
+# rows as a bf16 K-tile) run 64 v_mfma_scale_f32_16x16x128_f8f6f4 per tile, one per 16 x 16 block; the
+# LoRA extension tiles (bf16) run 128 v_mfma_f32_16x16x32_bf16 as in the bf16 programs.  A fragment is the
+# lo (16-B chunk g) and hi (chunk 4 + g) halves of its 16 rows = the bf16 substep-0 and substep-1 fragments,
+# so both tile kinds share one read pattern and one register map:
+#   X_i = v[128 + 8 i .. +7] (B rows wn*128 + 16 i, srcA), Y_j = v[192 + 8 j .. +7] (A rows, srcB);
+#   E8M0 scale words sX0 v112, sX1 v113 (B blocks 2 wn, 2 wn + 1), sY0 v114, sY1 v115 (A blocks), byte
+#   (i & 3) / (j & 3) picked by op_sel / op_sel_hi.
+# With a whole tile of fragments in 128 VGPRs there is no room for a second copy, so the next tile's
+# fragments replace the current ones as they retire.  MFMA order: half 0 (X_0..3 x every Y_j), then half 1
+# (X_4..7 x every Y_j), so X_0..3 retire at MFMA 31, Y_j at 35 + 4 j, X_4..7 at 60..63:
+#   gaps 30..37: X_0..3 of tile t+1; 37 + 4 j: Y_j of t+1 (j < 7); gaps 1..10 of t+1: Y_7, X_4..7 and the
+#   scale words sX1 / sY1 of t+1 (sX0 at gap 33, sY0 at gap 50 of t: their last uses are 31 / 47).
+# Every read lands >= 2 MFMAs after the last use of its registers.  Barrier 1 (gap 11) frees tile t's stage
+# (its last reads were X_4..7 / scales at gaps 2..9); tile t+2's 16 pieces (+ 2 scale pieces) follow at
+# gaps 13..30; barrier 2 (gap 29) retires tile t+1's pieces (vmcnt = the t+2 pieces already issued).
+# Accumulation order per output element: main tiles in order, then the extension tiles (substep 0, 1) --
+# that of gemm_nt_v5_kernel<.., MX = true>, so the results are bit-identical to it.
+MX_MFMA = "v_mfma_scale_f32_16x16x128_f8f6f4"
+
+
+def XM(i, h=None):
+    b = 128 + 8 * i
+    return f"v[{b}:{b + 7}]" if h is None else f"v[{b + 4 * h}:{b + 4 * h + 3}]"
+
+
+def YM(j, h=None):
+    b = 192 + 8 * j
+    return f"v[{b}:{b + 7}]" if h is None else f"v[{b + 4 * h}:{b + 4 * h + 3}]"
+
+
+SX = ["v112", "v113"]
+SY = ["v114", "v115"]
+
+
+class ProgMX(Prog):
+    def __init__(self):
+        super().__init__(False, None)
+
+    def rd_frag(self, kind, idx, h):
+        reg = XM(idx, h) if kind == "X" else YM(idx, h)
+        base = ("%[rB" if kind == "X" else "%[rA") + f"{h}]"
+        off = 2048 * idx
+        self.emit(f"ds_read_b128 {reg}, {base}" + (f" offset:{off}" if off else ""))
+        self.lgkm.append(reg)
+
+    def rd_scale(self, kind, w):
+        reg = (SX if kind == "X" else SY)[w]
+        base = "%[rSX]" if kind == "X" else "%[rSY]"
+        self.emit(f"ds_read_b32 {reg}, {base}" + (" offset:256" if w else ""))
+        self.lgkm.append(reg)
+
+    def scale_piece(self, op):
+        """The E8M0 scale block of this wave (A: rows block m0/64 + wave; B: n0/64 + wave) of the tile two ahead:
+        one 4-B LDS-DMA per lane into the scale stage (M0 = %[sMS] (+1024 for B))."""
+        self.emit(f"s_add_u32 m0, %[sMS], {1024 if op == 'B' else 0}")
+        self.emit("s_nop 0")
+        self.emit(f"buffer_load_dword %[oS{op}], %[rsS{op}], %[sKS] offen sc1 lds")
+
+    @staticmethod
+    def order(kind):
+        """MFMA list of a tile: (i, j, h) with h = None (MX) or the bf16 substep."""
+        seq = []
+        for h in ([None] if kind == "x" else [0, 1]):
+            for half in (0, 1):
+                for j in range(8):
+                    for i in range(4 * half, 4 * half + 4):
+                        seq.append((i, j, h))
+        return seq
+
+    def tile(self, kind, first=False, load=None, load_kind=None, nxt=None, loop=None):
+        """kind 'x' (MX main tile) or 'b' (bf16 extension tile).  load: source of the tile two ahead ('m', 'e0',
+        'e1') or None, load_kind its kind; nxt: the next tile's kind (None: last tile)."""
+        seq = self.order(kind)
+        G = len(seq)
+        sc = 1 if kind == "x" else 2  # gap scale: the bf16 tile's last-use pattern sits in its substep 1
+        off = 0 if kind == "x" else 64
+        post = {k: [] for k in range(G)}
+        pre = {k: [] for k in range(G)}
+        if not first:  # Y_7, X_4..7 (and sX1 / sY1 for an MX tile) of THIS tile, from its stage: their registers
+            # retired with the previous tile's last MFMAs (>= 2 MFMAs back)
+            post[1].append(("frag", "Y", 7, 0))
+            post[2].append(("frag", "Y", 7, 1))
+            for n, i in enumerate(range(4, 8)):
+                post[3 + 2 * n].append(("frag", "X", i, 0))
+                post[4 + 2 * n].append(("frag", "X", i, 1))
+            if kind == "x":
+                post[2].append(("scale", "X", 1))
+                post[3].append(("scale", "Y", 1))
+        # barrier 1: this tile's stage is free (every wave's reads of it are done) -> tile t+2's pieces
+        if load is not None:
+            pre[11].append(("lgkm0",))
+            pre[11].append(("s_barrier",))
+        post[12].append(("v_xor_b32 %[rA0], %[tA0], %[rA0]",))
+        post[12].append(("v_xor_b32 %[rB0], %[tB0], %[rB0]",))
+        post[13].append(("v_xor_b32 %[rA1], %[tA1], %[rA1]",))
+        post[13].append(("v_xor_b32 %[rB1], %[tB1], %[rB1]",))
+        post[14].append(("v_xor_b32 %[rSX], %[tSX], %[rSX]",))
+        post[14].append(("v_xor_b32 %[rSY], %[tSY], %[rSY]",))
+        npieces = 0
+        if load is not None:
+            slots = list(range(13, 29))
+            for n, (op, k) in enumerate([("A", k) for k in range(8)] + [("B", k) for k in range(8)]):
+                post[slots[n] - 1].append(("m0", op, k))
+                post[slots[n]].append(("piece", op, k, load, False))
+            npieces = 16
+            if load_kind == "x":
+                post[29].append(("spiece", "A"))
+                post[30].append(("spiece", "B"))
+                post[31].append(("s_add_u32 %[sKS], %[sKS], 256",))
+            if load == "m":
+                post[31].append(("s_add_u32 %[sK], %[sK], 128",))
+            post[32].append(("s_xor_b32 %[sM], %[sM], %[sMT]",))
+            post[32].append(("s_xor_b32 %[sMS], %[sMS], %[sMST]",))
+        if nxt is not None:
+            # barrier 2: the next tile's pieces (issued during the previous tile) retired in every wave
+            pre[off + 29].append((f"s_waitcnt vmcnt({npieces})",))
+            pre[off + 29].append(("s_barrier",))
+            reads = {}
+            for i in range(4):  # X_0..3 of the next tile, after their last use (MFMA 28 + i)
+                reads.setdefault(off + 30 + 2 * i, []).append(("frag", "X", i, 0))
+                reads.setdefault(off + 31 + 2 * i, []).append(("frag", "X", i, 1))
+            for j in range(7):  # Y_j, after its last use 35 + 4 j
+                reads.setdefault(off + 37 + 4 * j, []).append(("frag", "Y", j, 0))
+                reads.setdefault(off + 38 + 4 * j, []).append(("frag", "Y", j, 1))
+            if nxt == "x":
+                reads.setdefault(off + 33, []).append(("scale", "X", 0))
+                reads.setdefault(off + 50, []).append(("scale", "Y", 0))
+            for k, its in reads.items():
+                post[k].extend(its)
+        for k, (i, j, h) in enumerate(seq):
+            for it in pre[k]:
+                self._item(it)
+            if h is None:
+                self.need({XM(i, 0), XM(i, 1), YM(j, 0), YM(j, 1), SX[i >> 2], SY[j >> 2]})
+                c = "0" if first else ACC(i, j)
+                bi, bj = i & 3, j & 3
+                self.emit(f"{MX_MFMA} {ACC(i, j)}, {XM(i)}, {YM(j)}, {c}, {SX[i >> 2]}, {SY[j >> 2]} "
+                          f"op_sel:[{bi & 1},{bj & 1},0] op_sel_hi:[{bi >> 1},{bj >> 1},0]")
+            else:
+                self.need({XM(i, h), YM(j, h)})
+                c = "0" if (first and h == 0) else ACC(i, j)
+                self.emit(f"{MFMA} {ACC(i, j)}, {XM(i, h)}, {YM(j, h)}, {c}")
+            for it in post[k]:
+                self._item(it)
+        if loop is not None:
+            self.emit("s_sub_u32 %[cnt], %[cnt], 1")
+            self.emit("s_cmp_lg_u32 %[cnt], 0")
+            self.emit(f"s_cbranch_scc1 {loop}")
+
+    def _item(self, it):
+        if it[0] == "frag":
+            self.rd_frag(it[1], it[2], it[3])
+        elif it[0] == "scale":
+            self.rd_scale(it[1], it[2])
+        elif it[0] == "spiece":
+            self.scale_piece(it[1])
+        else:
+            super()._item(it)
+
+    def prologue_mx(self):
+        """Tiles 0 and 1 (both main) into stages 0 / 1 with their scales; every fragment and scale word of
+        tile 0 read."""
+        self.emit("s_mov_b32 %[sSave], m0")
+        self.emit("s_nop 4")
+        for _ in range(2):
+            for op in "AB":
+                for k in range(8):
+                    self.piece(op, k, "m")
+            self.scale_piece("A")
+            self.scale_piece("B")
+            self.emit("s_add_u32 %[sK], %[sK], 128")
+            self.emit("s_add_u32 %[sKS], %[sKS], 256")
+            self.emit("s_xor_b32 %[sM], %[sM], %[sMT]")
+            self.emit("s_xor_b32 %[sMS], %[sMS], %[sMST]")
+        self.emit("s_waitcnt vmcnt(18)")
+        self.emit("s_barrier")
+        for i in range(8):
+            self.rd_frag("X", i, 0)
+            self.rd_frag("X", i, 1)
+        for j in range(8):
+            self.rd_frag("Y", j, 0)
+            self.rd_frag("Y", j, 1)
+        for w in range(2):
+            self.rd_scale("X", w)
+            self.rd_scale("Y", w)
+
+
+def prog_mx(E):
+    """MX main tiles (nm >= 4) then E bf16 extension tiles.  Loop over main tiles 1 .. nm-3."""
+    p = ProgMX()
+    p.prologue_mx()
+    p.tile("x", first=True, load="m", load_kind="x", nxt="x")
+    p.emit("L_w4mx_%=:")
+    p.tile("x", load="m", load_kind="x", nxt="x", loop="L_w4mx_%=")
+    seq = [("m", "x"), ("m", "x")] + [("e0", "b"), ("e1", "b")][:E]
+    for n in range(len(seq)):
+        ld = seq[n + 2] if n + 2 < len(seq) else None
+        nk = seq[n + 1][1] if n + 1 < len(seq) else None
+        p.tile(seq[n][1], load=ld[0] if ld else None, load_kind=ld[1] if ld else None, nxt=nk)
+    p.epilogue()
+    return p
+
+
 HEADER = """// GENERATED by gen_gemm_w4.py -- do not edit.  The hand-placed K-loop programs of gemm_nt_w4_kernel
 // (gemm_w4.h): see the generator's docstring for the schedule.
 """
@@ -267,6 +472,24 @@ def asm_fn(name, prog, drop):
         ins += [f'[mk{j}] "v"(o.mk[{j}])' for j in range(8)] + ['[dsc] "s"(o.dsc)']
     clob = ['"memory"', '"scc"'] + [f'"v{r}"' for r in (120, 121)] + [f'"v{r}"' for r in range(128, 256)] + \
         [f'"a{r}"' for r in range(256)]
+    body = "\n".join(f'      "{l}\\n"' for l in prog.lines)
+    return (f"__device__ __forceinline__ void {name}(W4Ops& o) {{\n  asm volatile(\n{body}\n"
+            f"      : {', '.join(outs)}\n      : {', '.join(ins)}\n      : {', '.join(clob)});\n}}\n")
+
+
+def asm_fn_mx(name, prog):
+    outs = ['[sSave] "=&s"(o.save)', '[cnt] "+s"(o.cnt)', '[sK] "+s"(o.sK)', '[sM] "+s"(o.sM)',
+            '[sKS] "+s"(o.sKS)', '[sMS] "+s"(o.sMS)',
+            '[rA0] "+v"(o.rA0)', '[rA1] "+v"(o.rA1)', '[rB0] "+v"(o.rB0)', '[rB1] "+v"(o.rB1)',
+            '[rSX] "+v"(o.rSX)', '[rSY] "+v"(o.rSY)']
+    ins = ['[rsA] "s"(o.rsA)', '[rsB] "s"(o.rsB)', '[rsA2] "s"(o.rsA2)', '[rsB2] "s"(o.rsB2)',
+           '[rsSA] "s"(o.rsSA)', '[rsSB] "s"(o.rsSB)',
+           '[sE1] "s"(o.sE1)', '[sMT] "s"(o.sMT)', '[sMST] "s"(o.sMST)',
+           '[tA0] "v"(o.tA0)', '[tA1] "v"(o.tA1)', '[tB0] "v"(o.tB0)', '[tB1] "v"(o.tB1)',
+           '[tSX] "v"(o.tSX)', '[tSY] "v"(o.tSY)', '[oSA] "v"(o.oSA)', '[oSB] "v"(o.oSB)']
+    ins += [f'[oA{k}] "v"(o.oA[{k}])' for k in range(8)] + [f'[oB{k}] "v"(o.oB[{k}])' for k in range(8)]
+    ins += [f'[eA{k}] "v"(o.eA[{k}])' for k in range(8)] + [f'[eB{k}] "v"(o.eB[{k}])' for k in range(8)]
+    clob = ['"memory"', '"scc"'] + [f'"v{r}"' for r in range(112, 256)] + [f'"a{r}"' for r in range(256)]
     body = "\n".join(f'      "{l}\\n"' for l in prog.lines)
     return (f"__device__ __forceinline__ void {name}(W4Ops& o) {{\n  asm volatile(\n{body}\n"
             f"      : {', '.join(outs)}\n      : {', '.join(ins)}\n      : {', '.join(clob)});\n}}\n")
@@ -325,6 +548,8 @@ def main(out):
         parts.append(asm_fn(f"w4_plain{E}", prog_plain(E), False))
     for E in (1, 2):
         parts.append(asm_fn(f"w4_drop{E}", prog_drop(E), True))
+    for E in (0, 1, 2):
+        parts.append(asm_fn_mx(f"w4_mx{E}", prog_mx(E)))
     parts.append("#ifdef OSPO_ABLATION\n// decomposition (results invalid): no LDS-DMA after the prologue\n")
     parts.append(asm_fn("w4_plain0_noload", prog_plain(0, noload=True), False))
     parts.append("// schedule variants for A/B (w4v<V>_plain<E>, bf16 without dropout)\n")
