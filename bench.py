@@ -144,6 +144,15 @@ def t2i_bytes_per_step(dims, R, T_keys):
     return 2.0 * (w + kv)
 
 
+def t2i_traffic(nbytes):
+    """roofline.traffic of the T2I line: nbytes x the decode kernels' measured / algorithmic byte ratio of the
+    committed counter pass (profiles/t2i_pmc.json), or None without one."""
+    f = os.path.join(ROOT, "profiles", "t2i_pmc.json")
+    if not os.path.exists(f):
+        return None
+    return round(nbytes * json.load(open(f))["traffic_ratio"])
+
+
 def bench_t2i(args):
     """BASELINE config 4: step-3 AR T2I sampling, Janus-Pro-7B, 576 tokens, cfg 5, parallel_size 16
     (32 cond/uncond rows), hipGraph-captured decode.  One 'step' = one generate() call."""
@@ -206,7 +215,10 @@ def bench_t2i(args):
                    "prompt_len_max": Lp, "decode_steps": N - 1, "tokens_per_s": round(value * N, 1),
                    "vq_decode_ms_per_batch": round(decode_ms, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
-                     "frac": round(achieved / 8000.0, 4), "traffic": None,
+                     "frac": round(achieved / 8000.0, 4), "traffic": t2i_traffic(nbytes) if gen.fused else None,
+                     "traffic_note": ("HBM+Infinity-Cache bytes per decode step: this step's algorithmic bytes x the "
+                                      "measured / algorithmic ratio of the decode kernels (2*FETCH_SIZE+WRITE_SIZE, "
+                                      "profiles/t2i_pmc.json, tools/t2i_pmc_summary.py)"),
                      "kernel": ("decode step (hipGraph: 30 x (4 decode_linear + attn_cache) + gen_head + sampler)"
                                 if gen.fused else
                                 "decode step (hipGraph: 30 x (4 decode_gemv + split sums + attn_cache + norms) + gen_head"
