@@ -491,9 +491,11 @@ int ospo_vq_to_uint8(const float* x, long n, unsigned char* out, hipStream_t str
  * compute_total_grad_norm (ospo/wrapper/train.py:459-469) + PL clip
  * (ospo/utils/train.py:30, gradient_clip_val) + torch AdamW
  * (train.py:108-115) on bf16 params with bf16 moments, fp32 grads.
- * sumsq_out[0] += sum(g^2) (fp32 atomics; caller zeroes).  adamw reads the
- * device-resident sumsq, so no host sync is needed; step is 1-based. */
-int ospo_sumsq(const float* g, long n, float* sumsq_out, hipStream_t stream);
+ * sumsq_out[0] += sum(g^2), summed in an order that depends on n only (bit-identical
+ * on every DP rank holding the same grads; caller zeroes); ws: device scratch of
+ * 2048 floats.  adamw reads the device-resident sumsq, so no host sync is needed;
+ * step is 1-based. */
+int ospo_sumsq(const float* g, long n, float* sumsq_out, float* ws, hipStream_t stream);
 int ospo_adamw_clip(void* params, const float* grads, void* exp_avg, void* exp_avg_sq, long n,
                     float lr, float beta1, float beta2, float eps, float weight_decay, int step,
                     const float* sumsq, float max_norm, hipStream_t stream);

@@ -91,7 +91,7 @@ SIGNATURES = {
     "ospo_vq_embed_codes": [P, L, P, I, I, P, P],
     "ospo_vq_conv2d_up2": [P, I, I, I, I, P, I, I, I, I, P, P, P, P],
     "ospo_vq_to_uint8": [P, L, P, P],
-    "ospo_sumsq": [P, L, P, P],
+    "ospo_sumsq": [P, L, P, P, P],
     "ospo_adamw_clip": [P, P, P, P, L, F, F, F, F, F, I, P, F, P],
 }
 

@@ -660,12 +660,24 @@ __global__ __launch_bounds__(256) void lora_pack8_kernel(const bf16* __restrict_
 }
 
 // ---------------------------------------------------------------- optimizer
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, long n, float* __restrict__ out) {
+// sum(g^2) in a fixed order: per-block partials over a grid that depends on n only, then one block sums them in
+// block order (fp32 atomics made the clip coefficient, and with it the bf16 AdamW update, differ between DP
+// ranks that hold bit-identical all-reduced grads)
+constexpr int SUMSQ_BLOCKS = 2048;
+__global__ __launch_bounds__(256) void sumsq_part_kernel(const float* __restrict__ g, long n, float* __restrict__ part) {
   __shared__ float red[4];
   float a = 0.f;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) a += g[i] * g[i];
   a = block_sum256(a, red);
-  if (threadIdx.x == 0) atomicAdd(out, a);
+  if (threadIdx.x == 0) part[blockIdx.x] = a;
+}
+__global__ __launch_bounds__(256) void sumsq_final_kernel(const float* __restrict__ part, int nb,
+                                                          float* __restrict__ out) {
+  __shared__ float red[4];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) a += part[i];
+  a = block_sum256(a, red);
+  if (threadIdx.x == 0) out[0] += a;
 }
 
 __global__ void adamw_kernel(bf16* __restrict__ p, const float* __restrict__ g, bf16* __restrict__ m,
@@ -1067,12 +1079,14 @@ extern "C" int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods,
   return OSPO_OK;
 }
 
-extern "C" int ospo_sumsq(const float* g, long n, float* out, hipStream_t st) {
-  if (!g || !out) return OSPO_ERR_ARG;
+extern "C" int ospo_sumsq(const float* g, long n, float* out, float* ws, hipStream_t st) {
+  if (!g || !out || !ws) return OSPO_ERR_ARG;
   if (n <= 0) return OSPO_ERR_SHAPE;
   long nb = (n + 255) / 256;
-  if (nb > 2048) nb = 2048;
-  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)nb), dim3(256), 0, st, g, n, out);
+  if (nb > SUMSQ_BLOCKS) nb = SUMSQ_BLOCKS;
+  hipLaunchKernelGGL(sumsq_part_kernel, dim3((unsigned)nb), dim3(256), 0, st, g, n, ws);
+  OSPO_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, (int)nb, out);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

@@ -146,6 +146,7 @@ class SimPOEngine:
         self.exp_avg_sq = torch.zeros(n, dtype=BF16, device=dev)
         self.opt_step = 0
         self._sumsq = torch.zeros(1, dtype=F32, device=dev)
+        self._sumsq_ws = torch.zeros(2048, dtype=F32, device=dev)
         # packed LoRA operands, per group contiguous over layers ([L][...], one pack launch per group)
         r = self.layout.r
         self._packed_all = {
@@ -715,7 +716,7 @@ class SimPOEngine:
     # ------------------------------------------------------------ optimizer
     def grad_norm_sq(self) -> torch.Tensor:
         self._sumsq.zero_()
-        ops.sumsq(self.grads, self._sumsq)
+        ops.sumsq(self.grads, self._sumsq, self._sumsq_ws)
         return self._sumsq
 
     def optimizer_step(self, lr=4e-5, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0, max_norm=1.0):

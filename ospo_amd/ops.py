@@ -624,8 +624,11 @@ def swiglu_lora_gdb(dh, gu, dgu, bt, u, out, dB, M, M_out, scale, ws=None):
 
 
 # -------------------------------------------------------------- optimizer
-def sumsq(g, out):
-    call("ospo_sumsq", _p(g), g.numel(), _p(out), _s())
+def sumsq(g, out, ws=None):
+    """out[0] += sum(g^2) in a fixed order (ws: 2048-float scratch, allocated here when None)."""
+    if ws is None:
+        ws = torch.empty(2048, dtype=torch.float32, device=g.device)
+    call("ospo_sumsq", _p(g), g.numel(), _p(out), _p(ws), _s())
 
 
 def adamw_clip(p, g, m, v, lr, beta1, beta2, eps, wd, step, sumsq_buf, max_norm):

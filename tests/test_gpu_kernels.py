@@ -786,6 +786,20 @@ def test_clip_adamw_matches_torch():
     assert (p != ref).float().mean().item() < 0.02
 
 
+def test_sumsq_deterministic():
+    """The grad-norm sum is summed in a fixed order: repeated calls give the same bits (DP ranks holding the
+    same all-reduced grads must clip by the same coefficient), within 1e-5 of the fp64 sum."""
+    g = torch.randn(4_700_001, device=DEV) * 0.05
+    outs = []
+    for _ in range(4):
+        ss = torch.zeros(1, device=DEV)
+        ops().sumsq(g, ss)
+        outs.append(ss.item())
+    assert len(set(outs)) == 1, outs
+    ref = float((g.double() ** 2).sum())
+    assert abs(outs[0] - ref) / ref < 1e-5
+
+
 @pytest.mark.parametrize("split", [2, 3, 4])
 def test_gemm_split_tail_equals_unsplit(split):
     """Split-K tail tiles (partials + fixup, RoPE and residual epilogues applied in the fixup) give the
