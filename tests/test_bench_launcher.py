@@ -43,3 +43,19 @@ def test_bench_single_process_default():
 def test_bench_rejects_gpus_world_mismatch():
     p = _run(["--gpus", "4", "--workload", "stub"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stderr + p.stdout)
+
+
+def test_t2i_traffic_field_from_committed_counter_pass():
+    """The t2i line's roofline.traffic = its algorithmic bytes x the committed counter pass's measured /
+    algorithmic ratio (profiles/t2i_pmc.json, written by tools/t2i_pmc_summary.py); the file's ratio is its own
+    measured / algorithmic bytes and the decode kernels it counted are all present."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pmc = json.load(open(os.path.join(ROOT, "profiles", "t2i_pmc.json")))
+    ratio = pmc["measured_bytes"] / pmc["algorithmic_bytes"]
+    assert abs(ratio - pmc["traffic_ratio"]) < 1e-4
+    assert 1.0 <= ratio < 2.0
+    assert {"dlin_kernel", "attn_cache2_kernel"} <= set(pmc["per_kernel"])
+    nbytes = 18_037_604_352
+    assert bench.t2i_traffic(nbytes) == round(nbytes * pmc["traffic_ratio"])
