@@ -75,6 +75,17 @@ def simpo_setup(layers=30, lora_r=16, pairs=4, text_len=24, img_tokens=576, lora
     return dims, eng, batches, weights
 
 
+def gemm_pmc_path(pairs, layers, lora_r, linear_dtype):
+    """The committed GEMM counter summary (tools/pmc_summary.py) of one bench configuration: roofline.traffic
+    is reported only from counter passes of the same configuration (round 5: the 8-pair and MXFP8 lines used to
+    carry the default line's bytes)."""
+    if (pairs, layers, lora_r, linear_dtype) == (4, 30, 16, "bf16"):
+        name = "gemm_pmc.json"
+    else:
+        name = f"gemm_pmc_{linear_dtype}_p{pairs}_r{lora_r}_l{layers}.json"
+    return os.path.join(ROOT, "profiles", name)
+
+
 def host_cpu_info():
     """(usable CPUs, host CPU count, CPU model).  Usable = the affinity mask, capped by the cgroup
     CPU quota when one is set (a GPU box shows the whole machine in os.cpu_count() but grants a
@@ -608,14 +619,16 @@ def main():
         d = kern[dom]
         achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "gemm_pmc.json")
+        pmc = gemm_pmc_path(B, dims.n_layers, dims.lora_r, args.linear_dtype)
         if os.path.exists(pmc):
             traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
         mx = dom.startswith("gemm_nt_mx8")
         peak = PEAK_FP8_TFLOPS if mx else PEAK_BF16_TFLOPS
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "traffic_note": "HBM+Infinity-Cache bytes per launch (2*FETCH_SIZE+WRITE_SIZE, profiles/gemm_pmc.json)",
+                "traffic_note": ("HBM+Infinity-Cache bytes per launch (2*FETCH_SIZE+WRITE_SIZE, "
+                                 f"{os.path.relpath(pmc, ROOT)}, counter passes of this configuration)"
+                                 if traffic is not None else "no counter pass of this configuration committed"),
                 "algorithmic_bytes_per_launch": round(d["bytes"] / d["count"]),
                 "kernel": (f"{dom} (gemm_nt_v5_kernel SP-schedule MFMA MXFP8 e4m3 + split-K fixup)" if mx else
                            f"{dom} (gemm_nt_w4_kernel: 4 waves, hand-placed asm K loop, MFMA bf16; + split-K fixup)"),

@@ -26,20 +26,28 @@ __device__ __forceinline__ float round_bf(float x) { return (float)(bf16)x; }
 // LoRA dropout mask (counter-based; ospo_amd/dropout.py restates it bit for bit):
 // element idx = row * ncols + col of the adapter input, kept iff drop_keep(idx) (below);
 // kept values become bf16(x / (1 - p)).
-// Round 4: three multiply-xorshift rounds on 24-bit multiplies (v_mul_u32_u24, full rate) instead of three
-// 32-bit ones (v_mul_lo_u32, quarter rate): the hash was the issue-bound LoRA u products' largest VALU cost.
-// The first xorshift folds the high half into the low 24 bits the first multiply reads (injective for
-// idx < 2^24 pairs, i.e. M * K < 2^25; beyond it distinct elements may share a hash, still uniform).
-// Statistics on a [4800, 4096] mask at p = 0.05 (tools/hash_stats.py): keep rate, both halves of a hash,
-// rows 1-64 and columns 2-256 apart all uncorrelated to within sampling noise, as the round-3 hash.
+// Multiply rounds on 24-bit multiplies (v_mad_u32_u24, full rate; a 32-bit v_mul_lo_u32 is quarter rate).
+// Round 5: every step is a bijection of all 32 bits, so the hash is a permutation of the pair index for each
+// seed and no two pairs of any mask (up to 2^32 pairs) share a hash.  The round-4 form multiplied only the low
+// 24 bits and dropped the top byte (x = (x & 0xFFFFFF) * c): pairs p and p ^ 0x01000100 collided for every
+// seed, so masks beyond 2^24 pairs (the down adapter's [4800, 11008] input) repeated ~36 % of themselves
+// ~3048 rows later.  drop_mix24 keeps the top byte: the low 24 bits of the result are lo24(x) * c mod 2^24
+// (c odd: invertible), and the top byte is recovered from them.  The seed enters after the first multiply
+// + xorshift rather than as idx ^ seed, so the masks of two seeds are not one table re-indexed by an XOR.
+// Statistics (tools/hash_stats.py): keep rate, both halves of a hash, row / column lags (incl. the old
+// collision lag), cross-seed re-indexing and single-bit avalanche all at sampling noise.
+__host__ __device__ __forceinline__ uint32_t drop_mix24(uint32_t x, uint32_t c) {
+  return (x & 0xFFFFFFu) * c + (x & 0xFF000000u);
+}
 __host__ __device__ __forceinline__ uint32_t drop_hash(uint32_t idx, uint32_t seed) {
-  uint32_t x = idx ^ seed;
+  uint32_t x = drop_mix24(idx, 0xED5AD5u);
   x ^= x >> 16;
-  x = (x & 0xFFFFFFu) * 0xED5AD5u;
+  x ^= seed;
+  x = drop_mix24(x, 0xAC4C1Bu);
   x ^= x >> 15;
-  x = (x & 0xFFFFFFu) * 0xAC4C1Bu;
+  x = drop_mix24(x, 0x9E3779u);
   x ^= x >> 13;
-  x = (x & 0xFFFFFFu) * 0x9E3779u;
+  x = drop_mix24(x, 0xC2B2AFu);
   x ^= x >> 16;
   return x;
 }

@@ -22,18 +22,24 @@ GROUP_IDS = {"qkv": 0, "o": 1, "gu": 2, "down": 3}
 _M32 = np.uint32(0xFFFFFFFF)
 
 
+def _mix24(x, c):
+    """common.h drop_mix24: lo24(x) * c + the top byte, a bijection of uint32 for odd c."""
+    return (x & np.uint32(0xFFFFFF)) * np.uint32(c) + (x & np.uint32(0xFF000000))
+
+
 def drop_hash(idx, seed):
-    """uint32 hash of element (pair) index idx (array) under seed (int), as on the device: three
-    multiply-xorshift rounds on 24-bit multiplies (common.h drop_hash, round 4)."""
-    m24 = np.uint32(0xFFFFFF)
+    """uint32 hash of element (pair) index idx (array) under seed (int), as on the device: four
+    multiply-xorshift rounds on 24-bit multiplies, each a 32-bit bijection, the seed keyed in after the
+    first (common.h drop_hash, round 5)."""
     with np.errstate(over="ignore"):
-        x = np.asarray(idx, dtype=np.uint32) ^ np.uint32(seed & 0xFFFFFFFF)
+        x = _mix24(np.asarray(idx, dtype=np.uint32), 0xED5AD5)
         x ^= x >> np.uint32(16)
-        x = (x & m24) * np.uint32(0xED5AD5)
+        x ^= np.uint32(seed & 0xFFFFFFFF)
+        x = _mix24(x, 0xAC4C1B)
         x ^= x >> np.uint32(15)
-        x = (x & m24) * np.uint32(0xAC4C1B)
+        x = _mix24(x, 0x9E3779)
         x ^= x >> np.uint32(13)
-        x = (x & m24) * np.uint32(0x9E3779)
+        x = _mix24(x, 0xC2B2AF)
         x ^= x >> np.uint32(16)
     return x
 

@@ -326,6 +326,53 @@ def test_dropout_hash_host_c_and_numpy_agree(lib):
     assert D.layer_seed(42, 1, 3, "gu") != D.layer_seed(42, 2, 3, "gu")
 
 
+def _unhash(h, seed):
+    """Inverse of dropout.drop_hash: undo each xorshift and each lo24(x) * c + top-byte multiply (the low 24
+    bits of the product are lo24(x) * c mod 2^24, c odd, so lo24(x) comes back with c's inverse mod 2^24)."""
+    import numpy as np
+
+    def unxorshift(y, s):
+        x = y.copy()
+        for _ in range(32 // s + 1):
+            x = y ^ (x >> np.uint32(s))
+        return x
+
+    def unmix(y, c):
+        cinv = pow(c, -1, 1 << 24)
+        lo = ((y & np.uint32(0xFFFFFF)).astype(np.uint64) * np.uint64(cinv)) & np.uint64(0xFFFFFF)
+        top = (y.astype(np.uint64) - lo * np.uint64(c)) & np.uint64(0xFF000000)
+        return (lo | top).astype(np.uint32)
+
+    x = np.asarray(h, dtype=np.uint32)
+    for c, s in ((0xC2B2AF, 16), (0x9E3779, 13), (0xAC4C1B, 15)):
+        x = unmix(unxorshift(x, s), c)
+    x = unxorshift(x ^ np.uint32(seed), 16)
+    return unmix(x, 0xED5AD5)
+
+
+def test_dropout_hash_is_a_permutation_no_shared_hashes():
+    """the round-4 hash multiplied only the low 24 bits, so pairs p and p ^ 0x01000100
+    shared a hash for every seed and the down adapter's [4800, 11008] mask (26.4 M pairs) repeated ~36 % of
+    itself.  Round 5: every step is a 32-bit bijection, so the hash permutes the pair index for each seed --
+    shown by an explicit inverse (random pairs and seeds) -- and no two pairs of the bench's largest mask
+    share a hash."""
+    import numpy as np
+    from ospo_amd import dropout as D
+    rng = np.random.default_rng(5)
+    for seed in (0, 1, D.layer_seed(42, 1, 29, "down"), int(rng.integers(0, 2 ** 32))):
+        x = rng.integers(0, 2 ** 32, 1 << 16, dtype=np.uint64).astype(np.uint32)
+        assert np.array_equal(_unhash(D.drop_hash(x, seed), seed), x)
+        p = np.arange(1 << 20, dtype=np.uint32)
+        assert not np.any(D.drop_hash(p, seed) == D.drop_hash(p ^ np.uint32(0x01000100), seed))
+    M, K = 4800, 11008  # the bench's down_proj adapter input
+    h = D.drop_hash(np.arange(M * K // 2, dtype=np.uint32), D.layer_seed(42, 1, 0, "down"))
+    assert np.unique(h).size == h.size
+    # the masks of two seeds are not one table re-indexed by an XOR of the seeds (the round-4 relation)
+    s1, s2 = D.layer_seed(42, 1, 0, "down"), D.layer_seed(42, 1, 1, "down")
+    i = np.arange(1 << 20, dtype=np.uint32)
+    assert (D.drop_hash(i, s1) == D.drop_hash(i ^ np.uint32(s1 ^ s2), s2)).mean() < 1e-4
+
+
 def test_checkpoint_keys_resolve_in_the_reference_module_tree(tmp_path):
     """What ospo/inference.py:268-281 consumes: config.yaml read with yaml.safe_load as get_lora_config
     (ospo/utils/model.py:74-89) reads it, and every adapter key of the .ckpt naming a Linear of the

@@ -3,7 +3,8 @@
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: on gfx950
 FETCH_SIZE reports half the bytes of 16-B/lane streaming reads; WRITE_SIZE is exact),
 FETCH/WRITE_SIZE in KiB.  The NT GEMM's split-K fixup launches are charged to the GEMM
-(the bench times them inside the same launch window).  Writes profiles/gemm_pmc.json."""
+(the bench times them inside the same launch window).  Writes profiles/gemm_pmc.json, or the file named by
+the second argument (round 5: one file per bench configuration, bench.gemm_pmc_path)."""
 import collections
 import csv
 import glob
@@ -13,6 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc_bench")
+dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles", "gemm_pmc.json")
 
 
 def load(tag):
@@ -62,5 +64,6 @@ for k in sorted(set(fetch) | set(write), key=lambda k: -(2 * fetch[k]["FETCH_SIZ
     n = max(nf[(k, "FETCH_SIZE")], 1)
     out.setdefault("per_kernel_MiB_per_launch", {})[short(k)[:60]] = round(
         (2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"]) / 1024 / n, 2)
-json.dump(out, open(os.path.join(ROOT, "profiles", "gemm_pmc.json"), "w"), indent=1)
+out["bench_args"] = os.environ.get("BENCH_ARGS", "")
+json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out, indent=1))

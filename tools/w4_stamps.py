@@ -1,7 +1,9 @@
 """Where a w4 GEMM workgroup's time goes, and the clock the chip holds under it: s_memtime (core clock)
 and s_memrealtime (100 MHz) stamps per workgroup (ablation variant 42): entry, program start, program end,
 epilogue stores drained.  In-kernel clock = d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md
-'DVFS give-back' item 6), after >= 2 s of back-to-back launches on random data."""
+'DVFS give-back' item 6), after >= 2 s of back-to-back launches on random data.
+Round 5 (verdict r4 item 3b): W4_DATA=zero runs the same launches on all-zero operands, so the clock on random
+vs zero data separates MFMA data energy from the staging traffic (which is the same for both)."""
 import os as _os
 _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
                                                      "ospo_amd", "libospo_hip_ablation.so"))
@@ -22,10 +24,13 @@ SHAPES = [("sq4096", 4096, 4096, 4096, 0), ("qkv_fwd", 4800, 12288, 4096, 64), (
 def main():
     torch.manual_seed(0)
     for name, m, n, k, k2 in SHAPES:
-        a = (torch.rand(m, k, device="cuda") * 2 - 1).bfloat16()
-        b = (torch.rand(n, k, device="cuda") * 2 - 1).bfloat16()
-        a2 = (torch.rand(m, k2, device="cuda") * 2 - 1).bfloat16() if k2 else None
-        b2 = (torch.rand(n, k2, device="cuda") * 2 - 1).bfloat16() if k2 else None
+        zero = _os.environ.get("W4_DATA", "random") == "zero"
+        fill = (lambda r, c: torch.zeros(r, c, device="cuda", dtype=torch.bfloat16)) if zero else \
+            (lambda r, c: (torch.rand(r, c, device="cuda") * 2 - 1).bfloat16())
+        a = fill(m, k)
+        b = fill(n, k)
+        a2 = fill(m, k2) if k2 else None
+        b2 = fill(n, k2) if k2 else None
         out = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
         grid = ((m + 255) // 256) * (n // 256) * 8  # generous: split-K pieces included
         dbg = torch.zeros(grid * 8, dtype=torch.int64, device="cuda")
@@ -51,7 +56,7 @@ def main():
         loop_us = rt[:, 2] - rt[:, 1]
         r0 = rt[:, 0].min()
         med = lambda x: round(float(np.median(x)), 2)  # noqa: E731
-        line = {"shape": name, "wgs": int(len(st)), "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
+        line = {"shape": name, "data": "zero" if zero else "random", "wgs": int(len(st)), "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
                 "span_us": round(rt[:, 5].max() - r0, 1),
                 "clock_ghz_p10_p50_p90": [round(float(np.percentile(clk, q)), 3) for q in (10, 50, 90)],
                 "setup_us_p50": med(rt[:, 1] - rt[:, 0]),
