@@ -525,6 +525,11 @@ def main():
     # A/B only: a GEMM schedule of the ablation library (OSPO_HIP_LIB=ospo_amd/libospo_hip_ablation.so), e.g.
     # 27 = the round-3 SP8 kernel; the product library has no such knob and refuses the flag
     ap.add_argument("--gemm-variant", type=int, default=None)
+    # DP determinism audit (verdict r4 item 6): per-rank checksums after EVERY step at the three stages of the
+    # update -- the all-reduced grads, the grad-norm sum of squares the clip coefficient comes from, the AdamW-
+    # updated params -- gathered at the end, so a rank mismatch names its first step and stage (adds device
+    # reductions per step: a test flag, not a bench setting)
+    ap.add_argument("--stage-checks", action="store_true")
     args = ap.parse_args()
     if args.gemm_variant is not None:
         from ospo_amd._lib import call
@@ -565,11 +570,17 @@ def main():
     timer = None if args.no_kernel_timer else ops.KernelTimer()
     first = {}
 
+    stage_log = []
+
     def step(i):
         out = train_step(eng, *batches[i % 4], cfg, buf, allreduce=allreduce)
         if not first:  # the first step's loss (fresh weights): tests/test_gpu_step.py reproduces it
             first["loss"] = out["loss"].clone()
             first["logps"] = out["logps"].clone()
+        if args.stage_checks:  # device scalars only: no host sync inside the loop
+            stage_log.append(torch.stack([eng.grads.double().sum(), eng.grads.double().abs().sum(),
+                                          eng._sumsq.double().sum(), eng.lora.double().sum(),
+                                          eng.lora.double().abs().sum()]))
         return out
 
     # per-launch HIP events on the last timed step only: an event pair around every GEMM costs ~1 %
@@ -594,6 +605,16 @@ def main():
     # the engine path's all-reduced grads and updated LoRA params must be identical on every rank (taken before
     # the wrapper sub-measurement, which steps the same engine and zeroes its grads)
     checks = rank_checks([eng.grads.double().sum(), eng.grads.double().abs().sum(), eng.lora.double().sum()])
+    stage_checks = None
+    if args.stage_checks and world > 1:
+        import torch.distributed as tdist
+        c = torch.stack(stage_log)  # [warmup + steps, 5]
+        c = c.cpu() if backend == "gloo" else c
+        every = [torch.zeros_like(c) for _ in range(world)]
+        tdist.all_gather(every, c)
+        stage_checks = {"stages": ["allreduced_grads_sum", "allreduced_grads_abs_sum", "grad_sumsq",
+                                   "adamw_params_sum", "adamw_params_abs_sum"],
+                        "per_rank": [e.cpu().tolist() for e in every]}
     wrap = None
     if not args.no_wrapper:  # the drop-in path on the same engine and box
         wm, ww, wopt, wsch, war, wb, wls = wrapper_setup(args, world, rank, dev, engine=eng)
@@ -650,6 +671,7 @@ def main():
         "loss": round(loss, 5),
         "loss_first_step": round(float(first["loss"].item()), 6),
         "rank_checksums": checks,
+        **({"stage_checksums": stage_checks} if stage_checks is not None else {}),
         "gemm_kernels": {k: {"count": v["count"], "ms": round(v["ms"], 2),
                              "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)} for k, v in kern.items()},
     }

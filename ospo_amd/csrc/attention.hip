@@ -840,11 +840,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 // a whole chip-wide round apart and re-read their tiles from HBM.  Blocks of a group come in order
 // 0 .. nb - 1 (callers put the longest sweep first).
 // gm = 0: block-major instead (every group's block 0 first, chip-wide: heaviest sweeps first, no L2 reuse).
+// gm >= 2 (round 5): banded -- each XCD walks its own groups in bands of gm groups, block-major (heaviest
+// first) within a band: a band's blocks share that XCD's L2 (a few bands resident at once), and only the last
+// band's light blocks make the tail (group-major ended on heavy blocks; block-major re-reads from HBM).
 __device__ __forceinline__ void group_major(int nb, int ngroups, int& grp, int& j, int gm = 1) {
   const int i = blockIdx.x;
   if (!gm) {
     j = i / ngroups;
     grp = i - j * ngroups;
+  } else if (gm >= 2 && (ngroups & 7) == 0) {
+    const int q = i >> 3, ng8 = ngroups >> 3;  // this XCD's q-th workgroup; its groups are 8 g + (i & 7)
+    const int band = q / (gm * nb), base = band * gm;
+    const int gc = min(gm, ng8 - base);         // groups in this band (the last band may be short)
+    const int r = q - base * nb;
+    j = r / gc;
+    grp = (base + (r - j * gc)) * 8 + (i & 7);
   } else if ((ngroups & 7) == 0) {
     const int q = i >> 3;
     grp = (q / nb) * 8 + (i & 7);

@@ -596,3 +596,14 @@ def test_trainer_gradient_accumulation_matches_pl(accum, tmp_path):
             g += w_.grad
         assert torch.allclose(wr.steps[s], g, rtol=1e-6), (s, wr.steps[s], g)
         w = (w.detach() - g).requires_grad_(True)
+
+
+def test_w4_k_loop_include_regenerates_byte_identical(tmp_path):
+    """The committed hand-placed K loop (ospo_amd/csrc/gemm_w4_asm.inc) is what gen_gemm_w4.py generates; the
+    Makefile regenerates it only on `make regen-w4` (never by mtime order after a checkout)."""
+    import subprocess
+    import sys
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ospo_amd", "csrc")
+    out = tmp_path / "w4.inc"
+    subprocess.run([sys.executable, os.path.join(csrc, "gen_gemm_w4.py"), str(out)], check=True, cwd=csrc)
+    assert out.read_bytes() == open(os.path.join(csrc, "gemm_w4_asm.inc"), "rb").read()

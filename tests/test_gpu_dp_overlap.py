@@ -110,7 +110,7 @@ def test_bench_two_ranks_gloo_share_one_gpu():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
-                        "--layers", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
+                        "--layers", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--stage-checks"],
                        capture_output=True, text=True, timeout=600, env=env, cwd=root)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -120,6 +120,14 @@ def test_bench_two_ranks_gloo_share_one_gpu():
     assert ln["n_gpus"] == 2 and ln["config"]["backend"] == "gloo" and ln["config"]["parallelism"] == "dp2"
     assert ln["config"]["pairs_per_gpu"] == 8 and ln["config"]["global_batch"] == 16
     assert ln["value"] > 0 and ln["loss"] == ln["loss"]
+    # staged checksums after every step (verdict r4 item 6): the first mismatch names its step and stage --
+    # all-reduced grads, the grad-norm sum of squares (the clip coefficient's input), the AdamW-updated params
+    st = ln["stage_checksums"]
+    r0, r1 = st["per_rank"]
+    assert len(r0) == 4  # warmup + steps
+    for i, (a, b) in enumerate(zip(r0, r1)):
+        for name, x, y in zip(st["stages"], a, b):
+            assert x == y, f"ranks differ first at step {i}, stage {name}: {x!r} vs {y!r}"
     c0, c1 = ln["rank_checksums"]  # after the engine path's timed steps
     assert c0 == c1, (c0, c1)
     assert c0[1] > 0  # the grads are live

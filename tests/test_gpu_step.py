@@ -255,9 +255,12 @@ def test_step_full_depth_7b_30_layers():
     assert el32 < max(1e-3, floor_l), (el32, floor_l)
     worst = max(ge, key=lambda k: ge[k] / fl[k])
     assert ge[worst] < GRAD_FLOOR_RATIO * fl[worst], (worst, ge[worst], fl[worst])
-    # (no fixed absolute cap at 30 layers: the oracle's own bf16 autograd sits 0.12-0.16 from fp32 there
-    # (layer 29 above any fixed 0.15), so the bound is that spread, per tensor above and over all here)
+    # the oracle's own bf16 autograd sits 0.12-0.16 from fp32 at 30 layers, so the bound is that spread, per
+    # tensor above and over all here; plus a fixed ceiling just above the measured HIP errors (0.107 / 0.124 /
+    # 0.145 for layers 0 / 15 / 29, profiles/r04/parity_suite_r4v.jsonl), so a kernel change that
+    # doubled the HIP error while staying under the spread would still fail
     assert max(ge.values()) < GRAD_FLOOR_RATIO * max(fl.values()), (max(ge.values()), max(fl.values()))
+    assert max(ge.values()) < 0.16, max(ge.values())
 
 
 def test_bench_config_first_step_vs_oracle():
@@ -345,9 +348,14 @@ def test_trajectory_five_steps_7b_shapes_two_layers_vs_oracle():
     own trajectory (oracle.simpo_step + clip_and_adamw: PL clip -> torch AdamW on the bf16 LoRA tensors,
     ospo/utils/train.py:30, ospo/wrapper/train.py:107-115), the HIP dropout masks of every step replayed.
     Run in bf16 (the reference's path) and in fp32 (the value both approximate).
-    Bounds: every step's loss within max(1e-3, 1.25x the bf16 oracle's own gap) of the fp32 trajectory;
-    the LoRA update after 5 steps (params - init, all tensors) at most 1.25x as far from the fp32
-    trajectory's update as the bf16 oracle's update is."""
+    Bounds (fixed): every step's loss within 2e-3 relative of the bf16 oracle's trajectory and of the fp32
+    one; the LoRA update after 5 steps (params - init, all tensors) at most 1.25x as far from the fp32
+    trajectory's update as the bf16 oracle's update is.
+    Round 5: each trajectory starts from its own copy of the weights.  Until round 4, ``v.to(torch.bfloat16)``
+    of the already-bf16 LoRA tensors returned the same tensors, the bf16 trajectory's AdamW updated the
+    weights in place, and the fp32 trajectory started from the bf16 trajectory's step-5 params: that, not
+    bf16 arithmetic, was the 2-11 % "bf16-vs-fp32 gap" (tools/traj_diag.py: 5e-4 at step 1 from the same
+    weights, profiles/r05/traj_diag_step1.log)."""
     import bench
     from ospo_amd.simpo import SimPOConfig, SimPOLossBuffers, train_step
     dims, eng, batches, w = bench.simpo_setup(layers=2)
@@ -374,7 +382,7 @@ def test_trajectory_five_steps_7b_shapes_two_layers_vs_oracle():
     init = {k: v.float() for k, v in wc.items() if ".lora_" in k}
 
     def trajectory(dt):
-        ww = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in wc.items()}
+        ww = {k: (v.to(dt).clone() if v.is_floating_point() else v) for k, v in wc.items()}
         params = {k: ww[k] for k in ww if ".lora_" in k}
         state, losses = {}, []
         for s in range(steps):
@@ -399,15 +407,13 @@ def test_trajectory_five_steps_7b_shapes_two_layers_vs_oracle():
                   update_rel_vs_bf16=e_upd16, oracle_bf16_update_vs_fp32=floor_upd,
                   update_norm_rel=float(d_hip.norm() / d32.norm()))
     e16 = [abs(a - b) / abs(b) for a, b in zip(hip_loss, l16)]
+    record_parity("trajectory_5steps_7b_2l_vs_bf16", loss_rel_vs_bf16=e16)
     for s in range(steps):
-        assert e_loss[s] < max(1e-3, GRAD_FLOOR_RATIO * gap[s]), (s, e_loss[s], gap[s])
-        # and the HIP path follows the reference's own bf16 trajectory far more closely than bf16 and fp32
-        # differ (measured 4.8e-4 .. 2.9e-3 against gaps of 2-11 %)
-        assert e16[s] < max(1e-3, 0.25 * gap[s]), (s, e16[s], gap[s])
+        assert e16[s] < 2e-3, (s, e16[s], gap[s])
+        assert e_loss[s] < 2e-3, (s, e_loss[s], gap[s])
     assert hip_loss[-1] != hip_loss[0]  # the adapters did train
     assert e_upd32 < GRAD_FLOOR_RATIO * floor_upd, (e_upd32, floor_upd)
-    # the update itself: 0.09 from the bf16 oracle's, against 0.57 between the bf16 and fp32 oracles
-    assert e_upd16 < 0.5 * floor_upd, (e_upd16, floor_upd)
+    assert e_upd16 < GRAD_FLOOR_RATIO * floor_upd, (e_upd16, floor_upd)
 
 
 def test_engine_optimizer_step_matches_torch_adamw():

@@ -212,3 +212,65 @@ def test_concatenated_forward_returns_full_logits(tmp_path):
         ref = O.gen_head(O.llama_hidden(cb["concatenated_inputs_embeds"], wts, dims, training=False), wts)
     got = torch.cat([cl, rl]).float().cpu()
     assert FX.rel_err(got, ref) < 2e-2  # bf16 logits of a bf16 path vs fp32
+
+
+def test_wrapper_shipped_config_16_pairs_r32_dropout_7b_widths_vs_oracle(tmp_path):
+    """The reference's shipped training configuration (configs/step5.yaml: dataset.train.batch_size 16 pairs
+    per process, LoRA r = 32 / alpha 64, lora_dropout 0.05; /root/reference/configs/step5.yaml:15,23) through
+    the drop-in path -- JanusProTrainWrapper.training_step + loss.backward -- at Janus-Pro-7B widths with 2
+    decoder layers: M = 32 x 600 = 19 200 rows (memory fit and the int32 offset guards at twice config 3's
+    per-GPU batch).  Against the oracle with the HIP dropout masks replayed: log-probs 1e-3 relative (north
+    star) vs the bf16 and the fp32 oracle, loss 1e-3 of the fp32 oracle, LoRA grads vs the fp32 oracle within
+    the 7B-shape tolerance."""
+    from oracle import simpo_ref as O
+    from ospo_amd.engine import synthetic_weights
+    from tests.test_gpu_step import _LazyMasks
+    cfg, model, dl, w = make(tmp_path, extra=[
+        "model.arch=janus-pro-7b", "model.override={'n_layers': 2}", "lora.lora_rank=32", "lora.lora_alpha=64",
+        "lora.lora_dropout=0.05", "dataset.train.batch_size=16"])
+    batch = next(iter(dl))
+    eng = w.engine
+    d = eng.dims
+    assert (d.d_model, d.d_ff, d.n_layers, d.lora_r) == (4096, 11008, 2, 32)
+    eng.zero_grad()
+    loss = w.training_step(batch, 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    pre = w.preprocess_batch(batch)
+    B = pre["chosen_ids"].shape[0]
+    assert B == 16 and eng.M == 32 * eng.T and eng.M >= 19_000
+    grads = {k: v.float().cpu() for k, v in eng.grad_tensors().items()}
+    loss = float(loss)
+    call, p, M, base = eng._drop_call, eng.lora_dropout, eng.M, eng._drop_base
+    wts = {k: v.cpu() for k, v in synthetic_weights(d, "cuda", seed=0, lora_seed=1).items()}  # get_model's seeds
+    # the engine's own log-probs of the same forward (training_step keeps no copy): re-run the forward with the
+    # same dropout call so the masks are the ones replayed below
+    eng._drop_call = call - 1
+    lp = eng.forward(pre["text_ids"], pre["chosen_ids"], pre["rejected_ids"]).float().cpu()
+    assert eng._drop_call == call
+    del model, w, eng
+    torch.cuda.empty_cache()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    dims = O.JanusDims(n_layers=d.n_layers, d_model=d.d_model, d_ff=d.d_ff, n_heads=d.n_heads, head_dim=d.head_dim,
+                       vocab=d.vocab, img_vocab=d.img_vocab, img_embed=d.img_embed, gen_head_dim=d.gen_head_dim,
+                       lora_r=d.lora_r, lora_alpha=d.lora_alpha, lora_dropout=p)
+    masks = _LazyMasks(M, {"qkv": d.d_model, "o": d.d_model, "gu": d.d_model, "down": d.d_ff}, base, call, p)
+    text = [t.to(torch.int32) for t in batch[1]]
+    ch, rj = pre["chosen_ids"].cpu().long(), pre["rejected_ids"].cpu().long()
+    o16 = O.simpo_step(text, ch, rj, wts, dims, dtype=torch.bfloat16, backward=False, dropout_masks=masks)
+    o32 = O.simpo_step(text, ch, rj, wts, dims, dtype=torch.float32, dropout_masks=masks)
+    rel = FX.rel_err
+    e16 = max(rel(lp[:B], o16.chosen_logps), rel(lp[B:], o16.rejected_logps))
+    e32 = max(rel(lp[:B], o32.chosen_logps), rel(lp[B:], o32.rejected_logps))
+    l32 = float(o32.loss)
+    el32, floor_l = abs(loss - l32) / l32, abs(float(o16.loss) - l32) / l32
+    g32 = max(rel(grads[k], o32.lora_grads[k]) for k in o32.lora_grads)
+    from tests.conftest import record_parity
+    record_parity("wrapper_shipped_config_16_pairs_r32_7b_2l", logp=e16, logp_vs_fp32=e32, loss=loss,
+                  loss_bf16_oracle=float(o16.loss), loss_fp32_oracle=l32, loss_vs_fp32=el32,
+                  oracle_bf16_vs_fp32_loss=floor_l, grad_vs_fp32=g32, rows=M)
+    print(f"\nshipped config (16 pairs, r=32, dropout 0.05, 7B widths, 2 layers, M={M}): logp {e16:.2e} "
+          f"(fp32 {e32:.2e}), loss {loss:.6f} vs fp32 {l32:.6f} ({el32:.2e}), grads vs fp32 {g32:.2e}")
+    assert e16 < 1e-3 and e32 < 1e-3
+    assert el32 < max(1e-3, floor_l), (el32, floor_l)
+    assert g32 < 6.5e-2, g32
