@@ -31,23 +31,24 @@ __device__ __forceinline__ float round_bf(float x) { return (float)(bf16)x; }
 // seed and no two pairs of any mask (up to 2^32 pairs) share a hash.  The round-4 form multiplied only the low
 // 24 bits and dropped the top byte (x = (x & 0xFFFFFF) * c): pairs p and p ^ 0x01000100 collided for every
 // seed, so masks beyond 2^24 pairs (the down adapter's [4800, 11008] input) repeated ~36 % of themselves
-// ~3048 rows later.  drop_mix24 keeps the top byte: the low 24 bits of the result are lo24(x) * c mod 2^24
-// (c odd: invertible), and the top byte is recovered from them.  The seed enters after the first multiply
-// + xorshift rather than as idx ^ seed, so the masks of two seeds are not one table re-indexed by an XOR.
-// Statistics (tools/hash_stats.py): keep rate, both halves of a hash, row / column lags (incl. the old
-// collision lag), cross-seed re-indexing and single-bit avalanche all at sampling noise.
-__host__ __device__ __forceinline__ uint32_t drop_mix24(uint32_t x, uint32_t c) {
-  return (x & 0xFFFFFFu) * c + (x & 0xFF000000u);
+// ~3048 rows later.  A round is now x + lo24(x) * c with c even -- ONE v_mad_u32_u24 (x, c, x), as cheap as the
+// old multiply: the low 24 bits of the result are lo24(x) * (c + 1) mod 2^24 (c + 1 odd: invertible), and
+// x = result - lo24(x) * c recovers the top byte.  The seed enters after the first multiply + xorshift rather
+// than as idx ^ seed, so the masks of two seeds are not one table re-indexed by an XOR.  Statistics
+// (tools/hash_stats.py 'h6'): keep rate, both halves of a hash, row / column lags (incl. the old collision
+// lag), cross-seed re-indexing and single-bit avalanche all at sampling noise.
+__host__ __device__ __forceinline__ uint32_t drop_mad24(uint32_t x, uint32_t c) {
+  return (x & 0xFFFFFFu) * c + x;
 }
 __host__ __device__ __forceinline__ uint32_t drop_hash(uint32_t idx, uint32_t seed) {
-  uint32_t x = drop_mix24(idx, 0xED5AD5u);
+  uint32_t x = drop_mad24(idx, 0xED5AD4u);
   x ^= x >> 16;
   x ^= seed;
-  x = drop_mix24(x, 0xAC4C1Bu);
+  x = drop_mad24(x, 0xAC4C1Au);
   x ^= x >> 15;
-  x = drop_mix24(x, 0x9E3779u);
+  x = drop_mad24(x, 0x9E3778u);
   x ^= x >> 13;
-  x = drop_mix24(x, 0xC2B2AFu);
+  x = drop_mad24(x, 0xC2B2AEu);
   x ^= x >> 16;
   return x;
 }

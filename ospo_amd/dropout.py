@@ -22,9 +22,9 @@ GROUP_IDS = {"qkv": 0, "o": 1, "gu": 2, "down": 3}
 _M32 = np.uint32(0xFFFFFFFF)
 
 
-def _mix24(x, c):
-    """common.h drop_mix24: lo24(x) * c + the top byte, a bijection of uint32 for odd c."""
-    return (x & np.uint32(0xFFFFFF)) * np.uint32(c) + (x & np.uint32(0xFF000000))
+def _mad24(x, c):
+    """common.h drop_mad24: x + lo24(x) * c (c even), a bijection of uint32 (one v_mad_u32_u24)."""
+    return (x & np.uint32(0xFFFFFF)) * np.uint32(c) + x
 
 
 def drop_hash(idx, seed):
@@ -32,14 +32,14 @@ def drop_hash(idx, seed):
     multiply-xorshift rounds on 24-bit multiplies, each a 32-bit bijection, the seed keyed in after the
     first (common.h drop_hash, round 5)."""
     with np.errstate(over="ignore"):
-        x = _mix24(np.asarray(idx, dtype=np.uint32), 0xED5AD5)
+        x = _mad24(np.asarray(idx, dtype=np.uint32), 0xED5AD4)
         x ^= x >> np.uint32(16)
         x ^= np.uint32(seed & 0xFFFFFFFF)
-        x = _mix24(x, 0xAC4C1B)
+        x = _mad24(x, 0xAC4C1A)
         x ^= x >> np.uint32(15)
-        x = _mix24(x, 0x9E3779)
+        x = _mad24(x, 0x9E3778)
         x ^= x >> np.uint32(13)
-        x = _mix24(x, 0xC2B2AF)
+        x = _mad24(x, 0xC2B2AE)
         x ^= x >> np.uint32(16)
     return x
 

@@ -327,8 +327,9 @@ def test_dropout_hash_host_c_and_numpy_agree(lib):
 
 
 def _unhash(h, seed):
-    """Inverse of dropout.drop_hash: undo each xorshift and each lo24(x) * c + top-byte multiply (the low 24
-    bits of the product are lo24(x) * c mod 2^24, c odd, so lo24(x) comes back with c's inverse mod 2^24)."""
+    """Inverse of dropout.drop_hash: undo each xorshift and each x + lo24(x) * c round (the low 24 bits of the
+    result are lo24(x) * (c + 1) mod 2^24, c + 1 odd, so lo24(x) comes back with its inverse mod 2^24, and then
+    x = result - lo24(x) * c)."""
     import numpy as np
 
     def unxorshift(y, s):
@@ -337,17 +338,16 @@ def _unhash(h, seed):
             x = y ^ (x >> np.uint32(s))
         return x
 
-    def unmix(y, c):
-        cinv = pow(c, -1, 1 << 24)
+    def unmad(y, c):
+        cinv = pow(c + 1, -1, 1 << 24)
         lo = ((y & np.uint32(0xFFFFFF)).astype(np.uint64) * np.uint64(cinv)) & np.uint64(0xFFFFFF)
-        top = (y.astype(np.uint64) - lo * np.uint64(c)) & np.uint64(0xFF000000)
-        return (lo | top).astype(np.uint32)
+        return ((y.astype(np.uint64) - lo * np.uint64(c)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
 
     x = np.asarray(h, dtype=np.uint32)
-    for c, s in ((0xC2B2AF, 16), (0x9E3779, 13), (0xAC4C1B, 15)):
-        x = unmix(unxorshift(x, s), c)
+    for c, s in ((0xC2B2AE, 16), (0x9E3778, 13), (0xAC4C1A, 15)):
+        x = unmad(unxorshift(x, s), c)
     x = unxorshift(x ^ np.uint32(seed), 16)
-    return unmix(x, 0xED5AD5)
+    return unmad(x, 0xED5AD4)
 
 
 def test_dropout_hash_is_a_permutation_no_shared_hashes():

@@ -2,8 +2,9 @@
 
 Round 5: the round-4 hash ('h3') multiplied only the low 24 bits of its state and dropped
 the top byte, so pair indices p and p ^ 0x01000100 collide for every seed, and for two seeds
-h(p, s1) = h(p ^ s1 ^ s2, s2).  'h4' (3 rounds) and 'h5' (4 rounds, the round-5 hash) keep every step a
-32-bit bijection (drop_mix24 = lo24(x) * c + top byte) and key the seed in after the first round.
+h(p, s1) = h(p ^ s1 ^ s2, s2).  'h4' (3 rounds) and 'h5' (4 rounds) keep every step a 32-bit bijection
+(lo24(x) * c + top byte: v_and + v_mad_u32_u24 per round) and key the seed in after the first round; 'h6', the
+round-5 hash, has h5's structure with each round x + lo24(x) * c (c even), one v_mad_u32_u24 (x, c, x).
 
 Per hash, on [4800, 4096] (the q|k|v / o / gate|up inputs) and [4800, 11008] (the down input, 26.4 M pairs,
 beyond 2^24) masks at p = 0.05 and 4 seeds, worst |value| x 1e-4 (sampling noise ~2.3e-4 / ~1.4e-4):
@@ -16,6 +17,8 @@ beyond 2^24) masks at p = 0.05 and 4 seeds, worst |value| x 1e-4 (sampling noise
   aval    worst |P(output bit j flips when input bit i flips) - 0.5| over random inputs (x 1e-4)
   uniq    distinct hashes / pairs of the [4800, 11008] mask (1 = no two pairs share a hash)
 """
+import sys
+
 import numpy as np
 
 
@@ -52,8 +55,23 @@ def h4(i, s):  # 3 rounds
     return _hk(i, s, ((0xAC4C1B, 15), (0x9E3779, 16)))
 
 
-def h5(i, s):  # 4 rounds: the round-5 hash (common.h drop_hash)
+def h5(i, s):  # 4 rounds, lo24(x) * c + top byte (and + mad per round)
     return _hk(i, s, ((0xAC4C1B, 15), (0x9E3779, 13), (0xC2B2AF, 16)))
+
+
+def madself(x, c):  # x + lo24(x) * c, c even: one v_mad_u32_u24 (x, c, x); bijective since c + 1 is odd
+    return (x & np.uint32(0xFFFFFF)) * np.uint32(c) + x
+
+
+def h6(i, s):  # the round-5 hash (common.h drop_hash): h5's rounds as one mad each
+    with np.errstate(over="ignore"):
+        x = madself(i.astype(np.uint32), 0xED5AD4)
+        x ^= x >> np.uint32(16)
+        x ^= np.uint32(s)
+        for c, sh in ((0xAC4C1A, 15), (0x9E3778, 13), (0xC2B2AE, 16)):
+            x = madself(x, c)
+            x ^= x >> np.uint32(sh)
+    return x
 
 
 def keep(h, thr):
@@ -106,7 +124,7 @@ def main():
     rng = np.random.default_rng(0)
     p = 0.05
     thr = int(p * 65536)
-    for name, f in (("h3", h3), ("h4", h4), ("h5", h5)):
+    for name, f in ((a, globals()[a]) for a in (sys.argv[1:] or ("h3", "h4", "h5", "h6"))):
         for M, K in ((4800, 4096), (4800, 11008)):
             w = stats(f, M, K, rng, thr, p)
             print(name, f"[{M},{K}]", " ".join(f"{k}:{v * 1e4:.1f}" for k, v in w.items()), "(x1e-4)")
