@@ -256,11 +256,42 @@ __device__ __forceinline__ void store_rows16(const f32x4 (&v)[8], char* scr, bf1
 
 // ============================================================== forward ====
 // SPR (ablation): the next tile's K pieces issued after this tile's S MFMAs, its V pieces after the softmax
+// 1-D grid -> (group = s * H + h, block j of nb).  Workgroup i is dispatched to XCD i % 8, so with
+// this map the nb blocks of a group run back to back on ONE XCD and the group's operands (re-read by
+// every block) stay in that XCD's L2; with the (head, sequence, block) grid the blocks of a group were
+// a whole chip-wide round apart and re-read their tiles from HBM.  Blocks of a group come in order
+// 0 .. nb - 1 (callers put the longest sweep first).
+// gm = 0: block-major instead (every group's block 0 first, chip-wide: heaviest sweeps first, no L2 reuse).
+// gm >= 2 (round 5): banded -- each XCD walks its own groups in bands of gm groups, block-major (heaviest
+// first) within a band: a band's blocks share that XCD's L2 (a few bands resident at once), and only the last
+// band's light blocks make the tail (group-major ended on heavy blocks; block-major re-reads from HBM).
+__device__ __forceinline__ void group_major(int nb, int ngroups, int& grp, int& j, int gm = 1) {
+  const int i = blockIdx.x;
+  if (!gm) {
+    j = i / ngroups;
+    grp = i - j * ngroups;
+  } else if (gm >= 2 && (ngroups & 7) == 0) {
+    const int q = i >> 3, ng8 = ngroups >> 3;  // this XCD's q-th workgroup; its groups are 8 g + (i & 7)
+    const int band = q / (gm * nb), base = band * gm;
+    const int gc = min(gm, ng8 - base);         // groups in this band (the last band may be short)
+    const int r = q - base * nb;
+    j = r / gc;
+    grp = (base + (r - j * gc)) * 8 + (i & 7);
+  } else if ((ngroups & 7) == 0) {
+    const int q = i >> 3;
+    grp = (q / nb) * 8 + (i & 7);
+    j = q - (q / nb) * nb;
+  } else {
+    grp = i / nb;
+    j = i - grp * nb;
+  }
+}
+
 template <int NW, int DBG = 0, bool MXO = false, bool SPR = false>  // MXO: also the MXFP8 copy of O (config 5)
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc,
                                                        bf16* __restrict__ out, int ldo, float* __restrict__ lse,
                                                        int T, int H, float scale,
-                                                       const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0}) {
+                                                       const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0}, int gm = 0) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -523,14 +554,26 @@ __device__ __forceinline__ void fwd_pv(const uint32_t (&va)[8], uint32_t boff, c
 template <bool MXO = false, bool PIPE = false, int DBG = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd2_kernel(
     const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, bf16* __restrict__ out, int ldo,
-    float* __restrict__ lse, int T, int H, float scale, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0}) {
+    float* __restrict__ lse, int T, int H, float scale, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0},
+    int gm = 0) {
   constexpr int NW = 4, RB = 128;
   // PIPE: K0 K1 V0 V1; else K0 V0 K1 V1 (a tile's K and V side by side)
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int qb = gridDim.z - 1 - blockIdx.z;  // heaviest blocks first (LPT), as attn_fwd_kernel
-  const int h = blockIdx.x, s = blockIdx.y;
+  int qb, h, s;
+  if (gm >= 2) {  // 1-D grid, banded (round 5, group_major): a band's (sequence, head) K / V stay in its XCD's L2
+    const int nqb = (T + RB - 1) / RB;
+    int grp, j;
+    group_major(nqb, gridDim.x / nqb, grp, j, gm);
+    qb = nqb - 1 - j;  // heaviest first within the band
+    h = grp % H;
+    s = grp / H;
+  } else {
+    qb = gridDim.z - 1 - blockIdx.z;  // heaviest blocks first (LPT), as attn_fwd_kernel
+    h = blockIdx.x;
+    s = blockIdx.y;
+  }
   const int g = lane >> 4, l16 = lane & 15;
   const long rowbase = (long)s * T;
 
@@ -831,37 +874,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       *reinterpret_cast<uint2*>(kp + 16 * dt + 4 * g) = a;
       *reinterpret_cast<uint2*>(vp + 16 * dt + 4 * g) = b;
     }
-  }
-}
-
-// 1-D grid -> (group = s * H + h, block j of nb).  Workgroup i is dispatched to XCD i % 8, so with
-// this map the nb blocks of a group run back to back on ONE XCD and the group's operands (re-read by
-// every block) stay in that XCD's L2; with the (head, sequence, block) grid the blocks of a group were
-// a whole chip-wide round apart and re-read their tiles from HBM.  Blocks of a group come in order
-// 0 .. nb - 1 (callers put the longest sweep first).
-// gm = 0: block-major instead (every group's block 0 first, chip-wide: heaviest sweeps first, no L2 reuse).
-// gm >= 2 (round 5): banded -- each XCD walks its own groups in bands of gm groups, block-major (heaviest
-// first) within a band: a band's blocks share that XCD's L2 (a few bands resident at once), and only the last
-// band's light blocks make the tail (group-major ended on heavy blocks; block-major re-reads from HBM).
-__device__ __forceinline__ void group_major(int nb, int ngroups, int& grp, int& j, int gm = 1) {
-  const int i = blockIdx.x;
-  if (!gm) {
-    j = i / ngroups;
-    grp = i - j * ngroups;
-  } else if (gm >= 2 && (ngroups & 7) == 0) {
-    const int q = i >> 3, ng8 = ngroups >> 3;  // this XCD's q-th workgroup; its groups are 8 g + (i & 7)
-    const int band = q / (gm * nb), base = band * gm;
-    const int gc = min(gm, ng8 - base);         // groups in this band (the last band may be short)
-    const int r = q - base * nb;
-    j = r / gc;
-    grp = (base + (r - j * gc)) * 8 + (i & 7);
-  } else if ((ngroups & 7) == 0) {
-    const int q = i >> 3;
-    grp = (q / nb) * 8 + (i & 7);
-    j = q - (q / nb) * nb;
-  } else {
-    grp = i / nb;
-    j = i - grp * nb;
   }
 }
 
@@ -1796,8 +1808,15 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
 #endif
   const int rb = nw == 4 && kfn != attn_fwd_kernel<4, 0> ? 128 : 16 * nw;
   dim3 grid(n_heads, S, (T + rb - 1) / rb);
+  int order_fwd = 0;  // 0: (head, sequence, block) grid, heaviest blocks first chip-wide; >= 2: banded 1-D grid
+#ifdef OSPO_ABLATION
+  if (const char* e = getenv("OSPO_ATTN_ORDER_FWD")) order_fwd = atoi(e);
+#endif
+  if (order_fwd >= 2 && nw == 4 && rb == 128 && (S * n_heads) % 8 == 0)  // attn_fwd2_kernel only
+    grid = dim3(n_heads * S * ((T + rb - 1) / rb));
+  else order_fwd = 0;
   hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
-                     (bf16*)o, ld_o, lse, T, n_heads, scale, mo);
+                     (bf16*)o, ld_o, lse, T, n_heads, scale, mo, order_fwd);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

@@ -143,6 +143,7 @@ struct GemmArgs {
   // LoRA dropout backward with the forward's keep bits (ospo_lora_skinny keep_bits, [M][drop_ld / 8] bytes)
   // instead of re-hashing the mask: the v5 kernel stages the tile's 256 x 32-B block into LDS with tile 0
   const uint8_t* drop_bits = nullptr;
+  int epi_var = 0;  // ablation build (OSPO_GEMM_EPI): plain-epilogue store variants, see epi_plain_var
 };
 
 // the SwiGLU-backward store of 8 product columns (row m, columns n..n+7 of F = args.N)
@@ -932,6 +933,35 @@ __device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0
 // tiles stay bf16 (16 bf16 MFMAs per phase).
 // bf16 epilogue, second half: the tile's rounded products staged in LDS as [256][CPITCH] rows ->
 // RoPE / residual -> 16-B coalesced global stores (shared by the 256x256 kernels)
+#ifdef OSPO_ABLATION
+// Ablation (round 5): the plain epilogue (no residual, no RoPE) with BATCH LDS reads in flight before their
+// stores, and optionally non-temporal stores.  Same values and addresses as epi_rows: bit-identical output.
+template <int NTHR, int BATCH, bool NTS>
+__device__ __forceinline__ void epi_plain_var(const GemmArgs& args, const char* smem, int m0, int n0, int tid) {
+  constexpr int BM = 256, BN = 256, CPITCH = BN * 2 + 16, CPR = BN / 8, ITERS = BM * CPR / NTHR;
+  bf16* C = reinterpret_cast<bf16*>(args.C);
+#pragma unroll 1
+  for (int b0 = 0; b0 < ITERS; b0 += BATCH) {
+    u32x4 v[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int c = tid + (b0 + u) * NTHR;
+      v[u] = *reinterpret_cast<const u32x4*>(smem + (c / CPR) * CPITCH + (c % CPR) * 16);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int c = tid + (b0 + u) * NTHR;
+      const int m = m0 + c / CPR;
+      u32x4* dst = reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + (c % CPR) * 8);
+      if (m < args.M) {
+        if constexpr (NTS) __builtin_nontemporal_store(v[u], dst);
+        else *dst = v[u];
+      }
+    }
+  }
+}
+#endif
+
 template <int NTHR>
 __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem, int m0, int n0) {
   constexpr int BM = 256, BN = 256, CPITCH = BN * 2 + 16;
@@ -957,6 +987,17 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem,
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid), "+v"(m0), "+v"(n0));
   const bool rope_tile = n0 < args.rope_cols;  // (rope_cols % 128 == 0: a chunk's partner is in the tile)
+#ifdef OSPO_ABLATION
+  if (args.epi_var && !rope_tile && !args.res) {
+    switch (args.epi_var) {
+      case 1: epi_plain_var<NTHR, 8, false>(args, smem, m0, n0, tid); return;
+      case 2: epi_plain_var<NTHR, 4, true>(args, smem, m0, n0, tid); return;
+      case 3: epi_plain_var<NTHR, 8, true>(args, smem, m0, n0, tid); return;
+      case 4: epi_plain_var<NTHR, 16, false>(args, smem, m0, n0, tid); return;
+      default: epi_plain_var<NTHR, 4, false>(args, smem, m0, n0, tid); return;
+    }
+  }
+#endif
   if (rope_tile && !args.res) {
     // RoPE tiles: one thread per (row, head, 8-column group j < 8) computes BOTH outputs of the rotate-half
     // pair -- columns 8j.. and 64 + 8j.. -- from one unpack of x1, x2 and of the shared cos / sin entry
@@ -1961,7 +2002,13 @@ SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus
 // dropout unit that carries the extension tiles: 3).  Returns OSPO_ERR_UNSUPPORTED otherwise (the caller
 // then runs the v5 kernel).  DBG 1 (ablation): no loads after the prologue.
 template <bool DROP, int DBG = 0, int V = 0, bool MX = false>
-int launch_w4(const GemmArgs& a, hipStream_t s, const SplitOpts& so) {
+int launch_w4(const GemmArgs& a_in, hipStream_t s, const SplitOpts& so) {
+#ifdef OSPO_ABLATION
+  GemmArgs a = a_in;
+  if (const char* e = getenv("OSPO_GEMM_EPI")) a.epi_var = atoi(e);  // A/B: plain-epilogue store variants
+#else
+  const GemmArgs& a = a_in;
+#endif
   constexpr int EB = MX ? 1 : 2;
   if (a.N % 256 || a.K % (MX ? 128 : 64) || a.K2 % 64 || a.K2 > 128) return OSPO_ERR_UNSUPPORTED;
   if ((long)a.M * a.lda * EB >= (1L << 31) || (long)a.N * a.ldb * EB >= (1L << 31)) return OSPO_ERR_UNSUPPORTED;

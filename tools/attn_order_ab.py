@@ -76,6 +76,36 @@ def main():
         print(json.dumps({"order_dkdv": c[0], "order_dq": c[1], "bwd5_us_median": round(statistics.median(times[c]), 1),
                           "bwd5_us": [round(t, 1) for t in times[c]], "bit_identical": same[c]}), flush=True)
 
+    # the forward (attn_fwd2_kernel): OSPO_ATTN_ORDER_FWD 0 = (head, sequence, block) grid, g >= 2 banded
+    def fwd(k):
+        qkv, do, o, lse = sets[k]
+        ops.flash_attn_fwd(qkv, 0, D, 2 * D, o, lse, S, T, H, hd, sc)
+
+    os.environ["OSPO_ATTN_ORDER_FWD"] = "0"
+    fref = []
+    for k in range(2):
+        fwd(k)
+        fref.append((sets[k][2].clone(), sets[k][3].clone()))
+    forders = [int(x) for x in os.environ.get("AB_FWD_ORDERS", "0 2 4 8 16").split()]
+    ft = {c: [] for c in forders}
+    fsame = {c: True for c in forders}
+    for rnd in range(6):
+        for c in forders:
+            os.environ["OSPO_ATTN_ORDER_FWD"] = str(c)
+            for k in range(2):
+                fwd(k)
+                fsame[c] &= bool(torch.equal(sets[k][2], fref[k][0]) and torch.equal(sets[k][3], fref[k][1]))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for it in range(10):
+                fwd(it & 1)
+            e1.record()
+            torch.cuda.synchronize()
+            ft[c].append(e0.elapsed_time(e1) / 10 * 1e3)
+    for c in forders:
+        print(json.dumps({"order_fwd": c, "fwd_us_median": round(statistics.median(ft[c]), 1),
+                          "fwd_us": [round(t, 1) for t in ft[c]], "bit_identical": fsame[c]}), flush=True)
+
 
 if __name__ == "__main__":
     main()

@@ -1,7 +1,7 @@
 """Split-K tail sweep for the w4 GEMM on the step shapes: the library's cost model (split 0) against pinned
 tail splits 1..8 (ops.gemm_nt split=), interleaved, HIP events, medians.  The model's constants were fitted
 on the SP8 kernel (T = 1.9 us per K-tile); this checks them on the w4 loop.  Run on the GPU box:
-python tools/w4_split_sweep.py"""
+python tools/w4_split_sweep.py  (SWEEP_M=9600: config 3's per-GPU batch, 8 pairs; round 5)"""
 import json
 import os
 import sys
@@ -11,10 +11,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ospo_amd import ops  # noqa: E402
 
-M = 4800
+M = int(os.environ.get("SWEEP_M", "4800"))
+MG = M // 600 * 576  # gen_head rows: the 576 image positions of each sequence
 SHAPES = [("qkv_fwd", M, 12288, 4096, 64), ("o_fwd", M, 4096, 4096, 64), ("gu_fwd", M, 22016, 4096, 64),
           ("down_fwd", M, 4096, 11008, 64), ("down_dx", M, 11008, 4096, 64), ("gu_dx", M, 4096, 22016, 64),
-          ("qkv_dx", M, 4096, 12288, 64), ("gh2_fwd", 4608, 16384, 4096, 0), ("gh2_dx", 4608, 4096, 16384, 0)]
+          ("qkv_dx", M, 4096, 12288, 64), ("gh2_fwd", MG, 16384, 4096, 0), ("gh2_dx", MG, 4096, 16384, 0)]
 SPLITS = [0, 1, 2, 3, 4, 5, 6, 8]
 
 
