@@ -37,29 +37,44 @@ write, nw = load("WRITE_SIZE")
 sq, ns = load("SQ_VALU_MFMA_BUSY_CYCLES")
 out = {}
 GEMM_NAMES = ("gemm_nt_w4_kernel", "gemm_nt_v5_kernel")  # round 4 default / the SP8 schedule
-gemm = [k for k in fetch if any(g in k for g in GEMM_NAMES)]
+
+
+def is_mx(k):
+    """MXFP8 main operands: gemm_nt_v5_kernel<DBG, DROP, MX, SP> / gemm_nt_w4_kernel<DROP, DBG, V, MX>."""
+    args = [a.strip() for a in k.split("<", 1)[1].split(">", 1)[0].split(",")] if "<" in k else []
+    pos = 2 if "gemm_nt_v5_kernel" in k else 3
+    return len(args) > pos and args[pos] == "true"
+
+
+gemm_all = [k for k in fetch if any(g in k for g in GEMM_NAMES)]
 fix = [k for k in fetch if "splitk_fixup" in k]
-launches = sum(nf[(k, "FETCH_SIZE")] for k in gemm)
-kib = sum(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"] for k in gemm + fix)
-busy = sum(sq[k]["SQ_VALU_MFMA_BUSY_CYCLES"] for k in sq if any(g in k for g in GEMM_NAMES))
 # kernel wall time of the same dispatches (counter rows carry the dispatch timestamps)
 f = glob.glob(os.path.join(src, "SQ_VALU_MFMA_BUSY_CYCLES", "**", "*counter_collection.csv"), recursive=True)[0]
-durs = {}
+durs = collections.defaultdict(dict)
 for r in csv.DictReader(open(f)):
     if any(g in r["Kernel_Name"] for g in GEMM_NAMES):
-        durs[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-dur_s = sum(durs.values()) * 1e-9
-out["gemm_nt_256x256"] = {
-    "hbm_bytes_per_launch": round(kib * 1024 / launches),
-    "launches": int(launches),
-    "kernels": sorted({short(k) for k in gemm}),
-    "method": "2*FETCH_SIZE + WRITE_SIZE (KiB), the NT GEMM + splitk_fixup_kernel, averaged over launches",
-    # SQ_VALU_MFMA_BUSY_CYCLES: summed over the 1024 SIMDs (16 cycles per 16x16x32 bf16 MFMA), against
-    # the cycles of the counter pass's kernel durations at the 2.4 GHz peak clock.  (The round-3 clock from
-    # GRBM_GUI_ACTIVE / 8 / duration came out above 2.4 GHz and is no longer reported; in-kernel clocks come
-    # from s_memtime / s_memrealtime stamps, tools/w4_stamps.py.)
-    "mfma_busy_frac_at_2p4ghz_peak": round(busy / (dur_s * 2.4e9 * 1024), 4) if dur_s else None,
-}
+        durs[is_mx(r["Kernel_Name"])][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+fams = {False: [k for k in gemm_all if not is_mx(k)], True: [k for k in gemm_all if is_mx(k)]}
+fams = {m: ks for m, ks in fams.items() if ks}
+# the split-K fixups go with the family that launches most GEMMs (the bench times them inside its launches)
+main_fam = max(fams, key=lambda m: sum(nf[(k, "FETCH_SIZE")] for k in fams[m]))
+for m, ks in fams.items():
+    launches = sum(nf[(k, "FETCH_SIZE")] for k in ks)
+    kib = sum(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"] for k in ks + (fix if m == main_fam else []))
+    busy = sum(sq[k]["SQ_VALU_MFMA_BUSY_CYCLES"] for k in sq if k in ks)
+    dur_s = sum(durs[m].values()) * 1e-9
+    out["gemm_nt_mx8_256x256" if m else "gemm_nt_256x256"] = {
+        "hbm_bytes_per_launch": round(kib * 1024 / launches),
+        "launches": int(launches),
+        "kernels": sorted({short(k) for k in ks}),
+        "method": "2*FETCH_SIZE + WRITE_SIZE (KiB), the NT GEMM" + (" + splitk_fixup_kernel" if m == main_fam else "")
+                  + ", averaged over launches",
+        # SQ_VALU_MFMA_BUSY_CYCLES: summed over the 1024 SIMDs, against the cycles of the counter pass's kernel
+        # durations at the 2.4 GHz peak clock.  (The round-3 clock from GRBM_GUI_ACTIVE / 8 / duration came out
+        # above 2.4 GHz and is no longer reported; in-kernel clocks come from s_memtime / s_memrealtime stamps,
+        # tools/w4_stamps.py.)
+        "mfma_busy_frac_at_2p4ghz_peak": round(busy / (dur_s * 2.4e9 * 1024), 4) if dur_s else None,
+    }
 for k in sorted(set(fetch) | set(write), key=lambda k: -(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"]))[:15]:
     n = max(nf[(k, "FETCH_SIZE")], 1)
     out.setdefault("per_kernel_MiB_per_launch", {})[short(k)[:60]] = round(
