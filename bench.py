@@ -68,7 +68,8 @@ def simpo_setup(layers=30, lora_r=16, pairs=4, text_len=24, img_tokens=576, lora
                       lora_dropout=lora_dropout, dropout_seed=42, linear_dtype=linear_dtype, wgrad_wgs=wgrad_wgs,
                       da_stream=not (round2_lora or "da_tiles" in lora_variant), keep_bits=not round2_lora,
                       fuse_swiglu_u=not (round2_lora or "swiglu_unfused" in lora_variant),
-                      fuse_swiglu_gdb=not (round2_lora or "swiglu_gdb_unfused" in lora_variant))
+                      fuse_swiglu_gdb=not (round2_lora or "swiglu_gdb_unfused" in lora_variant),
+                      gdb_groups=("gu",) if "gdb_gu_only" in lora_variant else ("qkv", "o", "gu", "down"))
     # each rank draws its own pairs (the DistributedSampler shard of the global batch)
     batches = [synthetic_batch(pairs, text_len, img_tokens, dims.vocab, dims.img_vocab, seed=1000 * rank + i,
                                device=dev) for i in range(4)]
@@ -518,7 +519,9 @@ def main():
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--wgrad-wgs", type=int, default=0)  # A/B: LoRA weight grads as ospo_lora_wgrad streams
     ap.add_argument("--round2-lora", action="store_true")  # A/B: round 2's LoRA kernels (dA tiles, re-hashed masks, unfused u_d)
-    ap.add_argument("--lora-variant", default="")  # A/B: "da_tiles", "swiglu_unfused", "swiglu_gdb_unfused" (comma list): one change off
+    # A/B: "da_tiles", "swiglu_unfused", "swiglu_gdb_unfused", "gdb_gu_only" (q|k|v, o, down: g from the skinny
+    # product, dB on the side stream) (comma list): one change off
+    ap.add_argument("--lora-variant", default="")
     # process-group backend for N > 1: RCCL ("nccl", default on GPUs); "gloo" lets N ranks share one GPU
     # (the multi-rank rehearsal of tests/test_gpu_dp_overlap.py on a one-GPU box)
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None)

@@ -141,8 +141,8 @@ int ospo_gemm_f32acc(const void* A, int lda, int a_kmajor, const void* B, int ld
                      int M, int N, int K, int k_splits, float alpha, float* C, int ldc,
                      int diag_nblk, int diag_r, hipStream_t stream);
 /* As ospo_gemm_f32acc with LoRA dropout recomputed on a K-major B [K][N] (the dA product's
- * activations): element (m, n) enters as bf16(B[m][n] / (1 - p)) when drop_hash(m * N + n, seed)
- * >= p * 2^32, else 0 -- the values ospo_lora_skinny's dropout multiplied in the forward, so the
+ * activations): element (m, n) enters as bf16(B[m][n] / (1 - p)) when drop_keep(m * N + n, seed) (the
+ * 16-bit half (idx & 1) of drop_hash(idx >> 1, seed) is >= p * 2^16, common.h), else 0 -- the values ospo_lora_skinny's dropout multiplied in the forward, so the
  * forward need not store the masked copy.  Requires b_kmajor = 1 and 0 < p < 1.  keep_bits (optional):
  * the mask as ospo_lora_skinny's keep-bit output for B ([K][N / 8] bytes, N % 8 == 0), read instead of
  * re-hashed (same result). */
@@ -314,7 +314,8 @@ int ospo_lora_pack(const void* A_flat, const void* B_flat, int nmods, int r, int
  * allocation); every call leaves them zero again.  Calls sharing a ws must be
  * ordered (same stream).
  * drop_p > 0 (dense mode only): peft lora_dropout on A -- element (m, k) is kept
- * iff drop_hash(m*K + k, drop_seed) >= drop_p * 2^32 (common.h) and becomes
+ * iff drop_keep(m*K + k, drop_seed) (common.h: the 16-bit half (idx & 1) of drop_hash(idx >> 1) is
+ * >= drop_p * 2^16; drop_hash is a permutation of the 32-bit pair index for every seed) and becomes
  * bf16(A / (1 - drop_p)); the masked A is also written to xd [M, ld_xd] when xd
  * is non-NULL (the dA = g^T . dropout(x) operand of the backward).  keep_bits (non-NULL only with
  * drop_p > 0, lda % 8 == 0 and K % 64 == 0, xd NULL): the keep decision of every element of rows < M as

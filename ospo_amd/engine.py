@@ -80,7 +80,7 @@ class SimPOEngine:
                  dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0, fuse_gdb: bool = True,
                  fuse_swiglu_gdb: bool = True,
                  da_stream: bool = True, keep_bits: bool = True, fuse_swiglu_u: bool = True,
-                 side_after_norm: bool = True):
+                 side_after_norm: bool = True, gdb_groups=("qkv", "o", "gu", "down")):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
         if linear_dtype not in ("bf16", "mx8"):
@@ -162,6 +162,9 @@ class SimPOEngine:
         # fuse_swiglu_gdb (with fuse_gdb, bf16): the SwiGLU backward and the gate|up group's g / dB in one stream
         # over (dh, gu) -- dgu written once, never read back by a separate g / dB pass (ospo_swiglu_lora_gdb)
         self.fuse_swiglu_gdb = bool(fuse_swiglu_gdb) and self.fuse_gdb
+        # gdb_groups (round 5 A/B): the groups whose g / dB run as the fused ospo_lora_gdb stream; the others take
+        # g from the skinny product on the main stream (no separate split-sum launch) and dB on the side stream
+        self.gdb_groups = frozenset(gdb_groups)
         self.pack_lora()
         self._alloc(max_pairs, max_text_len, n_img_tokens)
         self._rope_T = -1
@@ -368,7 +371,8 @@ class SimPOEngine:
         """(g_s, dB done): with fuse_gdb, g_s = bf16(scale * dy . Bcat) and dB += dy^T . u in one stream over dy
         (ospo_lora_gdb); else _lora_g and the side stream computes dB."""
         r = self.layout.r
-        if not (self.fuse_gdb and self._gdb_ws is not None and r == 16 and g.Nmod % 128 == 0 and g.nmods <= 4):
+        if not (self.fuse_gdb and g.name in self.gdb_groups and self._gdb_ws is not None and r == 16
+                and g.Nmod % 128 == 0 and g.nmods <= 4):
             return self._lora_g(dy, g, Bcat, BT, M, par), False
         out = self.gsc2[g.name][par]
         b_off = gbase + g.b_off

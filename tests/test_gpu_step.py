@@ -526,6 +526,34 @@ def test_step_side_after_norm_same_grads():
     assert max(rel(g1[k], g0[k]) for k in g0) < 1e-5
 
 
+def test_step_gdb_gu_only_same_step():
+    """gdb_groups=("gu",) (round 5 A/B): the q|k|v, o and down groups take g from the skinny product on the main
+    stream and dB from the f32-atomic product on the side stream, instead of the fused ospo_lora_gdb stream (the
+    gate|up group stays fused with the SwiGLU backward).  The forward is untouched (log-probs and loss bit-equal);
+    g sums the same products in another order, so the grads agree to bf16 rounding of g, well inside the
+    oracle tolerances."""
+    dims = O.JanusDims(n_layers=4, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=2048,
+                       gen_head_dim=256, lora_r=16, lora_alpha=32, lora_dropout=0.05)
+    w = O.init_weights(dims, seed=43, dtype=torch.bfloat16, lora_b_std=1e-2)
+    g = torch.Generator().manual_seed(44)
+    B, Lt, N = 2, 8, 64
+    text = [torch.randint(0, dims.vocab, (1, Lt - i), generator=g, dtype=torch.int32) for i in range(B)]
+    chosen = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    rejected = torch.randint(0, dims.img_vocab, (B, N), generator=g)
+    algo = {"beta": 10.0, "gamma_beta_ratio": 0.5, "label_smoothing": 0.0, "loss_type": "sigmoid"}
+    from ospo_amd.engine import ModelDims, SimPOEngine
+    out = []
+    for groups in (("qkv", "o", "gu", "down"), ("gu",)):
+        eng = SimPOEngine(ModelDims.from_any(dims), w, device="cuda", max_pairs=B, max_text_len=Lt,
+                          n_img_tokens=N, lora_dropout=0.05, dropout_seed=9, gdb_groups=groups)
+        out.append(run_hip_step(eng, text, chosen, rejected, algo))
+    (l0, s0, g0), (l1, s1, g1) = out
+    assert torch.equal(l0, l1) and s0 == s1
+    err = max(rel(g1[k], g0[k]) for k in g0)
+    record_parity("gdb_gu_only_vs_fused", grad_rel=err)
+    assert err < 1e-2, err
+
+
 def _mx8_case(dims, seed, B, Lt, N):
     w = O.init_weights(dims, seed=seed, dtype=torch.bfloat16, lora_b_std=1e-2)
     g = torch.Generator().manual_seed(seed + 1)
