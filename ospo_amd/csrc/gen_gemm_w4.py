@@ -32,6 +32,9 @@ Programs (runtime-selected by the kernel; each one asm statement):
 import sys
 
 MFMA = "v_mfma_f32_16x16x32_bf16"
+# staged programs: a block's bf16 staging runs this many MFMAs after its final MFMA (>= 4 x 16 cycles: past the
+# 8-pass MFMA's result latency, which inline asm does not pad for the v_accvgpr_read)
+STAGE_LAG = 4
 RD_ORDER = [("X", 0)] + [("Y", j) for j in range(8)] + [("X", i) for i in range(1, 8)]
 
 
@@ -113,10 +116,14 @@ class Prog:
             so = "0" if src == "e0" else "%[sE1]"
             self.emit(f"buffer_load_dwordx4 %[e{op}{k}], %[rs{op}2], {so} offen{c} lds")
 
-    def tile(self, first=False, load=None, has_next=True, vm_next=None, loop=None):
+    def tile(self, first=False, load=None, has_next=True, vm_next=None, loop=None, stage=False):
         """One K-tile.  load: the source of the tile two ahead ('m', 'e0', 'e1') or None.  vm_next: the
         vmcnt that retires the next tile's pieces (pieces issued after them).  loop: label to branch back
-        to while --%[cnt] != 0."""
+        to while --%[cnt] != 0.  stage (the last tile of a staged program, round 5): once every wave has read
+        the tile's fragments (a barrier at gap 24; no LDS-DMA is in flight in the last tile), each accumulator
+        block is rounded to bf16 and written to the epilogue's LDS staging rows STAGE_LAG MFMAs after its final
+        MFMA (64 + n for block n), in the MFMA gaps; the blocks whose slot falls past the tile are staged by
+        epilogue(stage=True)."""
         if self.noload and not first:
             load = None
             vm_next = 0
@@ -130,9 +137,18 @@ class Prog:
         post[19].append(("v_xor_b32 %[rB0], %[tB0], %[rB0]",))
         post[20].append(("v_xor_b32 %[rA1], %[tA1], %[rA1]",))
         post[21].append(("v_xor_b32 %[rB1], %[tB1], %[rB1]",))
-        if load is not None and not self.opt["no_bar1"]:
+        if (load is not None and not self.opt["no_bar1"]) or stage:
             pre[24].append(("lgkm0",))
             pre[24].append(("s_barrier",))
+        if stage:
+            assert load is None and not has_next
+            self.deferred = []
+            for n in range(64):
+                k = 64 + n + STAGE_LAG
+                if k <= 127:
+                    post[k].append(("stage", n))
+                else:
+                    self.deferred.append(n)
         if load is not None:
             early = self.opt["m0_early"]
             for op, slots in (("A", self.opt["a_slots"]), ("B", self.opt["b_slots"])):
@@ -168,7 +184,22 @@ class Prog:
             self.emit("s_cmp_lg_u32 %[cnt], 0")
             self.emit(f"s_cbranch_scc1 {loop}")
 
+    def stage_block(self, n):
+        """Block n = 8 i + j of the accumulators -> bf16 (v_cvt_pk_bf16_f32, RNE) -> the staging rows at %[sb] +
+        8448 j + 32 i (w4_stage_bf16's layout and instructions, one block)."""
+        i, j = divmod(n, 8)
+        b = 120 + 4 * (n % 2)
+        for e in range(4):
+            self.emit(f"v_accvgpr_read_b32 v{b + e}, a{4 * n + e}")
+        self.emit(f"v_cvt_pk_bf16_f32 v{b}, v{b}, v{b + 1}")
+        self.emit(f"v_cvt_pk_bf16_f32 v{b + 1}, v{b + 2}, v{b + 3}")
+        off = 8448 * j + 32 * i
+        self.emit(f"ds_write_b64 %[sb], v[{b}:{b + 1}]" + (f" offset:{off}" if off else ""))
+
     def _item(self, it):
+        if it[0] == "stage":
+            self.stage_block(it[1])
+            return
         if it[0] == "read":
             self.read(it[1], it[2], it[3])
         elif it[0] == "lgkm0":
@@ -211,15 +242,19 @@ class Prog:
                     self.emit(f"v_accvgpr_write_b32 {a}, v120")
         self.emit("s_nop 7")
 
-    def epilogue(self):
+    def epilogue(self, stage=False):
         self.emit("s_waitcnt vmcnt(0) lgkmcnt(0)")
         self.emit("s_nop 15")
         self.emit("s_nop 15")
+        if stage:  # the blocks whose staging slot fell past the last MFMA, then every staging write retired
+            for n in self.deferred:
+                self.stage_block(n)
+            self.emit("s_waitcnt lgkmcnt(0)")
         self.emit("s_barrier")
         self.emit("s_mov_b32 m0, %[sSave]")
 
 
-def prog_plain(E, noload=False, opt=None):
+def prog_plain(E, noload=False, opt=None, stage=False):
     p = Prog(noload, opt)
     p.prologue("m", "m")
     p.tile(first=True, load="m", vm_next=16)
@@ -230,12 +265,12 @@ def prog_plain(E, noload=False, opt=None):
     for n in range(len(seq)):
         ld = seq[n + 2] if n + 2 < len(seq) else None
         nxt = n + 1 < len(seq)
-        p.tile(load=ld, has_next=nxt, vm_next=(16 if ld else 0))
-    p.epilogue()
+        p.tile(load=ld, has_next=nxt, vm_next=(16 if ld else 0), stage=stage and not nxt)
+    p.epilogue(stage)
     return p
 
 
-def prog_drop(E, noload=False):
+def prog_drop(E, noload=False, stage=False):
     p = Prog(noload)
     seq0 = ["e0", "e1"][:E] + ["m", "m"]
     p.prologue(seq0[0], seq0[1])
@@ -245,8 +280,8 @@ def prog_drop(E, noload=False):
     p.emit("L_w4loop_%=:")
     p.tile(load="m", vm_next=16, loop="L_w4loop_%=")
     p.tile(load=None, has_next=True, vm_next=0)
-    p.tile(load=None, has_next=False)
-    p.epilogue()
+    p.tile(load=None, has_next=False, stage=stage)
+    p.epilogue(stage)
     return p
 
 
@@ -460,7 +495,7 @@ HEADER = """// GENERATED by gen_gemm_w4.py -- do not edit.  The hand-placed K-lo
 """
 
 
-def asm_fn(name, prog, drop):
+def asm_fn(name, prog, drop, stage=False):
     outs = ['[sSave] "=&s"(o.save)', '[cnt] "+s"(o.cnt)', '[sK] "+s"(o.sK)', '[sM] "+s"(o.sM)',
             '[rA0] "+v"(o.rA0)', '[rA1] "+v"(o.rA1)', '[rB0] "+v"(o.rB0)', '[rB1] "+v"(o.rB1)']
     ins = ['[rsA] "s"(o.rsA)', '[rsB] "s"(o.rsB)', '[rsA2] "s"(o.rsA2)', '[rsB2] "s"(o.rsB2)',
@@ -470,7 +505,10 @@ def asm_fn(name, prog, drop):
     ins += [f'[eA{k}] "v"(o.eA[{k}])' for k in range(8)] + [f'[eB{k}] "v"(o.eB[{k}])' for k in range(8)]
     if drop:
         ins += [f'[mk{j}] "v"(o.mk[{j}])' for j in range(8)] + ['[dsc] "s"(o.dsc)']
-    clob = ['"memory"', '"scc"'] + [f'"v{r}"' for r in (120, 121)] + [f'"v{r}"' for r in range(128, 256)] + \
+    if stage:
+        ins += ['[sb] "v"(o.sb)']
+    scratch = range(120, 128) if stage else (120, 121)
+    clob = ['"memory"', '"scc"'] + [f'"v{r}"' for r in scratch] + [f'"v{r}"' for r in range(128, 256)] + \
         [f'"a{r}"' for r in range(256)]
     body = "\n".join(f'      "{l}\\n"' for l in prog.lines)
     return (f"__device__ __forceinline__ void {name}(W4Ops& o) {{\n  asm volatile(\n{body}\n"
@@ -548,6 +586,12 @@ def main(out):
         parts.append(asm_fn(f"w4_plain{E}", prog_plain(E), False))
     for E in (1, 2):
         parts.append(asm_fn(f"w4_drop{E}", prog_drop(E), True))
+    # round 5: the plain bf16 epilogue's staging inside the last tile (gemm_w4.h picks these when the tile is not
+    # a split-K piece and alpha == 1 without bias)
+    for E in (0, 1, 2):
+        parts.append(asm_fn(f"w4_plain{E}_st", prog_plain(E, stage=True), False, stage=True))
+    for E in (1, 2):
+        parts.append(asm_fn(f"w4_drop{E}_st", prog_drop(E, stage=True), True, stage=True))
     for E in (0, 1, 2):
         parts.append(asm_fn_mx(f"w4_mx{E}", prog_mx(E)))
     parts.append("#ifdef OSPO_ABLATION\n// decomposition (results invalid): no LDS-DMA after the prologue\n")

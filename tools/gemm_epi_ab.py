@@ -1,6 +1,7 @@
 """Plain-epilogue store variants of the w4 GEMM (verdict r4 item 3c), same process, interleaved, on the step's
 GEMM shapes.  OSPO_GEMM_EPI (ablation build, read per launch): 0 = the product epilogue (4 LDS reads in flight
-per batch), 1 = 8 in flight, 2 = non-temporal stores, 3 = both, 4 = 16 in flight.  Only launches whose
+per batch; round 5: staged inside the last K-tile), 1 = 8 in flight, 2 = non-temporal stores, 3 = both, 4 = 16 in
+flight, 9 = the round-4 staging after the K loop (w4_stage_bf16).  Only launches whose
 epilogue is plain (no residual, no RoPE) change; every variant must write the same bytes.  Prints one JSON
 line per shape: median us per variant and bit-identity."""
 import os as _os
@@ -21,7 +22,7 @@ MG = M // 600 * 576
 SHAPES = [("gu_fwd", M, 22016, 4096, 64), ("down_dx", M, 11008, 4096, 64), ("gu_dx", M, 4096, 22016, 64),
           ("qkv_dx", M, 4096, 12288, 64), ("o_dx", M, 4096, 4096, 64), ("gh2_fwd", MG, 16384, 4096, 0),
           ("sq4096", 4096, 4096, 4096, 0)]
-VARS = [int(v) for v in os.environ.get("AB_EPI", "0 1 2 3 4").split()]
+VARS = [int(v) for v in os.environ.get("AB_EPI", "0 9 1 2 3 4").split()]
 
 
 def main():
