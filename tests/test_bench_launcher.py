@@ -59,3 +59,18 @@ def test_t2i_traffic_field_from_committed_counter_pass():
     assert {"dlin_kernel", "attn_cache2_kernel"} <= set(pmc["per_kernel"])
     nbytes = 18_037_604_352
     assert bench.t2i_traffic(nbytes) == round(nbytes * pmc["traffic_ratio"])
+
+
+def test_gemm_traffic_only_from_counter_passes_of_the_same_configuration():
+    """roofline.traffic comes from the committed counter summary of the bench's own configuration (round 5: the
+    8-pair and MXFP8 lines used to carry the default 4-pair line's bytes); a configuration without its own
+    counter passes reports null."""
+    sys.path.insert(0, ROOT)
+    import bench
+    default = bench.gemm_pmc_path(4, 30, 16, "bf16")
+    assert os.path.basename(default) == "gemm_pmc.json" and os.path.exists(default)
+    p8 = bench.gemm_pmc_path(8, 30, 16, "bf16")
+    mx = bench.gemm_pmc_path(4, 30, 32, "mx8")
+    assert os.path.basename(p8) == "gemm_pmc_bf16_p8_r16_l30.json"
+    assert os.path.basename(mx) == "gemm_pmc_mx8_p4_r32_l30.json"
+    assert len({default, p8, mx, bench.gemm_pmc_path(4, 2, 16, "bf16")}) == 4
