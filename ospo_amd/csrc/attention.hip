@@ -464,6 +464,7 @@ __device__ __forceinline__ void fwd_scores(const char* Ks, const bf16x8 (&qf)[2]
 }
 
 // HF scores, causal mask (diagonal tiles only), online softmax of one tile for both groups -> P^T packs
+template <bool ALWAYS_RESCALE = false>  // (true: the round-4 form, ablation A/B)
 __device__ __forceinline__ void fwd_softmax(f32x4 (&st)[2][4], bool diag, int key0, const int (&lim)[2], float scale,
                                             float (&m_run)[2], float (&l_run)[2], f32x4 (&o)[2][8],
                                             bf16x8 (&pb)[2][2]) {
@@ -512,8 +513,13 @@ __device__ __forceinline__ void fwd_softmax(f32x4 (&st)[2][4], bool diag, int ke
     psum = grp_sum(psum);
     l_run[q] = l_run[q] * alpha + psum;
     m_run[q] = m_new;
+    // round 5: the 32 accumulator multiplies only when some row's running max moved in this tile (alpha is
+    // exactly 1 where it did not, and x * 1 = x exactly: bit-identical); past the first key tiles of a sweep the
+    // max of every row in the group usually holds, and this VALU sits on the issue-bound softmax path
+    if (ALWAYS_RESCALE || __any(alpha != 1.f)) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[q][i] *= alpha;
+      for (int i = 0; i < 8; ++i) o[q][i] *= alpha;
+    }
     pb[q][0] = pack_perm(st[q][0], st[q][1]);
     pb[q][1] = pack_perm(st[q][2], st[q][3]);
   }
@@ -632,7 +638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (kt + 1 < n_kv) fwd_scores(smem + (buf ^ 1) * KOFF, qf, sn, lane);
       if (kt + 2 < n_kv) stage64<NW>(kbase, ldq, (kt + 2) * KB, T, 0, smem + buf * KOFF, wave, lane);
       if (kt + 1 < n_kv) stage64<NW>(vbase, ldq, (kt + 1) * KB, T, 0, smem + V0 + (buf ^ 1) * TILE_BYTES, wave, lane);
-      fwd_softmax(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
+      fwd_softmax<DBG == 5>(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
       fwd_pv(va, (uint32_t)(buf * TILE_BYTES), pb, o);
       if (kt + 1 < n_kv) {
 #pragma unroll
@@ -668,7 +674,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           pb[q][1] = pack_perm(st[q][2], st[q][3]);
         }
       } else {
-        fwd_softmax(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
+        fwd_softmax<DBG == 5>(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
       }
       if constexpr (DBG != 2) fwd_pv(va, (uint32_t)(buf * KOFF), pb, o);
       else {
@@ -1791,6 +1797,7 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
     if (v == 2) kfn = attn_fwd2_kernel<false, false, 2>;
     if (v == 3) kfn = attn_fwd2_kernel<false, false, 3>;
     if (v == 4) kfn = attn_fwd2_kernel<false, false, 4>;
+    if (v == 5) kfn = attn_fwd2_kernel<false, false, 5>;  // A/B (bit-identical): rescale O on every tile (round 4)
   }
   // A/B: the 8-wave x 16-row kernel (rounds 1-3; OSPO_ATTN_FWD8), its decomposition / spread forms
   static const bool fwd8 = getenv("OSPO_ATTN_FWD8") != nullptr;

@@ -106,6 +106,30 @@ def main():
         print(json.dumps({"order_fwd": c, "fwd_us_median": round(statistics.median(ft[c]), 1),
                           "fwd_us": [round(t, 1) for t in ft[c]], "bit_identical": fsame[c]}), flush=True)
 
+    # round 5: the O rescale skipped where no row's running max moved (default) vs every tile (OSPO_ATTN_FWD2_DBG=5)
+    os.environ["OSPO_ATTN_ORDER_FWD"] = "0"
+    rt = {"skip": [], "always": []}
+    rsame = True
+    for rnd in range(6):
+        for v in ("skip", "always"):
+            if v == "always":
+                os.environ["OSPO_ATTN_FWD2_DBG"] = "5"
+            else:
+                os.environ.pop("OSPO_ATTN_FWD2_DBG", None)
+            for k in range(2):
+                fwd(k)
+                rsame &= bool(torch.equal(sets[k][2], fref[k][0]) and torch.equal(sets[k][3], fref[k][1]))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for it in range(10):
+                fwd(it & 1)
+            e1.record()
+            torch.cuda.synchronize()
+            rt[v].append(e0.elapsed_time(e1) / 10 * 1e3)
+    os.environ.pop("OSPO_ATTN_FWD2_DBG", None)
+    print(json.dumps({"fwd_rescale": {v: round(statistics.median(t), 1) for v, t in rt.items()},
+                      "bit_identical": rsame}), flush=True)
+
 
 if __name__ == "__main__":
     main()
