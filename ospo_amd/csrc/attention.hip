@@ -1903,7 +1903,10 @@ static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
     // Group-major (a group's blocks back to back on one XCD) cut the dK/dV kernel's HBM fetch 2.2x
     // (206 -> 92 MB) but ended on a few heavy workgroups: 215-221 vs 206-209 us per layer for the whole
     // backward (profiles/r02/attn)
-    int order_dkdv = 0, order_dq = 0;
+    // round 5: banded order (group_major gm = 4: per XCD, bands of 4 (sequence, head) groups, heaviest block
+    // first within a band) for both kernels: 184.6 -> 177.2 us per layer for the 5-product backward at the step
+    // shape, same bytes (profiles/r05/attn_order_ab.log; group-major 188.9, bands of 2: 186.1, of 8: 179.9)
+    int order_dkdv = 4, order_dq = 4;
 #ifdef OSPO_ABLATION
     if (const char* e = getenv("OSPO_ATTN_ORDER")) order_dkdv = order_dq = atoi(e);  // A/B: 0 block-, 1 group-major
     if (const char* e = getenv("OSPO_ATTN_ORDER_DQ")) order_dq = atoi(e);             // A/B: the dQ kernel alone

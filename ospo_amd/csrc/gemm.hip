@@ -933,6 +933,19 @@ __device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0
 // tiles stay bf16 (16 bf16 MFMAs per phase).
 // bf16 epilogue, second half: the tile's rounded products staged in LDS as [256][CPITCH] rows ->
 // RoPE / residual -> 16-B coalesced global stores (shared by the 256x256 kernels)
+// GEMM outputs (bf16 tiles, split-K fp32 partials) are stored non-temporally (round 5): no later access in the
+// launch re-reads them, and 'nt' stores leave the L2 to the operands being streamed.  Measured on the plain
+// epilogue (profiles/r05/gemm_epi_ab.log, variant 2): gu_fwd 613 -> 595 us, gh2_fwd 423 -> 413, down_dx 326 -> 320,
+// the others within noise.  A library built with -DOSPO_GEMM_NT_STORES=0 stores them plainly (step A/B).
+#ifndef OSPO_GEMM_NT_STORES
+#define OSPO_GEMM_NT_STORES 1
+#endif
+template <typename T>
+__device__ __forceinline__ void gemm_out_store(T* p, const T& v) {
+  if constexpr (OSPO_GEMM_NT_STORES) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 #ifdef OSPO_ABLATION
 // Ablation (round 5): the plain epilogue (no residual, no RoPE) with BATCH LDS reads in flight before their
 // stores, and optionally non-temporal stores.  Same values and addresses as epi_rows: bit-identical output.
@@ -1045,8 +1058,8 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem,
           v2 = o2;
         }
         if (m < args.M) {
-          *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cl * 8) = v1;
-          *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + (cl + 8) * 8) = v2;
+          gemm_out_store(reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cl * 8), v1);
+          gemm_out_store(reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + (cl + 8) * 8), v2);
         }
       }
     }
@@ -1104,7 +1117,7 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& args, const char* smem,
           v[qq] = pack2(lo, hi);
         }
       }
-      if (m < args.M) *reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8) = v;
+      if (m < args.M) gemm_out_store(reinterpret_cast<u32x4*>(C + (long)m * args.ldc + n0 + cc * 8), v);
     }
   }
 }
@@ -1804,7 +1817,7 @@ __global__ __launch_bounds__(512) void gemm_nt_v5_kernel(const GemmArgs args, in
         for (int i = 0; i < 4; ++i) {
           const int ml = ia * 128 + wm * 64 + i * 16 + l16;
           const int nl = ib * 128 + wn * 32 + n * 16 + 4 * g;
-          *reinterpret_cast<f32x4*>(wt + ml * BN + nl) = acc[j][i][n];
+          gemm_out_store(reinterpret_cast<f32x4*>(wt + ml * BN + nl), acc[j][i][n]);
         }
     }
     return;
@@ -1927,7 +1940,7 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
     swiglu_bwd_store8(args, m, n0 + c, o);
     return;
   }
-  *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(args.C) + (long)m * args.ldc + n0 + c) = o;
+  gemm_out_store(reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(args.C) + (long)m * args.ldc + n0 + c), o);
 }
 
 // The device's CU count: an immutable property, read once per device (std::call_once), so the

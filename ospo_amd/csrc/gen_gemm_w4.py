@@ -586,15 +586,16 @@ def main(out):
         parts.append(asm_fn(f"w4_plain{E}", prog_plain(E), False))
     for E in (1, 2):
         parts.append(asm_fn(f"w4_drop{E}", prog_drop(E), True))
-    # round 5: the plain bf16 epilogue's staging inside the last tile (gemm_w4.h picks these when the tile is not
-    # a split-K piece and alpha == 1 without bias)
+    for E in (0, 1, 2):
+        parts.append(asm_fn_mx(f"w4_mx{E}", prog_mx(E)))
+    parts.append("#ifdef OSPO_ABLATION\n// decomposition (results invalid): no LDS-DMA after the prologue\n")
+    # round 5, measured and rejected (same bytes, 0.3 % slower in the step: profiles/r05/gemm_epi_ab.log,
+    # bench_ab_r5c_hash_*.json): the plain bf16 epilogue's staging inside the last tile's MFMA gaps
+    parts.append("// staged programs (OSPO_GEMM_EPI=10)\n")
     for E in (0, 1, 2):
         parts.append(asm_fn(f"w4_plain{E}_st", prog_plain(E, stage=True), False, stage=True))
     for E in (1, 2):
         parts.append(asm_fn(f"w4_drop{E}_st", prog_drop(E, stage=True), True, stage=True))
-    for E in (0, 1, 2):
-        parts.append(asm_fn_mx(f"w4_mx{E}", prog_mx(E)))
-    parts.append("#ifdef OSPO_ABLATION\n// decomposition (results invalid): no LDS-DMA after the prologue\n")
     parts.append(asm_fn("w4_plain0_noload", prog_plain(0, noload=True), False))
     parts.append("// schedule variants for A/B (w4v<V>_plain<E>, bf16 without dropout)\n")
     for v, opt in ABL_VARIANTS.items():
