@@ -243,7 +243,10 @@ class SimPOEngine:
         # used by layer parity: main rewrites a copy in layer i only after the side stream finished
         # layer i+2's products, so the guards below practically never stall the main stream.
         self.gsc2 = {name: [z(Mc, g.Rp), z(Mc, g.Rp)] for name, g in self.layout.groups.items()}
-        self.dx2 = [z(Mc, D), z(Mc, D)]
+        # the gradient w.r.t. each layer's output, three copies (round 5; two before): layer i's copy is read by its
+        # side-stream dB / dA work and rewritten by layer i-2's input-norm backward, so main waits for the side work
+        # of the layer two above (as for every other side operand) instead of the layer just above
+        self.dx2 = [z(Mc, D), z(Mc, D), z(Mc, D)]
         self.dxmid2 = [z(Mc, D), z(Mc, D)]
         self.dqkv2 = [z(Mc, 3 * D), z(Mc, 3 * D)]
         self.dgu2 = [z(Mc, 2 * Fd), z(Mc, 2 * Fd)]
@@ -575,7 +578,7 @@ class SimPOEngine:
         ops.gemm_nt(self.dz[:R], self.gh_w1T, self.dhsel[:R])
         ops.scatter_rows(self.dhsel[:R], S, T, Lt - 1, N, self.dxn[:M])
         L = dims.n_layers
-        ops.rmsnorm_bwd(self.dxn[:M], self.x_final[:M], self.norm, self.rstd_f[:M], self.dx2[(L - 1) % 2][:M],
+        ops.rmsnorm_bwd(self.dxn[:M], self.x_final[:M], self.norm, self.rstd_f[:M], self.dx2[(L - 1) % 3][:M],
                         mx=self._mxo(D))
         scale_attn = 1.0 / math.sqrt(hd)
         lay = self.layout
@@ -583,23 +586,23 @@ class SimPOEngine:
         # layer's backward is on the main stream (one event each way per layer: an event record costs the
         # recording stream ~3.5 us and a wait ~1.4 us, tools/event_cost_probe.py; per-group events cost
         # ~0.4 ms per step).  Main waits before rewriting what pending side work reads: the g / dy copies of
-        # parity q (layer i+2's) at the start of layer i, dx copy 1-q (layer i+1's) before the input-norm
-        # backward that rewrites it.
+        # parity q (layer i+2's) at the start of layer i, and the dx copy (i - 1) % 3 (layer i+2's, three copies)
+        # before the input-norm backward that rewrites it.
         main, side = torch.cuda.current_stream(self.device), self._side
         side.wait_stream(main)
-        done = {}  # layer parity -> event after that layer's side work was enqueued
+        done = {}  # layer -> event after that layer's side work was enqueued
 
-        def wait_done(par):
-            ev = done.pop(par, None)
+        def wait_done(layer):
+            ev = done.get(layer)
             if ev is not None:
                 main.wait_event(ev)
 
         for i in reversed(range(dims.n_layers)):
             a, lw, pk = self.acts[i], self.layers[i], self.packed[i]
             gbase = lay.layer_off(i)
-            q = i % 2  # copy of every side-stream operand this layer writes
-            wait_done(q)  # layer i+2's side work read the copies this layer rewrites
-            dx = self.dx2[q]  # gradient w.r.t. this layer's output (bf16)
+            q = i % 2  # copy of every side-stream operand this layer writes (dx: i % 3)
+            wait_done(i + 2)  # layer i+2's side work read the copies this layer rewrites
+            dx = self.dx2[i % 3]  # gradient w.r.t. this layer's output (bf16)
             dgu, dxmid, dqkv = self.dgu2[q], self.dxmid2[q], self.dqkv2[q]
             pending = []  # (group, g_s, x_in, dy, u, dropout, dB done on main)
             # ---- down_proj: out = xmid + h W_d^T + s (h A_d^T) B_d^T
@@ -659,15 +662,15 @@ class SimPOEngine:
                         on_layer_grads(gbase, gbase + lay.per_layer)
                 ev2 = torch.cuda.Event()
                 ev2.record(side)
-                done[q] = ev2
+                done[i] = ev2
 
             late = self.side_after_norm and i > 0
             if not late:
                 enqueue_side()
             if i > 0:
-                wait_done(1 - q)  # dx copy 1-q: layer i+1's side work read it
-                # (writes dxn and dx copy 1-q: neither is read by this layer's side work)
-                ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[1 - q][:M],
+                # (writes dxn and dx copy (i - 1) % 3 = (i + 2) % 3, whose last reader, layer i+2's side work, main
+                # waited for at this layer's start; neither is read by this layer's side work)
+                ops.rmsnorm_bwd(self.dxn[:M], a["x"][:M], lw["ln_in"], a["rstd1"][:M], self.dx2[(i - 1) % 3][:M],
                                 dres=dxmid[:M], mx=self._mxo(D))
             if late:
                 enqueue_side()
