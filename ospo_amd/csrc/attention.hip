@@ -152,6 +152,17 @@ __device__ __forceinline__ void hf_scores2(float& a, float& b, float scale) {
   b *= scale;
   bf_round2(a, b);
 }
+// RAW (ablation only, verdict r4 item 2c): the scores scaled in fp32 without HF's two bf16 roundings -- a
+// measurement of how much the roundings matter for parity; forward and backward must agree (lse)
+template <bool RAW>
+__device__ __forceinline__ void scores2(float& a, float& b, float scale) {
+  if constexpr (RAW) {
+    a *= scale;
+    b *= scale;
+  } else {
+    hf_scores2(a, b, scale);
+  }
+}
 // Reductions over the 4 lane groups (lanes l, l^16, l^32, l^48) with the CDNA4 half-row swaps
 // (VALU, no LDS round trip like ds_bpermute); every lane gets the same bits (a+b == b+a).
 __device__ __forceinline__ float grp_max(float x) {
@@ -464,7 +475,7 @@ __device__ __forceinline__ void fwd_scores(const char* Ks, const bf16x8 (&qf)[2]
 }
 
 // HF scores, causal mask (diagonal tiles only), online softmax of one tile for both groups -> P^T packs
-template <bool ALWAYS_RESCALE = false>  // (true: the round-4 form, ablation A/B)
+template <bool ALWAYS_RESCALE = false, bool RAW = false>  // (true: the round-4 form / unrounded scores, ablation A/B)
 __device__ __forceinline__ void fwd_softmax(f32x4 (&st)[2][4], bool diag, int key0, const int (&lim)[2], float scale,
                                             float (&m_run)[2], float (&l_run)[2], f32x4 (&o)[2][8],
                                             bf16x8 (&pb)[2][2]) {
@@ -478,7 +489,7 @@ __device__ __forceinline__ void fwd_softmax(f32x4 (&st)[2][4], bool diag, int ke
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
           float a = st[q][t][j], b = st[q][t][j + 1];
-          hf_scores2(a, b, scale);
+          scores2<RAW>(a, b, scale);
           a = (16 * t + j > rel) ? -INFINITY : a;
           b = (16 * t + j + 1 > rel) ? -INFINITY : b;
           st[q][t][j] = a;
@@ -491,7 +502,7 @@ __device__ __forceinline__ void fwd_softmax(f32x4 (&st)[2][4], bool diag, int ke
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
           float a = st[q][t][j], b = st[q][t][j + 1];
-          hf_scores2(a, b, scale);
+          scores2<RAW>(a, b, scale);
           st[q][t][j] = a;
           st[q][t][j + 1] = b;
           tmax = fmaxf(tmax, fmaxf(a, b));
@@ -557,7 +568,7 @@ __device__ __forceinline__ void fwd_pv(const uint32_t (&va)[8], uint32_t boff, c
 
 // DBG (ablation build, results invalid): 1 no softmax VALU (P = S), 2 no PV products, 3 no S products,
 // 4 no K/V loads after the first tile
-template <bool MXO = false, bool PIPE = false, int DBG = 0>
+template <bool MXO = false, bool PIPE = false, int DBG = 0, bool RAW = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd2_kernel(
     const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, bf16* __restrict__ out, int ldo,
     float* __restrict__ lse, int T, int H, float scale, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0},
@@ -638,7 +649,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (kt + 1 < n_kv) fwd_scores(smem + (buf ^ 1) * KOFF, qf, sn, lane);
       if (kt + 2 < n_kv) stage64<NW>(kbase, ldq, (kt + 2) * KB, T, 0, smem + buf * KOFF, wave, lane);
       if (kt + 1 < n_kv) stage64<NW>(vbase, ldq, (kt + 1) * KB, T, 0, smem + V0 + (buf ^ 1) * TILE_BYTES, wave, lane);
-      fwd_softmax<DBG == 5>(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
+      fwd_softmax<DBG == 5, RAW>(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
       fwd_pv(va, (uint32_t)(buf * TILE_BYTES), pb, o);
       if (kt + 1 < n_kv) {
 #pragma unroll
@@ -674,7 +685,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           pb[q][1] = pack_perm(st[q][2], st[q][3]);
         }
       } else {
-        fwd_softmax<DBG == 5>(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
+        fwd_softmax<DBG == 5, RAW>(st, diag_of(kt), kt * KB + 4 * g, lim, scale, m_run, l_run, o, pb);
       }
       if constexpr (DBG != 2) fwd_pv(va, (uint32_t)(buf * KOFF), pb, o);
       else {
@@ -961,7 +972,7 @@ __device__ __forceinline__ void wait_tr_ld(TrBatch& t) {
 // before its MFMAs: ~18 % MFMA busy at 2 waves per SIMD).  The first batch of a tile is issued
 // right after the tile barrier.
 // DBG 1 (ablation build): s_memtime sums per wave of the tile phases -> dbg[8 per wave]
-template <int NW, int DBG = 0, bool MXO = false>
+template <int NW, int DBG = 0, bool MXO = false, bool RAW = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv3_kernel(
     const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, const bf16* __restrict__ dout, int ldd,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16* __restrict__ dqkv, int ldg, int T, int H,
@@ -1164,7 +1175,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int j = 0; j < 4; j += 2) {
         float x = sv[A][j], y = sv[A][j + 1];
-        hf_scores2(x, y, scale);
+        scores2<RAW>(x, y, scale);
         if (DIAG) {
           const int e = 16 * A + j;
           x = (e < lo || e >= hi) ? -INFINITY : x;
@@ -1790,6 +1801,10 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
   int nw = 4;  // attn_fwd2_kernel: 4 waves x 32 query rows
   auto kfn = mo.q ? attn_fwd2_kernel<true, false> : attn_fwd2_kernel<false, false>;
 #ifdef OSPO_ABLATION
+  if (getenv("OSPO_ATTN_RAW_SCORES")) {  // unrounded scores (parity measurement, verdict r4 item 2c)
+    if (mo.q) return OSPO_ERR_UNSUPPORTED;
+    kfn = attn_fwd2_kernel<false, false, 0, true>;
+  }
   if (getenv("OSPO_ATTN_FWD_PIPE")) kfn = mo.q ? attn_fwd2_kernel<true, true> : attn_fwd2_kernel<false, true>;
   if (const char* e = getenv("OSPO_ATTN_FWD2_DBG")) {  // decomposition (results invalid)
     const int v = atoi(e);
@@ -1928,6 +1943,12 @@ static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
                        n_chunks);
     OSPO_CHECK_LAUNCH();
     if (dkdv3 && mo.q) dkdv3 = attn_bwd_dkdv3_kernel<4, 0, true>;  // (the ablation forms are refused above)
+#ifdef OSPO_ABLATION
+    if (getenv("OSPO_ATTN_RAW_SCORES")) {  // unrounded scores, as the forward's (parity measurement)
+      if (mo.q || nwd != 4 || !dkdv3) return OSPO_ERR_UNSUPPORTED;
+      dkdv3 = attn_bwd_dkdv3_kernel<4, 0, false, true>;
+    }
+#endif
     if (dkdv3)
       hipLaunchKernelGGL(dkdv3, dim3(S * n_heads * ((T + 16 * nwd - 1) / (16 * nwd))), dim3(64 * nwd), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
                          (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc, rs,
