@@ -72,11 +72,15 @@ def correctness():
         b2 = rnd(N, K2) if K2 else None
         bias, res = rnd(N, scale=0.5), rnd(M, N, scale=0.5)
 
-        def g(a=a, b=b, a2=a2, b2=b2, out=out, bias=bias, res=res):
-            out.fill_(7)
-            ops.gemm_nt(a, b, out, a2=a2, b2=b2, alpha=0.75, bias=bias, residual=res)
-            return out.clone()
-        ok &= check(f"rnd+bias+res M{M} N{N} K{K} K2{K2}", g)
+        # (pinned splits: since the round-4 refit the two kernels' cost models may pick different tail splits,
+        # i.e. different fp32 summation orders -- M4608 N4096 K2048: SP8 4, w4 3 -- so the default split is
+        # not a bit-equality case; round 5)
+        for sp in (1, 3):
+            def g(a=a, b=b, a2=a2, b2=b2, out=out, bias=bias, res=res, sp=sp):
+                out.fill_(7)
+                ops.gemm_nt(a, b, out, a2=a2, b2=b2, alpha=0.75, bias=bias, residual=res, split=sp)
+                return out.clone()
+            ok &= check(f"rnd+bias+res split{sp} M{M} N{N} K{K} K2{K2}", g)
         for sp in (2, 3, 5):
             def h(a=a, b=b, a2=a2, b2=b2, out=out, sp=sp):
                 out.fill_(7)
