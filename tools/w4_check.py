@@ -81,7 +81,9 @@ def correctness():
                 ops.gemm_nt(a, b, out, a2=a2, b2=b2, alpha=0.75, bias=bias, residual=res, split=sp)
                 return out.clone()
             ok &= check(f"rnd+bias+res split{sp} M{M} N{N} K{K} K2{K2}", g)
-        for sp in (2, 3, 5):
+        # (splits both kernels honour: w4 caps the tail pieces at 25/32 of the CUs, so a pinned 5 on a 48-tile tail
+        # runs as 4 there and as 5 in SP8 -- a different summation order, not a bit-equality case; round 5)
+        for sp in (2, 3, 4):
             def h(a=a, b=b, a2=a2, b2=b2, out=out, sp=sp):
                 out.fill_(7)
                 ops.gemm_nt(a, b, out, a2=a2, b2=b2, split=sp)
