@@ -933,12 +933,13 @@ __device__ __forceinline__ void v5_tile(int L, int tiles_m, int tiles_n, int& m0
 // tiles stay bf16 (16 bf16 MFMAs per phase).
 // bf16 epilogue, second half: the tile's rounded products staged in LDS as [256][CPITCH] rows ->
 // RoPE / residual -> 16-B coalesced global stores (shared by the 256x256 kernels)
-// GEMM outputs (bf16 tiles, split-K fp32 partials) are stored non-temporally (round 5): no later access in the
-// launch re-reads them, and 'nt' stores leave the L2 to the operands being streamed.  Measured on the plain
-// epilogue (profiles/r05/gemm_epi_ab.log, variant 2): gu_fwd 613 -> 595 us, gh2_fwd 423 -> 413, down_dx 326 -> 320,
-// the others within noise.  A library built with -DOSPO_GEMM_NT_STORES=0 stores them plainly (step A/B).
+// GEMM outputs (bf16 tiles, split-K fp32 partials) are stored plainly.  Non-temporal stores (-DOSPO_GEMM_NT_STORES=1)
+// win in isolation -- no later access in the launch re-reads the tile, and 'nt' leaves the L2 to the streamed
+// operands (profiles/r05/gemm_epi_ab.log, variant 2: gu_fwd 613 -> 595 us, gh2_fwd 423 -> 413, down_dx 326 -> 320)
+// -- but lose 0.65% on the step (profiles/r05/step_ab_r5i.txt: 35.13 vs 35.36 pairs/s, both rounds): the next
+// kernel (SwiGLU, the fixup, the norm) re-reads the output, and plain stores leave it in the MALL for it.
 #ifndef OSPO_GEMM_NT_STORES
-#define OSPO_GEMM_NT_STORES 1
+#define OSPO_GEMM_NT_STORES 0
 #endif
 template <typename T>
 __device__ __forceinline__ void gemm_out_store(T* p, const T& v) {
