@@ -663,6 +663,140 @@ struct DlArgs {
   int part_bytes;
 };
 
+// The end of a decode-Linear workgroup (dlin_kernel, dlin_pipe_kernel): the split sum, then the consumer.
+// The workgroup holds the partials accs[u] of the nz consecutive splits z0 .. z0 + nz - 1 of row group grp.
+// nz < splits: each is stored write-through (sc1) at its split's slot, the workgroup takes nz tickets on the
+// group's counter, and the last arriver sums all splits' partials in split order; nz == splits: the same sum
+// in registers.  Either way every output is summed as ((0 + p_0) + p_1) + ..., the reduce kernels' order.
+template <int NT, int EPI, int U>
+__device__ __forceinline__ void dlin_finish(const DlArgs& a, const f32x4 (&accs)[U][NT], int nz, int grp, int z0,
+                                            int splits, int ngroups, char* xs, float (*ssr)[32], unsigned* flag) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int n = grp * G3_ROWS + wave * 16 + l16;
+  const int R = a.R;
+  const int nb = n >> 4, NB = ngroups * G3_WAVES;
+  const bool ticket = splits > 1 && nz < splits;
+  f32x4 acc[NT];
+  if (ticket) {
+    const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, a.part_bytes, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (u < nz) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, accs[u][j]), rsP,
+                                                 (uint32_t)(((((z0 + u) * NB + nb) * NT + j) * 64 + lane) * 16), 0, 16);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(a.cnt + grp, (unsigned)nz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (t + (unsigned)nz == (unsigned)splits) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (*flag == 0u) return;
+    // no instruction: keeps the sc1 partial loads below the ticket (sc1 stores drained before it, sc1 loads
+    // after it: the hand-off Valid form of cdna_hip_programming.md, where this replaces the agent-scope acquire)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int zs = 0; zs < splits; zs += 8) {  // 8 partials in flight, summed in split order
+        u32x4 pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (zs + u < splits)
+            pv[u] = __builtin_amdgcn_raw_buffer_load_b128(rsP, (uint32_t)(((((zs + u) * NB + nb) * NT + j) * 64 + lane) * 16),
+                                                          0, 16);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (zs + u < splits) v += __builtin_bit_cast(f32x4, pv[u]);
+      }
+      acc[j] = v;
+    }
+  } else if (splits > 1) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u < nz) v += accs[u][j];
+      acc[j] = v;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = accs[0][j];
+  }
+  if constexpr (EPI == DL_PLAIN) {
+    float ssq[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * j + 4 * g + q;
+        float y = acc[j][q] + (a.bias ? bf2f(a.bias[n]) : 0.f);
+        if (a.gelu) y = gelu_erf(round_bf(y));
+        if (a.res) y = round_bf(y) + bf2f(a.res[(long)(r < R ? r : 0) * a.ldr + n]);
+        y = round_bf(y);
+        if (r < R) a.out[(long)r * a.ldo + n] = f2bf(y);
+        ssq[j][q] = dpp_sum16(y * y);  // over the wave's 16 columns
+      }
+    if (a.ss_out) {
+      if (l16 == 0) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ssr[wave][16 * j + 4 * g + q] = ssq[j][q];
+      }
+      __syncthreads();
+      if (threadIdx.x < 16 * NT) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < G3_WAVES; ++w) s += ssr[w][threadIdx.x];
+        a.ss_out[grp * 32 + threadIdx.x] = s;
+      }
+    }
+  } else {
+    // the group's 128 columns x 16 NT rows, bf16-rounded sums, through LDS (the x staging is free)
+    float* ep = reinterpret_cast<float*>(xs);
+    __syncthreads();  // (dlin_pipe_kernel: every wave is past its last chunk's LDS reads)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ep[(16 * j + 4 * g + q) * 129 + wave * 16 + l16] = round_bf(acc[j][q]);
+    __syncthreads();
+    if constexpr (EPI == DL_KV) {
+      const int hs = grp, which = hs / a.H, h = hs % a.H;
+      const int p = *a.pos;
+      if (p < a.Tmax) {
+        for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
+          const int r = it >> 6, d = it & 63;
+          const float x1 = ep[r * 129 + d], x2 = ep[r * 129 + d + 64];
+          float o1 = x1, o2 = x2;
+          if (which < 2) {  // rotate-half RoPE, rounded per op as kv_store_kernel
+            const float c = bf2f(a.cs[(long)p * 64 + d]), sv = bf2f(a.sn[(long)p * 64 + d]);
+            o1 = round_bf(x1 * c) + round_bf(-x2 * sv);
+            o2 = round_bf(x2 * c) + round_bf(x1 * sv);
+          }
+          bf16* dst = which == 0 ? a.out + (long)r * a.ldo + h * HD
+                                 : (which == 1 ? a.kc : a.vc) + (((long)r * a.H + h) * a.Tmax + p) * HD;
+          dst[d] = f2bf(o1);
+          dst[d + 64] = f2bf(o2);
+        }
+      }
+    } else {
+      for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
+        const int r = it >> 6, c = it & 63;
+        const float gt = ep[r * 129 + c], up = ep[r * 129 + 64 + c];
+        a.out[(long)r * a.ldo + 64 * grp + c] = f2bf(round_bf(silu(gt)) * up);
+      }
+    }
+  }
+  if (ticket && threadIdx.x == 0) __hip_atomic_store(a.cnt + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NT, int EPI, bool NORM>
 __global__ __launch_bounds__(64 * G3_WAVES) void dlin_kernel(const DlArgs a) {
   static_assert(16 * NT * G2_PITCH >= 16 * NT * 129 * 4, "epilogue tile fits the x staging");
@@ -756,106 +890,168 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_kernel(const DlArgs a) {
     }
     __syncthreads();
   }
-  const int nb = n >> 4, NB = gridDim.x * G3_WAVES;
-  if (splits > 1) {
-    const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc((void*)a.part, 0, a.part_bytes, 0x00020000);
+  f32x4 accs[1][NT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j]), rsP,
-                                             (uint32_t)((((z * NB + nb) * NT + j) * 64 + lane) * 16), 0, 16);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned t = __hip_atomic_fetch_add(a.cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag = (t == (unsigned)splits - 1u) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (flag == 0u) return;
-    // no instruction: keeps the sc1 partial loads below the ticket (sc1 stores drained before it, sc1 loads
-    // after it: the hand-off Valid form of cdna_hip_programming.md, where this replaces the agent-scope acquire)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int j = 0; j < NT; ++j) accs[0][j] = acc[j];
+  dlin_finish<NT, EPI, 1>(a, accs, 1, blockIdx.x, z, splits, gridDim.x, xs, ssr, &flag);
+}
+
+// Pipelined decode Linear (round 5, verdict r4 item 8).  dlin_kernel's workgroup loads a 512-k chunk, waits,
+// computes, and only then loads the next: every chunk pays a full memory round trip, and a launch is one or
+// two such rounds of one-shot workgroups (q|k|v 26.6 us for 100 MB, gate|up 41.0 us for 180 MB, down 23.3 us
+// for 90 MB, cold weights; warm in the Infinity Cache only 5-10 % faster: tools/dlin_warm_ab.py,
+// profiles/r05/dlin_warm_ab.log).  Here a workgroup (grid ngroups x splits / U, at most one per CU: two
+// register sets) owns the U consecutive splits z0 = U blockIdx.y .. of its row group and streams their chunks
+// with the NEXT chunk's x rows (a second LDS image) and weight fragments (a second register set, 16 per wave)
+// in flight under the current chunk's MFMAs.  Per split the MFMA order is dlin_kernel's; the splits' partials
+// stay in registers and are summed in split order (dlin_finish): outputs bit-identical to dlin_kernel's.
+// Needs K % kper == 0 and splits % U == 0 (host).  All LDS in one array (a second __shared__ object can make
+// hipcc drain the LDS-DMA before every LDS read: cdna_hip_programming.md section 5, trap (a)).
+template <int NT, int EPI, bool NORM, int U>
+__global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a) {
+  constexpr int XB = 16 * NT * G2_PITCH;  // one x image: 16 NT rows x 512 k (padded pitch)
+  constexpr int SST = NORM ? 1024 : 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * XB + (32 + SST + G3_WAVES * 32 + 4) * 4];
+  float* rs = reinterpret_cast<float*>(smem + 2 * XB);
+  float* sst = rs + 32;
+  float(*ssr)[32] = reinterpret_cast<float(*)[32]>(sst + SST);
+  unsigned* flag = reinterpret_cast<unsigned*>(sst + SST + G3_WAVES * 32);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int n = blockIdx.x * G3_ROWS + wave * 16 + l16;
+  const int splits = gridDim.y * U, z0 = blockIdx.y * U;
+  const int K = a.K, R = a.R, kper = a.kper;
+  const int cpu = (kper + G2_KC - 1) / G2_KC;  // chunks per split (every split kper long: K % kper == 0)
+  const int C = U * cpu;                        // this workgroup's chunks
+  const bf16* wrow = a.W + ((long)(n >> 4) * (K >> 5) * 64 + lane) * 8;
+  float ssv[2] = {0.f, 0.f};
+  if constexpr (NORM) {  // issued first: the first chunk's vmcnt(16) covers them (as dlin_kernel)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int z0 = 0; z0 < splits; z0 += 8) {  // 8 partials in flight, summed in split order
-        u32x4 pv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (z0 + u < splits)
-            pv[u] = __builtin_amdgcn_raw_buffer_load_b128(rsP, (uint32_t)(((((z0 + u) * NB + nb) * NT + j) * 64 + lane) * 16),
-                                                          0, 16);
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (z0 + u < splits) v += __builtin_bit_cast(f32x4, pv[u]);
-      }
-      acc[j] = v;
+    for (int u = 0; u < 2; ++u) {
+      const int i = threadIdx.x + 512 * u;
+      if (i < a.ss_groups * 32) ssv[u] = a.ss_in[i];
     }
   }
-  if constexpr (EPI == DL_PLAIN) {
-    float ssq[NT][4];
+  const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6;  // NORM: 8 columns x rows tr, tr + 8, ...
+  bf16x8 wv[2][16];
+  u32x4 lw[2] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+  auto chunk_k = [&](int c, int& kc, int& nsteps) __attribute__((always_inline)) {
+    const int u = c / cpu, i = c - u * cpu;
+    const int kb = (z0 + u) * kper;
+    kc = kb + i * G2_KC;
+    nsteps = min(G2_KC, kb + kper - kc) >> 5;
+  };
+  // chunk c's x rows -> image B, its norm weights, its 16 weight fragments per wave -> wv[B] (dlin_kernel's
+  // order: x DMA and norm weights first, so a vmcnt(16) after them leaves exactly the weights in flight)
+  auto issue = [&](auto b_c, int c) __attribute__((always_inline)) {
+    constexpr int B = decltype(b_c)::value;
+    int kc, nsteps;
+    chunk_k(c, kc, nsteps);
+    for (int r = wave; r < 16 * NT; r += G3_WAVES) {
+      const int rr = r < R ? r : R - 1;
+      const int col = min(kc + 8 * lane, K - 8);
+      __builtin_amdgcn_global_load_lds(a.X + (long)rr * a.ldx + col, (LDS_AS void*)(smem + B * XB + r * G2_PITCH), 16,
+                                       0, 0);
+    }
+    if constexpr (NORM) lw[B] = *reinterpret_cast<const u32x4*>(a.ln_w + min(kc + 8 * tc, K - 8));
+    asm volatile("" ::: "memory");
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int s = 0; s < 16; ++s) {
+      const bf16x8* wp = reinterpret_cast<const bf16x8*>(wrow + (long)((kc >> 5) + min(s, nsteps - 1)) * 512);
+#if OSPO_DLIN_NTW
+      wv[B][s] = __builtin_nontemporal_load(wp);
+#else
+      wv[B][s] = *wp;
+#endif
+    }
+  };
+  f32x4 accs[U][NT], acc[NT];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = 16 * j + 4 * g + q;
-        float y = acc[j][q] + (a.bias ? bf2f(a.bias[n]) : 0.f);
-        if (a.gelu) y = gelu_erf(round_bf(y));
-        if (a.res) y = round_bf(y) + bf2f(a.res[(long)(r < R ? r : 0) * a.ldr + n]);
-        y = round_bf(y);
-        if (r < R) a.out[(long)r * a.ldo + n] = f2bf(y);
-        ssq[j][q] = dpp_sum16(y * y);  // over the wave's 16 columns
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) accs[u][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  // chunk c from image / register set B; the next chunk goes to B ^ 1 before the MFMAs.  At the barrier only
+  // chunk c's loads are in flight, so __syncthreads()'s drain costs nothing here.  (A third stage, two chunks
+  // in flight, needs 3 x 64 weight registers and spilled at 256 VGPRs.)
+  auto body = [&](auto b_c, int c) __attribute__((always_inline)) {
+    constexpr int B = decltype(b_c)::value;
+    char* xs = smem + B * XB;
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk c's x rows (+ norm weights) landed
+    __syncthreads();
+    if constexpr (NORM) {
+      if (c == 0) {  // rstd of the 32 rows: the partials summed in group order
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (threadIdx.x + 512 * u < 1024) sst[threadIdx.x + 512 * u] = ssv[u];
+        __syncthreads();
+        if (threadIdx.x < 32) {
+          float s = 0.f;
+          for (int q = 0; q < a.ss_groups; ++q) s += sst[q * 32 + threadIdx.x];
+          rs[threadIdx.x] = rsqrtf(s / (float)K + a.eps);
+        }
+        __syncthreads();
       }
-    if (a.ss_out) {
-      if (l16 == 0) {
+      float wf[8];
+      unpack8(lw[B], wf);
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
+      for (int i = 0; i < 2 * NT; ++i) {
+        const int r = tr + 8 * i;
+        u32x4* p = reinterpret_cast<u32x4*>(xs + r * G2_PITCH + tc * 16);
+        float f[8];
+        unpack8(*p, f);
+        const float rr = rs[r < R ? r : R - 1];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) ssr[wave][16 * j + 4 * g + q] = ssq[j][q];
+        for (int q = 0; q < 8; ++q) f[q] = wf[q] * round_bf(f[q] * rr);
+        *p = pack8(f);
       }
       __syncthreads();
-      if (threadIdx.x < 16 * NT) {
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < G3_WAVES; ++w) s += ssr[w][threadIdx.x];
-        a.ss_out[blockIdx.x * 32 + threadIdx.x] = s;
-      }
     }
-  } else {
-    // the group's 128 columns x 16 NT rows, bf16-rounded sums, through LDS (the x staging is free)
-    float* ep = reinterpret_cast<float*>(xs);
+    // the other image and register set were last read by chunk c - 1's MFMAs, before the barrier above
+    if (c + 1 < C) {
+      if constexpr (B == 0) issue(I1{}, c + 1);
+      else issue(I0{}, c + 1);
+    }
+    int kc, nsteps;
+    chunk_k(c, kc, nsteps);
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int s = 0; s < 16; ++s) {
+      if (s < nsteps) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ep[(16 * j + 4 * g + q) * 129 + wave * 16 + l16] = round_bf(acc[j][q]);
-    __syncthreads();
-    if constexpr (EPI == DL_KV) {
-      const int hs = blockIdx.x, which = hs / a.H, h = hs % a.H;
-      const int p = *a.pos;
-      if (p < a.Tmax) {
-        for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
-          const int r = it >> 6, d = it & 63;
-          const float x1 = ep[r * 129 + d], x2 = ep[r * 129 + d + 64];
-          float o1 = x1, o2 = x2;
-          if (which < 2) {  // rotate-half RoPE, rounded per op as kv_store_kernel
-            const float c = bf2f(a.cs[(long)p * 64 + d]), sv = bf2f(a.sn[(long)p * 64 + d]);
-            o1 = round_bf(x1 * c) + round_bf(-x2 * sv);
-            o2 = round_bf(x2 * c) + round_bf(x1 * sv);
-          }
-          bf16* dst = which == 0 ? a.out + (long)r * a.ldo + h * HD
-                                 : (which == 1 ? a.kc : a.vc) + (((long)r * a.H + h) * a.Tmax + p) * HD;
-          dst[d] = f2bf(o1);
-          dst[d + 64] = f2bf(o2);
+        for (int j = 0; j < NT; ++j) {
+          bf16x8 xf = *reinterpret_cast<const bf16x8*>(xs + (16 * j + l16) * G2_PITCH + (32 * s + 8 * g) * 2);
+          if (16 * j + l16 >= R) xf = bf16x8{};
+          acc[j] = MFMA(xf, wv[B][s], acc[j]);  // D[x row 4g+q][w row l16]
         }
       }
-    } else {
-      for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
-        const int r = it >> 6, c = it & 63;
-        const float gt = ep[r * 129 + c], up = ep[r * 129 + 64 + c];
-        a.out[(long)r * a.ldo + 64 * blockIdx.x + c] = f2bf(round_bf(silu(gt)) * up);
+    }
+    if (c - (c / cpu) * cpu == cpu - 1) {  // the split's last chunk: its partial enters a shift register
+#pragma unroll                               // (constant indices: a runtime index put accs in scratch)
+      for (int uu = U - 1; uu > 0; --uu)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) accs[uu][j] = accs[uu - 1][j];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        accs[0][j] = acc[j];
+        acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
+  };
+  issue(I0{}, 0);
+  for (int c = 0; c < C; c += 2) {
+    body(I0{}, c);
+    if (c + 1 < C) body(I1{}, c + 1);
   }
-  if (splits > 1 && threadIdx.x == 0) __hip_atomic_store(a.cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  f32x4 part[U][NT];  // split z0 + u's partial sits at accs[U - 1 - u]
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) part[u][j] = accs[U - 1 - u][j];
+  dlin_finish<NT, EPI, U>(a, part, U, blockIdx.x, z0, splits, gridDim.x, smem, ssr, flag);
 }
 
 #ifdef OSPO_ABLATION
@@ -1289,6 +1485,24 @@ int gemv3_kper(int N, int K) {
   return (kper + 31) / 32 * 32;
 }
 
+// dlin_pipe_kernel's splits per workgroup: the smallest U in {1, 2, 4} dividing splits that keeps the grid
+// within one workgroup per CU (its two register sets leave room for one 8-wave workgroup per CU); 0 = the
+// one-shot dlin_kernel.  The pipelined form is taken only where a split spans >= 2 chunks (gate|up: 4 splits
+// of 1024 k, down: 8 of 1376): with one chunk per split (q|k|v, o) it holds one chunk in flight per CU where
+// dlin_kernel's two resident workgroups hold two, and measured slower (q|k|v 26.8 -> 30.1 us, o equal;
+// gate|up 40.9 -> 38.3, down 23.2 -> 21.2: profiles/r05/dlin_pipe_ab.log).  all: every shape it fits (A/B).
+int dlin_pipe_units(int ngroups, int splits, int K, int kper, bool all = false) {
+  static int ncu[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (ncu[dev] == 0 && hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  if (K % kper != 0 || (!all && kper < 2 * G2_KC)) return 0;
+  for (int u = 1; u <= 4 && u <= splits; u *= 2)
+    if (splits % u == 0 && (long)ngroups * (splits / u) <= ncu[dev]) return u;
+  return 0;
+}
+
 }  // namespace
 
 extern "C" size_t ospo_decode_gemv_ws_bytes(int R, int N, int K) {
@@ -1427,27 +1641,42 @@ extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, 
   a.vc = (bf16*)v_cache; a.H = n_heads; a.Tmax = Tmax;
   a.cnt = (unsigned*)ws; a.part = (float*)((char*)ws + DL_CNT_BYTES); a.part_bytes = (int)(need - DL_CNT_BYTES);
   const bool norm = ss_in != nullptr;
-  // one workgroup per (row group, split); the ablation build's OSPO_DLIN_V2 selects the streaming form
-  // (~256 long-lived workgroups, bit-identical, 7 % slower per decode step: DESIGN.md section 9)
+  // the pipelined form (dlin_pipe_kernel, U splits per workgroup, at most one workgroup per CU) where the shape
+  // allows it, else one workgroup per (row group, split).  Ablation build: OSPO_DLIN_PIPE=0 runs dlin_kernel
+  // (the A/B), OSPO_DLIN_V2 the rejected streaming form (~256 long-lived workgroups)
   const int ngroups = N / G3_ROWS;
+  int U = dlin_pipe_units(ngroups, splits, K, kper);
+  bool v2 = false;
 #ifdef OSPO_ABLATION
   static const bool want_v2 = getenv("OSPO_DLIN_V2") != nullptr;
-  const bool v2 = want_v2 && (kper + G2_KC - 1) / G2_KC <= DL2_MAXC;
+  static const int pipe_env = getenv("OSPO_DLIN_PIPE") ? atoi(getenv("OSPO_DLIN_PIPE")) : -1;
+  if (pipe_env == 1) U = dlin_pipe_units(ngroups, splits, K, kper, true);  // A/B: every shape it fits
+  if (pipe_env == 0 || want_v2) U = 0;
+  v2 = want_v2 && (kper + G2_KC - 1) / G2_KC <= DL2_MAXC;
   const int G = std::max(1, (ngroups * splits + DL2_WGS - 1) / DL2_WGS), nsets = (ngroups + G - 1) / G;
-  const dim3 grid = v2 ? dim3(splits * nsets) : dim3(ngroups, splits);
-#define DLIN(NT_, EPI_)                                                                                              \
-  if (v2)                                                                                                            \
-    hipLaunchKernelGGL((norm ? dlin2_kernel<NT_, EPI_, true> : dlin2_kernel<NT_, EPI_, false>), grid,                \
+#define DLIN_V2(NT_, EPI_)                                                                                           \
+  if (v2) {                                                                                                          \
+    hipLaunchKernelGGL((norm ? dlin2_kernel<NT_, EPI_, true> : dlin2_kernel<NT_, EPI_, false>), dim3(splits * nsets), \
                        dim3(64 * G3_WAVES), 0, stream, a, splits, G, ngroups);                                       \
-  else                                                                                                               \
-    hipLaunchKernelGGL((norm ? dlin_kernel<NT_, EPI_, true> : dlin_kernel<NT_, EPI_, false>), grid,                  \
-                       dim3(64 * G3_WAVES), 0, stream, a)
+  } else
 #else
-  const dim3 grid(ngroups, splits);
-#define DLIN(NT_, EPI_)                                                                                             \
-  hipLaunchKernelGGL((norm ? dlin_kernel<NT_, EPI_, true> : dlin_kernel<NT_, EPI_, false>), grid, dim3(64 * G3_WAVES), \
-                     0, stream, a)
+#define DLIN_V2(NT_, EPI_)
 #endif
+#define DLIN_PIPE(NT_, EPI_, U_)                                                                                     \
+  hipLaunchKernelGGL((norm ? dlin_pipe_kernel<NT_, EPI_, true, U_> : dlin_pipe_kernel<NT_, EPI_, false, U_>),         \
+                     dim3(ngroups, splits / U_), dim3(64 * G3_WAVES), 0, stream, a)
+#define DLIN(NT_, EPI_)                                                                                              \
+  DLIN_V2(NT_, EPI_)                                                                                                 \
+  if (U == 1) {                                                                                                      \
+    DLIN_PIPE(NT_, EPI_, 1);                                                                                         \
+  } else if (U == 2) {                                                                                               \
+    DLIN_PIPE(NT_, EPI_, 2);                                                                                         \
+  } else if (U == 4) {                                                                                               \
+    DLIN_PIPE(NT_, EPI_, 4);                                                                                         \
+  } else {                                                                                                           \
+    hipLaunchKernelGGL((norm ? dlin_kernel<NT_, EPI_, true> : dlin_kernel<NT_, EPI_, false>), dim3(ngroups, splits),  \
+                       dim3(64 * G3_WAVES), 0, stream, a);                                                           \
+  }
 #define DLIN_NT(EPI_) \
   if (R <= 16) { DLIN(1, EPI_); } else { DLIN(2, EPI_); }
   if (epi == DL_PLAIN) {
@@ -1459,6 +1688,9 @@ extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, 
   }
 #undef DLIN_NT
 #undef DLIN
+#undef DLIN_PIPE
+#undef DLIN_V2
+  (void)v2;
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
