@@ -1353,16 +1353,32 @@ __global__ __launch_bounds__(256) void cfg_sample_kernel(const bf16* __restrict_
   const int nj = max(0, min(SMP_CHUNK, V - j0));
   float l[SMP_CHUNK];
   float m = -INFINITY;
-#pragma unroll 8
-  for (int q = 0; q < SMP_CHUNK; ++q) {
-    float v = -INFINITY;
-    if (q < nj) {
-      const float c = bf2f(lc[j0 + q]), un = bf2f(lu[j0 + q]);
-      v = round_bf(un + round_bf(cfg_w * round_bf(c - un)));
-      if (temp != 1.f) v = round_bf(v / temp);
+  const bool vec = nj == SMP_CHUNK && ((ldl | V) & 7) == 0 && ((uintptr_t)logits & 15) == 0;  // 16-B loads: 8 per row, not 64
+#pragma unroll
+  for (int q8 = 0; q8 < SMP_CHUNK; q8 += 8) {
+    float c8[8], u8[8];
+    if (vec) {
+      unpack8(*reinterpret_cast<const u32x4*>(lc + j0 + q8), c8);
+      unpack8(*reinterpret_cast<const u32x4*>(lu + j0 + q8), u8);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        c8[e] = q8 + e < nj ? bf2f(lc[j0 + q8 + e]) : 0.f;
+        u8[e] = q8 + e < nj ? bf2f(lu[j0 + q8 + e]) : 0.f;
+      }
     }
-    l[q] = v;
-    m = fmaxf(m, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = q8 + e;
+      float v = -INFINITY;
+      if (q < nj) {
+        const float c = c8[e], un = u8[e];
+        v = round_bf(un + round_bf(cfg_w * round_bf(c - un)));
+        if (temp != 1.f) v = round_bf(v / temp);
+      }
+      l[q] = v;
+      m = fmaxf(m, v);
+    }
   }
   m = wave_max(m);
   if (lane == 0) red[wave] = m;
@@ -1390,27 +1406,54 @@ __global__ __launch_bounds__(256) void cfg_sample_kernel(const bf16* __restrict_
   }
   csum[t] = cs;
   __syncthreads();
-  if (t == 0) {  // the chunk sums in order: total and the chunk holding the target
-    float tot = 0.f;
-    for (int c = 0; c < 256; ++c) tot += csum[c];
-    const float target = u[(long)step * B + b] * tot;
-    float run = 0.f, run_last = 0.f;
-    int c = 0, last = 0;
-    for (; c < 256; ++c) {
-      if (run + csum[c] > target) break;
-      if (csum[c] > 0.f) {
-        last = c;
-        run_last = run;
+  if (wave == 0) {
+    // The chunk sums in order: the running sum before every chunk (pre) and the total, as ONE serial chain of
+    // fp32 adds in chunk order -- the values of a sequential loop over chunks 0..255, bit for bit -- but with
+    // each sum broadcast from its lane by v_readlane into the add (one wave, register operands) instead of a
+    // dependent LDS load per chunk in one thread (round 5: that loop, twice over 256 chunks, was most of the
+    // kernel's 64 us).  Lane l holds chunks 4 l .. 4 l + 3.
+    float cv[4], pre[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cv[i] = csum[4 * lane + i];
+    float run = 0.f;
+#pragma unroll
+    for (int L = 0; L < 64; ++L) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float ci = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cv[i]), L));
+        if (lane == L) pre[i] = run;
+        run += ci;
       }
-      run += csum[c];
     }
-    if (c == 256) {  // target at the very top (rounding): the last chunk with mass
-      c = last;
-      run = run_last;
+    const float tot = run;
+    const float target = u[(long)step * B + b] * tot;
+    // the first chunk c with pre[c] + csum[c] > target (the loop's break), else the last chunk with mass
+    int fi = -1, li = -1;
+#pragma unroll
+    for (int i = 3; i >= 0; --i)
+      if (pre[i] + cv[i] > target) fi = i;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (cv[i] > 0.f) li = i;
+    const unsigned long long hit = __ballot(fi >= 0), mass = __ballot(li >= 0);
+    int src, idx;
+    if (hit) {
+      src = __builtin_ctzll(hit);
+      idx = __shfl(fi, src);
+    } else if (mass) {  // target at the very top (rounding): the last chunk with mass
+      src = 63 - __builtin_clzll(mass);
+      idx = __shfl(li, src);
+    } else {
+      src = 0;
+      idx = 0;
     }
-    pick[0] = c;
-    red[0] = run;
-    red[1] = target;
+    const float pv = idx == 0 ? pre[0] : (idx == 1 ? pre[1] : (idx == 2 ? pre[2] : pre[3]));
+    const float run_at = __shfl(pv, src);
+    if (lane == 0) {
+      pick[0] = 4 * src + idx;
+      red[0] = run_at;
+      red[1] = target;
+    }
   }
   __syncthreads();
   if (t == pick[0]) {
