@@ -55,7 +55,8 @@ int ospo_abi_version(void);
  * bytes) holds the partials; NULL or too small = no split.  The caller owns it; calls
  * sharing a ws must be stream-ordered.  tail_split: 0 = the library's cost model, 1 = never
  * split, 2..8 = that split (bounded by one round of pieces and K / 4 K-tiles per piece).
- * The split changes the order of the fp32 sum only. */
+ * The split changes the order of the fp32 sum only.  Partials use whole 256-KiB tiles of ws
+ * only (bytes past them are left alone). */
 int ospo_gemm_nt_bf16(const void* A, int lda, const void* B, int ldb, int M, int N, int K,
                       const void* A2, int lda2, const void* B2, int ldb2, int K2, float alpha,
                       const void* bias, const void* residual, int ldr, void* C, int ldc,

@@ -1898,10 +1898,12 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(const GemmArgs args, 
   f32x4 lo = f32x4{0.f, 0.f, 0.f, 0.f}, hi = lo;
   fixup_sum(ws + (long)tile * split * 65536 + r * 256 + c, split, lo, hi);
   float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  if (args.alpha != 1.f || args.bias) {  // the main epilogues' expression, v * alpha + b in one (contracted) step
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    v[q] *= args.alpha;
-    if (args.bias) v[q] += bf2f(args.bias[n0 + c + q]);
+    for (int q = 0; q < 8; ++q) {
+      const float bq = args.bias ? bf2f(args.bias[n0 + c + q]) : 0.f;
+      v[q] = v[q] * args.alpha + bq;
+    }
   }
   u32x4 o;
 #pragma unroll
@@ -2009,6 +2011,7 @@ SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus
   return pl;
 }
 
+constexpr size_t W4_CNT_BYTES = 4096;  // the w4 tail's arrival counters at the END of the split-K workspace
 #include "gemm_w4.h"
 
 // The 4-wave hand-scheduled kernel (gemm_w4.h) when the shape fits it: bf16, <= 2 LoRA extension tiles,
@@ -2042,10 +2045,23 @@ int launch_w4(const GemmArgs& a_in, hipStream_t s, const SplitOpts& so) {
   }
   if (pl.tail && ntot < 4) return OSPO_ERR_UNSUPPORTED;
   const int grid = pl.dp + pl.tail * pl.split;
+  // ablation build, OSPO_GEMM_INL=1: the tail's split-K combine inside the launch (round 5, measured and rejected:
+  // 33.40 / 33.44 pairs/s against 34.55 / 34.62 with the fixup launch on one box, GEMM 403 vs 386 us per launch,
+  // profiles/r05/gemm_inlaunch_ab.txt -- the last arriver reads (split - 1) x 256 KiB of partials at one CU's rate
+  // and every piece's write-through stores are slower than the fixup's streaming), when the workspace carries
+  // the arrival counters past its whole partial tiles (ws_bytes = n x 256 KiB + W4_CNT_BYTES, zero at allocation,
+  // left zero by every call; ops.gemm_workspace allocates them)
+  unsigned* cnt = nullptr;
+#ifdef OSPO_ABLATION
+  static const bool want_inl = getenv("OSPO_GEMM_INL") && atoi(getenv("OSPO_GEMM_INL")) == 1;
+  if (want_inl && pl.tail && so.ws && so.ws_bytes % (65536 * sizeof(float)) == W4_CNT_BYTES &&
+      pl.tail <= (int)(W4_CNT_BYTES / sizeof(unsigned)))
+    cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(so.ws) + so.ws_bytes - W4_CNT_BYTES);
+#endif
   hipLaunchKernelGGL((gemm_nt_w4_kernel<DROP, DBG, V, MX>), dim3(grid), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split,
-                     so.ws, g_v5_gm);
+                     so.ws, g_v5_gm, cnt);
   OSPO_CHECK_LAUNCH();
-  if (pl.tail) {
+  if (pl.tail && !cnt) {
     hipLaunchKernelGGL(splitk_fixup_kernel, dim3(pl.tail * 32), dim3(256), 0, s, a, tm, tn, pl.dp, pl.split,
                        (const float*)so.ws, g_v5_gm);
     OSPO_CHECK_LAUNCH();

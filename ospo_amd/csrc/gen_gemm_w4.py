@@ -559,6 +559,20 @@ def acc_reader():
             "  switch (n) {\n" + "\n".join(cases) + "\n    default: break;\n  }\n  return f32x4{x, y, z, w};\n}\n")
 
 
+def acc_writer():
+    """w4_acc_set(N, v): accumulator block N of a[0:255] := v (round 5: the in-launch split-K combine writes the
+    summed tile back before the epilogue); N folds to a constant.  The trailing s_nop keeps a later
+    v_accvgpr_read of the same registers clear of the write."""
+    cases = []
+    for n in range(64):
+        b = 4 * n
+        cases.append(f'    case {n}: asm volatile("v_accvgpr_write_b32 a{b}, %0\\n\\tv_accvgpr_write_b32 a{b + 1}, %1\\n\\t'
+                     f'v_accvgpr_write_b32 a{b + 2}, %2\\n\\tv_accvgpr_write_b32 a{b + 3}, %3\\n\\ts_nop 1" '
+                     f':: "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]) : "a{b}", "a{b + 1}", "a{b + 2}", "a{b + 3}"); break;')
+    return ("__device__ __forceinline__ void w4_acc_set(int n, const f32x4& v) {\n  switch (n) {\n" + "\n".join(cases) +
+            "\n    default: break;\n  }\n}\n")
+
+
 def stage_fn():
     """w4_stage_bf16: every accumulator block rounded to bf16 (v_cvt_pk_bf16_f32, RNE, as the C++ epilogue's
     pack2) and written to the epilogue's LDS staging rows (ml * 528 + nl * 2; %[sb] = this lane's block-(0,0)
@@ -581,7 +595,7 @@ def stage_fn():
 
 
 def main(out):
-    parts = [HEADER, acc_reader(), stage_fn()]
+    parts = [HEADER, acc_reader(), acc_writer(), stage_fn()]
     for E in (0, 1, 2):
         parts.append(asm_fn(f"w4_plain{E}", prog_plain(E), False))
     for E in (1, 2):

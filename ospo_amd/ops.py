@@ -86,8 +86,10 @@ def gemm_ws_bytes(M: int, N: int, K: int, K2: int = 0, mx: bool = False, split: 
 def gemm_workspace(device=None, stream=None) -> torch.Tensor:
     """The split-K workspace the GEMM wrappers pass when the caller gives none: one per (device,
     stream), so GEMMs that share it are stream-ordered.  The library splits at most one round of
-    tail pieces (tail x split <= CUs), so CUs x 256 KiB covers every shape; allocated once, on
-    the stream that uses it (the caching allocator reuses freed memory stream-ordered)."""
+    tail pieces (tail x split <= 25/32 CUs in the bf16 kernel), so CUs x 256 KiB covers every shape
+    plus 4 KiB of zeroed arrival counters that only the ablation library's in-launch tail combine reads
+    (OSPO_GEMM_INL=1, measured and rejected: DESIGN.md section 11b).  Allocated once, on the stream that uses it (the caching
+    allocator reuses freed memory stream-ordered)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     st = torch.cuda.current_stream(dev) if stream is None else stream
     key = (dev.index, st.cuda_stream)
@@ -95,7 +97,7 @@ def gemm_workspace(device=None, stream=None) -> torch.Tensor:
     if ws is None:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         with torch.cuda.stream(st):
-            ws = _GEMM_WS[key] = torch.empty(cus * 65536, dtype=torch.float32, device=dev)
+            ws = _GEMM_WS[key] = torch.zeros(cus * 65536 + 1024, dtype=torch.float32, device=dev)
     return ws
 
 

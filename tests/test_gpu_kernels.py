@@ -999,3 +999,4 @@ def test_lora_wgrad_dropout_recompute_equals_stored_mask():
     ops().lora_wgrad(x, g, out, mode=0, s_cols=48, splits=1, dropout=(seed, p))
     assert torch.equal(out, ref)
     assert relerr(out, (g[:, :48].float().T @ xd.float())) < 1e-5
+
