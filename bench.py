@@ -177,7 +177,8 @@ def bench_t2i(args):
     w = synthetic_weights(dims, dev, seed=0, lora_seed=1)
     vw = {**synthetic_vq_weights(0), **synthetic_vq_decoder_weights(1)}  # gen_vision_model (pixel decoder)
     gen = T2IGenerator(dims, w, device=dev, max_batch=B, max_prompt_len=Lp, n_img_tokens=N, cfg_weight=5.0,
-                       temperature=1.0, vq_weights=vw, fused_layers=not args.t2i_unfused)
+                       temperature=1.0, vq_weights=vw, fused_layers=not args.t2i_unfused,
+                       mlp_one_launch=not args.t2i_two_launch_mlp)
     del w
     torch.cuda.empty_cache()
     g = torch.Generator().manual_seed(0)
@@ -224,7 +225,8 @@ def bench_t2i(args):
         "config": {"workload": f"Janus-Pro-{'7B' if dims.n_layers == 30 else str(dims.n_layers) + 'L'} T2I generation, "
                                f"{B} prompts x (cond, uncond), {N} image tokens, hipGraph decode step, "
                                "VQ-16 pixel decode to uint8 384x384",
-                   "prompt_len_max": Lp, "decode_steps": N - 1, "tokens_per_s": round(value * N, 1),
+                   "prompt_len_max": Lp, "decode_steps": N - 1,
+                   "decode_mlp": "one launch" if gen.mlp_one_launch else "two launches", "tokens_per_s": round(value * N, 1),
                    "vq_decode_ms_per_batch": round(decode_ms, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                      "frac": round(achieved / 8000.0, 4), "traffic": t2i_traffic(nbytes) if gen.fused else None,
@@ -514,6 +516,8 @@ def main():
     ap.add_argument("--t2i-batch", type=int, default=16)       # parallel_size: prompts (x2 rows with CFG)
     ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
     ap.add_argument("--t2i-unfused", action="store_true")      # A/B: the round-2 decode step (GEMV + split-sum + norm launches)
+    ap.add_argument("--t2i-two-launch-mlp", action="store_true",
+                    help="t2i: the decode MLP as two launches (the round-4/5 form) instead of ops.decode_mlp (A/B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wrapper", action="store_true")  # skip the drop-in wrapper sub-measurement
     ap.add_argument("--no-kernel-timer", action="store_true")

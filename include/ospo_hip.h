@@ -451,6 +451,18 @@ int ospo_decode_linear(const void* W, const void* X, int ldx, int R, int N, int 
                        const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* pos_dev,
                        const void* rope_cos, const void* rope_sin, void* k_cache, void* v_cache, int n_heads,
                        int Tmax, void* ws, size_t ws_bytes, hipStream_t stream);
+/* The decode MLP in ONE launch (round 5): ospo_decode_linear(xmid, W_gu, h, epi 2, norm = (ss_in, ln_w,
+ * eps)) then ospo_decode_linear(h, W_down, out, epi 0, residual = xmid, ss_out), with the same outputs bit
+ * for bit.  The down workgroups issue their first weights while the gate|up workgroups finish, then wait for
+ * the h columns they read: flags (>= 2F / 128 words, ZERO the first time they are used with a given
+ * (*step_dev, layer) pair -- a value is the epoch step * 64 + layer + 1 of the call that wrote it) and tmo
+ * (set to nonzero if a wait gave up: the outputs are then invalid).  ws: ospo_decode_linear's workspace for
+ * the down product (>= ospo_decode_linear_ws_bytes(R, D, F)).  OSPO_ERR_UNSUPPORTED when the shapes do not
+ * map onto the one-launch form (the caller runs the two launches). */
+int ospo_decode_mlp(const void* W_gu, const void* W_down, const void* xmid, int ldx, int R, int D, int F,
+                    const float* ss_in, int ss_groups, const void* ln_w, float eps, void* h, int ldh, void* out,
+                    int ldo, float* ss_out, const int* step_dev, int layer, unsigned* flags, unsigned* tmo,
+                    void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* ------------------------------------------------------- VQ image tokenizer ---
  * janus/models/vq_model.py Encoder (:46-124) + quant_conv + VectorQuantizer

@@ -661,7 +661,23 @@ struct DlArgs {
   float* part;
   unsigned* cnt;
   int part_bytes;
+  // dmlp_kernel (round 5): h publish / consume flags, one per gate|up row group, tagged with the epoch
+  // (*epoch_step) * 64 + epoch_layer + 1 of this call; tmo: set when a consumer gives up waiting
+  unsigned* hflag = nullptr;
+  const int* epoch_step = nullptr;
+  int epoch_layer = 0;
+  unsigned* tmo = nullptr;
 };
+
+// Round 5, decode MLP in one launch (dmlp_kernel): the gate|up workgroups PUBLISH their group's h columns
+// (write-through stores, then the group's flag = epoch); the down workgroups CONSUME them: their first chunk's
+// weights are issued before they wait for the flags of the gate|up groups their K range reads.
+enum { DL_ROLE_PLAIN = 0, DL_ROLE_PUB = 1, DL_ROLE_CONS = 2 };
+constexpr unsigned DL_SPIN_LIMIT = 1u << 22;  // bounded wait (~1 s): a give-up sets the error word, never hangs
+
+__device__ __forceinline__ unsigned dl_epoch(const DlArgs& a) {
+  return (unsigned)(*a.epoch_step) * 64u + (unsigned)a.epoch_layer + 1u;  // never 0 (the flags' reset value)
+}
 
 // The end of a decode-Linear workgroup (dlin_kernel, dlin_pipe_kernel): the split sum, then the consumer.
 // The workgroup holds the partials accs[u] of the nz consecutive splits z0 .. z0 + nz - 1 of row group grp.
@@ -786,6 +802,21 @@ __device__ __forceinline__ void dlin_finish(const DlArgs& a, const f32x4 (&accs)
           dst[d + 64] = f2bf(o2);
         }
       }
+    } else if (a.hflag) {
+      // dmlp_kernel's producer: 8 columns per thread as one 16-B write-through store (the same rounding as the
+      // scalar path below), every storing wave drained, the barrier, then this group's flag = epoch (R1 publish)
+      const __amdgpu_buffer_rsrc_t rsH =
+          __builtin_amdgcn_make_buffer_rsrc((void*)a.out, 0, (int)((long)R * a.ldo * 2), 0x00020000);
+      for (int it = threadIdx.x; it < R * 8; it += 64 * G3_WAVES) {
+        const int r = it >> 3, c8 = (it & 7) * 8;
+        float hv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[e] = round_bf(silu(ep[r * 129 + c8 + e])) * ep[r * 129 + 64 + c8 + e];
+        __builtin_amdgcn_raw_buffer_store_b128(pack8(hv), rsH, (uint32_t)(((long)r * a.ldo + 64 * grp + c8) * 2), 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(a.hflag + grp, dl_epoch(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
         const int r = it >> 6, c = it & 63;
@@ -907,11 +938,41 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_kernel(const DlArgs a) {
 // stay in registers and are summed in split order (dlin_finish): outputs bit-identical to dlin_kernel's.
 // Needs K % kper == 0 and splits % U == 0 (host).  All LDS in one array (a second __shared__ object can make
 // hipcc drain the LDS-DMA before every LDS read: cdna_hip_programming.md section 5, trap (a)).
-template <int NT, int EPI, bool NORM, int U>
-__global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a) {
+// LDS of dlin_pipe_body: two x images, then rstd, the ss partials (NORM), the ss_out rows, the ticket flag
+template <int NT>
+constexpr int dl_pipe_lds(bool norm) {
+  return 2 * 16 * NT * G2_PITCH + (32 + (norm ? 1024 : 4) + G3_WAVES * 32 + 4) * 4;
+}
+
+// the gate|up groups g0 .. g1 - 1 published with this call's epoch: wave 0 polls (one flag per lane), then
+// the agent-scope acquire, then the workgroup's barrier (cdna_hip_programming.md Guideline 16, R1 consume)
+__device__ __forceinline__ void dl_wait_flags(const DlArgs& a, int g0, int g1) {
+  if (threadIdx.x < 64) {
+    const unsigned ep = dl_epoch(a);
+    const int lane = threadIdx.x;
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+      for (int g = g0 + lane; g < g1; g += 64)
+        ok &= __hip_atomic_load(a.hflag + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep;
+      if (__all(ok)) break;
+      if (++spins > DL_SPIN_LIMIT) {
+        if (lane == 0) __hip_atomic_store(a.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate done before the barrier releases the readers
+  }
+  __syncthreads();
+}
+
+template <int NT, int EPI, bool NORM, int U, int ROLE = DL_ROLE_PLAIN>
+__device__ __forceinline__ void dlin_pipe_body(const DlArgs& a, int gx, int gy, int ngroups, int splits,
+                                               char* smem) {
   constexpr int XB = 16 * NT * G2_PITCH;  // one x image: 16 NT rows x 512 k (padded pitch)
   constexpr int SST = NORM ? 1024 : 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * XB + (32 + SST + G3_WAVES * 32 + 4) * 4];
   float* rs = reinterpret_cast<float*>(smem + 2 * XB);
   float* sst = rs + 32;
   float(*ssr)[32] = reinterpret_cast<float(*)[32]>(sst + SST);
@@ -919,8 +980,8 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, g = lane >> 4;
-  const int n = blockIdx.x * G3_ROWS + wave * 16 + l16;
-  const int splits = gridDim.y * U, z0 = blockIdx.y * U;
+  const int n = gx * G3_ROWS + wave * 16 + l16;
+  const int z0 = gy * U;
   const int K = a.K, R = a.R, kper = a.kper;
   const int cpu = (kper + G2_KC - 1) / G2_KC;  // chunks per split (every split kper long: K % kper == 0)
   const int C = U * cpu;                        // this workgroup's chunks
@@ -944,7 +1005,7 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a
   };
   // chunk c's x rows -> image B, its norm weights, its 16 weight fragments per wave -> wv[B] (dlin_kernel's
   // order: x DMA and norm weights first, so a vmcnt(16) after them leaves exactly the weights in flight)
-  auto issue = [&](auto b_c, int c) __attribute__((always_inline)) {
+  auto issue_x = [&](auto b_c, int c) __attribute__((always_inline)) {
     constexpr int B = decltype(b_c)::value;
     int kc, nsteps;
     chunk_k(c, kc, nsteps);
@@ -956,6 +1017,11 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a
     }
     if constexpr (NORM) lw[B] = *reinterpret_cast<const u32x4*>(a.ln_w + min(kc + 8 * tc, K - 8));
     asm volatile("" ::: "memory");
+  };
+  auto issue_w = [&](auto b_c, int c) __attribute__((always_inline)) {
+    constexpr int B = decltype(b_c)::value;
+    int kc, nsteps;
+    chunk_k(c, kc, nsteps);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const bf16x8* wp = reinterpret_cast<const bf16x8*>(wrow + (long)((kc >> 5) + min(s, nsteps - 1)) * 512);
@@ -965,6 +1031,10 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a
       wv[B][s] = *wp;
 #endif
     }
+  };
+  auto issue = [&](auto b_c, int c) __attribute__((always_inline)) {
+    issue_x(b_c, c);
+    issue_w(b_c, c);
   };
   f32x4 accs[U][NT], acc[NT];
 #pragma unroll
@@ -981,7 +1051,10 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a
   auto body = [&](auto b_c, int c) __attribute__((always_inline)) {
     constexpr int B = decltype(b_c)::value;
     char* xs = smem + B * XB;
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk c's x rows (+ norm weights) landed
+    if (ROLE == DL_ROLE_CONS && c == 0)  // the consumer issued chunk 0's x rows after its weights
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk c's x rows (+ norm weights) landed
     __syncthreads();
     if constexpr (NORM) {
       if (c == 0) {  // rstd of the 32 rows: the partials summed in group order
@@ -1041,7 +1114,14 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a
       }
     }
   };
-  issue(I0{}, 0);
+  if constexpr (ROLE == DL_ROLE_CONS) {  // chunk 0's weights in flight while the producers finish
+    issue_w(I0{}, 0);
+    const int k0 = z0 * kper, k1 = min(K, (z0 + U) * kper);
+    dl_wait_flags(a, k0 / 64, (k1 + 63) / 64);
+    issue_x(I0{}, 0);
+  } else {
+    issue(I0{}, 0);
+  }
   for (int c = 0; c < C; c += 2) {
     body(I0{}, c);
     if (c + 1 < C) body(I1{}, c + 1);
@@ -1051,7 +1131,29 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int j = 0; j < NT; ++j) part[u][j] = accs[U - 1 - u][j];
-  dlin_finish<NT, EPI, U>(a, part, U, blockIdx.x, z0, splits, gridDim.x, smem, ssr, flag);
+  dlin_finish<NT, EPI, U>(a, part, U, gx, z0, splits, ngroups, smem, ssr, flag);
+}
+
+template <int NT, int EPI, bool NORM, int U>
+__global__ __launch_bounds__(64 * G3_WAVES) void dlin_pipe_kernel(const DlArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[dl_pipe_lds<NT>(NORM)];
+  dlin_pipe_body<NT, EPI, NORM, U>(a, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y * U, smem);
+}
+
+// The decode MLP in one launch (round 5): workgroups 0 .. ngu - 1 are gate|up (+ the folded RMSNorm, SwiGLU;
+// one workgroup per row group, all UG splits in registers) publishing h; the rest are down (+ residual, ss_out;
+// U = 1, split-K summed by ticket) consuming it.  Blocks dispatch in order, so every producer is resident or
+// done before a consumer occupies a CU, and the consumers' waits are bounded either way (tmo).
+template <int NT, int UG>
+__global__ __launch_bounds__(64 * G3_WAVES) void dmlp_kernel(const DlArgs gu, const DlArgs dn, int ngu, int ndn,
+                                                             int dn_splits) {
+  __shared__ __attribute__((aligned(16))) char smem[dl_pipe_lds<NT>(true)];
+  if ((int)blockIdx.x < ngu) {
+    dlin_pipe_body<NT, DL_SWIGLU, true, UG, DL_ROLE_PUB>(gu, blockIdx.x, 0, ngu, UG, smem);
+  } else {
+    const int u = blockIdx.x - ngu;
+    dlin_pipe_body<NT, DL_PLAIN, false, 1, DL_ROLE_CONS>(dn, u % ndn, u / ndn, ndn, dn_splits, smem);
+  }
 }
 
 #ifdef OSPO_ABLATION
@@ -1652,6 +1754,47 @@ extern "C" size_t ospo_decode_linear_ws_bytes(int R, int N, int K) {
   if (R <= 0 || R > 32 || N <= 0 || N % G3_ROWS || N / G3_ROWS > DL_CNT_BYTES / 4 || K < 32 || K % 32) return 0;
   const int kp = gemv3_kper(N, K), splits = (K + kp - 1) / kp;
   return DL_CNT_BYTES + (size_t)splits * (N / 16) * ((R + 15) / 16) * 64 * sizeof(f32x4);
+}
+
+extern "C" int ospo_decode_mlp(const void* W_gu, const void* W_down, const void* xmid, int ldx, int R, int D, int F,
+                               const float* ss_in, int ss_groups, const void* ln_w, float eps, void* h, int ldh,
+                               void* out, int ldo, float* ss_out, const int* step_dev, int layer, unsigned* flags,
+                               unsigned* tmo, void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (!W_gu || !W_down || !xmid || !ss_in || !ln_w || !h || !out || !step_dev || !flags || !tmo || !ws)
+    return OSPO_ERR_ARG;
+  if (R <= 0 || R > 32 || D <= 0 || F <= 0 || D % G3_ROWS || (2 * F) % G3_ROWS || F % 64 || D % 32) return OSPO_ERR_SHAPE;
+  if (ldx < D || ldx % 8 || ldh < F || ldh % 8 || ldo < D || layer < 0 || layer >= 63) return OSPO_ERR_SHAPE;
+  if (ss_groups <= 0 || ss_groups > 32 || !(eps >= 0.f)) return OSPO_ERR_ARG;
+  const size_t need = ospo_decode_linear_ws_bytes(R, D, F);
+  if (need == 0 || ws_bytes < need) return OSPO_ERR_ARG;
+  if (!aligned16(W_gu) || !aligned16(W_down) || !aligned16(xmid) || !aligned16(h) || !aligned16(ws) ||
+      !aligned16(ln_w))
+    return OSPO_ERR_ALIGN;
+  // the one-launch form needs exactly the plans of the two launches: gate|up one workgroup per row group with
+  // all its splits (U = splits = 4), down the pipelined form with one split per workgroup
+  const int kg = gemv3_kper(2 * F, D), sg = (D + kg - 1) / kg, ng = 2 * F / G3_ROWS;
+  const int kd = gemv3_kper(D, F), sd = (F + kd - 1) / kd, nd = D / G3_ROWS;
+  if (dlin_pipe_units(ng, sg, D, kg) != 4 || sg != 4 || dlin_pipe_units(nd, sd, F, kd) != 1) return OSPO_ERR_UNSUPPORTED;
+  if ((long)R * ldh * 2 >= (1L << 31)) return OSPO_ERR_UNSUPPORTED;  // the h stores' buffer range
+  DlArgs g;
+  g.W = (const bf16*)W_gu; g.X = (const bf16*)xmid; g.ldx = ldx; g.R = R; g.K = D; g.kper = kg;
+  g.ss_in = ss_in; g.ss_groups = ss_groups; g.ln_w = (const bf16*)ln_w; g.eps = eps;
+  g.bias = nullptr; g.gelu = 0; g.res = nullptr; g.ldr = 0; g.out = (bf16*)h; g.ldo = ldh; g.ss_out = nullptr;
+  g.pos = nullptr; g.cs = g.sn = nullptr; g.kc = g.vc = nullptr; g.H = 0; g.Tmax = 0;
+  g.cnt = nullptr; g.part = nullptr; g.part_bytes = 0;  // (all splits in registers: no partials, no tickets)
+  g.hflag = flags; g.epoch_step = step_dev; g.epoch_layer = layer; g.tmo = tmo;
+  DlArgs d = g;
+  d.W = (const bf16*)W_down; d.X = (const bf16*)h; d.ldx = ldh; d.K = F; d.kper = kd;
+  d.ss_in = nullptr; d.ss_groups = 0; d.ln_w = nullptr; d.eps = 0.f;
+  d.res = (const bf16*)xmid; d.ldr = ldx; d.out = (bf16*)out; d.ldo = ldo; d.ss_out = ss_out;
+  d.cnt = (unsigned*)ws; d.part = (float*)((char*)ws + DL_CNT_BYTES); d.part_bytes = (int)(need - DL_CNT_BYTES);
+  const dim3 grid(ng + nd * sd);
+  if (R <= 16)
+    hipLaunchKernelGGL((dmlp_kernel<1, 4>), grid, dim3(64 * G3_WAVES), 0, stream, g, d, ng, nd, sd);
+  else
+    hipLaunchKernelGGL((dmlp_kernel<2, 4>), grid, dim3(64 * G3_WAVES), 0, stream, g, d, ng, nd, sd);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
 }
 
 extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, int N, int K, const float* ss_in,

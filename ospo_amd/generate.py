@@ -48,7 +48,7 @@ class T2IGenerator:
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_batch: int = 16,
                  max_prompt_len: int = 64, n_img_tokens: int = 576, cfg_weight: float = 5.0,
                  temperature: float = 1.0, pad_id: int = PAD_ID, vq_weights: Optional[Dict[str, torch.Tensor]] = None,
-                 tiled_weights: bool = True, fused_layers: bool = True):
+                 tiled_weights: bool = True, fused_layers: bool = True, mlp_one_launch: bool = True):
         if dims.head_dim != 128:
             raise ValueError("head_dim must be 128 (Janus-Pro)")
         if 2 * max_batch > 64:
@@ -138,6 +138,11 @@ class T2IGenerator:
             # (x, xo: the layer stack ping-pongs them; xmid)
             self.ss_x, self.ss_xo, self.ss_mid = (torch.zeros(D // 128, 32, dtype=torch.float32, device=dev)
                                                   for _ in range(3))
+        # the decode MLP in one launch (ops.decode_mlp, round 5): per gate|up row group an h-ready flag tagged
+        # with (step, layer), zeroed before every generate(); tmo: nonzero if a down workgroup's wait gave up
+        self.mlp_one_launch = bool(mlp_one_launch) and self.fused and dims.n_layers < 63
+        self.mlp_flags = torch.zeros(max(2 * Fd // 128, 1), dtype=torch.int32, device=dev)
+        self.mlp_tmo = torch.zeros(1, dtype=torch.int32, device=dev)
         self._graph = None
         self._graph_B = None
         self.probs = None  # [n, B, V] fp32 when record_probs
@@ -272,9 +277,12 @@ class T2IGenerator:
             ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos, scale,
                            self.attn[:R])
             ops.decode_linear(self.attn[:R], lw["o_d"], self.xmid[:R], ws, residual=x, ss_out=self.ss_mid)
-            ops.decode_linear(self.xmid[:R], lw["gu_d"], self.h[:R], ws, epi="swiglu",
-                              norm=(self.ss_mid, lw["ln_post"], eps))
-            ops.decode_linear(self.h[:R], lw["down_d"], xo, ws, residual=self.xmid[:R], ss_out=sso)
+            if not (self.mlp_one_launch and ops.decode_mlp(
+                    self.xmid[:R], lw["gu_d"], lw["down_d"], self.h[:R], xo, ws, norm=(self.ss_mid, lw["ln_post"], eps),
+                    ss_out=sso, step=self.step, layer=i, flags=self.mlp_flags, tmo=self.mlp_tmo)):
+                ops.decode_linear(self.xmid[:R], lw["gu_d"], self.h[:R], ws, epi="swiglu",
+                                  norm=(self.ss_mid, lw["ln_post"], eps))
+                ops.decode_linear(self.h[:R], lw["down_d"], xo, ws, residual=self.xmid[:R], ss_out=sso)
             x, xo = xo, x
             ss, sso = sso, ss
         self._head_and_sample(x, R, ss)
@@ -322,6 +330,7 @@ class T2IGenerator:
         self.start[:R].copy_(start)
         self.pos.fill_(Lp)      # the first decoded token sits at position Lp
         self.step.fill_(0)
+        self.mlp_flags.zero_()  # (the flags' epochs restart with the step counter)
         self.tokens.zero_()
         self.probs = (torch.zeros(self.n_img, B, dims.img_vocab, dtype=torch.float32, device=self.device)
                       if record_probs else None)
@@ -342,4 +351,6 @@ class T2IGenerator:
             for s in range(n_rest):
                 self._host_step = s + 1
                 self._decode_step(R)
+        if self.mlp_one_launch and int(self.mlp_tmo.item()) != 0:
+            raise RuntimeError("decode_mlp: a down workgroup's wait for h gave up (outputs invalid)")
         return self.tokens[:B]

@@ -9,6 +9,7 @@ from typing import Optional
 
 import torch
 
+from . import _lib
 from ._lib import call, query
 
 BF16 = torch.bfloat16
@@ -691,6 +692,34 @@ def decode_linear_ws(R: int, N: int, K: int, device) -> torch.Tensor:
     if nbytes == 0:
         raise ValueError(f"decode_linear: unsupported shape R={R} N={N} K={K}")
     return torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=device)
+
+
+def decode_mlp(xmid: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, h: torch.Tensor, out: torch.Tensor,
+               ws: torch.Tensor, *, norm, ss_out, step, layer: int, flags: torch.Tensor, tmo: torch.Tensor) -> bool:
+    """The decode MLP in one launch (ospo_decode_mlp, round 5): decode_linear(xmid, w_gu, h, epi="swiglu",
+    norm=norm) then decode_linear(h, w_down, out, residual=xmid, ss_out=ss_out), bit for bit.  w_gu from
+    interleave_gate_up + tile_decode_weight, w_down tiled; step: the device decode-step counter (int32 [1]);
+    flags: int32 [>= 2F / 128], zero before the first use of each (step, layer); tmo: int32 [1] (nonzero after a
+    wait that gave up).  Returns False (nothing launched) when the shapes do not map onto the one-launch form."""
+    for t, nme in ((xmid, "xmid"), (h, "h"), (out, "out")):
+        _chk(t, BF16, nme)
+    R, D = xmid.shape
+    F = h.shape[1]
+    ss_in, ln_w, eps = norm
+    for t, nme in ((flags, "flags"), (tmo, "tmo"), (step, "step")):
+        if t.dtype != torch.int32 or not t.is_contiguous():
+            raise ValueError(f"decode_mlp: {nme} must be contiguous int32")
+    if flags.numel() < 2 * F // 128:
+        raise ValueError("decode_mlp: flags needs 2F / 128 words")
+    rc = getattr(_lib.lib(), "ospo_decode_mlp")(
+        _p(w_gu), _p(w_down), _p(xmid), _ld(xmid), R, D, F, _p(ss_in), ss_in.numel() // 32, _p(ln_w), float(eps),
+        _p(h), _ld(h), _p(out), _ld(out), _p(ss_out), _p(step), int(layer), _p(flags), _p(tmo), _p(ws),
+        ws.numel() * 4, _s())
+    if rc == 4:  # OSPO_ERR_UNSUPPORTED: the caller runs the two launches
+        return False
+    if rc != 0:
+        raise ValueError(f"ospo_decode_mlp: {_lib.lib().ospo_strerror(rc).decode()} (status {rc})")
+    return True
 
 
 def interleave_gate_up(gu: torch.Tensor) -> torch.Tensor:

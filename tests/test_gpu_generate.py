@@ -390,6 +390,44 @@ def test_generate_tiled_weights_same_tokens():
     assert all(torch.equal(t, toks[0]) for t in toks[1:])
 
 
+@pytest.mark.parametrize("R", [32, 12])
+def test_decode_mlp_one_launch_equals_two_launches(R):
+    """Round 5: ops.decode_mlp (gate|up + SwiGLU and down + residual in ONE launch, the down workgroups waiting on
+    per-group h flags) writes exactly what the two decode_linear launches write -- h, the output and its row sums
+    of squares -- over several calls with new inputs and new (step, layer) epochs; no wait gives up."""
+    D, F, eps = 4096, 11008, 1e-6
+    torch.manual_seed(100 + R)
+    T = ops().tile_decode_weight
+    wg = (torch.randn(2 * F, D, device=DEV) * 0.02).bfloat16()
+    wd = (torch.randn(D, F, device=DEV) * 0.02).bfloat16()
+    wgi_t, wd_t = T(ops().interleave_gate_up(wg)), T(wd)
+    lnw = (1 + 0.1 * torch.randn(D, device=DEV)).bfloat16()
+    ws = torch.zeros(max(ops().decode_linear_ws(R, n, k, DEV).numel() for n, k in ((2 * F, D), (D, F))), device=DEV)
+    flags = torch.zeros(2 * F // 128, dtype=torch.int32, device=DEV)
+    tmo = torch.zeros(1, dtype=torch.int32, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    z = lambda *sh: torch.zeros(*sh, dtype=torch.bfloat16, device=DEV)  # noqa: E731
+    for it, layer in ((1, 0), (1, 5), (2, 0), (7, 29)):
+        step.fill_(it)
+        xmid = torch.randn(R, D, device=DEV).bfloat16()
+        ss_mid = (xmid.float() ** 2).view(R, D // 128, 128).sum(-1).T.contiguous()
+        ss_mid = torch.cat([ss_mid, torch.zeros(D // 128, 32 - R, device=DEV)], 1).contiguous() if R < 32 else ss_mid
+        h1, o1, h2, o2 = z(R, F), z(R, D), z(R, F), z(R, D)
+        ss1 = torch.full((D // 128, 32), float("nan"), device=DEV)
+        ss2 = ss1.clone()
+        ops().decode_linear(xmid, wgi_t, h1, ws, epi="swiglu", norm=(ss_mid, lnw, eps))
+        ops().decode_linear(h1, wd_t, o1, ws, residual=xmid, ss_out=ss1)
+        assert ops().decode_mlp(xmid, wgi_t, wd_t, h2, o2, ws, norm=(ss_mid, lnw, eps), ss_out=ss2, step=step,
+                                layer=layer, flags=flags, tmo=tmo)
+        torch.cuda.synchronize()
+        assert int(tmo.item()) == 0
+        assert torch.equal(h1, h2), (it, layer)
+        assert torch.equal(o1, o2), (it, layer)
+        assert torch.equal(ss1[:, :R], ss2[:, :R]), (it, layer)
+        assert torch.all(flags == it * 64 + layer + 1)  # every gate|up group published this call's epoch
+        assert torch.all(ws[:1024] == 0)  # the down product's ticket counters
+
+
 @pytest.mark.parametrize("R", [32, 12, 4])
 def test_decode_linear_equals_unfused(R):
     """ops.decode_linear (one launch per Linear: split sum + consumer in the launch) writes exactly what
