@@ -451,6 +451,19 @@ int ospo_decode_linear(const void* W, const void* X, int ldx, int R, int N, int 
                        const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* pos_dev,
                        const void* rope_cos, const void* rope_sin, void* k_cache, void* v_cache, int n_heads,
                        int Tmax, void* ws, size_t ws_bytes, hipStream_t stream);
+/* Head-range forms (round 5), for a decode step that runs the attention of heads h0 .. h0 + nh - 1 while the
+ * projection of the other heads streams (two streams of one hipGraph):
+ * ospo_decode_qkv_heads == ospo_decode_linear(epi 1) for heads h0 .. h0 + nh - 1 only, on W_hm = the q|k|v
+ *   weight with its rows in head-major 128-row groups (q_h, k_h, v_h for h = 0 .. n_heads - 1; tiled as
+ *   ospo_decode_gemv ldw = 0); the same bits per head as the full launch.  D = n_heads * 128.
+ * ospo_attn_cache_heads == ospo_attn_cache for heads h0 .. h0 + nh - 1 (16-B aligned rows and caches). */
+int ospo_decode_qkv_heads(const void* W_hm, const void* X, int ldx, int R, int D, const float* ss_in, int ss_groups,
+                          const void* ln_w, float eps, void* q_out, int ldo, const int* pos_dev, const void* rope_cos,
+                          const void* rope_sin, void* k_cache, void* v_cache, int n_heads, int h0, int nh, int Tmax,
+                          void* ws, size_t ws_bytes, hipStream_t stream);
+int ospo_attn_cache_heads(const void* q, int ldq, const void* k_cache, const void* v_cache, int R, int nq,
+                          int n_heads, int h0, int nh, int Tmax, const int* start, const int* pos_dev, float scale,
+                          void* out, int ldo, hipStream_t stream);
 /* The decode MLP in ONE launch (round 5): ospo_decode_linear(xmid, W_gu, h, epi 2, norm = (ss_in, ln_w,
  * eps)) then ospo_decode_linear(h, W_down, out, epi 0, residual = xmid, ss_out), with the same outputs bit
  * for bit.  The down workgroups issue their first weights while the gate|up workgroups finish, then wait for

@@ -667,6 +667,7 @@ struct DlArgs {
   const int* epoch_step = nullptr;
   int epoch_layer = 0;
   unsigned* tmo = nullptr;
+  int kv_hm = 0;  // DL_KV: head-major row groups (round 5, ospo_decode_qkv_heads)
 };
 
 // Round 5, decode MLP in one launch (dmlp_kernel): the gate|up workgroups PUBLISH their group's h columns
@@ -784,7 +785,9 @@ __device__ __forceinline__ void dlin_finish(const DlArgs& a, const f32x4 (&accs)
       for (int q = 0; q < 4; ++q) ep[(16 * j + 4 * g + q) * 129 + wave * 16 + l16] = round_bf(acc[j][q]);
     __syncthreads();
     if constexpr (EPI == DL_KV) {
-      const int hs = grp, which = hs / a.H, h = hs % a.H;
+      // row groups q_0 .. q_H-1, k_0 .., v_0 .. (nn.Linear order), or head-major q_h, k_h, v_h (kv_hm: the
+      // head-range launches of ospo_decode_qkv_heads, whose out / cache pointers start at their first head)
+      const int hs = grp, which = a.kv_hm ? hs % 3 : hs / a.H, h = a.kv_hm ? hs / 3 : hs % a.H;
       const int p = *a.pos;
       if (p < a.Tmax) {
         for (int it = threadIdx.x; it < R * 64; it += 64 * G3_WAVES) {
@@ -1756,6 +1759,32 @@ extern "C" size_t ospo_decode_linear_ws_bytes(int R, int N, int K) {
   return DL_CNT_BYTES + (size_t)splits * (N / 16) * ((R + 15) / 16) * 64 * sizeof(f32x4);
 }
 
+extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, int N, int K, const float* ss_in,
+                                  int ss_groups, const void* ln_w, float eps, int epi, const void* bias, int gelu,
+                                  const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* pos_dev,
+                                  const void* rope_cos, const void* rope_sin, void* k_cache, void* v_cache, int n_heads,
+                                  int Tmax, void* ws, size_t ws_bytes, hipStream_t stream);
+static int decode_linear_impl(const void* W, const void* X, int ldx, int R, int N, int K, const float* ss_in,
+                              int ss_groups, const void* ln_w, float eps, int epi, const void* bias, int gelu,
+                              const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* pos_dev,
+                              const void* rope_cos, const void* rope_sin, void* k_cache, void* v_cache, int n_heads,
+                              int Tmax, void* ws, size_t ws_bytes, hipStream_t stream, int kv_hm, int nh);
+
+extern "C" int ospo_decode_qkv_heads(const void* W_hm, const void* X, int ldx, int R, int D, const float* ss_in,
+                                     int ss_groups, const void* ln_w, float eps, void* q_out, int ldo,
+                                     const int* pos_dev, const void* rope_cos, const void* rope_sin, void* k_cache,
+                                     void* v_cache, int n_heads, int h0, int nh, int Tmax, void* ws, size_t ws_bytes,
+                                     hipStream_t stream) {
+  if (!W_hm || !q_out || !k_cache || !v_cache) return OSPO_ERR_ARG;
+  if (n_heads <= 0 || h0 < 0 || nh <= 0 || h0 + nh > n_heads || D != n_heads * HD) return OSPO_ERR_SHAPE;
+  // head-major tiled rows: head h's q, k, v groups are rows 384 h .. 384 h + 383 (16-row tiles of K / 32 x 512)
+  const bf16* W = (const bf16*)W_hm + (long)h0 * 3 * HD * D;
+  return decode_linear_impl(W, X, ldx, R, 3 * nh * HD, D, ss_in, ss_groups, ln_w, eps, DL_KV, nullptr, 0, nullptr, 0,
+                            (bf16*)q_out + h0 * HD, ldo, nullptr, pos_dev, rope_cos, rope_sin,
+                            (bf16*)k_cache + (long)h0 * Tmax * HD, (bf16*)v_cache + (long)h0 * Tmax * HD, n_heads, Tmax,
+                            ws, ws_bytes, stream, 1, nh);
+}
+
 extern "C" int ospo_decode_mlp(const void* W_gu, const void* W_down, const void* xmid, int ldx, int R, int D, int F,
                                const float* ss_in, int ss_groups, const void* ln_w, float eps, void* h, int ldh,
                                void* out, int ldo, float* ss_out, const int* step_dev, int layer, unsigned* flags,
@@ -1802,6 +1831,18 @@ extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, 
                                   const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* pos_dev,
                                   const void* rope_cos, const void* rope_sin, void* k_cache, void* v_cache, int n_heads,
                                   int Tmax, void* ws, size_t ws_bytes, hipStream_t stream) {
+  return decode_linear_impl(W, X, ldx, R, N, K, ss_in, ss_groups, ln_w, eps, epi, bias, gelu, residual, ldr, out, ldo,
+                            ss_out, pos_dev, rope_cos, rope_sin, k_cache, v_cache, n_heads, Tmax, ws, ws_bytes, stream, 0,
+                            n_heads);
+}
+
+// kv_hm / nh: ospo_decode_qkv_heads' head-range launch (head-major row groups, nh heads of the n_heads the cache
+// strides use); ospo_decode_linear: 0 / n_heads
+static int decode_linear_impl(const void* W, const void* X, int ldx, int R, int N, int K, const float* ss_in,
+                              int ss_groups, const void* ln_w, float eps, int epi, const void* bias, int gelu,
+                              const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* pos_dev,
+                              const void* rope_cos, const void* rope_sin, void* k_cache, void* v_cache, int n_heads,
+                              int Tmax, void* ws, size_t ws_bytes, hipStream_t stream, int kv_hm, int nh) {
   if (!W || !X || !out || !ws) return OSPO_ERR_ARG;
   const size_t need = ospo_decode_linear_ws_bytes(R, N, K);
   if (need == 0 || ldx < K || ldx % 8) return OSPO_ERR_SHAPE;
@@ -1814,7 +1855,7 @@ extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, 
   } else if (epi == DL_KV) {
     if (bias || gelu || residual || ss_out) return OSPO_ERR_UNSUPPORTED;
     if (!pos_dev || !rope_cos || !rope_sin || !k_cache || !v_cache) return OSPO_ERR_ARG;
-    if (n_heads <= 0 || N != 3 * n_heads * HD || ldo < n_heads * HD || Tmax <= 0) return OSPO_ERR_SHAPE;
+    if (n_heads <= 0 || nh <= 0 || N != 3 * nh * HD || ldo < nh * HD || Tmax <= 0) return OSPO_ERR_SHAPE;
   } else if (epi == DL_SWIGLU) {
     if (bias || gelu || residual || ss_out) return OSPO_ERR_UNSUPPORTED;
     if (ldo < N / 2) return OSPO_ERR_SHAPE;
@@ -1828,7 +1869,7 @@ extern "C" int ospo_decode_linear(const void* W, const void* X, int ldx, int R, 
   a.bias = (const bf16*)bias; a.gelu = gelu; a.res = (const bf16*)residual; a.ldr = ldr;
   a.out = (bf16*)out; a.ldo = ldo; a.ss_out = ss_out;
   a.pos = pos_dev; a.cs = (const bf16*)rope_cos; a.sn = (const bf16*)rope_sin; a.kc = (bf16*)k_cache;
-  a.vc = (bf16*)v_cache; a.H = n_heads; a.Tmax = Tmax;
+  a.vc = (bf16*)v_cache; a.H = n_heads; a.Tmax = Tmax; a.kv_hm = kv_hm;
   a.cnt = (unsigned*)ws; a.part = (float*)((char*)ws + DL_CNT_BYTES); a.part_bytes = (int)(need - DL_CNT_BYTES);
   const bool norm = ss_in != nullptr;
   // the pipelined form (dlin_pipe_kernel, U splits per workgroup, at most one workgroup per CU) where the shape
@@ -1991,6 +2032,22 @@ extern "C" int ospo_attn_cache(const void* q, int ldq, const void* k_cache, cons
   hipLaunchKernelGGL(v2 ? attn_cache2_kernel : attn_cache_kernel, dim3(R * nq, n_heads), dim3(256), 0, stream,
                      (const bf16*)q, ldq, (const bf16*)k_cache, (const bf16*)v_cache, n_heads, Tmax, start, pos_dev, nq,
                      scale, (bf16*)out, ldo);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_attn_cache_heads(const void* q, int ldq, const void* k_cache, const void* v_cache, int R, int nq,
+                                     int n_heads, int h0, int nh, int Tmax, const int* start, const int* pos_dev,
+                                     float scale, void* out, int ldo, hipStream_t stream) {
+  if (!q || !k_cache || !v_cache || !start || !out) return OSPO_ERR_ARG;
+  if (R <= 0 || nq <= 0 || n_heads <= 0 || h0 < 0 || nh <= 0 || h0 + nh > n_heads || Tmax <= 0 || Tmax > ATT_MAXT)
+    return OSPO_ERR_SHAPE;
+  if (ldq < n_heads * HD || ldo < n_heads * HD || ldq % 8 || ldo % 8) return OSPO_ERR_SHAPE;
+  if (!aligned16(q) || !aligned16(out) || !aligned16(k_cache) || !aligned16(v_cache)) return OSPO_ERR_ALIGN;
+  // heads h0 .. h0 + nh - 1: the same kernel with its pointers at head h0 (the cache strides keep n_heads)
+  hipLaunchKernelGGL(attn_cache2_kernel, dim3(R * nq, nh), dim3(256), 0, stream, (const bf16*)q + h0 * HD, ldq,
+                     (const bf16*)k_cache + (long)h0 * Tmax * HD, (const bf16*)v_cache + (long)h0 * Tmax * HD, n_heads,
+                     Tmax, start, pos_dev, nq, scale, (bf16*)out + h0 * HD, ldo);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

@@ -48,7 +48,8 @@ class T2IGenerator:
     def __init__(self, dims: ModelDims, weights: Dict[str, torch.Tensor], device="cuda", max_batch: int = 16,
                  max_prompt_len: int = 64, n_img_tokens: int = 576, cfg_weight: float = 5.0,
                  temperature: float = 1.0, pad_id: int = PAD_ID, vq_weights: Optional[Dict[str, torch.Tensor]] = None,
-                 tiled_weights: bool = True, fused_layers: bool = True, mlp_one_launch: bool = True):
+                 tiled_weights: bool = True, fused_layers: bool = True, mlp_one_launch: bool = True,
+                 head_split: bool = False):
         if dims.head_dim != 128:
             raise ValueError("head_dim must be 128 (Janus-Pro)")
         if 2 * max_batch > 64:
@@ -103,9 +104,14 @@ class T2IGenerator:
                       and dims.img_vocab % 128 == 0 and all(k % 32 == 0 for k in (D, Fd, Dg, Fa))
                       and D // 128 <= 32 and Dg // 128 <= 32
                       and all(n // 128 <= 1024 for n in (3 * D, 2 * Fd, D, Dg, dims.img_vocab)))
+        # the attention of one half of the heads overlapped with the q|k|v projection of the other half (round 5):
+        # head-major q|k|v rows, two head-range launches, the second half on a side stream of the same graph
+        self.head_split = bool(head_split) and self.fused and dims.n_heads % 2 == 0
         for lw in self.layers:
             for k in ("qkv", "o", "gu", "down"):
                 src = ops.interleave_gate_up(lw[k]) if (k == "gu" and self.fused) else lw[k]
+                if k == "qkv" and self.head_split:
+                    src = ops.head_major_qkv(lw[k], dims.n_heads)
                 lw[k + "_d"] = dw(src)
         self.gh_w1_d, self.gh_w2_d, self.al_w2_d = dw(self.gh_w1), dw(self.gh_w2), dw(self.al_w2)
         # ---- KV cache and decode-step buffers (R = 2 * max_batch rows)
@@ -143,6 +149,7 @@ class T2IGenerator:
         self.mlp_one_launch = bool(mlp_one_launch) and self.fused and dims.n_layers < 63
         self.mlp_flags = torch.zeros(max(2 * Fd // 128, 1), dtype=torch.int32, device=dev)
         self.mlp_tmo = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._side = torch.cuda.Stream(device=dev) if self.head_split else None
         self._graph = None
         self._graph_B = None
         self.probs = None  # [n, B, V] fp32 when record_probs
@@ -272,10 +279,31 @@ class T2IGenerator:
         x, xo = self.x[:R], self.xo[:R]
         ss, sso = self.ss_x, self.ss_xo
         for i, lw in enumerate(self.layers):
-            ops.decode_linear(x, lw["qkv_d"], self.q[:R], ws, epi="kv", norm=(ss, lw["ln_in"], eps),
-                              kv=(self.pos, (self.cos, self.sin), self.kc[i], self.vc[i], H, self.Tmax))
-            ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos, scale,
-                           self.attn[:R])
+            kv = (self.pos, (self.cos, self.sin), self.kc[i], self.vc[i], H, self.Tmax)
+            if self.head_split:
+                # q|k|v of heads [0, H/2) -> (attention of [0, H/2) on this stream | q|k|v + attention of [H/2, H)
+                # on the side stream) -> o: the first half's attention streams the KV cache while the second
+                # half's projection streams its weights
+                H2 = H // 2
+                main = torch.cuda.current_stream(self.device)
+                ops.decode_qkv_heads(x, lw["qkv_d"], self.q[:R], ws, norm=(ss, lw["ln_in"], eps), kv=kv, h0=0, nh=H2)
+                ev_q = torch.cuda.Event()
+                ev_q.record(main)
+                self._side.wait_event(ev_q)
+                with torch.cuda.stream(self._side):
+                    ops.decode_qkv_heads(x, lw["qkv_d"], self.q[:R], ws, norm=(ss, lw["ln_in"], eps), kv=kv, h0=H2,
+                                         nh=H - H2)
+                    ops.attn_cache_heads(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos,
+                                         scale, self.attn[:R], H2, H - H2)
+                    ev_s = torch.cuda.Event()
+                    ev_s.record(self._side)
+                ops.attn_cache_heads(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos,
+                                     scale, self.attn[:R], 0, H2)
+                main.wait_event(ev_s)
+            else:
+                ops.decode_linear(x, lw["qkv_d"], self.q[:R], ws, epi="kv", norm=(ss, lw["ln_in"], eps), kv=kv)
+                ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos, scale,
+                               self.attn[:R])
             ops.decode_linear(self.attn[:R], lw["o_d"], self.xmid[:R], ws, residual=x, ss_out=self.ss_mid)
             if not (self.mlp_one_launch and ops.decode_mlp(
                     self.xmid[:R], lw["gu_d"], lw["down_d"], self.h[:R], xo, ws, norm=(self.ss_mid, lw["ln_post"], eps),

@@ -694,6 +694,37 @@ def decode_linear_ws(R: int, N: int, K: int, device) -> torch.Tensor:
     return torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
+def head_major_qkv(w: torch.Tensor, n_heads: int) -> torch.Tensor:
+    """[3D, K] q|k|v weight (nn.Linear rows q, k, v) -> rows in head-major 128-row groups q_h, k_h, v_h
+    (ospo_decode_qkv_heads' W_hm before tile_decode_weight)."""
+    N, K = w.shape
+    if N != 3 * n_heads * 128:
+        raise ValueError(f"head_major_qkv: {N} rows is not 3 x {n_heads} heads x 128")
+    return w.view(3, n_heads, 128, K).permute(1, 0, 2, 3).reshape(N, K).contiguous()
+
+
+def decode_qkv_heads(x: torch.Tensor, w_hm: torch.Tensor, q_out: torch.Tensor, ws: torch.Tensor, *, norm, kv,
+                     h0: int, nh: int) -> torch.Tensor:
+    """decode_linear(x, w, q_out, ws, epi="kv", norm=norm, kv=kv) for heads h0 .. h0 + nh - 1 only
+    (ospo_decode_qkv_heads): w_hm = tile_decode_weight(head_major_qkv(w))."""
+    _chk(x, BF16, "x")
+    _chk(q_out, BF16, "q_out")
+    R, D = x.shape
+    ss_in, ln_w, eps = norm
+    pos, (cs, sn), kc, vc, H, Tmax = kv
+    call("ospo_decode_qkv_heads", _p(w_hm), _p(x), _ld(x), R, D, _p(ss_in), ss_in.numel() // 32, _p(ln_w), float(eps),
+         _p(q_out), _ld(q_out), _p(pos), _p(cs), _p(sn), _p(kc), _p(vc), H, int(h0), int(nh), Tmax, _p(ws),
+         ws.numel() * 4, _s())
+    return q_out
+
+
+def attn_cache_heads(q, k_cache, v_cache, R, nq, n_heads, Tmax, start, pos, scale, out, h0: int, nh: int):
+    """attn_cache for heads h0 .. h0 + nh - 1 (ospo_attn_cache_heads)."""
+    call("ospo_attn_cache_heads", _p(q), _ld(q), _p(k_cache), _p(v_cache), int(R), int(nq), int(n_heads), int(h0),
+         int(nh), int(Tmax), _p(start), _p(pos), float(scale), _p(out), _ld(out), _s())
+    return out
+
+
 def decode_mlp(xmid: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, h: torch.Tensor, out: torch.Tensor,
                ws: torch.Tensor, *, norm, ss_out, step, layer: int, flags: torch.Tensor, tmo: torch.Tensor) -> bool:
     """The decode MLP in one launch (ospo_decode_mlp, round 5): decode_linear(xmid, w_gu, h, epi="swiglu",

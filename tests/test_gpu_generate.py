@@ -428,6 +428,67 @@ def test_decode_mlp_one_launch_equals_two_launches(R):
         assert torch.all(ws[:1024] == 0)  # the down product's ticket counters
 
 
+@pytest.mark.parametrize("R", [32, 12])
+def test_decode_qkv_heads_and_attn_heads_equal_full_launch(R):
+    """Round 5: the q|k|v projection and the cached attention split by head range (ops.decode_qkv_heads on the
+    head-major weight, ops.attn_cache_heads) write exactly what the full launches write -- q, the K/V cache rows
+    at pos, the attention output -- whether the halves run in order or on two streams."""
+    H, D, Tmax, p, eps = 32, 4096, 96, 37, 1e-6
+    torch.manual_seed(300 + R)
+    x = torch.randn(R, D, device=DEV).bfloat16()
+    wq = (torch.randn(3 * D, D, device=DEV) * 0.02).bfloat16()
+    lnw = (1 + 0.1 * torch.randn(D, device=DEV)).bfloat16()
+    ss = (x.float() ** 2).view(R, D // 128, 128).sum(-1).T.contiguous()
+    ss = torch.cat([ss, torch.zeros(D // 128, 32 - R, device=DEV)], 1).contiguous() if R < 32 else ss
+    T = ops().tile_decode_weight
+    wq_t, wq_hm = T(wq), T(ops().head_major_qkv(wq, H))
+    ws = torch.zeros(ops().decode_linear_ws(R, 3 * D, D, DEV).numel(), device=DEV)
+    pos = torch.tensor([p], dtype=torch.int32, device=DEV)
+    start = torch.randint(0, 5, (R,), dtype=torch.int32, device=DEV)
+    cos, sin = ops().rope_tables(Tmax, 128, 1e4, DEV)
+    z = lambda *sh: torch.zeros(*sh, dtype=torch.bfloat16, device=DEV)  # noqa: E731
+    hist = (torch.randn(R, H, Tmax, 128, device=DEV) * 0.5).bfloat16()
+    hist[:, :, p:] = 0
+    kc1, vc1, q1, o1 = hist.clone(), hist.flip(1).clone(), z(R, D), z(R, D)
+    ops().decode_linear(x, wq_t, q1, ws, epi="kv", norm=(ss, lnw, eps), kv=(pos, (cos, sin), kc1, vc1, H, Tmax))
+    ops().attn_cache(q1, kc1, vc1, R, 1, H, Tmax, start, pos, 128 ** -0.5, o1)
+    for two_streams in (False, True):
+        kc2, vc2, q2, o2 = hist.clone(), hist.flip(1).clone(), z(R, D), z(R, D)
+        kv = (pos, (cos, sin), kc2, vc2, H, Tmax)
+        side = torch.cuda.Stream(device=DEV)
+        torch.cuda.synchronize()
+        ops().decode_qkv_heads(x, wq_hm, q2, ws, norm=(ss, lnw, eps), kv=kv, h0=0, nh=H // 2)
+        ev = torch.cuda.Event()
+        ev.record()
+        st = side if two_streams else torch.cuda.current_stream()
+        st.wait_event(ev)
+        with torch.cuda.stream(st):
+            ops().decode_qkv_heads(x, wq_hm, q2, ws, norm=(ss, lnw, eps), kv=kv, h0=H // 2, nh=H // 2)
+            ops().attn_cache_heads(q2, kc2, vc2, R, 1, H, Tmax, start, pos, 128 ** -0.5, o2, H // 2, H // 2)
+        ops().attn_cache_heads(q2, kc2, vc2, R, 1, H, Tmax, start, pos, 128 ** -0.5, o2, 0, H // 2)
+        torch.cuda.synchronize()
+        assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2), two_streams
+        assert torch.equal(o1, o2), two_streams
+        assert torch.all(ws[:1024] == 0)
+
+
+def test_generate_head_split_same_tokens():
+    """The decode step with the q|k|v projection and attention split in two head ranges on two streams (an A/B
+    option, measured slower) draws the tokens and probabilities of the one-launch step bit for bit, eager and hipGraph."""
+    from ospo_amd.engine import ModelDims
+    from ospo_amd.generate import T2IGenerator
+    dims, w, prompts = _small_case()
+    res = []
+    for hs in (True, False):
+        gen = T2IGenerator(ModelDims.from_any(dims), w, device=DEV, max_batch=4, max_prompt_len=16, n_img_tokens=24,
+                           cfg_weight=5.0, temperature=1.0, pad_id=7, head_split=hs)
+        assert gen.head_split == hs and gen.fused
+        tok = gen.generate(prompts, seed=5, use_graph=False, record_probs=True).cpu().clone()
+        res.append((tok, gen.probs.cpu().clone()))
+        assert torch.equal(gen.generate(prompts, seed=5, use_graph=True).cpu(), tok)
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("R", [32, 12, 4])
 def test_decode_linear_equals_unfused(R):
     """ops.decode_linear (one launch per Linear: split sum + consumer in the launch) writes exactly what
