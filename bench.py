@@ -178,7 +178,8 @@ def bench_t2i(args):
     vw = {**synthetic_vq_weights(0), **synthetic_vq_decoder_weights(1)}  # gen_vision_model (pixel decoder)
     gen = T2IGenerator(dims, w, device=dev, max_batch=B, max_prompt_len=Lp, n_img_tokens=N, cfg_weight=5.0,
                        temperature=1.0, vq_weights=vw, fused_layers=not args.t2i_unfused,
-                       mlp_one_launch=not args.t2i_two_launch_mlp, head_split=args.t2i_head_split)
+                       mlp_one_launch=not args.t2i_two_launch_mlp, head_split=args.t2i_head_split,
+                       attn_o_one_launch=args.t2i_attn_o_one_launch)
     del w
     torch.cuda.empty_cache()
     g = torch.Generator().manual_seed(0)
@@ -228,6 +229,7 @@ def bench_t2i(args):
                    "prompt_len_max": Lp, "decode_steps": N - 1,
                    "decode_mlp": "one launch" if gen.mlp_one_launch else "two launches",
                    "qkv_attn": "two head halves, two streams" if gen.head_split else "one launch each",
+                   "attn_o": "one launch" if gen.attn_o_one_launch else "two launches",
                    "tokens_per_s": round(value * N, 1),
                    "vq_decode_ms_per_batch": round(decode_ms, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
@@ -518,6 +520,8 @@ def main():
     ap.add_argument("--t2i-batch", type=int, default=16)       # parallel_size: prompts (x2 rows with CFG)
     ap.add_argument("--t2i-prompt-len", type=int, default=48)  # max prompt tokens (left-padded)
     ap.add_argument("--t2i-unfused", action="store_true")      # A/B: the round-2 decode step (GEMV + split-sum + norm launches)
+    ap.add_argument("--t2i-attn-o-one-launch", action="store_true",
+                    help="T2I A/B: the cached attention and the o projection in one launch (measured slower)")
     ap.add_argument("--t2i-head-split", action="store_true",
                     help="T2I A/B: q|k|v + attention in two head halves, the second on a side stream (measured slower)")
     ap.add_argument("--t2i-two-launch-mlp", action="store_true",

@@ -477,6 +477,19 @@ int ospo_decode_mlp(const void* W_gu, const void* W_down, const void* xmid, int 
                     int ldo, float* ss_out, const int* step_dev, int layer, unsigned* flags, unsigned* tmo,
                     void* ws, size_t ws_bytes, hipStream_t stream);
 
+/* The decode layer's cached attention and o projection in ONE launch (round 5): ospo_attn_cache(q, ..., nq = 1,
+ * attn_out) then ospo_decode_linear(attn_out, W_o, out, epi 0, residual, ss_out), with the same outputs bit for
+ * bit.  The attention workgroups take a ticket per head when their rows are stored, the head's last one publishes
+ * the head's flag -- flags: >= 2 * n_heads words (flags, then tickets), ZERO before the first call and never
+ * touched by the caller between calls with distinct (*step_dev, layer) pairs (a flag's value: epoch step * 64 +
+ * layer + 1; the tickets are left zero) -- and the o workgroups, their weights already in flight, wait for the
+ * flags of their four heads; tmo is set nonzero if a wait gave up (outputs invalid).  W_o tiled as ospo_decode_gemv ldw = 0; ws: ospo_decode_linear's workspace for
+ * (R, D, D).  OSPO_ERR_UNSUPPORTED (nothing launched) unless the o split plan is one 512-k chunk per split. */
+int ospo_decode_attn_o(const void* q, int ldq, const void* k_cache, const void* v_cache, int R, int n_heads, int Tmax,
+                       const int* start, const int* pos_dev, float scale, void* attn_out, int ld_attn, const void* W_o,
+                       const void* residual, int ldr, void* out, int ldo, float* ss_out, const int* step_dev,
+                       int layer, unsigned* flags, unsigned* tmo, void* ws, size_t ws_bytes, hipStream_t stream);
+
 /* ------------------------------------------------------- VQ image tokenizer ---
  * janus/models/vq_model.py Encoder (:46-124) + quant_conv + VectorQuantizer
  * (:236-282) = gen_vision_model.encode, called per image at ospo/wrapper/train.py:246-264.  fp32

@@ -76,6 +76,7 @@ SIGNATURES = {
     "ospo_decode_linear_ws_bytes": [I, I, I],
     "ospo_decode_linear": [P, P, I, I, I, I, P, I, P, F, I, P, I, P, I, P, I, P, P, P, P, P, P, I, I, P, Z, P],
     "ospo_decode_mlp": [P, P, P, I, I, I, I, P, I, P, F, P, I, P, I, P, P, I, P, P, P, Z, P],
+    "ospo_decode_attn_o": [P, I, P, P, I, I, I, P, P, F, P, I, P, P, I, P, I, P, P, I, P, P, P, Z, P],
     "ospo_decode_qkv_heads": [P, P, I, I, I, P, I, P, F, P, I, P, P, P, P, P, I, I, I, I, P, Z, P],
     "ospo_attn_cache_heads": [P, I, P, P, I, I, I, I, I, I, P, P, F, P, I, P],
     "ospo_kv_store": [P, I, I, I, P, I, P, P, P, P, I, I, I, P, I, P],

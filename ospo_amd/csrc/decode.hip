@@ -1159,6 +1159,234 @@ __global__ __launch_bounds__(64 * G3_WAVES) void dmlp_kernel(const DlArgs gu, co
   }
 }
 
+// Round 5: the cached attention and the o projection in ONE launch (dattn_o_kernel, ospo_decode_attn_o).
+// Attention workgroups (8 waves = two 4-wave halves, one (row, head) each: attn_cache2_kernel's arithmetic, so
+// the same bits) store their output rows write-through and take a ticket on their head; the head's last one
+// publishes the head's flag = epoch.  The o workgroups (dlin_kernel's one-chunk form: kper = 512, four heads)
+// issue their weights first, wait for their four heads' flags, then stage x and run dlin_finish (split sum by
+// ticket, residual, ss_out) -- decode_linear's bits.  <= 80 VGPRs (6 waves per SIMD) and ~34 KB of LDS: three
+// workgroups per CU, so at R = 32 the 512 attention and 256 o workgroups are resident together.
+struct AttnArgs {
+  const bf16* q;
+  int ldq;
+  const bf16* kc;
+  const bf16* vc;
+  int H, Tmax;
+  const int* start;
+  const int* pos;
+  float scale;
+  bf16* out;
+  int ldo, R;
+};
+constexpr int ATT_HALF_LDS = ATT_MAXT * 4 + 16 * 16 * 2 * 16 + 8 * 4;  // sc, part, red of one half
+
+// one (row ri, head h) on the 256 threads tid of a half; no early return (the halves share the barriers): a padded
+// query position (or ri >= R) runs with L = 0 -- no loads, a zero output as attn_cache2_kernel writes -- and a row
+// ri >= R stores nothing.  Ends with this thread's write-through stores acknowledged.
+__device__ __forceinline__ void attn_row_pub(const AttnArgs& at, int ri, int h, int tid, char* hs) {
+  float* sc = reinterpret_cast<float*>(hs);
+  f32x4(*part)[16][2] = reinterpret_cast<f32x4(*)[16][2]>(hs + ATT_MAXT * 4);
+  float* red = reinterpret_cast<float*>(hs + ATT_MAXT * 4 + 16 * 16 * 2 * 16);
+  const bool inr = ri < at.R;
+  const int rc = inr ? ri : at.R - 1;
+  const int p = *at.pos;
+  const int s0 = at.start[rc];
+  const int L = (inr && p >= s0 && p < at.Tmax) ? p - s0 + 1 : 0;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 15, kg = wave * 4 + (lane >> 4);
+  float qf[8];
+  unpack8(*reinterpret_cast<const u32x4*>(at.q + (long)rc * at.ldq + h * HD + 8 * c), qf);
+  const long hb = ((long)rc * at.H + h) * at.Tmax;
+  const bf16* kb = at.kc + (hb + s0) * HD + 8 * c;
+  for (int k0 = kg; k0 < L; k0 += 64) {
+    u32x4 kv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) kv[u] = kv_load(kb + (long)min(k0 + 16 * u, L - 1) * HD);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float kf[8];
+      unpack8(kv[u], kf);
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(qf[e], kf[e], d);
+      d = dpp_sum16(d);
+      if (c == 0 && k0 + 16 * u < L) sc[k0 + 16 * u] = round_bf(round_bf(d) * at.scale);
+    }
+  }
+  __syncthreads();
+  float m = -INFINITY;
+  for (int k = tid; k < L; k += 256) m = fmaxf(m, sc[k]);
+  m = wave_max(m);
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+  for (int k = tid; k < L; k += 256) {
+    const float e = __expf(sc[k] - m);
+    sc[k] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  if (lane == 0) red[4 + wave] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  const bf16* vb = at.vc + (hb + s0) * HD + 8 * c;
+  float a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  for (int k0 = kg; k0 < L; k0 += 64) {
+    u32x4 vv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) vv[u] = kv_load(vb + (long)min(k0 + 16 * u, L - 1) * HD);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float pk = (k0 + 16 * u < L) ? round_bf(sc[min(k0 + 16 * u, L - 1)] * inv) : 0.f;
+      float vf[8];
+      unpack8(vv[u], vf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = fmaf(pk, vf[e], a[e]);
+    }
+  }
+  part[kg][c][0] = f32x4{a[0], a[1], a[2], a[3]};
+  part[kg][c][1] = f32x4{a[4], a[5], a[6], a[7]};
+  __syncthreads();
+  if (tid < 16 && inr) {
+    const int cc = tid;
+    f32x4 o0 = part[0][cc][0], o1 = part[0][cc][1];
+#pragma unroll
+    for (int g2 = 1; g2 < 16; ++g2) {
+      o0 += part[g2][cc][0];
+      o1 += part[g2][cc][1];
+    }
+    const float o[8] = {o0[0], o0[1], o0[2], o0[3], o1[0], o1[1], o1[2], o1[3]};
+    // write-through (sc1): visible device-wide once acknowledged, before the flag
+    const __amdgpu_buffer_rsrc_t rsO =
+        __builtin_amdgcn_make_buffer_rsrc((void*)at.out, 0, (int)((long)at.R * at.ldo * 2), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(L > 0 ? pack8(o) : u32x4{0u, 0u, 0u, 0u}, rsO,
+                                           (uint32_t)(((long)ri * at.ldo + h * HD + 8 * cc) * 2), 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// o workgroup (row group grp, split z of kper = G2_KC = 4 heads): dlin_kernel's one-chunk body with the weights
+// issued before the wait on the attention flags of heads [k_begin / 128, + 4) over rows 0 .. R - 1
+template <int NT, bool LATE_W = false>  // LATE_W (ablation A/B): the weights issued after the wait
+__device__ __forceinline__ void dlin_cons_heads(const DlArgs& a, int grp, int z, int ngroups, int splits, char* smem) {
+  char* xs = smem;
+  float(*ssr)[32] = reinterpret_cast<float(*)[32]>(smem + 16 * NT * G2_PITCH);
+  unsigned* flag = reinterpret_cast<unsigned*>(smem + 16 * NT * G2_PITCH + G3_WAVES * 32 * 4);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int n = grp * G3_ROWS + wave * 16 + l16;
+  const int K = a.K, R = a.R;
+  const int kc = z * G2_KC;
+  const bf16* wrow = a.W + ((long)(n >> 4) * (K >> 5) * 64 + lane) * 8;
+  bf16x8 wv[16];
+  auto issue_w = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bf16x8* wp = reinterpret_cast<const bf16x8*>(wrow + (long)((kc >> 5) + s) * 512);
+#if OSPO_DLIN_NTW
+      wv[s] = __builtin_nontemporal_load(wp);
+#else
+      wv[s] = *wp;
+#endif
+    }
+  };
+  if constexpr (!LATE_W) issue_w();
+  if (threadIdx.x < 64) {  // wave 0 polls its four heads' flags (one lane each), then the agent-scope acquire
+    const unsigned ep = dl_epoch(a);
+    const int h0 = kc / HD, nh = G2_KC / HD;
+    unsigned spins = 0;
+    for (;;) {
+      const bool ok = lane >= nh || __hip_atomic_load(a.hflag + h0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep;
+      if (__all(ok)) break;
+      if (++spins > DL_SPIN_LIMIT) {
+        if (lane == 0) __hip_atomic_store(a.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if constexpr (LATE_W) issue_w();
+  for (int r = wave; r < 16 * NT; r += G3_WAVES) {
+    const int rr = r < R ? r : R - 1;
+    __builtin_amdgcn_global_load_lds(a.X + (long)rr * a.ldx + kc + 8 * lane, (LDS_AS void*)(xs + r * G2_PITCH), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      bf16x8 xf = *reinterpret_cast<const bf16x8*>(xs + (16 * j + l16) * G2_PITCH + (32 * s + 8 * g) * 2);
+      if (16 * j + l16 >= R) xf = bf16x8{};
+      acc[j] = MFMA(xf, wv[s], acc[j]);
+    }
+  }
+  __syncthreads();
+  f32x4 accs[1][NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) accs[0][j] = acc[j];
+  dlin_finish<NT, DL_PLAIN, 1>(a, accs, 1, grp, z, splits, ngroups, xs, ssr, flag);
+}
+
+template <int NT>
+constexpr int dattn_o_lds() {
+  return std::max(2 * ATT_HALF_LDS, 16 * NT * G2_PITCH + G3_WAVES * 32 * 4 + 16);
+}
+
+// blocks 0 .. n_attn - 1: attention, head-major (h = b / nrp, rows 2 (b % nrp), + 1), so the heads of the first
+// o splits finish first; then the o workgroups split-major (z = u / ngroups).  Blocks dispatch in order: every
+// producer is resident or done before a consumer takes a slot, and the waits are bounded either way (tmo).
+template <int NT, bool LATE_W = false>
+__device__ __forceinline__ void dattn_o_body(const AttnArgs& at, const DlArgs& o, int n_attn, int nrp, int ngroups,
+                                             int splits, char* smem) {
+  if ((int)blockIdx.x < n_attn) {
+    const int h = blockIdx.x / nrp, rp = blockIdx.x - h * nrp;
+    const int half = threadIdx.x >> 8;
+    attn_row_pub(at, 2 * rp + half, h, threadIdx.x & 255, smem + half * ATT_HALF_LDS);
+    __syncthreads();
+    // both rows' stores acknowledged: a ticket on the head's counter (flags[H + h]); the head's last workgroup
+    // zeroes it and publishes the head's flag = epoch (flags[h])
+    if (threadIdx.x == 0) {
+      unsigned* tk = o.hflag + at.H + h;
+      if (__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nrp - 1u) {
+        __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(o.hflag + h, dl_epoch(o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else {
+    const int u = blockIdx.x - n_attn;
+    dlin_cons_heads<NT, LATE_W>(o, u % ngroups, u / ngroups, ngroups, splits, smem);
+  }
+}
+
+template <int NT, bool LATE_W = false>
+__global__ __launch_bounds__(64 * G3_WAVES) __attribute__((amdgpu_waves_per_eu(6))) void dattn_o_kernel(
+    const AttnArgs at, const DlArgs o, int n_attn, int nrp, int ngroups, int splits) {
+  __shared__ __attribute__((aligned(16))) char smem[dattn_o_lds<NT>()];
+  dattn_o_body<NT, LATE_W>(at, o, n_attn, nrp, ngroups, splits, smem);
+}
+#ifdef OSPO_ABLATION
+// A/B (ablation build, OSPO_ATTN_O_VAR=2): the compiler's register budget (~86 VGPRs: two workgroups per CU, the o
+// workgroups dispatched only as attention workgroups retire)
+template <int NT>
+__global__ __launch_bounds__(64 * G3_WAVES) void dattn_o2_kernel(const AttnArgs at, const DlArgs o, int n_attn, int nrp,
+                                                                 int ngroups, int splits) {
+  __shared__ __attribute__((aligned(16))) char smem[dattn_o_lds<NT>()];
+  dattn_o_body<NT>(at, o, n_attn, nrp, ngroups, splits, smem);
+}
+#endif
+
 #ifdef OSPO_ABLATION
 // ABLATION BUILD ONLY (measured and rejected): ospo_decode_linear v2 (round 3): the same units, partials, summation order and consumers as dlin_kernel
 // (bit-identical outputs), but ~256 long-lived workgroups instead of one workgroup per (row group, split).
@@ -1822,6 +2050,50 @@ extern "C" int ospo_decode_mlp(const void* W_gu, const void* W_down, const void*
     hipLaunchKernelGGL((dmlp_kernel<1, 4>), grid, dim3(64 * G3_WAVES), 0, stream, g, d, ng, nd, sd);
   else
     hipLaunchKernelGGL((dmlp_kernel<2, 4>), grid, dim3(64 * G3_WAVES), 0, stream, g, d, ng, nd, sd);
+  OSPO_CHECK_LAUNCH();
+  return OSPO_OK;
+}
+
+extern "C" int ospo_decode_attn_o(const void* q, int ldq, const void* k_cache, const void* v_cache, int R, int n_heads,
+                                  int Tmax, const int* start, const int* pos_dev, float scale, void* attn_out,
+                                  int ld_attn, const void* W_o, const void* residual, int ldr, void* out, int ldo,
+                                  float* ss_out, const int* step_dev, int layer, unsigned* flags, unsigned* tmo,
+                                  void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (!q || !k_cache || !v_cache || !start || !pos_dev || !attn_out || !W_o || !residual || !out || !step_dev ||
+      !flags || !tmo || !ws)
+    return OSPO_ERR_ARG;
+  const int D = n_heads * HD;
+  if (R <= 0 || R > 32 || n_heads <= 0 || Tmax <= 0 || Tmax > ATT_MAXT || layer < 0 || layer >= 63) return OSPO_ERR_SHAPE;
+  if (ldq < D || ldq % 8 || ld_attn < D || ld_attn % 8 || ldr < D || ldo < D) return OSPO_ERR_SHAPE;
+  const size_t need = ospo_decode_linear_ws_bytes(R, D, D);
+  if (need == 0 || ws_bytes < need) return OSPO_ERR_ARG;
+  if (!aligned16(q) || !aligned16(k_cache) || !aligned16(v_cache) || !aligned16(attn_out) || !aligned16(W_o) ||
+      !aligned16(ws))
+    return OSPO_ERR_ALIGN;
+  // the o workgroups take one 512-k chunk = four heads each, with decode_linear's split plan
+  const int kper = gemv3_kper(D, D), splits = (D + kper - 1) / kper, ngroups = D / G3_ROWS;
+  if (kper != G2_KC || D % G2_KC || (long)R * ld_attn * 2 >= (1L << 31)) return OSPO_ERR_UNSUPPORTED;
+  AttnArgs at;
+  at.q = (const bf16*)q; at.ldq = ldq; at.kc = (const bf16*)k_cache; at.vc = (const bf16*)v_cache;
+  at.H = n_heads; at.Tmax = Tmax; at.start = start; at.pos = pos_dev; at.scale = scale;
+  at.out = (bf16*)attn_out; at.ldo = ld_attn; at.R = R;
+  DlArgs o;
+  o.W = (const bf16*)W_o; o.X = (const bf16*)attn_out; o.ldx = ld_attn; o.R = R; o.K = D; o.kper = kper;
+  o.ss_in = nullptr; o.ss_groups = 0; o.ln_w = nullptr; o.eps = 0.f;
+  o.bias = nullptr; o.gelu = 0; o.res = (const bf16*)residual; o.ldr = ldr;
+  o.out = (bf16*)out; o.ldo = ldo; o.ss_out = ss_out;
+  o.pos = nullptr; o.cs = o.sn = nullptr; o.kc = o.vc = nullptr; o.H = n_heads; o.Tmax = 0;
+  o.cnt = (unsigned*)ws; o.part = (float*)((char*)ws + DL_CNT_BYTES); o.part_bytes = (int)(need - DL_CNT_BYTES);
+  o.hflag = flags; o.epoch_step = step_dev; o.epoch_layer = layer; o.tmo = tmo;
+  const int nrp = (R + 1) / 2, n_attn = nrp * n_heads;
+  const dim3 grid(n_attn + ngroups * splits);
+  auto kfn = R <= 16 ? dattn_o_kernel<1> : dattn_o_kernel<2>;
+#ifdef OSPO_ABLATION
+  static const int var = getenv("OSPO_ATTN_O_VAR") ? atoi(getenv("OSPO_ATTN_O_VAR")) : 0;
+  if (var == 1) kfn = R <= 16 ? dattn_o_kernel<1, true> : dattn_o_kernel<2, true>;
+  if (var == 2) kfn = R <= 16 ? dattn_o2_kernel<1> : dattn_o2_kernel<2>;
+#endif
+  hipLaunchKernelGGL(kfn, grid, dim3(64 * G3_WAVES), 0, stream, at, o, n_attn, nrp, ngroups, splits);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }

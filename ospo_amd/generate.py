@@ -49,7 +49,7 @@ class T2IGenerator:
                  max_prompt_len: int = 64, n_img_tokens: int = 576, cfg_weight: float = 5.0,
                  temperature: float = 1.0, pad_id: int = PAD_ID, vq_weights: Optional[Dict[str, torch.Tensor]] = None,
                  tiled_weights: bool = True, fused_layers: bool = True, mlp_one_launch: bool = True,
-                 head_split: bool = False):
+                 head_split: bool = False, attn_o_one_launch: bool = False):
         if dims.head_dim != 128:
             raise ValueError("head_dim must be 128 (Janus-Pro)")
         if 2 * max_batch > 64:
@@ -150,6 +150,12 @@ class T2IGenerator:
         self.mlp_flags = torch.zeros(max(2 * Fd // 128, 1), dtype=torch.int32, device=dev)
         self.mlp_tmo = torch.zeros(1, dtype=torch.int32, device=dev)
         self._side = torch.cuda.Stream(device=dev) if self.head_split else None
+        # the cached attention and o in one launch (ops.decode_attn_o, round 5; an A/B option, measured 1.6-2.7 %
+        # slower than the two launches): a flag and a ticket per head, the same epochs; tmo shared with the MLP's waits
+        self.attn_o_one_launch = (bool(attn_o_one_launch) and self.fused and not self.head_split
+                                  and dims.n_layers < 63)
+        self.attn_o_used = False  # (set when a decode step took the one-launch form: its shapes fit)
+        self.attn_flags = torch.zeros(2 * dims.n_heads, dtype=torch.int32, device=dev)
         self._graph = None
         self._graph_B = None
         self.probs = None  # [n, B, V] fp32 when record_probs
@@ -302,9 +308,16 @@ class T2IGenerator:
                 main.wait_event(ev_s)
             else:
                 ops.decode_linear(x, lw["qkv_d"], self.q[:R], ws, epi="kv", norm=(ss, lw["ln_in"], eps), kv=kv)
-                ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos, scale,
-                               self.attn[:R])
-            ops.decode_linear(self.attn[:R], lw["o_d"], self.xmid[:R], ws, residual=x, ss_out=self.ss_mid)
+            if self.attn_o_one_launch and ops.decode_attn_o(
+                    self.q[:R], self.kc[i], self.vc[i], R, H, self.Tmax, self.start, self.pos, scale, self.attn[:R],
+                    lw["o_d"], x, self.xmid[:R], self.ss_mid, ws, step=self.step, layer=i, flags=self.attn_flags,
+                    tmo=self.mlp_tmo):
+                self.attn_o_used = True
+            else:
+                if not self.head_split:
+                    ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos,
+                                   scale, self.attn[:R])
+                ops.decode_linear(self.attn[:R], lw["o_d"], self.xmid[:R], ws, residual=x, ss_out=self.ss_mid)
             if not (self.mlp_one_launch and ops.decode_mlp(
                     self.xmid[:R], lw["gu_d"], lw["down_d"], self.h[:R], xo, ws, norm=(self.ss_mid, lw["ln_post"], eps),
                     ss_out=sso, step=self.step, layer=i, flags=self.mlp_flags, tmo=self.mlp_tmo)):
@@ -359,6 +372,7 @@ class T2IGenerator:
         self.pos.fill_(Lp)      # the first decoded token sits at position Lp
         self.step.fill_(0)
         self.mlp_flags.zero_()  # (the flags' epochs restart with the step counter)
+        self.attn_flags.zero_()
         self.tokens.zero_()
         self.probs = (torch.zeros(self.n_img, B, dims.img_vocab, dtype=torch.float32, device=self.device)
                       if record_probs else None)
@@ -379,6 +393,6 @@ class T2IGenerator:
             for s in range(n_rest):
                 self._host_step = s + 1
                 self._decode_step(R)
-        if self.mlp_one_launch and int(self.mlp_tmo.item()) != 0:
-            raise RuntimeError("decode_mlp: a down workgroup's wait for h gave up (outputs invalid)")
+        if (self.mlp_one_launch or self.attn_o_one_launch) and int(self.mlp_tmo.item()) != 0:
+            raise RuntimeError("decode_mlp / decode_attn_o: a consumer workgroup's wait gave up (outputs invalid)")
         return self.tokens[:B]

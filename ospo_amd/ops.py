@@ -753,6 +753,32 @@ def decode_mlp(xmid: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, h: 
     return True
 
 
+def decode_attn_o(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, R: int, n_heads: int, Tmax: int,
+                  start: torch.Tensor, pos: torch.Tensor, scale: float, attn_out: torch.Tensor, w_o: torch.Tensor,
+                  residual: torch.Tensor, out: torch.Tensor, ss_out: torch.Tensor, ws: torch.Tensor, *, step,
+                  layer: int, flags: torch.Tensor, tmo: torch.Tensor) -> bool:
+    """The cached attention and the o projection in one launch (ospo_decode_attn_o, round 5): attn_cache(q, ...,
+    attn_out) then decode_linear(attn_out, w_o, out, residual=residual, ss_out=ss_out), bit for bit.  flags: int32
+    [>= 2 * n_heads] (per-head flags, then tickets), zero before the first call; tmo: int32 [1].  Returns False (nothing
+    launched) when the o split plan does not map onto the one-launch form."""
+    for t, nme in ((q, "q"), (attn_out, "attn_out"), (residual, "residual"), (out, "out")):
+        _chk(t, BF16, nme)
+    for t, nme in ((flags, "flags"), (tmo, "tmo"), (step, "step"), (start, "start"), (pos, "pos")):
+        if t.dtype != torch.int32 or not t.is_contiguous():
+            raise ValueError(f"decode_attn_o: {nme} must be contiguous int32")
+    if flags.numel() < 2 * n_heads:
+        raise ValueError("decode_attn_o: flags needs 2 * n_heads words")
+    rc = getattr(_lib.lib(), "ospo_decode_attn_o")(
+        _p(q), _ld(q), _p(k_cache), _p(v_cache), int(R), int(n_heads), int(Tmax), _p(start), _p(pos), float(scale),
+        _p(attn_out), _ld(attn_out), _p(w_o), _p(residual), _ld(residual), _p(out), _ld(out), _p(ss_out), _p(step),
+        int(layer), _p(flags), _p(tmo), _p(ws), ws.numel() * 4, _s())
+    if rc == 4:  # OSPO_ERR_UNSUPPORTED: the caller runs the two launches
+        return False
+    if rc != 0:
+        raise ValueError(f"ospo_decode_attn_o: {_lib.lib().ospo_strerror(rc).decode()} (status {rc})")
+    return True
+
+
 def interleave_gate_up(gu: torch.Tensor) -> torch.Tensor:
     """[gate; up] rows [2F, K] -> the order ospo_decode_linear's swiglu epilogue reads: 128-row group g =
     gate rows 64g .. 64g+63, then up rows F + 64g .. (F % 64 == 0)."""

@@ -183,9 +183,9 @@ def test_cfg_sample_inverse_cdf_bit_exact(V, temp):
     assert bool((tokens[:, [0, 1, 3]] == -1).all())  # only step 2 written
 
 
-def _small_case(seed=11, B=3, n=24):
-    dims = O.JanusDims(n_layers=2, d_model=256, d_ff=512, n_heads=2, vocab=512, img_vocab=2048, gen_head_dim=256,
-                       lora_r=16, lora_alpha=32)
+def _small_case(seed=11, B=3, n=24, d_model=256, d_ff=512):
+    dims = O.JanusDims(n_layers=2, d_model=d_model, d_ff=d_ff, n_heads=d_model // 128, vocab=512, img_vocab=2048,
+                       gen_head_dim=256, lora_r=16, lora_alpha=32)
     w = O.init_weights(dims, seed=seed, dtype=torch.bfloat16, lora_b_std=1e-2)
     g = torch.Generator().manual_seed(seed)
     prompts = [torch.randint(8, dims.vocab, (int(L),), generator=g).tolist() for L in (9, 5, 7)[:B]]
@@ -426,6 +426,65 @@ def test_decode_mlp_one_launch_equals_two_launches(R):
         assert torch.equal(ss1[:, :R], ss2[:, :R]), (it, layer)
         assert torch.all(flags == it * 64 + layer + 1)  # every gate|up group published this call's epoch
         assert torch.all(ws[:1024] == 0)  # the down product's ticket counters
+
+
+@pytest.mark.parametrize("R", [32, 12, 7])
+def test_decode_attn_o_one_launch_equals_two_launches(R):
+    """Round 5: ops.decode_attn_o (the cached attention and the o projection in ONE launch, the o workgroups waiting
+    on per-head flags) writes exactly what attn_cache + decode_linear write -- the attention rows, the o
+    output and its row sums of squares -- over calls with new positions and (step, layer) epochs, padded rows
+    included; no wait gives up."""
+    H, D, Tmax = 32, 4096, 160
+    torch.manual_seed(500 + R)
+    wo = (torch.randn(D, D, device=DEV) * 0.02).bfloat16()
+    wo_t = ops().tile_decode_weight(wo)
+    ws = torch.zeros(ops().decode_linear_ws(R, D, D, DEV).numel(), device=DEV)
+    flags = torch.zeros(2 * H, dtype=torch.int32, device=DEV)
+    tmo = torch.zeros(1, dtype=torch.int32, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    kc = (torch.randn(R, H, Tmax, 128, device=DEV) * 0.5).bfloat16()
+    vc = (torch.randn(R, H, Tmax, 128, device=DEV) * 0.5).bfloat16()
+    start = torch.randint(0, 20, (R,), dtype=torch.int32, device=DEV)
+    start[0] = 150  # a padded query position at the first positions below
+    z = lambda *sh: torch.zeros(*sh, dtype=torch.bfloat16, device=DEV)  # noqa: E731
+    for it, layer, p in ((1, 0, 37), (1, 29, 37), (2, 0, 38), (9, 3, 155)):
+        step.fill_(it)
+        pos = torch.tensor([p], dtype=torch.int32, device=DEV)
+        q = torch.randn(R, D, device=DEV).bfloat16()
+        x = torch.randn(R, D, device=DEV).bfloat16()
+        a1, o1, a2, o2 = z(R, D), z(R, D), torch.full((R, D), 7.0, device=DEV).bfloat16(), z(R, D)
+        ss1 = torch.full((D // 128, 32), float("nan"), device=DEV)
+        ss2 = ss1.clone()
+        ops().attn_cache(q, kc, vc, R, 1, H, Tmax, start, pos, 128 ** -0.5, a1)
+        ops().decode_linear(a1, wo_t, o1, ws, residual=x, ss_out=ss1)
+        assert ops().decode_attn_o(q, kc, vc, R, H, Tmax, start, pos, 128 ** -0.5, a2, wo_t, x, o2, ss2, ws,
+                                   step=step, layer=layer, flags=flags, tmo=tmo)
+        torch.cuda.synchronize()
+        assert int(tmo.item()) == 0
+        assert torch.equal(a1, a2), (it, layer)
+        assert torch.equal(o1, o2), (it, layer)
+        assert torch.equal(ss1[:, :R], ss2[:, :R]), (it, layer)
+        assert torch.all(flags[:H] == it * 64 + layer + 1)  # every head published this call's epoch
+        assert torch.all(flags[H:] == 0)  # the head tickets, left zero
+        assert torch.all(ws[:1024] == 0)
+
+
+def test_generate_attn_o_one_launch_same_tokens():
+    """The decode step with attention + o in one launch (an A/B option) draws the tokens and probabilities of the
+    two-launch step bit for bit, eager and hipGraph."""
+    from ospo_amd.engine import ModelDims
+    from ospo_amd.generate import T2IGenerator
+    dims, w, prompts = _small_case(d_model=1024, d_ff=2048)  # o: 8 heads, two 512-k splits (the one-launch plan)
+    res = []
+    for one in (True, False):
+        gen = T2IGenerator(ModelDims.from_any(dims), w, device=DEV, max_batch=4, max_prompt_len=16, n_img_tokens=24,
+                           cfg_weight=5.0, temperature=1.0, pad_id=7, attn_o_one_launch=one)
+        assert gen.fused
+        tok = gen.generate(prompts, seed=5, use_graph=False, record_probs=True).cpu().clone()
+        assert gen.attn_o_used == one
+        res.append((tok, gen.probs.cpu().clone()))
+        assert torch.equal(gen.generate(prompts, seed=5, use_graph=True).cpu(), tok)
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
 @pytest.mark.parametrize("R", [32, 12])
