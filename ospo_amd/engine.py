@@ -80,7 +80,7 @@ class SimPOEngine:
                  dadb_splits=(8, 4, 4, 8), side_priority: int = -1, wgrad_wgs: int = 0, fuse_gdb: bool = True,
                  fuse_swiglu_gdb: bool = True,
                  da_stream: bool = True, keep_bits: bool = True, fuse_swiglu_u: bool = True,
-                 side_after_norm: bool = True, gdb_groups=("qkv", "o", "gu", "down")):
+                 side_after_norm: bool = True, gdb_groups=("qkv", "o", "gu", "down"), side_main=()):
         if not 0.0 <= float(lora_dropout) < 1.0:
             raise ValueError(f"lora_dropout must be in [0, 1), got {lora_dropout}")
         if linear_dtype not in ("bf16", "mx8"):
@@ -192,6 +192,8 @@ class SimPOEngine:
         # layer's down dX GEMM instead of that memory-bound norm (+0.4 % at the step, 3 of 3 alternating rounds,
         # profiles/r03/step_side_order_ab.jsonl); off: enqueued right after the q|k|v dX GEMM
         self.side_after_norm = bool(side_after_norm)
+        # side_main: the groups whose dA / dB run on the main stream instead of the side stream (A/B, round 5)
+        self.side_main = tuple(side_main)
         if len(self._dadb_splits) != 4 or min(self._dadb_splits) < 1:
             raise ValueError("dadb_splits must be four positive split counts")
         self._side = torch.cuda.Stream(device=self.device, priority=int(side_priority))
@@ -650,14 +652,20 @@ class SimPOEngine:
                           keep_bits=self._bits_bwd(i, "qkv", dr, D))
             pending.append(("qkv", gs, a["xn1"], dqkv, a["u_qkv"], dr, fdb))
             def enqueue_side():
-                # this layer's LoRA weight grads on the side stream (one event from main)
+                # this layer's LoRA weight grads on the side stream (one event from main); side_main groups on
+                # main, in the same order (the grads of a group are summed by the same kernels either way)
+                for name, gs_, x_in, dy, u, dr_, fdb_ in pending:
+                    if name in self.side_main:
+                        self._lora_grads(gs_, x_in, dy, u, lay.groups[name], gbase, dr_, fdb_,
+                                         self._bits_bwd(i, name, dr_, x_in.shape[1]))
                 ev = torch.cuda.Event()
                 ev.record(main)
                 side.wait_event(ev)
                 with torch.cuda.stream(side):
                     for name, gs_, x_in, dy, u, dr_, fdb_ in pending:
-                        self._lora_grads(gs_, x_in, dy, u, lay.groups[name], gbase, dr_, fdb_,
-                                         self._bits_bwd(i, name, dr_, x_in.shape[1]))
+                        if name not in self.side_main:
+                            self._lora_grads(gs_, x_in, dy, u, lay.groups[name], gbase, dr_, fdb_,
+                                             self._bits_bwd(i, name, dr_, x_in.shape[1]))
                     if on_layer_grads is not None:  # this layer's dA/dB are the last side-stream work so far
                         on_layer_grads(gbase, gbase + lay.per_layer)
                 ev2 = torch.cuda.Event()
