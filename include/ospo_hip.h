@@ -346,8 +346,9 @@ int ospo_swiglu_fwd_lora_down(const void* gu, int ld_gu, void* h, int ld_h, int 
  *                      columns 16*nmods..out_cols-1 written zero) -- g, bf16
  *   dB[j*Nmod + k][c] += sum_{m<M} dy[m][j*Nmod + k] * u[m][16 j + c]       -- fp32 atomic adds
  * dy [M, >= nmods*Nmod], Bt [nmods*16, Nmod] (ldb), u [M, >= 16*nmods].  Nmod % 128 == 0, nmods <= 4.
- * ws (>= ospo_lora_gdb_ws_bytes(M, nmods, Nmod) bytes): the fp32 partials of g, summed by a second
- * launch; calls sharing a ws must be ordered (same stream). */
+ * ws (>= ospo_lora_gdb_ws_bytes(M, nmods, Nmod) bytes, ZERO at allocation): a head of row-block counters
+ * (used only by the ablation library's in-launch sum, left zero), then the fp32 partials of g, summed by a
+ * second launch.  Calls sharing a ws must be ordered (same stream). */
 size_t ospo_lora_gdb_ws_bytes(int M, int nmods, int Nmod);
 int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M, int M_out,
                   int nmods, int Nmod, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,

@@ -644,11 +644,27 @@ __device__ __forceinline__ void tr4_wait(i16x4& a, i16x4& b, i16x4& c, i16x4& d)
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int RSB, int NS = 4, int YA = 0>  // YA: cache-policy bits of the dy loads
+// In-launch sum of the g partials (INL, round 5, ablation A/B: bit-identical, no faster in the step than
+// gdb_reduce_kernel's launch, ~7.7 us each, 90 per step):
+// every workgroup stores its partials write-through (sc1) and takes a ticket on its row block's counter; once
+// all gridDim.y workgroups of the row block have (a bounded wait; the host launches this form only when the whole
+// grid fits on the device at once), each sums its share of the row block's output quads in gdb_reduce_kernel's
+// order (bit-identical), then takes a second ticket, and the row block's last one zeroes both counters.
+struct GdbInl {
+  unsigned* cnt;  // [2][1024] row-block counters (zero at allocation, left zero), then a give-up word
+  int M_out;
+  float scale;
+  bf16* out;
+  int ldo, out_cols;
+};
+constexpr int GDB_CNT_BYTES = 8192 + 16;
+constexpr unsigned GDB_SPIN_LIMIT = 1u << 24;
+
+template <int RSB, int NS = 4, int YA = 0, bool INL = false>  // YA: cache-policy bits of the dy loads
 __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ dy, int ldy, const bf16* __restrict__ Bt,
                                                        int ldb, const bf16* __restrict__ u, int ldu, int M, int Nmod,
                                                        int nch, float* __restrict__ ws, int Mw,
-                                                       float* __restrict__ dB) {
+                                                       float* __restrict__ dB, const GdbInl inl = GdbInl{}) {
   // NS-stage ring of 8-KiB dy sub-tiles, NS - 1 in flight (a 6-stage ring measured 10-30 % slower)
   constexpr int STAGE = 8192;
   constexpr int BT_OFF = NS * STAGE, BT_BYTES = 16 * 4 * 128;  // up to nch = 4
@@ -754,7 +770,7 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
         const i16x8 bv = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
         accb = MFMA(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), accb);  // D[n = 4g+i][j = l16]
       }
-      if (rb == RSB - 1) {  // the chunk's dB over the workgroup's rows
+      if (rb == RSB - 1 && !(INL && cc == nch - 1)) {  // the chunk's dB over the workgroup's rows
         const long n0 = col0 + cc * 64 + 16 * wave + 4 * g;
 #pragma unroll
         for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[i]);
@@ -762,11 +778,78 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
       }
     }
   }
-  // g partials of this column block: ws [mod][sp][Mw][16]
+  if constexpr (!INL) {
+    // g partials of this column block: ws [mod][sp][Mw][16]
 #pragma unroll
-  for (int rb = 0; rb < RSB; ++rb) {
-    const int m = rb0 + rb * 64 + grow;
-    if (m < Mw) *reinterpret_cast<f32x4*>(ws + (((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[rb];
+    for (int rb = 0; rb < RSB; ++rb) {
+      const int m = rb0 + rb * 64 + grow;
+      if (m < Mw) *reinterpret_cast<f32x4*>(ws + (((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[rb];
+    }
+  } else {
+    const int nmods = gridDim.y / nsplit;
+    const __amdgpu_buffer_rsrc_t rsW =
+        __builtin_amdgcn_make_buffer_rsrc((void*)ws, 0, (int)((long)nmods * nsplit * Mw * 64), 0x00020000);
+#pragma unroll
+    for (int rb = 0; rb < RSB; ++rb) {
+      const int m = rb0 + rb * 64 + grow;
+      if (m < Mw)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, accg[rb]), rsW,
+                                               (uint32_t)(((((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) * 4), 0, 16);
+    }
+    {  // the last chunk's dB atomics after the partial stores: the wait below leaves them in flight
+      const long n0 = col0 + (nch - 1) * 64 + 16 * wave + 4 * g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[i]);
+    }
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this lane's partial stores acknowledged
+    __syncthreads();
+    const unsigned W = gridDim.y;  // the row block's workgroups
+    unsigned* c1 = inl.cnt + blockIdx.x;
+    unsigned* c2 = inl.cnt + 1024 + blockIdx.x;
+    if (threadIdx.x < 64) {
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(c1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned spins = 0;
+      while (__hip_atomic_load(c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < W) {
+        if (++spins > GDB_SPIN_LIMIT) {
+          if (threadIdx.x == 0) __hip_atomic_store(inl.cnt + 2048, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // this workgroup's share of the row block's output quads (rows up to M_out in the last row block)
+    const int rows = (blockIdx.x == gridDim.x - 1) ? inl.M_out - rb0 : min(ROWS, inl.M_out - rb0);
+    const int cq = inl.out_cols / 4;
+    const int total = rows > 0 ? rows * cq : 0;
+    const int per = (total + (int)W - 1) / (int)W;
+    const int q0 = (int)blockIdx.y * per, q1 = min(total, q0 + per);
+    for (int qq = q0 + (int)threadIdx.x; qq < q1; qq += 256) {
+      const int m = rb0 + qq / cq, c = (qq % cq) * 4, md = c / 16;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < M && md < nmods) {
+        for (int s0 = 0; s0 < nsplit; s0 += 8) {  // gdb_reduce_kernel's order: ((0 + p_0) + p_1) + ...
+          f32x4 pv[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (s0 + k < nsplit) pv[k] = *reinterpret_cast<const f32x4*>(ws + (((long)md * nsplit + s0 + k) * Mw + m) * 16 + (c & 15));
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (s0 + k < nsplit) v += pv[k];
+        }
+      }
+      uint2 pk;
+      pk.x = pack2(v[0] * inl.scale, v[1] * inl.scale);
+      pk.y = pack2(v[2] * inl.scale, v[3] * inl.scale);
+      *reinterpret_cast<uint2*>(inl.out + (long)m * inl.ldo + c) = pk;
+    }
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(c2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == W - 1u) {
+      __hip_atomic_store(c1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1513,8 +1596,27 @@ static int gdb_nch(int M, int nmods, int Nmod) {
 extern "C" size_t ospo_lora_gdb_ws_bytes(int M, int nmods, int Nmod) {
   if (M <= 0 || nmods <= 0 || Nmod <= 0 || Nmod % 128) return 0;
   const size_t Mw = (size_t)(M + 63) / 64 * 64;
-  return (size_t)nmods * (Nmod / 128) * Mw * 16 * sizeof(float) + 16;  // the nch = 2 worst case
+  // the in-launch sum's counters (head), then the partials (the nch = 2 worst case)
+  return GDB_CNT_BYTES + (size_t)nmods * (Nmod / 128) * Mw * 16 * sizeof(float) + 16;
 }
+
+#ifdef OSPO_ABLATION
+// lora_gdb_kernel's in-launch sum needs every workgroup of the grid resident at once (its row blocks wait for
+// all their workgroups): the device's capacity for the kernel, cached per device
+static long gdb_inl_capacity() {
+  static long cap[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (cap[dev] == 0) {
+    int ncu = 0, per = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lora_gdb_kernel<8, 4, 0, true>, 256, 0) != hipSuccess)
+      return 0;
+    cap[dev] = (long)ncu * per;
+  }
+  return cap[dev];
+}
+#endif
 
 extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M, int M_out,
                              int nmods, int Nmod, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
@@ -1532,6 +1634,22 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   const int nsplit = Nmod / (64 * nch);
   const int Mw = (M + 63) / 64 * 64;
   const dim3 grid((M + 511) / 512, nmods * nsplit);
+  float* part = (float*)((char*)ws + GDB_CNT_BYTES);
+  // A/B (ablation build, OSPO_GDB_INL=1): the partials summed inside the launch where the whole grid fits on the
+  // device at once -- bit-identical, and no faster in the step (36.44 / 36.37 against 36.47 / 36.37 pairs/s,
+  // profiles/r05/gdb_inlaunch_ab.txt): the product keeps the reduce launch
+  bool inl = false;
+#ifdef OSPO_ABLATION
+  if (getenv("OSPO_GDB_INL"))
+    inl = grid.x <= 1024 && (long)grid.x * grid.y <= gdb_inl_capacity() && (long)M_out * out_cols < (1L << 31);
+#endif
+  if (inl) {
+    const GdbInl gi{(unsigned*)ws, M_out, scale, (bf16*)out, ldo, out_cols};
+    hipLaunchKernelGGL((lora_gdb_kernel<8, 4, 0, true>), grid, dim3(256), 0, stream, (const bf16*)dy, ldy,
+                       (const bf16*)Bt, ldb, (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, gi);
+    OSPO_CHECK_LAUNCH();
+    return OSPO_OK;
+  }
   auto kfn = lora_gdb_kernel<8, 4>;
 #ifdef OSPO_ABLATION
   if (getenv("OSPO_GDB_NS6")) kfn = lora_gdb_kernel<8, 6>;  // A/B: a 6-stage ring
@@ -1539,12 +1657,12 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   if (getenv("OSPO_GDB_NS3")) kfn = lora_gdb_kernel<8, 3>;
   if (getenv("OSPO_NT_GDB")) kfn = lora_gdb_kernel<8, 4, 2>;  // A/B: non-temporal dy loads
 #endif
-  hipLaunchKernelGGL(kfn, grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
-                     (const bf16*)u, ldu, M, Nmod, nch, (float*)ws, Mw, dB);
-  OSPO_CHECK_LAUNCH();
   const long n = (long)M_out * (out_cols / 4);
   if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
-  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)ws,
+  hipLaunchKernelGGL(kfn, grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
+                     (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, GdbInl{});
+  OSPO_CHECK_LAUNCH();
+  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part,
                      nmods, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
@@ -1589,13 +1707,14 @@ extern "C" int ospo_swiglu_lora_gdb(const void* dh, int ld_dh, const void* gu, i
     }
   }
 #endif
-  hipLaunchKernelGGL(kfn, dim3((M + rows - 1) / rows, nsplit), dim3(256), 0, stream,
-                     (const bf16*)dh, ld_dh, (const bf16*)gu, ld_gu, (bf16*)dgu, ld_dgu, (const bf16*)Bt, ldb,
-                     (const bf16*)u, ldu, M, F, (float*)ws, Mw, dB);
-  OSPO_CHECK_LAUNCH();
   const long n = (long)M_out * (out_cols / 4);
   if (n >= (1L << 31)) return OSPO_ERR_SHAPE;
-  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)ws, 2,
+  float* part = (float*)((char*)ws + GDB_CNT_BYTES);  // (ospo_lora_gdb's layout: the counters' head first)
+  hipLaunchKernelGGL(kfn, dim3((M + rows - 1) / rows, nsplit), dim3(256), 0, stream,
+                     (const bf16*)dh, ld_dh, (const bf16*)gu, ld_gu, (bf16*)dgu, ld_dgu, (const bf16*)Bt, ldb,
+                     (const bf16*)u, ldu, M, F, part, Mw, dB);
+  OSPO_CHECK_LAUNCH();
+  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part, 2,
                      nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;

@@ -268,7 +268,7 @@ class SimPOEngine:
             nb = max((int(ops.query_gdb_ws(Mc, g.nmods, g.Nmod)) for g in self.layout.groups.values()
                       if g.Nmod % 128 == 0 and g.nmods <= 4), default=0)
             if nb > 0:
-                self._gdb_ws = torch.empty((nb + 15) // 16 * 4, dtype=F32, device=dev)
+                self._gdb_ws = torch.zeros((nb + 15) // 16 * 4, dtype=F32, device=dev)  # (counters: zero)
         # MXFP8 activation operands, one per contraction size (main-stream GEMMs only, reused in order)
         self._mx = {K: ops.MX8(Mc, K, dev) for K in {D, Fd, 2 * Fd, 3 * D}} if self.linear_dtype == "mx8" else {}
 

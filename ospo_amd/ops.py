@@ -597,9 +597,10 @@ def query_gdb_ws(M, nmods, Nmod) -> int:
 
 
 def lora_gdb_ws(M, nmods, Nmod, device="cuda") -> torch.Tensor:
-    """Workspace for ospo_lora_gdb's fp32 partials of g."""
+    """Workspace for ospo_lora_gdb: its row-block counters (zero at allocation, left zero) and the fp32 partials
+    of g."""
     n = int(query("ospo_lora_gdb_ws_bytes", M, nmods, Nmod))
-    return torch.empty((n + 15) // 16 * 4, dtype=torch.float32, device=device)
+    return torch.zeros((n + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
 def lora_gdb(dy, bt, u, out, dB, M, M_out, nmods, Nmod, scale, ws=None):

@@ -719,6 +719,34 @@ def test_lora_gdb_exact_integers(M, M_out, nm, Nmod):
     assert torch.equal(dB.double(), dB_ref)
 
 
+@pytest.mark.parametrize("M,M_out,nm,Nmod", [(4800, 4864, 1, 4096), (4800, 4800, 3, 4096), (1000, 1100, 1, 1024),
+                                            (130, 130, 2, 512)])
+def test_lora_gdb_in_launch_sum(M, M_out, nm, Nmod):
+    """Round 5 (the workspace's counter head; with OSPO_HIP_LIB = the ablation library and OSPO_GDB_INL=1 the
+    in-launch partial sum): g exact on small integers (rows M .. M_out -- also past the last row block -- and pad
+    columns zero), the same bits over repeated calls on one workspace, whose counter head is zero after every
+    call (no wait gave up)."""
+    r = 16
+    dy = ints(M_out, nm * Nmod, lo=-2, hi=3)
+    BT = ints(nm * r, Nmod, lo=-2, hi=3)
+    Rp = 64 if nm * r <= 64 else 128
+    u = ints(M_out, Rp, lo=-2, hi=3)
+    ws = ops().lora_gdb_ws(M, nm, Nmod, DEV)
+    dyd, Bd = dy[:M].double(), BT.double()
+    g_ref = torch.cat([dyd[:, j * Nmod:(j + 1) * Nmod] @ Bd[j * r:(j + 1) * r].T for j in range(nm)], 1)
+    first = None
+    for it in range(3):
+        out = torch.full((M_out, Rp), 7.0, device=DEV, dtype=torch.bfloat16)
+        dB = torch.zeros(nm * Nmod, r, device=DEV, dtype=torch.float32)
+        ops().lora_gdb(dy, BT, u, out, dB, M, M_out, nm, Nmod, 0.5, ws=ws)
+        torch.cuda.synchronize()
+        assert torch.all(ws[:2052] == 0), it  # the counters (and the give-up word) left zero
+        assert torch.equal(out[:M, : nm * r].float(), bf(0.5 * g_ref.float()).float())
+        assert torch.all(out[M:] == 0) and torch.all(out[:, nm * r:] == 0)
+        first = out.clone() if first is None else first
+        assert torch.equal(out, first)
+
+
 @pytest.mark.parametrize("M,M_out,F", [(4800, 4800, 11008), (4800, 4864, 11008), (777, 832, 4096), (100, 128, 1024),
                                        (1000, 1024, 384), (64, 64, 128), (3001, 3008, 2816)])
 def test_swiglu_lora_gdb_equals_two_launches(M, M_out, F):
