@@ -427,6 +427,13 @@ class SimPOEngine:
         B, Lt = text_ids.shape
         N = chosen_ids.shape[1]
         self.ensure_capacity(B, Lt)
+        # the in-launch split sums' counters (workspace heads: lora_skinny SK_CNT_BYTES = 4096, lora_gdb 8208 B) are
+        # left zero by every call that completes; re-zeroing them once per step (two small fills) bounds the damage of
+        # one that did not (an aborted step) to that step
+        if getattr(self, "_sk_ws", None) is not None:
+            self._sk_ws[:1024].zero_()
+        if getattr(self, "_gdb_ws", None) is not None:
+            self._gdb_ws[:2052].zero_()
         if N != self.N:
             raise ValueError(f"batch (B={B}, Lt={Lt}, N={N}) exceeds engine capacity "
                              f"(pairs={self.cap_pairs}, T={self.cap_T}, N={self.N})")

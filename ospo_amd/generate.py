@@ -373,6 +373,8 @@ class T2IGenerator:
         self.step.fill_(0)
         self.mlp_flags.zero_()  # (the flags' epochs restart with the step counter)
         self.attn_flags.zero_()
+        if self.fused:
+            self.lws[:1024].zero_()  # the decode Linears' split-sum counters (DL_CNT_BYTES), left zero by every call
         self.tokens.zero_()
         self.probs = (torch.zeros(self.n_img, B, dims.img_vocab, dtype=torch.float32, device=self.device)
                       if record_probs else None)
