@@ -1,5 +1,6 @@
 # Round 5: T2I bench with the VQ pixel decode pipelined on a side stream (default) vs serial, 2 alternating rounds;
 # tokens and pixels checksums must agree
+# (ran against the bench.py of that experiment, which had --t2i-serial-decode and a pipelined default; the bench keeps the serial step)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
