@@ -147,6 +147,46 @@ def cpu_baseline(Lt=24, N=576, L=30, reps=2):
                       f"{', '.join(f'{t:.2f}' for t in times)} s, median {t_pair:.2f} s/pair, {threads} threads"}
 
 
+def box_probe(dev, seconds=2.0, size=4096, reps=50):
+    """A fixed random-data GEMM on this box, outside the timed region: the product's bf16
+    K loop (gemm_nt_w4_kernel, plain, unsplit) on size^3 random bf16 in [-1, 1), after >= `seconds` of
+    back-to-back launches (MI355X_MICROARCH.md 'DVFS give-back' item 6), then `reps` launches timed with HIP
+    events and the per-workgroup in-kernel clock of the last one (d s_memtime / d s_memrealtime x 100 MHz over
+    the K loop).  Box-to-box spread of the step tracks this probe, so step changes measured on different boxes
+    are compared as value / probe TF/s."""
+    import numpy as np
+    from ospo_amd import ops
+    g = torch.Generator(device=dev).manual_seed(20260)
+    a = (torch.rand(size, size, generator=g, device=dev) * 2 - 1).bfloat16()
+    b = (torch.rand(size, size, generator=g, device=dev) * 2 - 1).bfloat16()
+    c = torch.empty(size, size, dtype=torch.bfloat16, device=dev)
+    tiles = (size // 256) ** 2
+    stamps = torch.zeros(tiles * 8, dtype=torch.int64, device=dev)
+    t0, warm = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(20):
+            ops.gemm_clock_probe(a, b, c, stamps)
+        warm += 20
+        torch.cuda.synchronize()
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        ops.gemm_clock_probe(a, b, c, stamps)
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    tf = 2.0 * size ** 3 / (us * 1e-6) / 1e12
+    s = stamps.cpu().numpy().reshape(tiles, 8).astype(np.float64)
+    clk = (s[:, 3] - s[:, 0]) / np.maximum(s[:, 4] - s[:, 2], 1) * 0.1  # GHz
+    cyc = (s[:, 3] - s[:, 0]) / (size // 64)
+    return {"kernel": f"gemm_nt_w4_kernel, plain, unsplit, {size}^3 bf16, random operands in [-1, 1)",
+            "warm_launches": warm, "warm_s": round(time.perf_counter() - t0, 2), "avg_launch_us": round(us, 2),
+            "tflops": round(tf, 1), "frac": round(tf / PEAK_BF16_TFLOPS, 4),
+            "clock_ghz_p10_p50_p90": [round(float(np.percentile(clk, q)), 3) for q in (10, 50, 90)],
+            "cycles_per_ktile_p50": round(float(np.median(cyc)), 1)}
+
+
 def t2i_bytes_per_step(dims, R, T_keys):
     """Algorithmic HBM bytes of one decode step: every weight once (decoder
     Linears, gen_head, aligner W2; bf16), the KV cache read by attention (K and V of T_keys
@@ -358,15 +398,19 @@ def wrapper_setup(args, world, rank, dev, engine=None):
 
 
 def time_wrapper(model, w, opt, sched, allreduce, batches, log_steps, args, world, dev):
-    """A Trainer step as ospo_amd.trainer.Trainer runs it: training_step -> loss.backward() -> all-reduce ->
+    """A Trainer step as ospo_amd.trainer.Trainer runs it: training_step -> loss.backward() with the all-reduce
+    overlapped (layer ranges pushed from the backward) ->
     on_before_optimizer_step (grad-norm log) -> FusedLoraAdamW.step -> scheduler -> zero_grad, the logged
     metrics read on the host every log_steps optimizer steps."""
     from ospo_amd import dist as odist
 
     def step(i):
         loss = w.training_step(batches[i % 2], i)
+        allreduce.begin(model.engine.grads)  # overlapped with the backward, as Trainer.fit runs it
+        model.engine.layer_grads_hook = allreduce.push
         loss.backward()
-        allreduce(model.engine.grads)
+        model.engine.layer_grads_hook = None
+        allreduce.finish()
         w.on_before_optimizer_step()
         opt.step()
         sched.step()
@@ -530,6 +574,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wrapper", action="store_true")  # skip the drop-in wrapper sub-measurement
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--no-box-probe", action="store_true")  # skip the fixed-GEMM box probe (outside the timed region)
     ap.add_argument("--wgrad-wgs", type=int, default=0)  # A/B: LoRA weight grads as ospo_lora_wgrad streams
     ap.add_argument("--round2-lora", action="store_true")  # A/B: round 2's LoRA kernels (dA tiles, re-hashed masks, unfused u_d)
     # A/B: "da_tiles", "swiglu_unfused", "swiglu_gdb_unfused", "gdb_gu_only" (q|k|v, o, down: g from the skinny
@@ -698,6 +743,9 @@ def main():
     if wrap is not None:
         wrap["vs_engine_path"] = round(wrap["value"] / value, 4)
         line["drop_in_wrapper"] = wrap
+    if not args.no_box_probe:
+        line["box_probe"] = box_probe(dev)
+        line["box_probe"]["value_per_probe_pflops"] = round(value / (line["box_probe"]["tflops"] / 1e3), 3)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(Lt=Lt, N=N)
     print(json.dumps(line), flush=True)

@@ -32,7 +32,37 @@ typedef enum {
 } ospo_status;
 
 const char* ospo_strerror(int status);
+
+/* ABI revision; bumped whenever a signature, a workspace layout or the dropout masks a seed produces change.
+ * 2 (round 6): ospo_lora_gdb's partials sit behind a zero-at-allocation counter head (OSPO_WS_LORA_GDB), the
+ * round-5 dropout hash (new masks for every seed), ospo_ws_counter_bytes and ospo_gemm_clock_probe_bf16.
+ * Bindings check it when they load the library (ospo_amd/_lib.py). */
+#define OSPO_ABI_VERSION 2
 int ospo_abi_version(void);
+
+/* Box probe (measurement aid, no reference counterpart): C = A . B^T with the product's bf16 256 x 256 K loop,
+ * unsplit, M % 256 == N % 256 == 0, K % 64 == 0, K >= 256, each 256 x 256 tile's workgroup writing 8 uint64
+ * stamps (stamps_bytes >= (M/256)(N/256) * 64): [0] s_memtime at the K loop's start, [1] s_memrealtime at entry,
+ * [2] s_memrealtime at the loop's start, [3] s_memtime and [4] s_memrealtime at its end, [5..7] s_memrealtime
+ * after the epilogue's staging, store issue and drain.  In-kernel clock = ([3]-[0]) / ([4]-[2]) x 100 MHz. */
+int ospo_gemm_clock_probe_bf16(const void* A, const void* B, void* C, int M, int N, int K, void* stamps,
+                               size_t stamps_bytes, hipStream_t stream);
+
+/* Counter heads at the START of a caller-owned workspace: they must be zero when the workspace is allocated and
+ * every call leaves them zero again (a host-side reset after an aborted stream zeroes exactly this many bytes). */
+typedef enum {
+  OSPO_WS_GEMM_TAIL = 0,      /* 4 KiB at the END of a split-K workspace, read only by the ablation build's
+                                 in-launch combine (the product library ignores them) */
+  OSPO_WS_SKINNY = 1,         /* ospo_lora_skinny / ospo_swiglu_fwd_lora_down: 4 KiB of row-block counters */
+  OSPO_WS_LORA_GDB = 2,       /* ospo_lora_gdb / ospo_swiglu_lora_gdb: 8 KiB of column-block counters + 16 B */
+  OSPO_WS_DECODE_LINEAR = 3   /* ospo_decode_linear / ospo_decode_mlp / ospo_decode_attn_o: 4 KiB */
+} ospo_ws_kind;
+#define OSPO_WS_GEMM_TAIL_CNT_BYTES 4096
+#define OSPO_WS_SKINNY_CNT_BYTES 4096
+#define OSPO_WS_LORA_GDB_CNT_BYTES (8192 + 16)
+#define OSPO_WS_DECODE_LINEAR_CNT_BYTES 4096
+/* bytes of that head (0 for an unknown kind) */
+size_t ospo_ws_counter_bytes(int kind);
 
 /* ------------------------------------------------------------------ GEMM ---
  * Linear layers of the Llama decoder with fused peft LoRA (peft lora.Linear
@@ -246,7 +276,7 @@ int ospo_gather_rows(const void* src, int ld_src, int S, int T, int t0, int N, i
 int ospo_scatter_rows(const void* src, int S, int T, int t0, int N, int D, void* dst, int ld_dst,
                       int total_rows, hipStream_t stream);
 
-/* Grouped row-vector sums (the logits/* metrics of get_batch_loss_metrics, ospo/wrapper/train.py:441-442,
+/* Grouped row-vector sums (the logits/... metrics of get_batch_loss_metrics, ospo/wrapper/train.py:441-442,
  * without the [S, T, V] logits: sum_v logits = z . colsum(W2) + sum(b2)):
  *   out[g] = (accumulate ? out[g] : 0) + sum_{r < rows_per_group} x[g*rows_per_group + r] . w
  *            [+ add_scale * add[0] when add != NULL]

@@ -16,9 +16,15 @@ LIB_PATH = os.environ.get("OSPO_HIP_LIB", os.path.join(_HERE, "libospo_hip.so"))
 
 P, I, L, F, Z, U = c_void_p, c_int, c_long, c_float, c_size_t, c_uint
 
+# include/ospo_hip.h OSPO_ABI_VERSION: a library built from other sources (another workspace layout, other
+# dropout masks) is refused at load instead of silently mis-driven
+ABI_VERSION = 2
+
 # name -> argtypes (restype is c_int = ospo_status unless listed in RESTYPES)
 SIGNATURES = {
     "ospo_abi_version": [],
+    "ospo_ws_counter_bytes": [I],
+    "ospo_gemm_clock_probe_bf16": [P, P, P, I, I, I, P, Z, P],
     "ospo_dropout_hash": [U, U],
     "ospo_gemm_nt_bf16": [P, I, P, I, I, I, I, P, I, P, I, I, F, P, P, I, P, I, I, P, Z, P],
     "ospo_gemm_nt_ws_bytes": [I, I, I, I, I, I],
@@ -104,7 +110,7 @@ ABLATION_SIGNATURES = {"ospo_set_gemm_variant": [I], "ospo_set_gemv_variant": [I
                        "ospo_set_skinny_variant": [I], "ospo_gemm_set_debug_buffer": [P],
                        "ospo_attn_set_stamps": [P]}
 
-RESTYPES = {"ospo_gemm_nt_ws_bytes": c_size_t, "ospo_row_dot_sum_ws_bytes": c_size_t, "ospo_lora_gdb_ws_bytes": c_size_t, "ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_decode_linear_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
+RESTYPES = {"ospo_ws_counter_bytes": c_size_t, "ospo_gemm_nt_ws_bytes": c_size_t, "ospo_row_dot_sum_ws_bytes": c_size_t, "ospo_lora_gdb_ws_bytes": c_size_t, "ospo_flash_attn_bwd_ws_bytes": c_size_t, "ospo_lora_skinny_ws_bytes": c_size_t, "ospo_mx8_scale_bytes": c_size_t, "ospo_decode_gemv_ws_bytes": c_size_t, "ospo_decode_linear_ws_bytes": c_size_t, "ospo_vq_groupnorm_ws_bytes": c_size_t, "ospo_dropout_hash": c_uint}
 
 _lib = None
 
@@ -132,6 +138,9 @@ def lib():
                 fn.restype = c_int
         h.ospo_strerror.argtypes = [c_int]
         h.ospo_strerror.restype = ctypes.c_char_p
+        if h.ospo_abi_version() != ABI_VERSION:
+            raise OspoError(f"{LIB_PATH}: ABI version {h.ospo_abi_version()}, this binding needs {ABI_VERSION} "
+                            "(rebuild the library from this tree)")
         _lib = h
     return _lib
 

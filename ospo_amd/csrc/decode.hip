@@ -636,7 +636,7 @@ __global__ __launch_bounds__(256) void attn_cache2_kernel(const bf16* __restrict
 //    The last arriver zeroes its counter again.  No fence: sc1 stores are visible device-wide once
 //    acknowledged (vmcnt(0) before the ticket) and sc1 loads do not hit a stale line.
 enum { DL_PLAIN = 0, DL_KV = 1, DL_SWIGLU = 2 };
-constexpr int DL_CNT_BYTES = 4096;  // workspace head: one counter per 128-row group (N <= 131072)
+constexpr int DL_CNT_BYTES = OSPO_WS_DECODE_LINEAR_CNT_BYTES;  // workspace head: one counter per 128-row group (N <= 131072)
 struct DlArgs {
   const bf16* W;
   const bf16* X;

@@ -2011,7 +2011,7 @@ SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus
   return pl;
 }
 
-constexpr size_t W4_CNT_BYTES = 4096;  // the w4 tail's arrival counters at the END of the split-K workspace
+constexpr size_t W4_CNT_BYTES = OSPO_WS_GEMM_TAIL_CNT_BYTES;  // the w4 tail's arrival counters at the END of the split-K workspace
 #include "gemm_w4.h"
 
 // The 4-wave hand-scheduled kernel (gemm_w4.h) when the shape fits it: bf16, <= 2 LoRA extension tiles,
@@ -2860,6 +2860,23 @@ extern "C" int ospo_gemm_nt_mx8(const void* A8, int lda, const void* Asc, const 
     return launch_mx<true>(a, stream, so);
   }
   return launch_mx<false>(a, stream, so);
+}
+
+// Box probe (bench.py box_probe, outside the timed region): the product's plain w4 program on A [M][K] . B [N][K]^T,
+// never split, with s_memtime / s_memrealtime stamps per workgroup (gemm_w4.h DBG 2) -- the same K loop as every
+// bf16 GEMM of the step, so its rate and in-kernel clock on fixed random data say how fast this box's GEMM runs.
+extern "C" int ospo_gemm_clock_probe_bf16(const void* A, const void* B, void* C, int M, int N, int K, void* stamps,
+                                          size_t stamps_bytes, hipStream_t stream) {
+  if (!A || !B || !C || !stamps) return OSPO_ERR_ARG;
+  if (M <= 0 || M % 256 || N <= 0 || N % 256 || K < 4 * BK || K % BK) return OSPO_ERR_SHAPE;
+  if ((long)M * K * 2 >= (1L << 31) || (long)N * K * 2 >= (1L << 31)) return OSPO_ERR_SHAPE;
+  if (stamps_bytes < (size_t)(M / 256) * (N / 256) * 8 * sizeof(uint64_t)) return OSPO_ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(B) || !aligned16(C) || !aligned16(stamps)) return OSPO_ERR_ALIGN;
+  GemmArgs a{(const bf16*)A, (const bf16*)B, nullptr, nullptr, K, K, 0, 0, M, N, K, 0, 1.f, nullptr, nullptr, 0, C, N,
+             1, 0, 0};
+  a.dbg = (uint32_t*)stamps;
+  const SplitOpts so{1, nullptr, 0};
+  return launch_w4<false, 2>(a, stream, so);
 }
 
 extern "C" size_t ospo_gemm_nt_ws_bytes(int M, int N, int K, int K2, int mx, int tail_split) {

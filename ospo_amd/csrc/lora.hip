@@ -657,7 +657,7 @@ struct GdbInl {
   bf16* out;
   int ldo, out_cols;
 };
-constexpr int GDB_CNT_BYTES = 8192 + 16;
+constexpr int GDB_CNT_BYTES = OSPO_WS_LORA_GDB_CNT_BYTES;
 constexpr unsigned GDB_SPIN_LIMIT = 1u << 24;
 
 template <int RSB, int NS = 4, int YA = 0, bool INL = false>  // YA: cache-policy bits of the dy loads
@@ -1253,7 +1253,7 @@ static int skinny_splits(int M_out, int K) {
 }
 
 // skinny workspace head: one counter per 64-row block for the in-launch split sum (M_out <= 65536)
-constexpr int SK_CNT_BYTES = 4096;
+constexpr int SK_CNT_BYTES = OSPO_WS_SKINNY_CNT_BYTES;
 #ifdef OSPO_ABLATION
 static bool g_sk_reduce_launch = getenv("OSPO_SK_REDUCE_LAUNCH") != nullptr;  // A/B: the separate reduce kernel
 #else

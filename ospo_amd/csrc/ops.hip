@@ -797,7 +797,17 @@ extern "C" const char* ospo_strerror(int s) {
     default: return "unknown ospo status";
   }
 }
-extern "C" int ospo_abi_version(void) { return 1; }
+extern "C" int ospo_abi_version(void) { return OSPO_ABI_VERSION; }
+
+extern "C" size_t ospo_ws_counter_bytes(int kind) {
+  switch (kind) {
+    case OSPO_WS_GEMM_TAIL: return OSPO_WS_GEMM_TAIL_CNT_BYTES;
+    case OSPO_WS_SKINNY: return OSPO_WS_SKINNY_CNT_BYTES;
+    case OSPO_WS_LORA_GDB: return OSPO_WS_LORA_GDB_CNT_BYTES;
+    case OSPO_WS_DECODE_LINEAR: return OSPO_WS_DECODE_LINEAR_CNT_BYTES;
+    default: return 0;
+  }
+}
 
 // host restatement of the device dropout hash (tests pin ospo_amd/dropout.py against it)
 extern "C" unsigned ospo_dropout_hash(unsigned idx, unsigned seed) { return drop_hash(idx, seed); }

@@ -98,6 +98,7 @@ class SimPOEngine:
         self.training = True
         self._drop_base = int(dropout_seed)
         self._drop_call = 0
+        self.layer_grads_hook = None  # on_layer_grads for backward() reached through autograd (Trainer.fit)
         if dims.head_dim != 128:
             raise ValueError("head_dim must be 128 (Janus-Pro)")
         if dims.d_model % 256 or dims.d_ff % 256 or dims.gen_head_dim % 256 or dims.img_vocab % 256:
@@ -427,13 +428,13 @@ class SimPOEngine:
         B, Lt = text_ids.shape
         N = chosen_ids.shape[1]
         self.ensure_capacity(B, Lt)
-        # the in-launch split sums' counters (workspace heads: lora_skinny SK_CNT_BYTES = 4096, lora_gdb 8208 B) are
+        # the in-launch split sums' counters (workspace heads, sized by the library: ops.ws_counter_bytes) are
         # left zero by every call that completes; re-zeroing them once per step (two small fills) bounds the damage of
         # one that did not (an aborted step) to that step
         if getattr(self, "_sk_ws", None) is not None:
-            self._sk_ws[:1024].zero_()
+            ops.zero_ws_counters(self._sk_ws, ops.WS_SKINNY)
         if getattr(self, "_gdb_ws", None) is not None:
-            self._gdb_ws[:2052].zero_()
+            ops.zero_ws_counters(self._gdb_ws, ops.WS_LORA_GDB)
         if N != self.N:
             raise ValueError(f"batch (B={B}, Lt={Lt}, N={N}) exceeds engine capacity "
                              f"(pairs={self.cap_pairs}, T={self.cap_T}, N={self.N})")

@@ -155,6 +155,7 @@ class T2IGenerator:
         self.attn_o_one_launch = (bool(attn_o_one_launch) and self.fused and not self.head_split
                                   and dims.n_layers < 63)
         self.attn_o_used = False  # (set when a decode step took the one-launch form: its shapes fit)
+        self.mlp_used = False  # (set when a decode step ran the MLP as one launch: ops.decode_mlp took the shape)
         self.attn_flags = torch.zeros(2 * dims.n_heads, dtype=torch.int32, device=dev)
         self._graph = None
         self._graph_B = None
@@ -318,9 +319,11 @@ class T2IGenerator:
                     ops.attn_cache(self.q[:R], self.kc[i], self.vc[i], R, 1, H, self.Tmax, self.start, self.pos,
                                    scale, self.attn[:R])
                 ops.decode_linear(self.attn[:R], lw["o_d"], self.xmid[:R], ws, residual=x, ss_out=self.ss_mid)
-            if not (self.mlp_one_launch and ops.decode_mlp(
+            if self.mlp_one_launch and ops.decode_mlp(
                     self.xmid[:R], lw["gu_d"], lw["down_d"], self.h[:R], xo, ws, norm=(self.ss_mid, lw["ln_post"], eps),
-                    ss_out=sso, step=self.step, layer=i, flags=self.mlp_flags, tmo=self.mlp_tmo)):
+                    ss_out=sso, step=self.step, layer=i, flags=self.mlp_flags, tmo=self.mlp_tmo):
+                self.mlp_used = True
+            else:
                 ops.decode_linear(self.xmid[:R], lw["gu_d"], self.h[:R], ws, epi="swiglu",
                                   norm=(self.ss_mid, lw["ln_post"], eps))
                 ops.decode_linear(self.h[:R], lw["down_d"], xo, ws, residual=self.xmid[:R], ss_out=sso)
@@ -373,8 +376,9 @@ class T2IGenerator:
         self.step.fill_(0)
         self.mlp_flags.zero_()  # (the flags' epochs restart with the step counter)
         self.attn_flags.zero_()
+        self.mlp_tmo.zero_()  # a wait that gave up in an earlier generate() does not fail this one
         if self.fused:
-            self.lws[:1024].zero_()  # the decode Linears' split-sum counters (DL_CNT_BYTES), left zero by every call
+            ops.zero_ws_counters(self.lws, ops.WS_DECODE_LINEAR)  # split-sum counters, left zero by every call
         self.tokens.zero_()
         self.probs = (torch.zeros(self.n_img, B, dims.img_vocab, dtype=torch.float32, device=self.device)
                       if record_probs else None)

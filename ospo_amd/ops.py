@@ -10,7 +10,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import call, query
+from ._lib import OspoError, call, query
 
 BF16 = torch.bfloat16
 
@@ -43,6 +43,24 @@ class KernelTimer:
             d["bytes"] += nb
             d["ms"] += e0.elapsed_time(e1)
         return out
+
+
+# workspace counter heads (include/ospo_hip.h ospo_ws_kind): queried from the library, so a resize of a C-side
+# head cannot leave Python zeroing the wrong range
+WS_GEMM_TAIL, WS_SKINNY, WS_LORA_GDB, WS_DECODE_LINEAR = 0, 1, 2, 3
+
+
+def ws_counter_bytes(kind: int) -> int:
+    n = int(query("ospo_ws_counter_bytes", kind))
+    if n <= 0 or n % 4:
+        raise OspoError(f"ospo_ws_counter_bytes({kind}) = {n}")
+    return n
+
+
+def zero_ws_counters(ws: torch.Tensor, kind: int) -> None:
+    """Zero the counter head at the start of a caller-owned workspace (any dtype)."""
+    n = ws_counter_bytes(kind)
+    ws.view(torch.uint8)[:n].zero_()
 
 
 def set_kernel_timer(t: Optional[KernelTimer]):
@@ -98,7 +116,8 @@ def gemm_workspace(device=None, stream=None) -> torch.Tensor:
     if ws is None:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         with torch.cuda.stream(st):
-            ws = _GEMM_WS[key] = torch.zeros(cus * 65536 + 1024, dtype=torch.float32, device=dev)
+            ws = _GEMM_WS[key] = torch.zeros(cus * 65536 + ws_counter_bytes(WS_GEMM_TAIL) // 4,
+                                              dtype=torch.float32, device=dev)
     return ws
 
 
@@ -107,6 +126,20 @@ def _ws_args(ws: Optional[torch.Tensor], device, stream):
         ws = gemm_workspace(device, stream)
     _chk(ws, torch.float32, "ws")
     return ws.data_ptr(), ws.numel() * 4
+
+
+def gemm_clock_probe(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, stamps: torch.Tensor) -> None:
+    """out = a . b^T through the product's bf16 K loop, unsplit, with per-workgroup s_memtime / s_memrealtime
+    stamps (int64 [tiles, 8]; ospo_gemm_clock_probe_bf16): bench.py's box probe."""
+    for t, nme in ((a, "a"), (b, "b"), (out, "out")):
+        _chk(t, BF16, nme)
+    M, K = a.shape
+    N = b.shape[0]
+    if b.shape[1] != K or tuple(out.shape) != (M, N) or any(t.stride(0) != t.shape[1] for t in (a, b, out)):
+        raise ValueError("gemm_clock_probe: a [M, K], b [N, K], out [M, N], all dense")
+    if stamps.dtype != torch.int64 or not stamps.is_contiguous():
+        raise ValueError("gemm_clock_probe: stamps must be contiguous int64")
+    call("ospo_gemm_clock_probe_bf16", _p(a), _p(b), _p(out), M, N, K, _p(stamps), stamps.numel() * 8, _s())
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a2=None, b2=None, alpha: float = 1.0,

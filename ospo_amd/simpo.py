@@ -101,7 +101,9 @@ class PolicyLogps(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        ctx.engine.backward(g.contiguous().float())
+        # engine.layer_grads_hook (Trainer.fit sets it to GradAllReduce.push on the step's last micro-batch): the
+        # DP all-reduce of each layer's grads starts while the backward runs on, as in train_step
+        ctx.engine.backward(g.contiguous().float(), on_layer_grads=getattr(ctx.engine, "layer_grads_hook", None))
         return None, None, None, None, None
 
 

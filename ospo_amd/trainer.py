@@ -6,6 +6,11 @@ Per optimizer step: ``accumulate_grad_batches`` x (training_step -> loss.backwar
 -> RCCL all-reduce of the flat LoRA grads -> on_before_optimizer_step (grad-norm
 log) -> clip + AdamW (fused) -> scheduler.step -> metrics JSONL (TensorBoard is
 absent) -> ModelCheckpoint every ``save_steps``.
+
+The all-reduce overlaps the last micro-batch's backward exactly as the timed path
+(simpo.train_step) does: GradAllReduce.begin, each layer's range pushed from the
+engine's backward hook as soon as its grads are final, finish before the optimizer
+(DDP's bucketed all-reduce during backward, ospo/utils/train.py:26-28).
 """
 from __future__ import annotations
 
@@ -34,6 +39,18 @@ class Trainer:
         self.global_step = 0
         self.allreduce = odist.GradAllReduce(world)
 
+    def backward(self, wrapper, loss, last: bool):
+        """loss.backward(); on the optimizer step's last micro-batch the grads' all-reduce is begun and fed layer by
+        layer from the engine's backward (GradAllReduce.push via engine.layer_grads_hook); the caller finishes it."""
+        eng = wrapper.engine
+        if last:
+            self.allreduce.begin(eng.grads)
+            eng.layer_grads_hook = self.allreduce.push
+        try:
+            (loss / self.accum).backward() if self.accum > 1 else loss.backward()
+        finally:
+            eng.layer_grads_hook = None
+
     def fit(self, wrapper, train_dataloaders, ckpt_path: Optional[str] = None):
         wrapper.trainer = self
         wrapper.setup("fit", self.log_dir)
@@ -55,11 +72,11 @@ class Trainer:
                 sampler.set_epoch(epoch)
             for idx, batch in enumerate(train_dataloaders):
                 loss = wrapper.training_step(batch, idx)
-                (loss / self.accum).backward() if self.accum > 1 else loss.backward()
+                self.backward(wrapper, loss, last=(micro + 1) % self.accum == 0)
                 micro += 1
                 if micro % self.accum:
                     continue
-                self.allreduce(wrapper.engine.grads)
+                self.allreduce.finish()
                 wrapper.on_before_optimizer_step()
                 opt.step()
                 sched.step()

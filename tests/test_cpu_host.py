@@ -41,8 +41,32 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version_and_strerror(lib):
-    assert lib.ospo_abi_version() == 1
+    from ospo_amd import _lib
+    assert lib.ospo_abi_version() == _lib.ABI_VERSION == 2
     assert lib.ospo_strerror(1) == b"shape / leading-dimension violation"
+
+
+def test_workspace_counter_heads_from_the_library(lib):
+    """The counter heads Python zeroes are the library's own sizes (no hard-coded 1024 / 2052)."""
+    from ospo_amd import ops
+    assert [ops.ws_counter_bytes(k) for k in (ops.WS_GEMM_TAIL, ops.WS_SKINNY, ops.WS_LORA_GDB,
+                                               ops.WS_DECODE_LINEAR)] == [4096, 4096, 8208, 4096]
+    assert lib.ospo_ws_counter_bytes(99) == 0
+    ws = torch.full((4000,), 7.0)
+    ops.zero_ws_counters(ws, ops.WS_LORA_GDB)
+    assert int((ws == 0).sum()) == 8208 // 4 and float(ws[8208 // 4]) == 7.0
+
+
+def test_abi_version_mismatch_is_refused(monkeypatch):
+    """A library of another ABI revision is refused at load, not silently mis-driven."""
+    from ospo_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "ABI_VERSION", 999)
+    with pytest.raises(_lib.OspoError, match="ABI version"):
+        _lib.lib()
+    monkeypatch.setattr(_lib, "ABI_VERSION", 2)
+    monkeypatch.setattr(_lib, "_lib", None)
+    _lib.lib()
 
 
 def test_validation_before_launch(lib):

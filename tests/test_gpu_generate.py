@@ -487,6 +487,30 @@ def test_generate_attn_o_one_launch_same_tokens():
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+def test_generate_mlp_one_launch_taken_and_same_tokens():
+    """The default decode step runs the MLP as ONE launch (ops.decode_mlp) where its plan fits -- the 7B widths
+    (D 4096, F 11008) -- with each (step, layer) epoch read from the device step counter, also under hipGraph
+    replay.  At those widths the generator must take that form (mlp_used), and it must draw the tokens and
+    probabilities of the two-launch step bit for bit, eager and hipGraph (no generate-level test
+    reached the one-launch form before)."""
+    from ospo_amd.engine import ModelDims
+    from ospo_amd.generate import T2IGenerator
+    dims, w, prompts = _small_case(seed=21, B=3, d_model=4096, d_ff=11008)
+    res = []
+    for one in (True, False):
+        gen = T2IGenerator(ModelDims.from_any(dims), w, device=DEV, max_batch=4, max_prompt_len=16, n_img_tokens=24,
+                           cfg_weight=5.0, temperature=1.0, pad_id=7, mlp_one_launch=one)
+        assert gen.fused
+        tok = gen.generate(prompts, seed=5, use_graph=False, record_probs=True).cpu().clone()
+        assert gen.mlp_used == one
+        res.append((tok, gen.probs.cpu().clone()))
+        assert torch.equal(gen.generate(prompts, seed=5, use_graph=True).cpu(), tok)
+        assert torch.equal(gen.generate(prompts, seed=5, use_graph=True).cpu(), tok)  # graph replayed again
+        del gen
+        torch.cuda.empty_cache()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("R", [32, 12])
 def test_decode_qkv_heads_and_attn_heads_equal_full_launch(R):
     """Round 5: the q|k|v projection and the cached attention split by head range (ops.decode_qkv_heads on the
