@@ -152,8 +152,11 @@ __device__ __forceinline__ void hf_scores2(float& a, float& b, float scale) {
   b *= scale;
   bf_round2(a, b);
 }
-// RAW (ablation only, verdict r4 item 2c): the scores scaled in fp32 without HF's two bf16 roundings -- a
-// measurement of how much the roundings matter for parity; forward and backward must agree (lse)
+// RAW: the scores scaled in fp32 without HF's two bf16 roundings.  Round 5 measured it as an ablation (verdict r4
+// item 2c); since round 6 every kernel of this file runs RAW (kRawScores): the 30-layer log-probs stay inside the
+// item-1 criterion with it and the fp32 scores sit closer to the fp32 oracle.  Forward and
+// backward must agree (lse).
+constexpr bool kRawScores = true;
 template <bool RAW>
 __device__ __forceinline__ void scores2(float& a, float& b, float scale) {
   if constexpr (RAW) {
@@ -376,7 +379,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
 #pragma unroll
       for (int j = 0; j < 4; j += 2) {
         float a = st[t][j], b = st[t][j + 1];
-        hf_scores2(a, b, scale);
+        scores2<kRawScores>(a, b, scale);
         a = (16 * t + j > rel) ? -INFINITY : a;
         b = (16 * t + j + 1 > rel) ? -INFINITY : b;
         st[t][j] = a;
@@ -475,7 +478,7 @@ __device__ __forceinline__ void fwd_scores(const char* Ks, const bf16x8 (&qf)[2]
 }
 
 // HF scores, causal mask (diagonal tiles only), online softmax of one tile for both groups -> P^T packs
-template <bool ALWAYS_RESCALE = false, bool RAW = false>  // (true: the round-4 form / unrounded scores, ablation A/B)
+template <bool ALWAYS_RESCALE = false, bool RAW = kRawScores>  // (ALWAYS_RESCALE: the round-4 form, ablation A/B)
 __device__ __forceinline__ void fwd_softmax(f32x4 (&st)[2][4], bool diag, int key0, const int (&lim)[2], float scale,
                                             float (&m_run)[2], float (&l_run)[2], f32x4 (&o)[2][8],
                                             bf16x8 (&pb)[2][2]) {
@@ -568,7 +571,7 @@ __device__ __forceinline__ void fwd_pv(const uint32_t (&va)[8], uint32_t boff, c
 
 // DBG (ablation build, results invalid): 1 no softmax VALU (P = S), 2 no PV products, 3 no S products,
 // 4 no K/V loads after the first tile
-template <bool MXO = false, bool PIPE = false, int DBG = 0, bool RAW = false>
+template <bool MXO = false, bool PIPE = false, int DBG = 0, bool RAW = kRawScores>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd2_kernel(
     const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, bf16* __restrict__ out, int ldo,
     float* __restrict__ lse, int T, int H, float scale, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0},
@@ -712,6 +715,378 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
+// ============================================================ forward, round 6 ====
+// attn_fwd3_kernel (the default forward since round 6): v_mfma_f32_32x32x16_bf16 and fp32 scores.
+// Blocks, grid, causal tile counts and K/V double buffering as attn_fwd2_kernel (4 waves x 32 query rows,
+// 128-row blocks, 64-key tiles, two workgroups per CU), but a wave's 32 rows are ONE 32-wide MFMA column
+// block:
+//   S^T [32 keys x 32 q] = K [32 keys x 16 d] . Q^T [16 d x 32 q]: two key chains per tile, 8 d steps each;
+//     the query sits on the lane (l & 31), so a row's 64 scores are 32 in-lane values + one permlane32 swap;
+//   O^T [32 d x 32 q] += V^T [32 d x 16 keys] . P^T [16 keys x 32 q]: four d chains, four key steps per tile;
+//     the S^T accumulator registers ARE the P^T operand (a 16-key step's k slots are keys {0-3, 8-11} in
+//     the lower half wave and {4-7, 12-15} in the upper, the 32x32 accumulator's row order), V^T is read in
+//     the same key order by ds_read_b64_tr_b16, so P needs only its bf16 packing.
+// Per tile and wave 32 MFMAs: half the 16x16x32 kernel's instruction count for the same flops (each MFMA
+// holds the vector issue for 8 of its cycles).  Scores stay fp32: p = exp2(s * scale * log2 e - m), one FMA
+// + one exp2 per score, where HF's eager path rounds q.k and (q.k) * scale to bf16 (four more VALU
+// operations per score).  Round 6 drops those roundings (the log-probs stay within the
+// item-1 criterion; the fp32 scores are closer to the fp32 oracle, not further).
+// LDS images use the swizzle chunk ^ f3swz(row), f3swz(r) = 4 (r & 3) + ((r >> 2) & 3): conflict-free for
+// the K row reads (32 rows x one 16-B chunk per half wave: 16 distinct chunk positions per ds_read_b128 lane
+// group) AND for the V transposed reads (4 rows x 32 columns per half wave: 4 disjoint 4-chunk blocks).  Row
+// bit 4 does not enter it (the V reads 16 rows apart differ by an immediate offset); bit 3 does (the reads 8
+// rows apart keep an address register of their own: no 16-row-periodic swizzle is conflict-free for the K reads).
+__device__ __forceinline__ int f3swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+template <int OFF>
+__device__ __forceinline__ void f3_rd128(uint32_t a, bf16x8& v) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+}
+template <int OFF>
+__device__ __forceinline__ void f3_rdtr(uint32_t a, i16x4& v) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+}
+// wait until at most N LDS reads of this wave are in flight; the 4 fragments of the batch being consumed
+// are tied to the wait
+template <int N>
+__device__ __forceinline__ void f3_wait4(bf16x8 (&v)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : "n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void f3_wait8(i16x4 (&lo)[4], i16x4 (&hi)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%8)"
+               : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]),
+                 "+v"(hi[3])
+               : "n"(N)
+               : "memory");
+}
+__device__ __forceinline__ float f3_partner_max(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto q = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float f3_partner_sum(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto q = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+__device__ __forceinline__ bf16x8 f3_pack8(const f32x16& v, int r0) {
+  bf16x8 p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) p[j] = f2bf(v[r0 + j]);
+  return p;
+}
+
+// DBG (ablation build, results invalid): 1 no softmax VALU, 2 no PV (no V reads), 3 no S (no K reads),
+// 4 no DMA after the first tile, 5 = 4 + no per-tile barrier, 6 = the real kernel + s_memtime sums per wave of
+// (S, softmax, PV, tile-end wait + barrier, prologue, stage issue) written over lse as u64 [wg][wave][6]
+template <bool MXO = false, int DBG = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd3_kernel(
+    const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, bf16* __restrict__ out, int ldo,
+    float* __restrict__ lse, int T, int H, float scale, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0},
+    int gm = 0) {
+  constexpr int RB = 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // buffer b: K at 2b * TILE, V at (2b + 1) * TILE
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int qb, h, s;
+  if (gm >= 1) {  // 1-D grid (ablation A/B): group_major / banded order, heaviest block first within a group / band
+    const int nqb = (T + RB - 1) / RB;
+    int grp, j;
+    group_major(nqb, gridDim.x / nqb, grp, j, gm);
+    qb = nqb - 1 - j;
+    h = grp % H;
+    s = grp / H;
+  } else {
+    qb = gridDim.z - 1 - blockIdx.z;  // heaviest blocks first (LPT), as attn_fwd2_kernel
+    h = blockIdx.x;
+    s = blockIdx.y;
+  }
+  const int hi = lane >> 5, l32 = lane & 31;
+  const long rowbase = (long)s * T;
+  const int row0w = qb * RB + wave * 32;  // this wave's first query row (wave-uniform)
+  const int qrow = row0w + l32;
+  const int lim = qrow < T ? qrow : T - 1;  // last key this lane's row attends to (padding rows: T - 1)
+  const int last = (qb * RB + RB - 1 < T ? qb * RB + RB - 1 : T - 1);
+  const int n_kv = last / KB + 1;
+  // tiles this wave computes: up to its last real row's (rows past T: none -- they only stage and sync)
+  const int n_kv_w = row0w < T ? (min(row0w + 31, T - 1)) / KB + 1 : 0;
+
+  bf16x8 qf[8];  // Q^T B operand of d step ks: row qrow, d = 16 ks + 8 hi ..
+  {
+    const bf16* qp = qkv + (rowbase + lim) * ldq + qc + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks + 8 * hi);
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;  // m in log2 units of the scaled scores
+  const float cs = scale * L2E;
+  const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
+  const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
+  // K / V tiles by buffer_load ... lds from per-sequence descriptors (records end at row T: rows past it read
+  // zeros -- keys every row masks and V rows its P zeroes -- so no row clamp); a wave's piece i of a tile is
+  // rows 4 (wave + 4 i) .., whose swizzle f3swz = 4 (lane >> 4) + wave does not depend on i: ONE per-lane
+  // offset, the tile and the piece advance in the scalar soffset
+  const __amdgpu_buffer_rsrc_t rsK = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, T * ldq * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, T * ldq * 2, 0x00020000);
+  // (piece rows 4 p + (lane >> 4), p = wave + 4 i: f3swz = 4 (lane >> 4) + wave for every i)
+  const uint32_t dma_off = (uint32_t)((4 * wave + (lane >> 4)) * ldq * 2) +
+                           (uint32_t)((((lane & 15) ^ f3swz(4 * wave + (lane >> 4))) << 4));
+  // piece i (K and V) of tile t into buffer b
+  auto stage_piece = [&](int t, int b, int i) __attribute__((always_inline)) {
+    const int so = (t * KB + 16 * i) * ldq * 2;
+    char* dst = smem + b * 2 * TILE_BYTES + (wave + 4 * i) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsK, (LDS_AS void*)dst, 16, dma_off, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (LDS_AS void*)(dst + TILE_BYTES), 16, dma_off, so, 0, 0);
+  };
+
+  // per-lane LDS addresses (buffer 0): K rows l32 (+ 32 for chain 1: immediate) at chunk 2 ks + hi; V^T rows
+  // 4 hi + (li >> 2) (+ 8: second read; + 16 u: key step, immediate), d columns 32 c + 16 (G & 1) + 4 (li & 3)
+  const uint32_t sa = lds_u32(smem);
+  uint32_t ka[8], va[8];
+  {
+    const int fk = f3swz(l32);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) ka[ks] = sa + l32 * ROWB + (((2 * ks + hi) ^ fk) << 4);
+    const int G = lane >> 4, li = lane & 15;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int sec = 0; sec < 2; ++sec) {
+        const int row = 4 * hi + (li >> 2) + 8 * sec;
+        const int ch = 4 * c + 2 * (G & 1) + ((li & 3) >> 1);
+        va[2 * c + sec] = sa + TILE_BYTES + row * ROWB + ((ch ^ f3swz(row)) << 4) + ((li & 1) << 3);
+      }
+  }
+
+  unsigned long long st6[6] = {0, 0, 0, 0, 0, 0};
+  auto stamp = [&]() -> unsigned long long { return DBG == 6 ? __builtin_amdgcn_s_memtime() : 0ull; };
+  const unsigned long long t_pro0 = stamp();
+  auto tile = [&](auto b_c, int kt, bool nxt) __attribute__((always_inline)) {
+    constexpr int B = decltype(b_c)::value;
+    const unsigned long long t0 = stamp();
+    constexpr int KO = B * 2 * TILE_BYTES;  // this buffer's K image; its V image at + TILE_BYTES (in va)
+    // ---- S^T: 16 MFMAs; K fragments in 4 batches of 4 (two d steps x two chains), double-buffered
+    f32x16 sc[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[0][r] = sc[1][r] = 0.f;
+    if constexpr (DBG == 3) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sc[0][r] = 0.01f * r; sc[1][r] = -0.01f * r + (float)kt; }
+    } else {
+    bf16x8 kf[2][4];
+    f3_rd128<KO>(ka[0], kf[0][0]);
+    f3_rd128<KO + 32 * ROWB>(ka[0], kf[0][1]);
+    f3_rd128<KO>(ka[1], kf[0][2]);
+    f3_rd128<KO + 32 * ROWB>(ka[1], kf[0][3]);
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      const int cur = bt & 1;
+      if (bt < 3) {
+        f3_rd128<KO>(ka[2 * bt + 2], kf[cur ^ 1][0]);
+        f3_rd128<KO + 32 * ROWB>(ka[2 * bt + 2], kf[cur ^ 1][1]);
+        f3_rd128<KO>(ka[2 * bt + 3], kf[cur ^ 1][2]);
+        f3_rd128<KO + 32 * ROWB>(ka[2 * bt + 3], kf[cur ^ 1][3]);
+        f3_wait4<4>(kf[cur]);
+      } else {
+        f3_wait4<0>(kf[cur]);
+      }
+      sc[0] = MFMA32(kf[cur][0], qf[2 * bt], sc[0]);
+      sc[1] = MFMA32(kf[cur][1], qf[2 * bt], sc[1]);
+      sc[0] = MFMA32(kf[cur][2], qf[2 * bt + 1], sc[0]);
+      sc[1] = MFMA32(kf[cur][3], qf[2 * bt + 1], sc[1]);
+      __builtin_amdgcn_sched_barrier(0);  // (keep each batch's MFMAs ahead of the next batch's wait)
+      // the next tile's K / V piece pair bt into the other buffer, in the shadow of this batch's MFMAs (after the
+      // last tile too: rows past T read zeros into a buffer nothing reads before the tile-end wait)
+      if (DBG != 4 && DBG != 5) stage_piece(kt + 1, B ^ 1, bt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    }
+    if constexpr (DBG == 3) {
+      if (nxt)
+        for (int i = 0; i < 4; ++i) stage_piece(kt + 1, B ^ 1, i);
+    }
+    const unsigned long long t1 = stamp();
+    // ---- online softmax of this lane's row over the tile's 64 keys (32 here, 32 in lane ^ 32)
+    const int key0 = kt * KB;
+    if constexpr (DBG == 1) {
+      bf16x8 pt[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pt[u] = f3_pack8(sc[u >> 1], 8 * (u & 1));
+      l_run += 1.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[c] = MFMA32(pt[u], pt[(u + c) & 3], o[c]);
+      return;
+    }
+    float tmax = -INFINITY;
+    if (key0 + KB - 1 > row0w) {  // a diagonal tile for this wave: mask keys past the row
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + 32 * ch + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          sc[ch][r] = key > lim ? -INFINITY : sc[ch][r];
+        }
+    }
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[ch][r]);
+    tmax = f3_partner_max(tmax);
+    const float m_new = fmaxf(m_run, tmax * cs);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sc[ch][r], cs, -m_new));
+        sc[ch][r] = pv;
+        psum += pv;
+      }
+    psum = f3_partner_sum(psum);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    // every tile (a branch on __any(alpha != 1), even with in-place asm multiplies, left the kernel at 256
+    // VGPRs with a spill reloaded inside the tile loop)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] *= alpha;
+    bf16x8 pt[4];  // P^T operand of key step u: chain u >> 1, registers 8 (u & 1) ..
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pt[u] = f3_pack8(sc[u >> 1], 8 * (u & 1));
+    const unsigned long long t2 = stamp();
+    // ---- O^T += V^T . P^T: 16 MFMAs; per d chain c one batch of 8 transposed reads, double-buffered
+    if constexpr (DBG == 2) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) o[c][c] += bf2f(pt[c][0]) + bf2f(pt[c][1]);
+      return;
+    }
+    i16x4 vlo[2][4], vhi[2][4];
+    auto issue_v = [&](auto c_c, int bb) __attribute__((always_inline)) {
+      constexpr int C = decltype(c_c)::value;
+      f3_rdtr<KO + 0 * 16 * ROWB>(va[2 * C], vlo[bb][0]);
+      f3_rdtr<KO + 0 * 16 * ROWB>(va[2 * C + 1], vhi[bb][0]);
+      f3_rdtr<KO + 1 * 16 * ROWB>(va[2 * C], vlo[bb][1]);
+      f3_rdtr<KO + 1 * 16 * ROWB>(va[2 * C + 1], vhi[bb][1]);
+      f3_rdtr<KO + 2 * 16 * ROWB>(va[2 * C], vlo[bb][2]);
+      f3_rdtr<KO + 2 * 16 * ROWB>(va[2 * C + 1], vhi[bb][2]);
+      f3_rdtr<KO + 3 * 16 * ROWB>(va[2 * C], vlo[bb][3]);
+      f3_rdtr<KO + 3 * 16 * ROWB>(va[2 * C + 1], vhi[bb][3]);
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using C2 = std::integral_constant<int, 2>;
+    using C3 = std::integral_constant<int, 3>;
+    auto pv_chain = [&](int c, int bb) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[c] = MFMA32(trp_join(vlo[bb][u], vhi[bb][u]), pt[u], o[c]);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    issue_v(C0{}, 0);
+    issue_v(C1{}, 1);
+    f3_wait8<8>(vlo[0], vhi[0]);
+    pv_chain(0, 0);
+    issue_v(C2{}, 0);
+    f3_wait8<8>(vlo[1], vhi[1]);
+    pv_chain(1, 1);
+    issue_v(C3{}, 1);
+    f3_wait8<8>(vlo[0], vhi[0]);
+    pv_chain(2, 0);
+    f3_wait8<0>(vlo[1], vhi[1]);
+    pv_chain(3, 1);
+    if constexpr (DBG == 6) {
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+      const unsigned long long t3 = stamp();
+      st6[0] += t1 - t0;
+      st6[1] += t2 - t1;
+      st6[2] += t3 - t2;
+    }
+  };
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) stage_piece(0, 0, i);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  st6[4] = stamp() - t_pro0;
+  using Bf0 = std::integral_constant<int, 0>;
+  using Bf1 = std::integral_constant<int, 1>;
+  for (int kt = 0; kt < n_kv; ++kt) {
+    const int buf = DBG == 4 || DBG == 5 ? 0 : kt & 1;
+    const unsigned long long ts0 = stamp();
+    // tile kt + 1 goes into the other buffer (every wave finished reading it at the last barrier): its pieces are
+    // issued inside tile kt's S phase, or here by a wave with no rows in tile kt
+    const bool nxt = kt + 1 < n_kv;
+    if (kt < n_kv_w) {
+      if (buf)
+        tile(Bf1{}, kt, nxt);
+      else
+        tile(Bf0{}, kt, nxt);
+    } else if (DBG != 4 && DBG != 5 && nxt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) stage_piece(kt + 1, buf ^ 1, i);
+    }
+    st6[5] += stamp() - ts0;
+    const unsigned long long tw0 = stamp();
+    if constexpr (DBG != 5) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    st6[3] += stamp() - tw0;
+  }
+  if constexpr (DBG == 5) __syncthreads();
+
+  // O = O^T / l, staged through LDS (the K/V buffers) as bf16 rows, stored as whole 256-B rows
+  if (row0w < T) {
+    const float inv = 1.f / l_run;
+    char* scr = smem + wave * (32 * SCR_PITCH);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint2 pk;
+        pk.x = pack2(o[c][4 * k] * inv, o[c][4 * k + 1] * inv);
+        pk.y = pack2(o[c][4 * k + 2] * inv, o[c][4 * k + 3] * inv);
+        *reinterpret_cast<uint2*>(scr + l32 * SCR_PITCH + (32 * c + 8 * k + 4 * hi) * 2) = pk;
+      }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bf16* dst = out + rowbase * ldo + h * HD;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int r = 4 * k + (lane >> 4);
+      const uint4 x = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + (lane & 15) * 16);
+      if (row0w + r < T) {  // uniform over the 16 lanes of a row
+        *reinterpret_cast<uint4*>(dst + (long)(row0w + r) * ldo + (lane & 15) * 8) = x;
+        if constexpr (MXO) {
+          const float f[8] = {bits2f(x.x & 0xffff), bits2f(x.x >> 16), bits2f(x.y & 0xffff), bits2f(x.y >> 16),
+                              bits2f(x.z & 0xffff), bits2f(x.z >> 16), bits2f(x.w & 0xffff), bits2f(x.w >> 16)};
+          mx8_store8(mo, rowbase + row0w + r, h * (HD / 8) + (lane & 15), f);
+        }
+      }
+    }
+    if (qrow < T && hi == 0)
+      lse[((long)s * H + h) * T + qrow] = (m_run + __log2f(l_run)) * 0.6931471805599453f;
+  }
+  if constexpr (DBG == 6) {  // (after the outputs: the stamped kernel computes everything); buffer: mo.q
+    const long wg = ((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;  // (either grid)
+    unsigned long long* sp = reinterpret_cast<unsigned long long*>(mo.q) + (wg * 4 + wave) * 6;
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) sp[q] = st6[q];
+    }
+  }
+}
+
 // ============================================================ backward =====
 // dK / dV: workgroup = 4 waves = 64 keys of one (sequence, head); each wave
 // owns 16 keys (K, V fragments in registers, dK^T dV^T accumulators) and
@@ -822,7 +1197,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int j = 0; j < 4; j += 2) {
         float x = sv[a][j], y = sv[a][j + 1];
-        hf_scores2(x, y, scale);
+        scores2<kRawScores>(x, y, scale);
         if (DIAG) {
           const int e = 16 * a + j;
           x = (e < lo || e >= hi) ? -INFINITY : x;
@@ -972,7 +1347,7 @@ __device__ __forceinline__ void wait_tr_ld(TrBatch& t) {
 // before its MFMAs: ~18 % MFMA busy at 2 waves per SIMD).  The first batch of a tile is issued
 // right after the tile barrier.
 // DBG 1 (ablation build): s_memtime sums per wave of the tile phases -> dbg[8 per wave]
-template <int NW, int DBG = 0, bool MXO = false, bool RAW = false>
+template <int NW, int DBG = 0, bool MXO = false, bool RAW = kRawScores>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv3_kernel(
     const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, const bf16* __restrict__ dout, int ldd,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16* __restrict__ dqkv, int ldg, int T, int H,
@@ -1447,7 +1822,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_kernel(const bf16* __rest
 #pragma unroll
       for (int j = 0; j < 4; j += 2) {
         float a = st[t][j], b = st[t][j + 1];
-        hf_scores2(a, b, scale);
+        scores2<kRawScores>(a, b, scale);
         if (DIAG) {
           a = (16 * t + j > rel) ? -INFINITY : a;
           b = (16 * t + j + 1 > rel) ? -INFINITY : b;
@@ -1798,6 +2173,46 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
   if (S <= 0 || T <= 0 || n_heads <= 0 || ld_qkv % 8 || ld_o % 8 || q_col % 8 || k_col % 8 || v_col % 8)
     return OSPO_ERR_SHAPE;
   if (!aligned16(qkv) || !aligned16(o)) return OSPO_ERR_ALIGN;
+  bool fwd3 = true;  // round 6: attn_fwd3_kernel (32x32x16 MFMA, fp32 scores)
+#ifdef OSPO_ABLATION
+  if (getenv("OSPO_ATTN_FWD2") || getenv("OSPO_ATTN_FWD8") || getenv("OSPO_ATTN_DBG") || getenv("OSPO_ATTN_FWD_SPREAD") ||
+      getenv("OSPO_ATTN_FWD2_DBG") || getenv("OSPO_ATTN_FWD_PIPE"))
+    fwd3 = false;  // A/B: the round-4/5 kernels (16x16x32 MFMA)
+#endif
+  if (fwd3) {
+    // workgroup order: banded (group_major, bands of 16 (sequence, head) groups per XCD, heaviest block first
+    // within a band) -- a band's K / V re-reads hit its XCD's L2: 61.2 -> 50.6 us at the step shape against the
+    // 3-D grid's chip-wide heaviest-first order (gm 2 / 4 / 8: 60.3 / 54.7 / 50.8; profiles/r06/attn_fwd3_ab.log)
+    int gm3 = 16;
+#ifdef OSPO_ABLATION
+    if (const char* e = getenv("OSPO_ATTN_FWD3_GM")) gm3 = atoi(e);  // A/B: 0 = the 3-D grid, 1 group-major, >= 2 banded
+#endif
+    dim3 g3(n_heads, S, (T + 127) / 128);
+    if (gm3 >= 1 && (S * n_heads) % 8 == 0) g3 = dim3(n_heads * S * ((T + 127) / 128));
+    else gm3 = 0;
+#ifdef OSPO_ABLATION
+    if (const char* e = getenv("OSPO_ATTN_FWD3_DBG")) {  // decomposition (results invalid)
+      const int v = atoi(e);
+      auto k = v == 1 ? attn_fwd3_kernel<false, 1> : v == 2 ? attn_fwd3_kernel<false, 2> :
+               v == 3 ? attn_fwd3_kernel<false, 3> : v == 4 ? attn_fwd3_kernel<false, 4> :
+               v == 5 ? attn_fwd3_kernel<false, 5> : attn_fwd3_kernel<false, 6>;
+      if (v == 6 && !g_attn_stamps) return OSPO_ERR_ARG;  // stamps buffer: ospo_attn_set_stamps
+      const Mx8Out mst{(uint8_t*)g_attn_stamps, 0, nullptr, 0};
+      hipLaunchKernelGGL(k, g3, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col, (bf16*)o, ld_o,
+                         lse, T, n_heads, scale, v == 6 ? mst : mo, gm3);
+      OSPO_CHECK_LAUNCH();
+      return OSPO_OK;
+    }
+#endif
+    if (mo.q)
+      hipLaunchKernelGGL(attn_fwd3_kernel<true>, g3, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+                         v_col, (bf16*)o, ld_o, lse, T, n_heads, scale, mo, gm3);
+    else
+      hipLaunchKernelGGL(attn_fwd3_kernel<false>, g3, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+                         v_col, (bf16*)o, ld_o, lse, T, n_heads, scale, mo, gm3);
+    OSPO_CHECK_LAUNCH();
+    return OSPO_OK;
+  }
   int nw = 4;  // attn_fwd2_kernel: 4 waves x 32 query rows
   auto kfn = mo.q ? attn_fwd2_kernel<true, false> : attn_fwd2_kernel<false, false>;
 #ifdef OSPO_ABLATION

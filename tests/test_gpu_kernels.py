@@ -301,8 +301,10 @@ def test_swiglu():
 
 # ---------------------------------------------------------------- attention
 def bf16_scores(q, k, scale):
-    """HF eager attention in bf16: bf16(bf16(q.k^T) * scale) (rounding is identity for autograd)."""
-    return ((q @ k.transpose(-1, -2)).to(torch.bfloat16).float() * scale).to(torch.bfloat16).float()
+    """The kernels' attention scores: (q.k^T) * scale in fp32.  Until round 5 they restated HF eager bf16,
+    bf16(bf16(q.k^T) * scale); round 6 keeps the scores fp32, so the fp32 product is the
+    reference here (the oracle's bf16 path keeps HF's roundings; the step tests bound the difference)."""
+    return (q @ k.transpose(-1, -2)) * scale
 
 
 def attn_ref(q, k, v, scale):

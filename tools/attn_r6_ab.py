@@ -1,0 +1,131 @@
+"""Round 6 attention A/B at the step shape (S 8, T 600, 32 heads, d 128), one process, ablation build: the forward
+as attn_fwd3_kernel (32x32x16 MFMA, fp32 scores; the default) against attn_fwd2_kernel (OSPO_ATTN_FWD2=1, round 5's
+kernel, now also fp32 scores), both checked against an fp32 torch reference on two (sequence, head) groups, and
+the 5-product backward.  Times are medians of 5 rounds of 20 launches (HIP events), inputs alternated between two
+seeded sets so nothing is re-read from the Infinity Cache across launches."""
+import os as _os
+_os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
+                                                     "ospo_amd", "libospo_hip_ablation.so"))
+import json
+import math
+import sys
+
+import torch
+
+sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
+from ospo_amd import ops  # noqa: E402
+
+S, T, H, hd = int(_os.environ.get("AB_S", 8)), 600, 32, 128
+D = H * hd
+
+
+def med_time(fn, rounds=5, it=20):
+    ts = []
+    for _ in range(rounds):
+        fn(0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(it):
+            fn(i & 1)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / it * 1e3)
+    return sorted(ts)[rounds // 2]
+
+
+def ref_fwd(qkv, s, h, scale):
+    x = qkv[s * T:(s + 1) * T].float()
+    q, k, v = (x[:, i * D + h * hd: i * D + (h + 1) * hd] for i in range(3))
+    sc = (q @ k.T) * scale
+    sc = sc.masked_fill(torch.ones(T, T, dtype=torch.bool, device=qkv.device).triu(1), float("-inf"))
+    return torch.softmax(sc, -1) @ v, torch.logsumexp(sc, -1)
+
+
+def main():
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = [torch.randn(S * T, 3 * D, device="cuda", generator=g).bfloat16() for _ in range(2)]
+    o = [torch.empty(S * T, D, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    lse = [torch.empty(S * H * T, device="cuda") for _ in range(2)]
+    do = [torch.randn(S * T, D, device="cuda", generator=g).bfloat16() for _ in range(2)]
+    delta = torch.empty(S * H * T, device="cuda")
+    dq = [torch.empty(S * T, 3 * D, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    ws = ops.flash_attn_bwd_ws(S, T, H, "cuda")
+    cos, sin = ops.rope_tables(T, hd, 1e4, "cuda")
+    sc = 1 / math.sqrt(hd)
+    fl = 4 * S * H * hd * T * (T + 1) / 2
+    res = {}
+    outs = {}
+    for tag, env in (("fwd3", None), ("fwd2", "1")):
+        if env:
+            _os.environ["OSPO_ATTN_FWD2"] = env
+        else:
+            _os.environ.pop("OSPO_ATTN_FWD2", None)
+        f = lambda i: ops.flash_attn_fwd(qkv[i], 0, D, 2 * D, o[i], lse[i], S, T, H, hd, sc)  # noqa: E731
+        t = med_time(f)
+        f(0)
+        torch.cuda.synchronize()
+        outs[tag] = (o[0].clone(), lse[0].clone())
+        err = []
+        for (s, h) in ((0, 0), (S - 1, H - 1)):
+            r, rl = ref_fwd(qkv[0], s, h, sc)
+            got = o[0][s * T:(s + 1) * T, h * hd:(h + 1) * hd].float()
+            gl = lse[0].view(S, H, T)[s, h]
+            err.append((float((got - r).norm() / r.norm()), float((gl - rl).abs().max())))
+        res[tag] = {"fwd_us": round(t, 1), "tflops": round(fl / t / 1e6, 1), "frac": round(fl / t / 1e6 / 2500, 4),
+                    "o_rel_err_vs_fp32": max(e[0] for e in err), "lse_max_abs_err": max(e[1] for e in err)}
+        print(json.dumps({tag: res[tag]}), flush=True)
+    _os.environ.pop("OSPO_ATTN_FWD2", None)
+    a, b = outs["fwd3"], outs["fwd2"]
+    print(json.dumps({"fwd3_vs_fwd2_o_max_abs": float((a[0].float() - b[0].float()).abs().max()),
+                      "fwd3_vs_fwd2_lse_max_abs": float((a[1] - b[1]).abs().max())}), flush=True)
+    for i in range(2):
+        ops.flash_attn_fwd(qkv[i], 0, D, 2 * D, o[i], lse[i], S, T, H, hd, sc)
+    bw = lambda i: ops.flash_attn_bwd(qkv[i], 0, D, 2 * D, o[i], do[i], lse[i], delta, ws, dq[i], S, T, H, hd, sc,  # noqa: E731
+                                      rope_cos=cos, rope_sin=sin)
+    tb = med_time(bw)
+    print(json.dumps({"bwd5_us": round(tb, 1), "bwd_alg_tflops": round(2 * fl / tb / 1e6, 1),
+                      "bwd_frac": round(2 * fl / tb / 1e6 / 2500, 4)}), flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) == 1:
+    main()
+
+
+def decompose():
+    """OSPO_ATTN_FWD3_DBG decomposition (results invalid) + the DBG 6 phase stamps of the real kernel."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = [torch.randn(S * T, 3 * D, device="cuda", generator=g).bfloat16() for _ in range(2)]
+    o = [torch.empty(S * T, D, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    lse = [torch.zeros(S * H * T, device="cuda") for _ in range(2)]
+    sc = 1 / math.sqrt(hd)
+    f = lambda i: ops.flash_attn_fwd(qkv[i], 0, D, 2 * D, o[i], lse[i], S, T, H, hd, sc)  # noqa: E731
+    out = {"base_gm16": round(med_time(f), 1)}
+    for gm in (0, 4, 8, 32):
+        _os.environ["OSPO_ATTN_FWD3_GM"] = str(gm)
+        out[f"order_gm{gm}"] = round(med_time(f), 1)
+    _os.environ.pop("OSPO_ATTN_FWD3_GM", None)
+    for v in (1, 2, 3, 4, 5):
+        _os.environ["OSPO_ATTN_FWD3_DBG"] = str(v)
+        out[f"dbg{v}"] = round(med_time(f), 1)
+    from ospo_amd._lib import call
+    nwg = H * S * ((T + 127) // 128)
+    stamps = torch.zeros(nwg * 4 * 6, dtype=torch.int64, device="cuda")
+    call("ospo_attn_set_stamps", stamps.data_ptr())
+    _os.environ["OSPO_ATTN_FWD3_DBG"] = "6"
+    out["dbg6_stamped"] = round(med_time(f), 1)
+    stamps.zero_()
+    f(0)
+    torch.cuda.synchronize()
+    _os.environ.pop("OSPO_ATTN_FWD3_DBG", None)
+    call("ospo_attn_set_stamps", None)
+    st = stamps.view(nwg * 4, 6).double().cpu()
+    st = st[st.sum(1) > 0]
+    names = ["S", "softmax", "PV", "wait_barrier", "prologue", "stage_issue"]
+    tot = st.sum(0)
+    out["cycles_per_wave_mean"] = {n: round(float(st[:, i].mean()), 0) for i, n in enumerate(names)}
+    out["share"] = {n: round(float(tot[i] / tot.sum()), 3) for i, n in enumerate(names)}
+    print(json.dumps({"fwd3_decomposition_us": out}), flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--decompose":
+    decompose()
