@@ -2009,6 +2009,326 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_dq_ds_kernel(const bf16* __r
   }
 }
 
+#ifdef OSPO_ABLATION
+// ------------------------------------------------------- dK / dV, round 6 ----
+// attn_bwd_dkdv5_kernel (round 6, ablation build only: OSPO_ATTN_DKDV5=1): the dK / dV half of the 5-product backward on
+// v_mfma_f32_32x32x16_bf16 with fp32 scores.  Workgroup = 4 waves x 32 keys = one 128-key block of a (sequence,
+// head); each wave keeps dV^T and dK^T of its 32 keys (4 d chains x 16 accumulators each, 128 VGPRs) and its K
+// fragments in registers, and sweeps the 32-query tiles from its own diagonal on.  Per tile and wave 32 MFMAs:
+//   S  [32 q x 32 keys] = Q [32 q x 16 d] . K^T:  the key on the lane (l & 31), so the accumulator IS the B
+//      operand of dV^T; initialised to -lse(q) / scale (the row constant, read as broadcast float4s), so
+//      p = exp2(scale log2e S) needs no subtraction;
+//   dP [32 q x 32 keys] = dO . V^T, initialised to -delta(q): dS = p dP scale;
+//   dV^T [32 d x 32 keys] += dO^T [32 d x 16 q] . P,  dK^T += Q^T . dS: the A operands by ds_read_b64_tr_b16 in
+//      the accumulator's q order ({0-3, 8-11 | 4-7, 12-15} per 16-query step, as attn_fwd3_kernel's V^T).
+// dS^T (bf16, scale included) goes to the workspace for attn_bwd_dq_ring_kernel, as attn_bwd_dkdv3_kernel's.
+// Against the 16x16x32 kernel: half the MFMA instructions, half the LDS bytes per flop (32 keys per wave share
+// every Q / dO fragment), and no HF score roundings (one multiply + one exp2 per score instead of seven VALU).
+// Measured SLOWER (whole backward 248.2 vs 176.9 us at the step shape, profiles/r06/attn_bwd_ab.log): the 128
+// dK / dV accumulators + 32 K-fragment registers + the S / dP tiles and operand buffers do not fit 256 registers
+// (at 2 waves per SIMD every variant spilled), so it runs at one wave per SIMD with no latency hiding between
+// the dependent S -> P -> dV / dK phases, and the compiler still moves the loop-carried accumulators between
+// register files each tile (~800 v_accvgpr moves per tile body).  A wave-pair split (one wave S / P / dV, its
+// partner dP / dS / dK, P exchanged through LDS) would halve the accumulators; not built.
+// LDS (66 KiB: two workgroups per CU): the block's V rows [128][256 B]; Q and dO tiles [32][256 B], double-
+// buffered by buffer_load ... lds (rows past T read zeros); lse / delta of the tile.  Swizzle f3swz.
+template <bool MXO = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_dkdv5_kernel(
+    const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, const bf16* __restrict__ dout, int ldd,
+    const float* __restrict__ lse, const float* __restrict__ delta, bf16* __restrict__ dqkv, int ldg, int T, int H,
+    float scale, const bf16* __restrict__ rcs, const bf16* __restrict__ rsn, bf16* __restrict__ dsT, int ds_ld, int gm,
+    const Mx8Out mo) {
+  constexpr int KBW = 128, QT = 32;
+  constexpr int V_OFF = 0, QB_OFF = 32768, QBUF = 16384, DO_OFF = 8192, L_OFF = 65536;
+  __shared__ __attribute__((aligned(16))) char smem[L_OFF + 2 * 256];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hi = lane >> 5, l32 = lane & 31;
+  const int nkb = (T + KBW - 1) / KBW;
+  asm volatile("s_nop 7" ::: "memory");  // (zeroed accumulators written before the first asm MFMA; placed early)
+  int grp, kb;  // kb = 0 (the longest sweep) first within the group / band
+  group_major(nkb, gridDim.x / nkb, grp, kb, gm);
+  const int h = grp % H, s = grp / H;
+  const long rowbase = (long)s * T;
+  const int nq = (T + QT - 1) / QT;
+  const int key0w = kb * KBW + wave * 32;  // this wave's first key (wave-uniform)
+  const int key = key0w + l32;
+  const int key_c = key < T ? key : T - 1;
+  const int qt_first = key0w / QT;  // this wave's diagonal tile; the workgroup's first tile is kb * 4
+  const int qt0 = kb * (KBW / QT);
+
+  bf16x8 kr[8];  // K^T B operand of d step ks: K[key][16 ks + 8 hi ..]
+  {
+    const bf16* kp = qkv + (rowbase + key_c) * ldq + kc + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kr[ks] = *reinterpret_cast<const bf16x8*>(kp + 16 * ks + 8 * hi);
+  }
+  // dV^T / dK^T accumulators pinned to the accumulator file by inline-asm MFMAs (MFMA32A): with compiler-chosen
+  // MFMAs the loop-carried accumulators were copied between register files every tile (~800 v_accvgpr moves)
+  f32x16 dv[4], dk[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dv[c][r] = dk[c][r] = 0.f;
+#define MFMA32A(acc, a, b) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b))
+
+  bf16* dsrow = dsT + ((long)s * H + h) * ds_ld * (long)ds_ld + (long)key * ds_ld;
+  // causal zeros the dQ kernel reads: this wave's keys x the block's queries before its diagonal tile
+  if (key < ds_ld) {
+    const uint4 z = {0u, 0u, 0u, 0u};
+    for (int q = qt0 * QT + 8 * hi; q < qt_first * QT; q += 16) *reinterpret_cast<uint4*>(dsrow + q) = z;
+  }
+
+  // descriptors (records end at row T: rows past it read zeros) and per-lane DMA offsets: piece p = wave + 4 i of
+  // an image covers rows 4 p .. 4 p + 3, swizzle f3swz = 4 (lane >> 4) + wave for every i
+  const bf16* qbase = qkv + rowbase * ldq + qc + h * HD;
+  const bf16* obase = dout + rowbase * ldd + h * HD;
+  const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
+  const __amdgpu_buffer_rsrc_t rsQ = __builtin_amdgcn_make_buffer_rsrc((void*)qbase, 0, T * ldq * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc((void*)obase, 0, T * ldd * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, T * ldq * 2, 0x00020000);
+  const uint32_t chk = (uint32_t)((((lane & 15) ^ f3swz(4 * wave + (lane >> 4))) << 4));
+  const uint32_t offq = (uint32_t)((4 * wave + (lane >> 4)) * ldq * 2) + chk;
+  const uint32_t offo = (uint32_t)((4 * wave + (lane >> 4)) * ldd * 2) + chk;
+  const float* lse_sh = lse + ((long)s * H + h) * T;
+  const float* del_sh = delta + ((long)s * H + h) * T;
+  auto stage_tile = [&](int t, int b) __attribute__((always_inline)) {
+    char* qd = smem + QB_OFF + b * QBUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsQ, (LDS_AS void*)(qd + (wave + 4 * i) * 1024), 16, offq,
+                                               (t * QT + 16 * i) * ldq * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsO, (LDS_AS void*)(qd + DO_OFF + (wave + 4 * i) * 1024), 16, offo,
+                                               (t * QT + 16 * i) * ldd * 2, 0, 0);
+    }
+    if (wave == 0) {  // lse (lanes 0-31) and delta (32-63) of the tile's rows, clamped to row T - 1
+      int q = t * QT + l32;
+      q = q < T ? q : T - 1;
+      __builtin_amdgcn_global_load_lds(hi ? del_sh + q : lse_sh + q, (LDS_AS void*)(smem + L_OFF + b * 256), 4, 0, 0);
+    }
+  };
+  // the block's V rows, once
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (LDS_AS void*)(smem + V_OFF + (wave + 4 * i) * 1024), 16, offq,
+                                             (kb * KBW + 16 * i) * ldq * 2, 0, 0);
+  stage_tile(qt0, 0);
+
+  // per-lane LDS addresses: row reads (Q / dO images of buffer 0: row l32, chunk 2 ks + hi; V: row 32 w + l32),
+  // transposed reads (Q^T / dO^T: rows 4 hi + (li >> 2) (+ 8: sec; + 16 u: immediate), columns 32 c + 16 (G & 1)
+  // + 4 (li & 3))
+  const uint32_t sa = lds_u32(smem);
+  // Register-lean addressing (the 128 dK / dV accumulators and the K fragments leave ~60 VGPRs): with the LDS
+  // block at address 0 (the kernel's only __shared__ object; the tests would catch anything else), the swizzled
+  // chunk of d step ks is (2 ks + hi) ^ f = 2 (ks ^ (f >> 1)) + (hi ^ (f & 1)), so the address of step ks is
+  // ra0 ^ (32 ks) -- one v_xor per read -- and a transposed read of d chain c is ta0[sec] ^ (64 c)
+  // ((4 c + x) ^ f3swz(row) = 4 (c ^ (li >> 2)) + (x ^ (hi + 2 sec)) for the rows 4 hi + (li >> 2) + 8 sec).
+  // V rows: the Q row address + (V_OFF - QB_OFF + 32 w rows): one more v_add.
+  const uint32_t vdel = (uint32_t)(V_OFF - QB_OFF + 32 * wave * ROWB);
+  uint32_t ra0, ta0[2];
+  {
+    const int f = f3swz(l32);  // == f3swz(32 w + l32)
+    ra0 = sa + QB_OFF + l32 * ROWB + (uint32_t)((hi ^ f) << 4);
+    const int G = lane >> 4, li = lane & 15;
+#pragma unroll
+    for (int sec = 0; sec < 2; ++sec) {
+      const int row = 4 * hi + (li >> 2) + 8 * sec;
+      const int ch = 2 * (G & 1) + ((li & 3) >> 1);
+      ta0[sec] = sa + QB_OFF + row * ROWB + ((ch ^ f3swz(row)) << 4) + ((li & 1) << 3);
+    }
+  }
+  const uint32_t rv0 = ra0 + vdel;  // (vdel is a multiple of 8 KiB: bits 5-7 of the sum are ra0's)
+  const float cs = scale * L2E, inv_scale = 1.f / scale;
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // one tile body with the buffer as a run-time offset (two compile-time instances kept two copies of the 128
+  // loop-carried dK / dV accumulators and spilled)
+  auto tile = [&](int b, int qt) __attribute__((always_inline)) {
+    const uint32_t bo = (uint32_t)(b * QBUF);  // (bit 14: the XOR-derived addresses below stay valid)
+    const uint32_t rab = ra0 + bo, tab0 = ta0[0] + bo, tab1 = ta0[1] + bo;
+    auto ra = [&](int ks) __attribute__((always_inline)) { return rab ^ (uint32_t)(32 * ks); };
+    const int q0 = qt * QT;
+    const char* lsb = smem + L_OFF + b * 256;
+    // ---- S, dP: accumulators start at the row constants -lse / scale and -delta
+    f32x16 sa16, dp16;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f32x4 lq = *reinterpret_cast<const f32x4*>(lsb + (8 * k + 4 * hi) * 4);
+      const f32x4 dq4 = *reinterpret_cast<const f32x4*>(lsb + 128 + (8 * k + 4 * hi) * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sa16[4 * k + j] = -lq[j] * inv_scale;
+        dp16[4 * k + j] = -dq4[j];
+      }
+    }
+    bf16x8 fr[2][3];  // per d step: Q row, dO row, V row (double-buffered)
+    f3_rd128<0>(ra(0), fr[0][0]);
+    f3_rd128<DO_OFF>(ra(0), fr[0][1]);
+    f3_rd128<0>(rv0, fr[0][2]);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int cur = ks & 1;
+      if (ks < 7) {
+        const uint32_t an = ra(ks + 1);
+        f3_rd128<0>(an, fr[cur ^ 1][0]);
+        f3_rd128<DO_OFF>(an, fr[cur ^ 1][1]);
+        f3_rd128<0>(rv0 ^ (uint32_t)(32 * (ks + 1)), fr[cur ^ 1][2]);
+        asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(fr[cur][0]), "+v"(fr[cur][1]), "+v"(fr[cur][2])::"memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fr[cur][0]), "+v"(fr[cur][1]), "+v"(fr[cur][2])::"memory");
+      }
+      sa16 = MFMA32(fr[cur][0], kr[ks], sa16);
+      dp16 = MFMA32(fr[cur][1], fr[cur][2], dp16);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // (phase fences: nothing of the next phase hoisted into this one's registers)
+    // ---- P, dS (this lane's key; rows q0 + crow(r, hi)); causal mask on the diagonal tile, rows past T zero
+    const bool edge = qt == qt_first || q0 + QT > T;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = __builtin_amdgcn_exp2f(sa16[r] * cs);
+      if (edge) {
+        const int q = q0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        p = (key > q || q >= T) ? 0.f : p;
+      }
+      sa16[r] = p;
+      dp16[r] = p * dp16[r] * scale;
+    }
+    bf16x8 pp[2], dd[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      pp[u] = f3_pack8(sa16, 8 * u);
+      dd[u] = f3_pack8(dp16, 8 * u);
+    }
+    {  // dS^T[key][q0 + 8 k + 4 hi .. + 3] (bf16, 8 B each)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint2 pk;
+        pk.x = pack2(dp16[4 * k], dp16[4 * k + 1]);
+        pk.y = pack2(dp16[4 * k + 2], dp16[4 * k + 3]);
+        *reinterpret_cast<uint2*>(dsrow + q0 + 8 * k + 4 * hi) = pk;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- dV^T += dO^T . P, dK^T += Q^T . dS: per d chain c one batch (2 query steps x 2 images x 2 reads)
+    // per d chain c: the dO^T fragments (4 reads x 2) and the Q^T fragments, each batch waited alone and refilled
+    // with chain c + 1's right after its two MFMAs (16 registers in flight: a double-buffered pair of whole-chain
+    // batches did not fit next to the 128 accumulators)
+    i16x4 olo[2], ohi[2], qlo[2], qhi[2];  // [u]
+    auto issue_o = [&](int c) __attribute__((always_inline)) {
+      const uint32_t t0 = tab0 ^ (uint32_t)(64 * c), t1 = tab1 ^ (uint32_t)(64 * c);
+      f3_rdtr<DO_OFF>(t0, olo[0]);
+      f3_rdtr<DO_OFF>(t1, ohi[0]);
+      f3_rdtr<DO_OFF + 16 * ROWB>(t0, olo[1]);
+      f3_rdtr<DO_OFF + 16 * ROWB>(t1, ohi[1]);
+    };
+    auto issue_q = [&](int c) __attribute__((always_inline)) {
+      const uint32_t t0 = tab0 ^ (uint32_t)(64 * c), t1 = tab1 ^ (uint32_t)(64 * c);
+      f3_rdtr<0>(t0, qlo[0]);
+      f3_rdtr<0>(t1, qhi[0]);
+      f3_rdtr<16 * ROWB>(t0, qlo[1]);
+      f3_rdtr<16 * ROWB>(t1, qhi[1]);
+    };
+#define DKDV5_WAIT(N, a, b)                                                                                    \
+  asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1])::"memory")
+    auto chain = [&](auto c_c) __attribute__((always_inline)) {
+      constexpr int C = decltype(c_c)::value;
+      DKDV5_WAIT(4, olo, ohi);  // (the Q^T batch issued after it may stay in flight)
+      MFMA32A(dv[C], trp_join(olo[0], ohi[0]), pp[0]);
+      MFMA32A(dv[C], trp_join(olo[1], ohi[1]), pp[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (C < 3) issue_o(C + 1);
+      if constexpr (C < 3) DKDV5_WAIT(4, qlo, qhi); else DKDV5_WAIT(0, qlo, qhi);
+      MFMA32A(dk[C], trp_join(qlo[0], qhi[0]), dd[0]);
+      MFMA32A(dk[C], trp_join(qlo[1], qhi[1]), dd[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (C < 3) issue_q(C + 1);
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using C2 = std::integral_constant<int, 2>;
+    using C3 = std::integral_constant<int, 3>;
+    issue_o(0);
+    issue_q(0);
+    asm volatile("s_nop 4" ::: "memory");  // (VALU-written P / dS operands before the first asm MFMA reads them)
+    chain(C0{});
+    chain(C1{});
+    chain(C2{});
+    chain(C3{});
+#undef DKDV5_WAIT
+  };
+
+  for (int qt = qt0; qt < nq; ++qt) {
+    const int b = (qt - qt0) & 1;
+    if (qt + 1 < nq) stage_tile(qt + 1, b ^ 1);  // (every wave finished reading buffer b ^ 1 at the last barrier)
+    if (qt >= qt_first) tile(b, qt);
+    // own DMA pieces landed (the dS^T stores may stay in flight: they are older, so vmcnt(0) waits for them too)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+#undef MFMA32A
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // (the last asm MFMAs' results settle)
+  // RoPE backward on dK (d pairs (d, d + 64) = chains (c, c + 2), same register), then both outputs as bf16 rows
+  // through LDS (the Q / dO / V images are free after the last barrier)
+  if (rcs) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = 32 * c + 8 * k + 4 * hi;
+        const uint2 cw = *reinterpret_cast<const uint2*>(rcs + (long)key_c * 64 + i);
+        const uint2 sw = *reinterpret_cast<const uint2*>(rsn + (long)key_c * 64 + i);
+        const float cv[4] = {bits2f(cw.x & 0xffff), bits2f(cw.x >> 16), bits2f(cw.y & 0xffff), bits2f(cw.y >> 16)};
+        const float sv[4] = {bits2f(sw.x & 0xffff), bits2f(sw.x >> 16), bits2f(sw.y & 0xffff), bits2f(sw.y >> 16)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float a = dk[c][4 * k + j], bb = dk[c + 2][4 * k + j];
+          dk[c][4 * k + j] = a * cv[j] + bb * sv[j];
+          dk[c + 2][4 * k + j] = bb * cv[j] - a * sv[j];
+        }
+      }
+  }
+  char* scr = smem + wave * (32 * SCR_PITCH);
+  auto store_rows = [&](f32x16 (&acc)[4], int col, float mul) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint2 pk;
+        pk.x = pack2(acc[c][4 * k] * mul, acc[c][4 * k + 1] * mul);
+        pk.y = pack2(acc[c][4 * k + 2] * mul, acc[c][4 * k + 3] * mul);
+        *reinterpret_cast<uint2*>(scr + l32 * SCR_PITCH + (32 * c + 8 * k + 4 * hi) * 2) = pk;
+      }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bf16* dst = dqkv + rowbase * ldg + col + h * HD;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int r = 4 * k + (lane >> 4);
+      const uint4 x = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + (lane & 15) * 16);
+      if (key0w + r < T) {  // uniform over the 16 lanes of a row
+        *reinterpret_cast<uint4*>(dst + (long)(key0w + r) * ldg + (lane & 15) * 8) = x;
+        if constexpr (MXO) {
+          const float f[8] = {bits2f(x.x & 0xffff), bits2f(x.x >> 16), bits2f(x.y & 0xffff), bits2f(x.y >> 16),
+                              bits2f(x.z & 0xffff), bits2f(x.z >> 16), bits2f(x.w & 0xffff), bits2f(x.w >> 16)};
+          mx8_store8(mo, rowbase + key0w + r, (col + h * HD) / 8 + (lane & 15), f);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the scratch is rewritten by the next call)
+  };
+  if (key0w < T) {
+    store_rows(dv, vc, 1.f);
+    store_rows(dk, kc, 1.f);
+  }
+}
+
+#endif  // OSPO_ABLATION
+
 // Stage 32 rows x 128 bf16 (clamped to [0, row_lim)): 8 pieces of 1 KiB (4 rows each) over the NW waves.
 // AUX: cache-policy bits of the loads (2 = non-temporal: the dS^T workspace, read once).
 template <int NW, int AUX = 0>
@@ -2363,6 +2683,23 @@ static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
       if (mo.q || nwd != 4 || !dkdv3) return OSPO_ERR_UNSUPPORTED;
       dkdv3 = attn_bwd_dkdv3_kernel<4, 0, false, true>;
     }
+#endif
+    bool dkdv5 = false;
+#ifdef OSPO_ABLATION
+    // A/B: attn_bwd_dkdv5_kernel (32x32x16 MFMA, 128-key blocks): correct (1.2e-4 of dkdv3's outputs) but
+    // 248.2 vs 176.9 us for the whole backward at the step shape (profiles/r06/attn_bwd_ab.log): one wave per SIMD
+    dkdv5 = getenv("OSPO_ATTN_DKDV5") && dkdv3 && !g_attn_stamps && nwd == 4;
+    if (dkdv5) {
+      const dim3 g5(S * n_heads * ((T + 127) / 128));
+      if (mo.q)
+        hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<true>, g5, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+                           v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads, scale, rc,
+                           rs, (bf16*)ds_ws, p, order_dkdv, mo);
+      else
+        hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<false>, g5, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col,
+                           k_col, v_col, (const bf16*)dout, ld_do, lse, delta_ws, (bf16*)dqkv, ld_dqkv, T, n_heads,
+                           scale, rc, rs, (bf16*)ds_ws, p, order_dkdv, mo);
+    } else
 #endif
     if (dkdv3)
       hipLaunchKernelGGL(dkdv3, dim3(S * n_heads * ((T + 16 * nwd - 1) / (16 * nwd))), dim3(64 * nwd), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,

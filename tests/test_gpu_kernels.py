@@ -886,8 +886,9 @@ def test_gemm_swiglu_bwd_fused_equals_two_launches(M, F, K, K2, p, split):
 @pytest.mark.parametrize("S,T,H", [(2, 600, 4), (1, 200, 2)])
 def test_flash_attention_bwd_5_product_form_equals_7(S, T, H):
     """The 5-product backward (dK/dV store dS^T, dQ = dS.K) against the 7-product one (dQ recomputes S
-    and dP): dV is bit-identical (same kernel, same operands); dK and dQ differ only by the fp32
-    summation order of delta and of the S / dP recompute."""
+    and dP): all three outputs agree to fp32 summation order; dV is bit-identical while both forms run
+    the same 16x16x32 dK / dV kernel (the default; the 32x32x16 attn_bwd_dkdv5_kernel, an ablation
+    build option since round 6, agrees to 1.2e-4)."""
     hd = 128
     D = H * hd
     rows = S * T
@@ -903,9 +904,9 @@ def test_flash_attention_bwd_5_product_form_equals_7(S, T, H):
     ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, ops().flash_attn_bwd_ws(S, T, H, DEV), a, S, T, H, hd,
                          scale)
     ops().flash_attn_bwd(qkv, 0, D, 2 * D, o, do, lse, delta, None, b, S, T, H, hd, scale)
-    assert torch.equal(a[:, 2 * D:], b[:, 2 * D:])
-    for i in range(2):
+    for i in range(3):
         assert relerr(a[:, i * D:(i + 1) * D].float(), b[:, i * D:(i + 1) * D].float()) < 4e-3
+    assert torch.equal(a[:, 2 * D:], b[:, 2 * D:])
 
 
 @pytest.mark.parametrize("K,N,used,Rp,splits", [(4800, 4096, 48, 64, 8), (320, 11008, 16, 64, 2),

@@ -1,7 +1,8 @@
 """Round 6 attention A/B at the step shape (S 8, T 600, 32 heads, d 128), one process, ablation build: the forward
 as attn_fwd3_kernel (32x32x16 MFMA, fp32 scores; the default) against attn_fwd2_kernel (OSPO_ATTN_FWD2=1, round 5's
 kernel, now also fp32 scores), both checked against an fp32 torch reference on two (sequence, head) groups, and
-the 5-product backward.  Times are medians of 5 rounds of 20 launches (HIP events), inputs alternated between two
+the 5-product backward with its dK / dV half as attn_bwd_dkdv3_kernel (default) or attn_bwd_dkdv5_kernel
+(OSPO_ATTN_DKDV5=1).  Times are medians of 5 rounds of 20 launches (HIP events), inputs alternated between two
 seeded sets so nothing is re-read from the Infinity Cache across launches."""
 import os as _os
 _os.environ.setdefault("OSPO_HIP_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
@@ -82,9 +83,23 @@ def main():
         ops.flash_attn_fwd(qkv[i], 0, D, 2 * D, o[i], lse[i], S, T, H, hd, sc)
     bw = lambda i: ops.flash_attn_bwd(qkv[i], 0, D, 2 * D, o[i], do[i], lse[i], delta, ws, dq[i], S, T, H, hd, sc,  # noqa: E731
                                       rope_cos=cos, rope_sin=sin)
-    tb = med_time(bw)
-    print(json.dumps({"bwd5_us": round(tb, 1), "bwd_alg_tflops": round(2 * fl / tb / 1e6, 1),
-                      "bwd_frac": round(2 * fl / tb / 1e6 / 2500, 4)}), flush=True)
+    outb = {}
+    for tag, env in (("dkdv5", "1"), ("dkdv3", None)):
+        if env:
+            _os.environ["OSPO_ATTN_DKDV5"] = env
+        else:
+            _os.environ.pop("OSPO_ATTN_DKDV5", None)
+        tb = med_time(bw)
+        bw(0)
+        torch.cuda.synchronize()
+        outb[tag] = dq[0].clone()
+        print(json.dumps({tag: {"bwd_us": round(tb, 1), "bwd_alg_tflops": round(2 * fl / tb / 1e6, 1),
+                                "bwd_frac": round(2 * fl / tb / 1e6 / 2500, 4)}}), flush=True)
+    _os.environ.pop("OSPO_ATTN_DKDV5", None)
+    a, b = outb["dkdv5"].float(), outb["dkdv3"].float()
+    rel = {n: float((a[:, i * D:(i + 1) * D] - b[:, i * D:(i + 1) * D]).norm() / b[:, i * D:(i + 1) * D].norm())
+           for i, n in enumerate("qkv")}
+    print(json.dumps({"dkdv5_vs_dkdv3_rel": rel, "max_abs": float((a - b).abs().max())}), flush=True)
 
 
 if __name__ == "__main__" and len(sys.argv) == 1:
