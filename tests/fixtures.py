@@ -20,6 +20,10 @@ def load(name: str):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 
 
+def exists(name: str) -> bool:
+    return os.path.exists(os.path.join(GOLDEN, name))
+
+
 def dims_of(z) -> O.JanusDims:
     return O.JanusDims(**json.loads(str(z["dims"])))
 
