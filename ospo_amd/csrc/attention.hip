@@ -784,7 +784,13 @@ __device__ __forceinline__ bf16x8 f3_pack8(const f32x16& v, int r0) {
 // DBG (ablation build, results invalid): 1 no softmax VALU, 2 no PV (no V reads), 3 no S (no K reads),
 // 4 no DMA after the first tile, 5 = 4 + no per-tile barrier, 6 = the real kernel + s_memtime sums per wave of
 // (S, softmax, PV, tile-end wait + barrier, prologue, stage issue) written over lse as u64 [wg][wave][6]
-template <bool MXO = false, int DBG = 0>
+// PL (ablation build): where a wave issues its 8 LDS-DMA pieces of the next K / V tile: 0 (default) one K + V
+// pair after each S batch, 1 the four pairs spread over the softmax VALU, 2 one pair after each PV chain,
+// 3 K pieces after the S batches and V pieces after the PV chains.  Bit-identical; 50.2 / 51.3 / 52.4 / 51.6 us
+// at the step shape (profiles/r06/attn_fwd3_placement_ab.log), so 0 stays.
+// RS (ablation build): 1 = deferred running max (rescale only when some row's max grows by more than 2^8):
+// 49.9 vs 50.2 us, O 2.01e-3 vs 1.96e-3 from fp32 (same log): not adopted
+template <bool MXO = false, int DBG = 0, int PL = 0, int RS = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd3_kernel(
     const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, bf16* __restrict__ out, int ldo,
     float* __restrict__ lse, int T, int H, float scale, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0},
@@ -841,11 +847,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const uint32_t dma_off = (uint32_t)((4 * wave + (lane >> 4)) * ldq * 2) +
                            (uint32_t)((((lane & 15) ^ f3swz(4 * wave + (lane >> 4))) << 4));
   // piece i (K and V) of tile t into buffer b
-  auto stage_piece = [&](int t, int b, int i) __attribute__((always_inline)) {
+  auto stage_k = [&](int t, int b, int i) __attribute__((always_inline)) {
     const int so = (t * KB + 16 * i) * ldq * 2;
     char* dst = smem + b * 2 * TILE_BYTES + (wave + 4 * i) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsK, (LDS_AS void*)dst, 16, dma_off, so, 0, 0);
+  };
+  auto stage_v = [&](int t, int b, int i) __attribute__((always_inline)) {
+    const int so = (t * KB + 16 * i) * ldq * 2;
+    char* dst = smem + b * 2 * TILE_BYTES + (wave + 4 * i) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (LDS_AS void*)(dst + TILE_BYTES), 16, dma_off, so, 0, 0);
+  };
+  auto stage_piece = [&](int t, int b, int i) __attribute__((always_inline)) {
+    stage_k(t, b, i);
+    stage_v(t, b, i);
   };
 
   // per-lane LDS addresses (buffer 0): K rows l32 (+ 32 for chain 1: immediate) at chunk 2 ks + hi; V^T rows
@@ -906,7 +920,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       __builtin_amdgcn_sched_barrier(0);  // (keep each batch's MFMAs ahead of the next batch's wait)
       // the next tile's K / V piece pair bt into the other buffer, in the shadow of this batch's MFMAs (after the
       // last tile too: rows past T read zeros into a buffer nothing reads before the tile-end wait)
-      if (DBG != 4 && DBG != 5) stage_piece(kt + 1, B ^ 1, bt);
+      if (DBG != 4 && DBG != 5) {
+        if constexpr (PL == 0) stage_piece(kt + 1, B ^ 1, bt);
+        if constexpr (PL == 3) stage_k(kt + 1, B ^ 1, bt);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     }
@@ -928,6 +945,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int u = 0; u < 4; ++u) o[c] = MFMA32(pt[u], pt[(u + c) & 3], o[c]);
       return;
     }
+    auto pl1 = [&](int i) __attribute__((always_inline)) {  // PL 1: piece pair i inside the softmax
+      if constexpr (PL == 1 && DBG != 4 && DBG != 5) {
+        __builtin_amdgcn_sched_barrier(0);
+        stage_piece(kt + 1, B ^ 1, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    pl1(0);
     float tmax = -INFINITY;
     if (key0 + KB - 1 > row0w) {  // a diagonal tile for this wave: mask keys past the row
 #pragma unroll
@@ -943,7 +968,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[ch][r]);
     tmax = f3_partner_max(tmax);
-    const float m_new = fmaxf(m_run, tmax * cs);
+    pl1(1);
+    float m_new = fmaxf(m_run, tmax * cs);
+    bool resc = true;
+    if constexpr (RS == 1) {
+      // deferred max: the running max stays unless some row's grows by more than 8 (log2 units; P <= 2^8), and
+      // the 64 O multiplies are skipped on the tiles where none did (alpha = 1 exactly: l is unchanged by it)
+      resc = __builtin_amdgcn_ballot_w64(m_new > m_run + 8.f) != 0;
+      if (!resc) m_new = m_run;
+    }
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     float psum = 0.f;
 #pragma unroll
@@ -954,16 +987,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         sc[ch][r] = pv;
         psum += pv;
       }
+    pl1(2);
     psum = f3_partner_sum(psum);
     l_run = l_run * alpha + psum;
     m_run = m_new;
     // every tile (a branch on __any(alpha != 1), even with in-place asm multiplies, left the kernel at 256
     // VGPRs with a spill reloaded inside the tile loop)
+    if (resc) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) o[c] *= alpha;
+      for (int c = 0; c < 4; ++c) o[c] *= alpha;
+    }
     bf16x8 pt[4];  // P^T operand of key step u: chain u >> 1, registers 8 (u & 1) ..
 #pragma unroll
     for (int u = 0; u < 4; ++u) pt[u] = f3_pack8(sc[u >> 1], 8 * (u & 1));
+    pl1(3);
     const unsigned long long t2 = stamp();
     // ---- O^T += V^T . P^T: 16 MFMAs; per d chain c one batch of 8 transposed reads, double-buffered
     if constexpr (DBG == 2) {
@@ -991,6 +1028,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[c] = MFMA32(trp_join(vlo[bb][u], vhi[bb][u]), pt[u], o[c]);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((PL == 2 || PL == 3) && DBG != 4 && DBG != 5) {
+        if constexpr (PL == 2) stage_piece(kt + 1, B ^ 1, c);
+        else stage_v(kt + 1, B ^ 1, c);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     };
     issue_v(C0{}, 0);
     issue_v(C1{}, 1);
@@ -1020,20 +1062,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   st6[4] = stamp() - t_pro0;
   using Bf0 = std::integral_constant<int, 0>;
   using Bf1 = std::integral_constant<int, 1>;
-  for (int kt = 0; kt < n_kv; ++kt) {
-    const int buf = DBG == 4 || DBG == 5 ? 0 : kt & 1;
+  // one tile and its end: tile kt + 1 goes into the other buffer (every wave finished reading it at the last
+  // barrier); its pieces are issued inside tile kt, or here by a wave with no rows in tile kt
+  auto step = [&](auto b_c, int kt) __attribute__((always_inline)) {
+    constexpr int B = decltype(b_c)::value;
     const unsigned long long ts0 = stamp();
-    // tile kt + 1 goes into the other buffer (every wave finished reading it at the last barrier): its pieces are
-    // issued inside tile kt's S phase, or here by a wave with no rows in tile kt
     const bool nxt = kt + 1 < n_kv;
     if (kt < n_kv_w) {
-      if (buf)
-        tile(Bf1{}, kt, nxt);
-      else
-        tile(Bf0{}, kt, nxt);
+      tile(b_c, kt, nxt);
     } else if (DBG != 4 && DBG != 5 && nxt) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) stage_piece(kt + 1, buf ^ 1, i);
+      for (int i = 0; i < 4; ++i) stage_piece(kt + 1, B ^ 1, i);
     }
     st6[5] += stamp() - ts0;
     const unsigned long long tw0 = stamp();
@@ -1042,7 +1081,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       __syncthreads();
     }
     st6[3] += stamp() - tw0;
+  };
+  // unrolled by the two buffers: with the buffer chosen per iteration, the two tile bodies kept the 64 O
+  // accumulators (and m, l) in different registers and every tile ended in 66 v_mov_b32 copying them across
+  int kt = 0;
+  for (; kt + 1 < n_kv; kt += 2) {
+    step(Bf0{}, kt);
+    step(Bf1{}, kt + 1);
   }
+  if (kt < n_kv) step(Bf0{}, kt);
   if constexpr (DBG == 5) __syncthreads();
 
   // O = O^T / l, staged through LDS (the K/V buffers) as bf16 rows, stored as whole 256-B rows
@@ -2511,6 +2558,22 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
     if (gm3 >= 1 && (S * n_heads) % 8 == 0) g3 = dim3(n_heads * S * ((T + 127) / 128));
     else gm3 = 0;
 #ifdef OSPO_ABLATION
+    const char* epl = getenv("OSPO_ATTN_FWD3_PL");  // A/B: where the next tile's DMA pieces are issued
+    const char* ers = getenv("OSPO_ATTN_FWD3_RS");  // A/B: deferred running max
+    if (epl || ers) {
+      const int v = epl ? atoi(epl) : 0, r = ers ? atoi(ers) : 0;
+      if (mo.q || v < 0 || v > 3 || r < 0 || r > 1) return OSPO_ERR_UNSUPPORTED;
+      using Fn = decltype(&attn_fwd3_kernel<false, 0, 0, 0>);
+      const Fn tab[2][4] = {{attn_fwd3_kernel<false, 0, 0, 0>, attn_fwd3_kernel<false, 0, 1, 0>,
+                             attn_fwd3_kernel<false, 0, 2, 0>, attn_fwd3_kernel<false, 0, 3, 0>},
+                            {attn_fwd3_kernel<false, 0, 0, 1>, attn_fwd3_kernel<false, 0, 1, 1>,
+                             attn_fwd3_kernel<false, 0, 2, 1>, attn_fwd3_kernel<false, 0, 3, 1>}};
+      auto k = tab[r][v];
+      hipLaunchKernelGGL(k, g3, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col, (bf16*)o, ld_o,
+                         lse, T, n_heads, scale, mo, gm3);
+      OSPO_CHECK_LAUNCH();
+      return OSPO_OK;
+    }
     if (const char* e = getenv("OSPO_ATTN_FWD3_DBG")) {  // decomposition (results invalid)
       const int v = atoi(e);
       auto k = v == 1 ? attn_fwd3_kernel<false, 1> : v == 2 ? attn_fwd3_kernel<false, 2> :

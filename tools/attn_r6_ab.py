@@ -169,3 +169,56 @@ def decompose():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--decompose":
     decompose()
+
+
+def place():
+    """OSPO_ATTN_FWD3_PL / _RS A/B: where each wave issues the next K / V tile's 8 LDS-DMA pieces (pl 0 = after
+    the S batches, the default; 1 = inside the softmax VALU; 2 = after the PV chains; 3 = K after S, V after PV)
+    and the deferred running max (rs 1).  rs 0 forms must be bit-identical to the default; rs 1 is checked
+    against the fp32 reference.  Interleaved passes after 2 s of warm launches."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = [torch.randn(S * T, 3 * D, device="cuda", generator=g).bfloat16() for _ in range(2)]
+    o = [torch.empty(S * T, D, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    lse = [torch.zeros(S * H * T, device="cuda") for _ in range(2)]
+    sc = 1 / math.sqrt(hd)
+    f = lambda i: ops.flash_attn_fwd(qkv[i], 0, D, 2 * D, o[i], lse[i], S, T, H, hd, sc)  # noqa: E731
+    t_end = time.time() + 2.0
+    while time.time() < t_end:
+        for i in range(20):
+            f(i & 1)
+        torch.cuda.synchronize()
+    forms = [(0, 0), (1, 0), (2, 0), (3, 0), (0, 1), (1, 1), (2, 1)]
+    times, outs = {fm: [] for fm in forms}, {}
+    for _ in range(3):
+        for pl, rs in forms:
+            _os.environ.pop("OSPO_ATTN_FWD3_PL", None)
+            _os.environ.pop("OSPO_ATTN_FWD3_RS", None)
+            if pl:
+                _os.environ["OSPO_ATTN_FWD3_PL"] = str(pl)
+            if rs:
+                _os.environ["OSPO_ATTN_FWD3_RS"] = str(rs)
+            times[(pl, rs)].append(med_time(f))
+            f(0)
+            torch.cuda.synchronize()
+            outs[(pl, rs)] = (o[0].clone(), lse[0].clone())
+    _os.environ.pop("OSPO_ATTN_FWD3_PL", None)
+    _os.environ.pop("OSPO_ATTN_FWD3_RS", None)
+    err = {}
+    for fm in forms:
+        e = []
+        for (s_, h) in ((0, 0), (S - 1, H - 1)):
+            r, rl = ref_fwd(qkv[0], s_, h, sc)
+            got = outs[fm][0][s_ * T:(s_ + 1) * T, h * hd:(h + 1) * hd].float()
+            gl = outs[fm][1].view(S, H, T)[s_, h]
+            e.append((float((got - r).norm() / r.norm()), float((gl - rl).abs().max())))
+        err[f"pl{fm[0]}_rs{fm[1]}"] = [max(x[0] for x in e), max(x[1] for x in e)]
+    print(json.dumps({"fwd3_placement_us": {f"pl{a}_rs{b}": round(sorted(v)[1], 1) for (a, b), v in times.items()},
+                      "passes": {f"pl{a}_rs{b}": [round(x, 1) for x in v] for (a, b), v in times.items()},
+                      "bit_identical_to_default": {f"pl{a}_rs{b}": bool(torch.equal(outs[(a, b)][0], outs[(0, 0)][0])
+                                                                         and torch.equal(outs[(a, b)][1], outs[(0, 0)][1]))
+                                                   for (a, b) in forms[1:]},
+                      "o_rel_err_vs_fp32_and_lse_max_abs": err}), flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--place":
+    place()
