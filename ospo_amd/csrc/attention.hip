@@ -1134,6 +1134,300 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
+#ifdef OSPO_ABLATION
+// attn_fwd4_kernel (round 6): attn_fwd3_kernel software-pipelined across tiles.  Per wave and tile j the S
+// MFMAs computed are those of tile j + 1, and tile j's softmax (on the S of the previous iteration) runs in four
+// slices between their four batches, so the VALU issues while the MFMAs execute (a wave's softmax and its own S
+// product no longer serialise; fwd3 left that overlap to the other wave on the SIMD).  Then PV(j).  K is
+// staged two tiles ahead and V one (K(j + 2) into K(j)'s buffer, V(j + 1) into V(j - 1)'s; both last read
+// before the previous tile-end barrier), so the LDS stays 4 x 16 KiB.  Same arithmetic in the same order:
+// bit-identical to attn_fwd3_kernel.  One more barrier per workgroup (after the prologue's S(0)).
+// Measured SLOWER (ablation build, OSPO_ATTN_FWD4=1): 53.3 vs 51.9 us at the step shape, bit-identical
+// (profiles/r06/attn_fwd4_swp_ab.log); 241 VGPRs against fwd3's 192.  With two waves per SIMD the other wave's
+// MFMAs already fill a wave's softmax gaps, so the pipelining only added registers and a barrier.
+template <bool MXO = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd4_kernel(
+    const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, bf16* __restrict__ out, int ldo,
+    float* __restrict__ lse, int T, int H, float scale, const Mx8Out mo = Mx8Out{nullptr, 0, nullptr, 0},
+    int gm = 0) {
+  constexpr int RB = 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // buffer b: K at 2b * TILE, V at (2b + 1) * TILE
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int qb, h, s;
+  if (gm >= 1) {  // 1-D grid (ablation A/B): group_major / banded order, heaviest block first within a group / band
+    const int nqb = (T + RB - 1) / RB;
+    int grp, j;
+    group_major(nqb, gridDim.x / nqb, grp, j, gm);
+    qb = nqb - 1 - j;
+    h = grp % H;
+    s = grp / H;
+  } else {
+    qb = gridDim.z - 1 - blockIdx.z;  // heaviest blocks first (LPT), as attn_fwd2_kernel
+    h = blockIdx.x;
+    s = blockIdx.y;
+  }
+  const int hi = lane >> 5, l32 = lane & 31;
+  const long rowbase = (long)s * T;
+  const int row0w = qb * RB + wave * 32;  // this wave's first query row (wave-uniform)
+  const int qrow = row0w + l32;
+  const int lim = qrow < T ? qrow : T - 1;  // last key this lane's row attends to (padding rows: T - 1)
+  const int last = (qb * RB + RB - 1 < T ? qb * RB + RB - 1 : T - 1);
+  const int n_kv = last / KB + 1;
+  // tiles this wave computes: up to its last real row's (rows past T: none -- they only stage and sync)
+  const int n_kv_w = row0w < T ? (min(row0w + 31, T - 1)) / KB + 1 : 0;
+
+  bf16x8 qf[8];  // Q^T B operand of d step ks: row qrow, d = 16 ks + 8 hi ..
+  {
+    const bf16* qp = qkv + (rowbase + lim) * ldq + qc + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks + 8 * hi);
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;  // m in log2 units of the scaled scores
+  const float cs = scale * L2E;
+  const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
+  const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
+  // K / V tiles by buffer_load ... lds from per-sequence descriptors (records end at row T: rows past it read
+  // zeros -- keys every row masks and V rows its P zeroes -- so no row clamp); a wave's piece i of a tile is
+  // rows 4 (wave + 4 i) .., whose swizzle f3swz = 4 (lane >> 4) + wave does not depend on i: ONE per-lane
+  // offset, the tile and the piece advance in the scalar soffset
+  const __amdgpu_buffer_rsrc_t rsK = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, T * ldq * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, T * ldq * 2, 0x00020000);
+  // (piece rows 4 p + (lane >> 4), p = wave + 4 i: f3swz = 4 (lane >> 4) + wave for every i)
+  const uint32_t dma_off = (uint32_t)((4 * wave + (lane >> 4)) * ldq * 2) +
+                           (uint32_t)((((lane & 15) ^ f3swz(4 * wave + (lane >> 4))) << 4));
+  // piece i (K and V) of tile t into buffer b
+  auto stage_k = [&](int t, int b, int i) __attribute__((always_inline)) {
+    const int so = (t * KB + 16 * i) * ldq * 2;
+    char* dst = smem + b * 2 * TILE_BYTES + (wave + 4 * i) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsK, (LDS_AS void*)dst, 16, dma_off, so, 0, 0);
+  };
+  auto stage_v = [&](int t, int b, int i) __attribute__((always_inline)) {
+    const int so = (t * KB + 16 * i) * ldq * 2;
+    char* dst = smem + b * 2 * TILE_BYTES + (wave + 4 * i) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (LDS_AS void*)(dst + TILE_BYTES), 16, dma_off, so, 0, 0);
+  };
+
+  // per-lane LDS addresses (buffer 0): K rows l32 (+ 32 for chain 1: immediate) at chunk 2 ks + hi; V^T rows
+  // 4 hi + (li >> 2) (+ 8: second read; + 16 u: key step, immediate), d columns 32 c + 16 (G & 1) + 4 (li & 3)
+  const uint32_t sa = lds_u32(smem);
+  uint32_t ka[8], va[8];
+  {
+    const int fk = f3swz(l32);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) ka[ks] = sa + l32 * ROWB + (((2 * ks + hi) ^ fk) << 4);
+    const int G = lane >> 4, li = lane & 15;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int sec = 0; sec < 2; ++sec) {
+        const int row = 4 * hi + (li >> 2) + 8 * sec;
+        const int ch = 4 * c + 2 * (G & 1) + ((li & 3) >> 1);
+        va[2 * c + sec] = sa + TILE_BYTES + row * ROWB + ((ch ^ f3swz(row)) << 4) + ((li & 1) << 3);
+      }
+  }
+
+  using Bf0 = std::integral_constant<int, 0>;
+  using Bf1 = std::integral_constant<int, 1>;
+  f32x16 sc[2][2];  // [tile parity][key chain]: S^T of tile j in sc[j & 1]
+  // S^T of a tile from K buffer KB_ into acc, in 4 batches of 4 MFMAs; after(bt) runs between the batches
+  auto s_tile = [&](auto b_c, f32x16 (&acc)[2], auto&& after) __attribute__((always_inline)) {
+    constexpr int KO = decltype(b_c)::value * 2 * TILE_BYTES;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][r] = acc[1][r] = 0.f;
+    bf16x8 kf[2][4];
+    f3_rd128<KO>(ka[0], kf[0][0]);
+    f3_rd128<KO + 32 * ROWB>(ka[0], kf[0][1]);
+    f3_rd128<KO>(ka[1], kf[0][2]);
+    f3_rd128<KO + 32 * ROWB>(ka[1], kf[0][3]);
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      const int cur = bt & 1;
+      if (bt < 3) {
+        f3_rd128<KO>(ka[2 * bt + 2], kf[cur ^ 1][0]);
+        f3_rd128<KO + 32 * ROWB>(ka[2 * bt + 2], kf[cur ^ 1][1]);
+        f3_rd128<KO>(ka[2 * bt + 3], kf[cur ^ 1][2]);
+        f3_rd128<KO + 32 * ROWB>(ka[2 * bt + 3], kf[cur ^ 1][3]);
+        f3_wait4<4>(kf[cur]);
+      } else {
+        f3_wait4<0>(kf[cur]);
+      }
+      acc[0] = MFMA32(kf[cur][0], qf[2 * bt], acc[0]);
+      acc[1] = MFMA32(kf[cur][1], qf[2 * bt], acc[1]);
+      acc[0] = MFMA32(kf[cur][2], qf[2 * bt + 1], acc[0]);
+      acc[1] = MFMA32(kf[cur][3], qf[2 * bt + 1], acc[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      after(bt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // prologue: K(0) V(0) into buffer 0, K(1) into buffer 1; S(0)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    stage_k(0, 0, i);
+    stage_v(0, 0, i);
+    if (n_kv > 1) stage_k(1, 1, i);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (0 < n_kv_w) s_tile(Bf0{}, sc[0], [](int) {});
+  __syncthreads();  // every wave's K(0) reads done: body 0 stages K(2) over them
+
+  // body j: stage K(j + 2) / V(j + 1); S(j + 1) with softmax(j) in its gaps; PV(j); tile-end wait + barrier
+  auto body = [&](auto b_c, int j) __attribute__((always_inline)) {
+    constexpr int B = decltype(b_c)::value;  // j & 1
+    const bool k2 = j + 2 < n_kv, v1 = j + 1 < n_kv;
+    auto dma = [&](int bt) __attribute__((always_inline)) {
+      if (k2) stage_k(j + 2, B, bt);
+      if (v1) stage_v(j + 1, B ^ 1, bt);
+    };
+    if (j < n_kv_w) {
+      f32x16 (&sp)[2] = sc[B];
+      const int key0 = j * KB;
+      float tmax = -INFINITY, m_new = 0.f, alpha = 0.f, psum = 0.f;
+      bf16x8 pt[4];  // P^T operand of key step u: chain u >> 1, registers 8 (u & 1) ..
+      auto slice = [&](int bt) __attribute__((always_inline)) {
+        dma(bt);
+        if (bt == 0) {  // mask (diagonal tile) and the row max
+          if (key0 + KB - 1 > row0w) {
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const int key = key0 + 32 * ch + (r & 3) + 8 * (r >> 2) + 4 * hi;
+                sp[ch][r] = key > lim ? -INFINITY : sp[ch][r];
+              }
+          }
+#pragma unroll
+          for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sp[ch][r]);
+          tmax = f3_partner_max(tmax);
+        } else if (bt == 1) {  // the new max; chain 0's probabilities
+          m_new = fmaxf(m_run, tmax * cs);
+          alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(sp[0][r], cs, -m_new));
+            sp[0][r] = pv;
+            psum += pv;
+          }
+        } else if (bt == 2) {  // chain 1's; the row sum
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(sp[1][r], cs, -m_new));
+            sp[1][r] = pv;
+            psum += pv;
+          }
+          psum = f3_partner_sum(psum);
+          l_run = l_run * alpha + psum;
+          m_run = m_new;
+        } else {  // rescale O; pack P
+#pragma unroll
+          for (int c = 0; c < 4; ++c) o[c] *= alpha;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) pt[u] = f3_pack8(sp[u >> 1], 8 * (u & 1));
+        }
+      };
+      if (j + 1 < n_kv_w) {
+        s_tile(std::integral_constant<int, B ^ 1>{}, sc[B ^ 1], slice);
+      } else {
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+          slice(bt);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // ---- O^T += V^T . P^T (V buffer B): per d chain c one batch of 8 transposed reads, double-buffered
+      constexpr int KO = B * 2 * TILE_BYTES;
+      i16x4 vlo[2][4], vhi[2][4];
+      auto issue_v = [&](auto c_c, int bb) __attribute__((always_inline)) {
+        constexpr int C = decltype(c_c)::value;
+        f3_rdtr<KO + 0 * 16 * ROWB>(va[2 * C], vlo[bb][0]);
+        f3_rdtr<KO + 0 * 16 * ROWB>(va[2 * C + 1], vhi[bb][0]);
+        f3_rdtr<KO + 1 * 16 * ROWB>(va[2 * C], vlo[bb][1]);
+        f3_rdtr<KO + 1 * 16 * ROWB>(va[2 * C + 1], vhi[bb][1]);
+        f3_rdtr<KO + 2 * 16 * ROWB>(va[2 * C], vlo[bb][2]);
+        f3_rdtr<KO + 2 * 16 * ROWB>(va[2 * C + 1], vhi[bb][2]);
+        f3_rdtr<KO + 3 * 16 * ROWB>(va[2 * C], vlo[bb][3]);
+        f3_rdtr<KO + 3 * 16 * ROWB>(va[2 * C + 1], vhi[bb][3]);
+      };
+      auto pv_chain = [&](int c, int bb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[c] = MFMA32(trp_join(vlo[bb][u], vhi[bb][u]), pt[u], o[c]);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      using C0 = std::integral_constant<int, 0>;
+      using C1 = std::integral_constant<int, 1>;
+      using C2 = std::integral_constant<int, 2>;
+      using C3 = std::integral_constant<int, 3>;
+      issue_v(C0{}, 0);
+      issue_v(C1{}, 1);
+      f3_wait8<8>(vlo[0], vhi[0]);
+      pv_chain(0, 0);
+      issue_v(C2{}, 0);
+      f3_wait8<8>(vlo[1], vhi[1]);
+      pv_chain(1, 1);
+      issue_v(C3{}, 1);
+      f3_wait8<8>(vlo[0], vhi[0]);
+      pv_chain(2, 0);
+      f3_wait8<0>(vlo[1], vhi[1]);
+      pv_chain(3, 1);
+    } else {
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) dma(bt);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  int j = 0;
+  for (; j + 1 < n_kv; j += 2) {
+    body(Bf0{}, j);
+    body(Bf1{}, j + 1);
+  }
+  if (j < n_kv) body(Bf0{}, j);
+
+  // O = O^T / l, staged through LDS (the K/V buffers) as bf16 rows, stored as whole 256-B rows
+  if (row0w < T) {
+    const float inv = 1.f / l_run;
+    char* scr = smem + wave * (32 * SCR_PITCH);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint2 pk;
+        pk.x = pack2(o[c][4 * k] * inv, o[c][4 * k + 1] * inv);
+        pk.y = pack2(o[c][4 * k + 2] * inv, o[c][4 * k + 3] * inv);
+        *reinterpret_cast<uint2*>(scr + l32 * SCR_PITCH + (32 * c + 8 * k + 4 * hi) * 2) = pk;
+      }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bf16* dst = out + rowbase * ldo + h * HD;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int r = 4 * k + (lane >> 4);
+      const uint4 x = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + (lane & 15) * 16);
+      if (row0w + r < T) {  // uniform over the 16 lanes of a row
+        *reinterpret_cast<uint4*>(dst + (long)(row0w + r) * ldo + (lane & 15) * 8) = x;
+        if constexpr (MXO) {
+          const float f[8] = {bits2f(x.x & 0xffff), bits2f(x.x >> 16), bits2f(x.y & 0xffff), bits2f(x.y >> 16),
+                              bits2f(x.z & 0xffff), bits2f(x.z >> 16), bits2f(x.w & 0xffff), bits2f(x.w >> 16)};
+          mx8_store8(mo, rowbase + row0w + r, h * (HD / 8) + (lane & 15), f);
+        }
+      }
+    }
+    if (qrow < T && hi == 0)
+      lse[((long)s * H + h) * T + qrow] = (m_run + __log2f(l_run)) * 0.6931471805599453f;
+  }
+}
+#endif  // OSPO_ABLATION
+
 // ============================================================ backward =====
 // dK / dV: workgroup = 4 waves = 64 keys of one (sequence, head); each wave
 // owns 16 keys (K, V fragments in registers, dK^T dV^T accumulators) and
@@ -2583,6 +2877,18 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
       const Mx8Out mst{(uint8_t*)g_attn_stamps, 0, nullptr, 0};
       hipLaunchKernelGGL(k, g3, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col, (bf16*)o, ld_o,
                          lse, T, n_heads, scale, v == 6 ? mst : mo, gm3);
+      OSPO_CHECK_LAUNCH();
+      return OSPO_OK;
+    }
+#endif
+#ifdef OSPO_ABLATION
+    if (getenv("OSPO_ATTN_FWD4")) {  // A/B: the software-pipelined form
+      if (mo.q)
+        hipLaunchKernelGGL(attn_fwd4_kernel<true>, g3, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,
+                           v_col, (bf16*)o, ld_o, lse, T, n_heads, scale, mo, gm3);
+      else
+        hipLaunchKernelGGL(attn_fwd4_kernel<false>, g3, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col,
+                           k_col, v_col, (bf16*)o, ld_o, lse, T, n_heads, scale, mo, gm3);
       OSPO_CHECK_LAUNCH();
       return OSPO_OK;
     }

@@ -66,19 +66,21 @@ def main():
         for i in range(20):
             f(i & 1)
         torch.cuda.synchronize()
-    times = {"fwd3": [], "fwd2": []}
-    for _ in range(3):
-        for tag, env in (("fwd3", None), ("fwd2", "1")):
-            if env:
-                _os.environ["OSPO_ATTN_FWD2"] = env
-            else:
-                _os.environ.pop("OSPO_ATTN_FWD2", None)
-            times[tag].append(med_time(f))
-    for tag, env in (("fwd3", None), ("fwd2", "1")):
+    forms = (("fwd3", None), ("fwd4", "OSPO_ATTN_FWD4"), ("fwd2", "OSPO_ATTN_FWD2"))
+    times = {tag: [] for tag, _ in forms}
+
+    def select(env):
+        for _, e in forms:
+            if e:
+                _os.environ.pop(e, None)
         if env:
-            _os.environ["OSPO_ATTN_FWD2"] = env
-        else:
-            _os.environ.pop("OSPO_ATTN_FWD2", None)
+            _os.environ[env] = "1"
+    for _ in range(3):
+        for tag, env in forms:
+            select(env)
+            times[tag].append(med_time(f))
+    for tag, env in forms:
+        select(env)
         t = sorted(times[tag])[1]
         f(0)
         torch.cuda.synchronize()
@@ -92,10 +94,12 @@ def main():
         res[tag] = {"fwd_us": round(t, 1), "passes_us": [round(x, 1) for x in times[tag]], "tflops": round(fl / t / 1e6, 1), "frac": round(fl / t / 1e6 / 2500, 4),
                     "o_rel_err_vs_fp32": max(e[0] for e in err), "lse_max_abs_err": max(e[1] for e in err)}
         print(json.dumps({tag: res[tag]}), flush=True)
-    _os.environ.pop("OSPO_ATTN_FWD2", None)
+    select(None)
     a, b = outs["fwd3"], outs["fwd2"]
     print(json.dumps({"fwd3_vs_fwd2_o_max_abs": float((a[0].float() - b[0].float()).abs().max()),
-                      "fwd3_vs_fwd2_lse_max_abs": float((a[1] - b[1]).abs().max())}), flush=True)
+                      "fwd3_vs_fwd2_lse_max_abs": float((a[1] - b[1]).abs().max()),
+                      "fwd4_bit_identical_to_fwd3": bool(torch.equal(outs["fwd4"][0], a[0]) and
+                                                         torch.equal(outs["fwd4"][1], a[1]))}), flush=True)
     for i in range(2):
         ops.flash_attn_fwd(qkv[i], 0, D, 2 * D, o[i], lse[i], S, T, H, hd, sc)
     bw = lambda i: ops.flash_attn_bwd(qkv[i], 0, D, 2 * D, o[i], do[i], lse[i], delta, ws, dq[i], S, T, H, hd, sc,  # noqa: E731
