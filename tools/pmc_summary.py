@@ -75,7 +75,8 @@ for m, ks in fams.items():
         # tools/w4_stamps.py.)
         "mfma_busy_frac_at_2p4ghz_peak": round(busy / (dur_s * 2.4e9 * 1024), 4) if dur_s else None,
     }
-for k in sorted(set(fetch) | set(write), key=lambda k: -(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"]))[:15]:
+ranked = sorted(set(fetch) | set(write), key=lambda k: -(2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"]))
+for k in ranked[:15] + [k for k in ranked[15:] if "attn" in k]:  # (round 6: every attention kernel)
     n = max(nf[(k, "FETCH_SIZE")], 1)
     out.setdefault("per_kernel_MiB_per_launch", {})[short(k)[:60]] = round(
         (2 * fetch[k]["FETCH_SIZE"] + write[k]["WRITE_SIZE"]) / 1024 / n, 2)
