@@ -2841,10 +2841,13 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
     fwd3 = false;  // A/B: the round-4/5 kernels (16x16x32 MFMA)
 #endif
   if (fwd3) {
-    // workgroup order: banded (group_major, bands of 16 (sequence, head) groups per XCD, heaviest block first
+    // workgroup order: banded (group_major, bands of 8 (sequence, head) groups per XCD, heaviest block first
     // within a band) -- a band's K / V re-reads hit its XCD's L2: 61.2 -> 50.6 us at the step shape against the
-    // 3-D grid's chip-wide heaviest-first order (gm 2 / 4 / 8: 60.3 / 54.7 / 50.8; profiles/r06/attn_fwd3_ab.log)
-    int gm3 = 16;
+    // 3-D grid's chip-wide heaviest-first order (gm 2 / 4 / 8 / 16: 60.3 / 54.7 / 50.8 / 50.6;
+    // profiles/r06/attn_fwd3_ab.log).  Bands of 8 (2.4 MB of K / V, inside the XCD's 4 MB L2) against 16: the
+    // same time (50.3 / 50.5 us, attn_fwd3_order_ab.log) and 160 against 184 MiB of HBM per launch, 1.06x the
+    // algorithmic 150.6 MiB (attn_fwd3_pmc_by_band.log)
+    int gm3 = 8;
 #ifdef OSPO_ABLATION
     if (const char* e = getenv("OSPO_ATTN_FWD3_GM")) gm3 = atoi(e);  // A/B: 0 = the 3-D grid, 1 group-major, >= 2 banded
 #endif

@@ -226,3 +226,36 @@ def place():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--place":
     place()
+
+
+def order():
+    """OSPO_ATTN_FWD3_GM A/B after the round-6 unroll: band sizes 4 / 8 / 16 interleaved over 3 passes (2 s of
+    warm launches first); bit-identical outputs (the order moves no arithmetic)."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = [torch.randn(S * T, 3 * D, device="cuda", generator=g).bfloat16() for _ in range(2)]
+    o = [torch.empty(S * T, D, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    lse = [torch.zeros(S * H * T, device="cuda") for _ in range(2)]
+    sc = 1 / math.sqrt(hd)
+    f = lambda i: ops.flash_attn_fwd(qkv[i], 0, D, 2 * D, o[i], lse[i], S, T, H, hd, sc)  # noqa: E731
+    t_end = time.time() + 2.0
+    while time.time() < t_end:
+        for i in range(20):
+            f(i & 1)
+        torch.cuda.synchronize()
+    bands = (4, 8, 16)
+    times, outs = {b: [] for b in bands}, {}
+    for _ in range(3):
+        for b in bands:
+            _os.environ["OSPO_ATTN_FWD3_GM"] = str(b)
+            times[b].append(med_time(f))
+            f(0)
+            torch.cuda.synchronize()
+            outs[b] = o[0].clone()
+    _os.environ.pop("OSPO_ATTN_FWD3_GM", None)
+    print(json.dumps({"fwd3_band_us": {f"gm{b}": round(sorted(v)[1], 1) for b, v in times.items()},
+                      "passes": {f"gm{b}": [round(x, 1) for x in v] for b, v in times.items()},
+                      "bit_identical": all(torch.equal(outs[b], outs[16]) for b in bands)}), flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--order":
+    order()
