@@ -1428,6 +1428,247 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 #endif  // OSPO_ABLATION
 
+#ifdef OSPO_ABLATION
+// attn_fwd5_kernel (round 6, ablation build, OSPO_ATTN_FWD5=NL): attn_fwd3_kernel with the K / V tiles staged by
+// NL dedicated loader waves (waves 4 .. 3 + NL) instead of 8 LDS-DMA pieces per compute wave and tile (the
+// decomposition put ~11 of fwd3's 50.6 us in those pieces: 39.7 us without them).  A loader wave issues its share
+// of the next tile's 32 pieces right after a tile-end barrier, waits for them (vmcnt(0)) and meets the compute
+// waves at the next barrier.  Register diet for 3 waves per SIMD (2 workgroups of 4 + NL waves per CU): the K /
+// V read addresses XOR-derived from one register each (ka(ks) = ka0 ^ 32 ks, va(c) = va0 ^ 64 c: the swizzled
+// chunk bits of those steps are exactly the XORed address bits; the LDS block starts at 0), K batches
+// single-buffered.  Same arithmetic in the same order as fwd3: bit-identical.
+// Measured SLOWER: 60.0-63.0 us against fwd3's 50.1 at the step shape, bit-identical (1 or 2 loader waves, V
+// double- or single-buffered; profiles/r06/attn_fwd5_loader_ab.log): the 168-VGPR compute body (single-buffered
+// K batches, 5-7 spilled VGPRs) and a third wave per SIMD cost more than the pieces' issue saved.
+// VSB: the V^T batches single-buffered too
+template <int NL, bool VSB = false>
+__global__ __launch_bounds__(64 * (4 + NL)) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_fwd5_kernel(
+    const bf16* __restrict__ qkv, int ldq, int qc, int kc, int vc, bf16* __restrict__ out, int ldo,
+    float* __restrict__ lse, int T, int H, float scale, int gm) {
+  constexpr int RB = 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // buffer b: K at 2b * TILE, V at (2b + 1) * TILE
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int qb, h, s;
+  {
+    const int nqb = (T + RB - 1) / RB;
+    int grp, j;
+    group_major(nqb, gridDim.x / nqb, grp, j, gm);
+    qb = nqb - 1 - j;
+    h = grp % H;
+    s = grp / H;
+  }
+  const long rowbase = (long)s * T;
+  const int last = (qb * RB + RB - 1 < T ? qb * RB + RB - 1 : T - 1);
+  const int n_kv = last / KB + 1;
+  if (wave >= 4) {  // ---- loader wave l: pieces p = l + NL i of each K / V image (rows 4 p .. 4 p + 3)
+    const int l = wave - 4;
+    const bf16* kbase = qkv + rowbase * ldq + kc + h * HD;
+    const bf16* vbase = qkv + rowbase * ldq + vc + h * HD;
+    const __amdgpu_buffer_rsrc_t rsK = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, T * ldq * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, T * ldq * 2, 0x00020000);
+    // the swizzle of row 4 p + (lane >> 4) is 4 (lane >> 4) + (p & 3): one per-lane offset per p & 3
+    uint32_t off[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      off[q] = (uint32_t)((lane >> 4) * ldq * 2) + (uint32_t)((((lane & 15) ^ (4 * (lane >> 4) + q)) << 4));
+    auto stage = [&](int t, int b) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 16 / NL; ++i) {
+        const int pc = l + NL * i;
+        const int so = (t * KB + 4 * pc) * ldq * 2;
+        char* dst = smem + b * 2 * TILE_BYTES + pc * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsK, (LDS_AS void*)dst, 16, off[pc & 3], so, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (LDS_AS void*)(dst + TILE_BYTES), 16, off[pc & 3], so, 0, 0);
+      }
+    };
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < n_kv; ++kt) {
+      if (kt + 1 < n_kv) stage(kt + 1, (kt + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    return;  // (the compute waves' epilogue uses no workgroup barrier)
+  }
+  const Mx8Out mo{nullptr, 0, nullptr, 0};
+  // ---- compute waves 0..3: 32 query rows each
+  const int hi = lane >> 5, l32 = lane & 31;
+  const int row0w = qb * RB + wave * 32;
+  const int qrow = row0w + l32;
+  const int lim = qrow < T ? qrow : T - 1;
+  const int n_kv_w = row0w < T ? (min(row0w + 31, T - 1)) / KB + 1 : 0;
+  bf16x8 qf[8];
+  {
+    const bf16* qp = qkv + (rowbase + lim) * ldq + qc + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks + 8 * hi);
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+  const float cs = scale * L2E;
+  const uint32_t sa = lds_u32(smem);
+  uint32_t ka0, va0[2];
+  {
+    const int fk = f3swz(l32);
+    ka0 = sa + l32 * ROWB + (((0 + hi) ^ fk) << 4);  // ka(ks) = ka0 ^ (32 ks)
+    const int G = lane >> 4, li = lane & 15;
+#pragma unroll
+    for (int sec = 0; sec < 2; ++sec) {
+      const int row = 4 * hi + (li >> 2) + 8 * sec;
+      const int ch = 2 * (G & 1) + ((li & 3) >> 1);
+      va0[sec] = sa + TILE_BYTES + row * ROWB + ((ch ^ f3swz(row)) << 4) + ((li & 1) << 3);  // va(c) = va0 ^ 64 c
+    }
+  }
+  auto tile = [&](auto b_c, int kt) __attribute__((always_inline)) {
+    constexpr int B = decltype(b_c)::value;
+    constexpr int KO = B * 2 * TILE_BYTES;
+    f32x16 sc[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[0][r] = sc[1][r] = 0.f;
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {  // K fragments in 4 batches of 4 (single-buffered)
+      bf16x8 kf[4];
+      const uint32_t a0 = ka0 ^ (uint32_t)(64 * bt), a1 = ka0 ^ (uint32_t)(64 * bt + 32);
+      f3_rd128<KO>(a0, kf[0]);
+      f3_rd128<KO + 32 * ROWB>(a0, kf[1]);
+      f3_rd128<KO>(a1, kf[2]);
+      f3_rd128<KO + 32 * ROWB>(a1, kf[3]);
+      f3_wait4<0>(kf);
+      sc[0] = MFMA32(kf[0], qf[2 * bt], sc[0]);
+      sc[1] = MFMA32(kf[1], qf[2 * bt], sc[1]);
+      sc[0] = MFMA32(kf[2], qf[2 * bt + 1], sc[0]);
+      sc[1] = MFMA32(kf[3], qf[2 * bt + 1], sc[1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int key0 = kt * KB;
+    float tmax = -INFINITY;
+    if (key0 + KB - 1 > row0w) {
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + 32 * ch + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          sc[ch][r] = key > lim ? -INFINITY : sc[ch][r];
+        }
+    }
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[ch][r]);
+    tmax = f3_partner_max(tmax);
+    const float m_new = fmaxf(m_run, tmax * cs);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sc[ch][r], cs, -m_new));
+        sc[ch][r] = pv;
+        psum += pv;
+      }
+    psum = f3_partner_sum(psum);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] *= alpha;
+    bf16x8 pt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pt[u] = f3_pack8(sc[u >> 1], 8 * (u & 1));
+    i16x4 vlo[2][4], vhi[2][4];
+    auto issue_v = [&](int c, int bb) __attribute__((always_inline)) {
+      const uint32_t v0 = va0[0] ^ (uint32_t)(64 * c), v1 = va0[1] ^ (uint32_t)(64 * c);
+      f3_rdtr<KO + 0 * 16 * ROWB>(v0, vlo[bb][0]);
+      f3_rdtr<KO + 0 * 16 * ROWB>(v1, vhi[bb][0]);
+      f3_rdtr<KO + 1 * 16 * ROWB>(v0, vlo[bb][1]);
+      f3_rdtr<KO + 1 * 16 * ROWB>(v1, vhi[bb][1]);
+      f3_rdtr<KO + 2 * 16 * ROWB>(v0, vlo[bb][2]);
+      f3_rdtr<KO + 2 * 16 * ROWB>(v1, vhi[bb][2]);
+      f3_rdtr<KO + 3 * 16 * ROWB>(v0, vlo[bb][3]);
+      f3_rdtr<KO + 3 * 16 * ROWB>(v1, vhi[bb][3]);
+    };
+    auto pv_chain = [&](int c, int bb) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[c] = MFMA32(trp_join(vlo[bb][u], vhi[bb][u]), pt[u], o[c]);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if constexpr (VSB) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        issue_v(c, 0);
+        f3_wait8<0>(vlo[0], vhi[0]);
+        pv_chain(c, 0);
+      }
+    } else {
+      issue_v(0, 0);
+      issue_v(1, 1);
+      f3_wait8<8>(vlo[0], vhi[0]);
+      pv_chain(0, 0);
+      issue_v(2, 0);
+      f3_wait8<8>(vlo[1], vhi[1]);
+      pv_chain(1, 1);
+      issue_v(3, 1);
+      f3_wait8<8>(vlo[0], vhi[0]);
+      pv_chain(2, 0);
+      f3_wait8<0>(vlo[1], vhi[1]);
+      pv_chain(3, 1);
+    }
+  };
+  using Bf0 = std::integral_constant<int, 0>;
+  using Bf1 = std::integral_constant<int, 1>;
+  __syncthreads();  // tile 0 landed (the loaders' prologue wait)
+  auto step = [&](auto b_c, int kt) __attribute__((always_inline)) {
+    if (kt < n_kv_w) tile(b_c, kt);
+    __syncthreads();  // every wave done with this buffer; the loaders' next tile landed
+  };
+  int kt = 0;
+  for (; kt + 1 < n_kv; kt += 2) {
+    step(Bf0{}, kt);
+    step(Bf1{}, kt + 1);
+  }
+  if (kt < n_kv) step(Bf0{}, kt);
+  // O = O^T / l, staged through LDS (the K/V buffers) as bf16 rows, stored as whole 256-B rows
+  if (row0w < T) {
+    const float inv = 1.f / l_run;
+    char* scr = smem + wave * (32 * SCR_PITCH);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint2 pk;
+        pk.x = pack2(o[c][4 * k] * inv, o[c][4 * k + 1] * inv);
+        pk.y = pack2(o[c][4 * k + 2] * inv, o[c][4 * k + 3] * inv);
+        *reinterpret_cast<uint2*>(scr + l32 * SCR_PITCH + (32 * c + 8 * k + 4 * hi) * 2) = pk;
+      }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bf16* dst = out + rowbase * ldo + h * HD;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int r = 4 * k + (lane >> 4);
+      const uint4 x = *reinterpret_cast<const uint4*>(scr + r * SCR_PITCH + (lane & 15) * 16);
+      if (row0w + r < T) {  // uniform over the 16 lanes of a row
+        *reinterpret_cast<uint4*>(dst + (long)(row0w + r) * ldo + (lane & 15) * 8) = x;
+        if constexpr (false) {
+          const float f[8] = {bits2f(x.x & 0xffff), bits2f(x.x >> 16), bits2f(x.y & 0xffff), bits2f(x.y >> 16),
+                              bits2f(x.z & 0xffff), bits2f(x.z >> 16), bits2f(x.w & 0xffff), bits2f(x.w >> 16)};
+          mx8_store8(mo, rowbase + row0w + r, h * (HD / 8) + (lane & 15), f);
+        }
+      }
+    }
+    if (qrow < T && hi == 0)
+      lse[((long)s * H + h) * T + qrow] = (m_run + __log2f(l_run)) * 0.6931471805599453f;
+  }
+}
+
+#endif  // OSPO_ABLATION
+
 // ============================================================ backward =====
 // dK / dV: workgroup = 4 waves = 64 keys of one (sequence, head); each wave
 // owns 16 keys (K, V fragments in registers, dK^T dV^T accumulators) and
@@ -2885,6 +3126,17 @@ static int flash_attn_fwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
     }
 #endif
 #ifdef OSPO_ABLATION
+    if (const char* e5 = getenv("OSPO_ATTN_FWD5")) {  // A/B: dedicated loader waves (1 or 2)
+      const int nl = atoi(e5) % 10, vsb = atoi(e5) / 10;  // 1, 2: loader waves; + 10: V single-buffered
+      if (mo.q || (nl != 1 && nl != 2) || vsb > 1 || gm3 < 1) return OSPO_ERR_UNSUPPORTED;
+      using F5 = decltype(&attn_fwd5_kernel<1>);
+      const F5 k5 = nl == 1 ? (vsb ? attn_fwd5_kernel<1, true> : attn_fwd5_kernel<1>)
+                            : (vsb ? attn_fwd5_kernel<2, true> : attn_fwd5_kernel<2>);
+      hipLaunchKernelGGL(k5, g3, dim3(64 * (4 + nl)), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col, v_col,
+                         (bf16*)o, ld_o, lse, T, n_heads, scale, gm3);
+      OSPO_CHECK_LAUNCH();
+      return OSPO_OK;
+    }
     if (getenv("OSPO_ATTN_FWD4")) {  // A/B: the software-pipelined form
       if (mo.q)
         hipLaunchKernelGGL(attn_fwd4_kernel<true>, g3, dim3(256), 0, stream, (const bf16*)qkv, ld_qkv, q_col, k_col,

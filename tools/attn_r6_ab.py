@@ -66,15 +66,18 @@ def main():
         for i in range(20):
             f(i & 1)
         torch.cuda.synchronize()
-    forms = (("fwd3", None), ("fwd4", "OSPO_ATTN_FWD4"), ("fwd2", "OSPO_ATTN_FWD2"))
+    forms = (("fwd3", None), ("fwd4", "OSPO_ATTN_FWD4"), ("fwd5_1", "OSPO_ATTN_FWD5=1"), ("fwd5_2", "OSPO_ATTN_FWD5=2"),
+             ("fwd5_1v", "OSPO_ATTN_FWD5=11"), ("fwd5_2v", "OSPO_ATTN_FWD5=12"),
+             ("fwd2", "OSPO_ATTN_FWD2"))
     times = {tag: [] for tag, _ in forms}
 
     def select(env):
         for _, e in forms:
             if e:
-                _os.environ.pop(e, None)
+                _os.environ.pop(e.split("=")[0], None)
         if env:
-            _os.environ[env] = "1"
+            k, _, v = env.partition("=")
+            _os.environ[k] = v or "1"
     for _ in range(3):
         for tag, env in forms:
             select(env)
@@ -98,8 +101,9 @@ def main():
     a, b = outs["fwd3"], outs["fwd2"]
     print(json.dumps({"fwd3_vs_fwd2_o_max_abs": float((a[0].float() - b[0].float()).abs().max()),
                       "fwd3_vs_fwd2_lse_max_abs": float((a[1] - b[1]).abs().max()),
-                      "fwd4_bit_identical_to_fwd3": bool(torch.equal(outs["fwd4"][0], a[0]) and
-                                                         torch.equal(outs["fwd4"][1], a[1]))}), flush=True)
+                      **{f"{t}_bit_identical_to_fwd3": bool(torch.equal(outs[t][0], a[0]) and
+                                                            torch.equal(outs[t][1], a[1]))
+                         for t in ("fwd4", "fwd5_1", "fwd5_2", "fwd5_1v", "fwd5_2v")}}), flush=True)
     for i in range(2):
         ops.flash_attn_fwd(qkv[i], 0, D, 2 * D, o[i], lse[i], S, T, H, hd, sc)
     bw = lambda i: ops.flash_attn_bwd(qkv[i], 0, D, 2 * D, o[i], do[i], lse[i], delta, ws, dq[i], S, T, H, hd, sc,  # noqa: E731
