@@ -57,6 +57,20 @@ def test_workspace_counter_heads_from_the_library(lib):
     assert int((ws == 0).sum()) == 8208 // 4 and float(ws[8208 // 4]) == 7.0
 
 
+def test_clock_probe_validation_before_launch(lib):
+    """ospo_gemm_clock_probe_bf16 (bench.py's box probe) refuses bad shapes, a short stamp buffer, null and
+    misaligned pointers with a status before any HIP call."""
+    P = ctypes.c_void_p
+    buf = (ctypes.c_char * 4096)()
+    a = ctypes.addressof(buf)
+    st = 4 * 8 * 8  # (512 / 256)^2 tiles x 8 stamps x 8 B
+    assert lib.ospo_gemm_clock_probe_bf16(P(a), P(a), P(a), 500, 512, 512, P(a), st, None) == 1  # M % 256
+    assert lib.ospo_gemm_clock_probe_bf16(P(a), P(a), P(a), 512, 512, 96, P(a), st, None) == 1  # K % 64, K < 256
+    assert lib.ospo_gemm_clock_probe_bf16(P(a), P(a), P(a), 512, 512, 512, P(a), st - 8, None) == 1  # stamps
+    assert lib.ospo_gemm_clock_probe_bf16(P(a), P(a), None, 512, 512, 512, P(a), st, None) == 5  # null C
+    assert lib.ospo_gemm_clock_probe_bf16(P(a + 2), P(a), P(a), 512, 512, 512, P(a), st, None) == 2  # align
+
+
 def test_abi_version_mismatch_is_refused(monkeypatch):
     """A library of another ABI revision is refused at load, not silently mis-driven."""
     from ospo_amd import _lib

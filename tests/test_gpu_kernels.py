@@ -1031,3 +1031,23 @@ def test_lora_wgrad_dropout_recompute_equals_stored_mask():
     assert torch.equal(out, ref)
     assert relerr(out, (g[:, :48].float().T @ xd.float())) < 1e-5
 
+
+
+def test_gemm_clock_probe_product_and_stamps():
+    """ospo_gemm_clock_probe_bf16 (bench.py's box probe): the w4 product unsplit, bit-exact on integer operands
+    (every partial sum an integer below 2^24, one bf16 rounding as torch's fp32 product rounded), and its
+    per-workgroup stamps ordered with an in-kernel clock in a plausible range (s_memtime ticks over
+    s_memrealtime's 100 MHz)."""
+    M = N = K = 512
+    g = torch.Generator(device=DEV).manual_seed(5)
+    a = torch.randint(-4, 5, (M, K), device=DEV, generator=g).bfloat16()
+    b = torch.randint(-4, 5, (N, K), device=DEV, generator=g).bfloat16()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    stamps = torch.zeros((M // 256) * (N // 256), 8, dtype=torch.int64, device=DEV)
+    ops().gemm_clock_probe(a, b, out, stamps)
+    torch.cuda.synchronize()
+    assert torch.equal(out, (a.float() @ b.float().T).bfloat16())
+    st = stamps.cpu()
+    assert bool((st[:, 4] >= st[:, 2]).all()) and bool((st[:, 3] > st[:, 0]).all())
+    ghz = (st[:, 3] - st[:, 0]).double() / (st[:, 4] - st[:, 2]).clamp_min(1).double() * 0.1
+    assert bool(((ghz > 0.3) & (ghz < 3.5)).all()), ghz.tolist()
