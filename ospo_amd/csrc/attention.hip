@@ -3308,11 +3308,10 @@ static int flash_attn_bwd(const void* qkv, int ld_qkv, int q_col, int k_col, int
       dkdv3 = attn_bwd_dkdv3_kernel<4, 0, false, true>;
     }
 #endif
-    bool dkdv5 = false;
 #ifdef OSPO_ABLATION
     // A/B: attn_bwd_dkdv5_kernel (32x32x16 MFMA, 128-key blocks): correct (1.2e-4 of dkdv3's outputs) but
     // 248.2 vs 176.9 us for the whole backward at the step shape (profiles/r06/attn_bwd_ab.log): one wave per SIMD
-    dkdv5 = getenv("OSPO_ATTN_DKDV5") && dkdv3 && !g_attn_stamps && nwd == 4;
+    const bool dkdv5 = getenv("OSPO_ATTN_DKDV5") && dkdv3 && !g_attn_stamps && nwd == 4;
     if (dkdv5) {
       const dim3 g5(S * n_heads * ((T + 127) / 128));
       if (mo.q)
