@@ -1870,11 +1870,6 @@ __device__ __forceinline__ void lds_rdtr(uint32_t a, i16x4& v) {
 __device__ __forceinline__ void dk_lds16(__amdgpu_buffer_rsrc_t rs, char* dst, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, voff, 0, 0, 0);
 }
-// a batch of 8 row fragments (one query sub-tile) + the lse / delta quads of the previous sub-tile
-struct RowBatch {
-  bf16x8 f[8];
-  f32x4 l, d;
-};
 // half of a transposed batch: 4 dO^T (or Q^T) fragments, 8 reads (+ lse / delta quads in the first)
 struct TrHalf {
   i16x4 lo[4], hi[4];
@@ -1892,28 +1887,6 @@ struct HalfBatch {
 };
 __device__ __forceinline__ void wait_half(HalfBatch& r) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r.f[0]), "+v"(r.f[1]), "+v"(r.f[2]), "+v"(r.f[3]), "+v"(r.x)::"memory");
-}
-__device__ __forceinline__ void wait_rows(RowBatch& r) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(r.f[0]), "+v"(r.f[1]), "+v"(r.f[2]), "+v"(r.f[3]), "+v"(r.f[4]), "+v"(r.f[5]), "+v"(r.f[6]),
-                 "+v"(r.f[7]), "+v"(r.l), "+v"(r.d)::"memory");
-}
-// a batch of 8 transposed fragments (dO^T and Q^T, 4 column tiles each), 16 reads (+ lse / delta)
-struct TrBatch {
-  i16x4 lo[8], hi[8];
-  f32x4 l, d;
-};
-__device__ __forceinline__ void wait_tr(TrBatch& t) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(t.lo[0]), "+v"(t.lo[1]), "+v"(t.lo[2]), "+v"(t.lo[3]), "+v"(t.lo[4]), "+v"(t.lo[5]),
-                 "+v"(t.lo[6]), "+v"(t.lo[7]), "+v"(t.hi[0]), "+v"(t.hi[1]), "+v"(t.hi[2]), "+v"(t.hi[3]),
-                 "+v"(t.hi[4]), "+v"(t.hi[5]), "+v"(t.hi[6]), "+v"(t.hi[7])::"memory");
-}
-__device__ __forceinline__ void wait_tr_ld(TrBatch& t) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(t.lo[0]), "+v"(t.lo[1]), "+v"(t.lo[2]), "+v"(t.lo[3]), "+v"(t.lo[4]), "+v"(t.lo[5]),
-                 "+v"(t.lo[6]), "+v"(t.lo[7]), "+v"(t.hi[0]), "+v"(t.hi[1]), "+v"(t.hi[2]), "+v"(t.hi[3]),
-                 "+v"(t.hi[4]), "+v"(t.hi[5]), "+v"(t.hi[6]), "+v"(t.hi[7]), "+v"(t.l), "+v"(t.d)::"memory");
 }
 
 // The same product and outputs as attn_bwd_dkdv_kernel (bit-identical: same MFMA operands and
@@ -2040,34 +2013,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       lds_rdtr<O + 16 * ROWB>(tro[4 * DH + i], t.hi[i]);
     }
   };
-  auto issue_rows = [&](auto b_c, auto a_c, RowBatch& r) {
-    constexpr int B = decltype(b_c)::value, A = decltype(a_c)::value;
-    constexpr int O = B * 2 * TILE_BYTES + A * 16 * ROWB;
-    lds_rd128<O>(rowo[0], r.f[0]);
-    lds_rd128<O + TILE_BYTES>(rowo[0], r.f[4]);
-    lds_rd128<O>(rowo[1], r.f[1]);
-    lds_rd128<O + TILE_BYTES>(rowo[1], r.f[5]);
-    lds_rd128<O>(rowo[2], r.f[2]);
-    lds_rd128<O + TILE_BYTES>(rowo[2], r.f[6]);
-    lds_rd128<O>(rowo[3], r.f[3]);
-    lds_rd128<O + TILE_BYTES>(rowo[3], r.f[7]);
-    if constexpr (A > 0) {  // lse / delta of sub-tile A - 1, whose softmax runs beside S / dP of A
-      lds_rdf4<B * 256 + (A - 1) * 64>(la, r.l);
-      lds_rdf4<B * 256 + (A - 1) * 64 + 512>(la, r.d);
-    }
-  };
-  // batch issue: dO^T and Q^T fragments of query half U, column tiles 4*DH .. 4*DH + 3
-  auto issue_tr = [&](auto b_c, auto u_c, auto dh_c, TrBatch& t) {
-    constexpr int B = decltype(b_c)::value, U = decltype(u_c)::value, DH = decltype(dh_c)::value;
-    constexpr int O = B * 2 * TILE_BYTES + U * 32 * ROWB;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      lds_rdtr<O + TILE_BYTES>(tro[4 * DH + i], t.lo[i]);
-      lds_rdtr<O + TILE_BYTES + 16 * ROWB>(tro[4 * DH + i], t.hi[i]);
-      lds_rdtr<O>(tro[4 * DH + i], t.lo[4 + i]);
-      lds_rdtr<O + 16 * ROWB>(tro[4 * DH + i], t.hi[4 + i]);
-    }
-  };
 
   const int qt0 = (kb * KBW) / QB;
   if (dsrow && (qt0 & 1)) {  // causal zeros of the dQ kernel's 128-query block (see attn_bwd_dkdv_kernel)
@@ -2116,16 +2061,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int d = 0; d < 4; ++d) dp[A] = MFMA(r.f[d], vf[d], dp[A]);
     };
-    auto sdp = [&](auto a_c, RowBatch& r) {  // S, dP of sub-tile A: 8 MFMAs
-      constexpr int A = decltype(a_c)::value;
-      sv[A] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[A] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        sv[A] = MFMA(r.f[d], kf[d], sv[A]);
-        dp[A] = MFMA(r.f[4 + d], vf[d], dp[A]);
-      }
-    };
     auto softmax = [&](auto a_c, const f32x4& lq, const f32x4& dq4) {
       constexpr int A = decltype(a_c)::value;
       const f32x4 lq2 = lq * L2E;
@@ -2160,14 +2095,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
           dv[4 * DH + i] = MFMA(trp_join(t.lo[i], t.hi[i]), pb[U], dv[4 * DH + i]);
         else
           dk[4 * DH + i] = MFMA(trp_join(t.lo[i], t.hi[i]), sb[U], dk[4 * DH + i]);
-      }
-    };
-    auto dvdk = [&](auto u_c, auto dh_c, TrBatch& t) {  // 8 MFMAs
-      constexpr int U = decltype(u_c)::value, DH = decltype(dh_c)::value;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        dv[4 * DH + i] = MFMA(trp_join(t.lo[i], t.hi[i]), pb[U], dv[4 * DH + i]);
-        dk[4 * DH + i] = MFMA(trp_join(t.lo[4 + i], t.hi[4 + i]), sb[U], dk[4 * DH + i]);
       }
     };
     using I0 = std::integral_constant<int, 0>;
