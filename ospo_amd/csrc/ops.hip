@@ -179,7 +179,10 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_w_kernel(const bf16* __restri
   if (lane == 0) rstd[row] = r;
 }
 
-template <int IT, bool FULL>
+// EARLY (ablation build, OSPO_RMS_EARLY=1): the residual-grad loads issued with x and dy, before the dot (one
+// memory round trip per row instead of two; 154 against 150 VGPRs, both 3 waves per SIMD): bit-identical and
+// slower, 31.2 / 32.7 against 30.1 / 30.4 us at M 4800 x D 4096 (profiles/r06/rmsnorm_bwd_early_ab.log)
+template <int IT, bool FULL, bool EARLY = false>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                             const bf16* __restrict__ w, const float* __restrict__ rstd,
                                                             const bf16* __restrict__ dres, bf16* __restrict__ dx,
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
   const u32x4* wr = reinterpret_cast<const u32x4*>(w);
   const u32x4* rr = dres ? reinterpret_cast<const u32x4*>(dres + row * D) : nullptr;
   // x and dy (the dot's operands) first; the residual grad is loaded after the dot, so it does not
-  // hold IT more registers across it (160 -> ~110 VGPRs: 4 waves per SIMD instead of 3)
+  // hold IT more registers across it (round 2: 160 -> ~110 VGPRs; 150 on the round-6 compiler, 3 waves per SIMD)
   u32x4 xv[IT], dv[IT], rv[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -202,6 +205,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
     if (FULL || c < nch) {
       xv[it] = __builtin_nontemporal_load(xr + c);  // (read once: non-temporal)
       dv[it] = __builtin_nontemporal_load(dr + c);
+      if (EARLY && rr) rv[it] = __builtin_nontemporal_load(rr + c);
     }
   }
   float dot = 0.f;
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_w_kernel(const bf16* __restri
   }
   const float mdot = wave_sum(dot) / (float)D;
   asm volatile("" ::: "memory");  // the residual loads stay below the dot
-  if (rr) {
+  if (!EARLY && rr) {
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int c = it * 64 + lane;
@@ -843,6 +847,14 @@ static int rmsnorm_bwd_impl(const void* dy, const void* x, const void* w, const 
   const dim3 gw((M + 3) / 4);
   const bf16 *dyb = (const bf16*)dy, *xb = (const bf16*)x, *wb = (const bf16*)w, *rb = (const bf16*)dres;
   const long Ml = M;
+#ifdef OSPO_ABLATION
+  static const bool early = getenv("OSPO_RMS_EARLY") != nullptr;
+  if (D == 4096 && early) {
+    hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<8, true, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
+    OSPO_CHECK_LAUNCH();
+    return OSPO_OK;
+  }
+#endif
   if (D == 4096) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<8, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
   else if (D == 2048) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<4, true>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
   else if (it <= 1) hipLaunchKernelGGL((rmsnorm_bwd_w_kernel<1, false>), gw, dim3(256), 0, st, dyb, xb, wb, rstd, rb, (bf16*)dx, Ml, D, mo);
