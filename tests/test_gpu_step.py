@@ -277,20 +277,20 @@ def test_step_full_depth_7b_30_layers():
 BENCH_SEEDS_FIXTURE = "bench_config_seeds_oracle.npz"
 
 
-def bench_seed_runs():
-    """The HIP side of the 3-seed bench-config check: bench.simpo_setup's workload, the forward + SimPO loss of
-    the bench's batches 0, 1, 2.  Returns (runs, weights on the host, dims, dropout p, digest); a run is (text,
+def bench_seed_runs(n_seeds=3, **setup):
+    """The HIP side of the bench-config checks: bench.simpo_setup(**setup)'s workload, the forward + SimPO loss of
+    the bench's batches 0 .. n_seeds - 1.  Returns (runs, weights on the host, dims, dropout p, digest); a run is (text,
     chosen, rejected, HIP log-probs, HIP loss, the forward call index, M), digest the float64 sums and sums of
     squares of every weight and input (on the device), which pin the fixture to this exact workload."""
     import bench
     from ospo_amd.simpo import SimPOConfig, SimPOLossBuffers, simpo_forward
-    dims, eng, batches, w = bench.simpo_setup()
+    dims, eng, batches, w = bench.simpo_setup(**setup)
     dig = []
     for k in sorted(w):
         x = w[k].double()
         dig += [float(x.sum()), float((x * x).sum())]
     runs = []
-    for s in range(3):
+    for s in range(n_seeds):
         text, chosen, rejected = batches[s]
         dig += [float(t.double().sum()) for t in (text, chosen, rejected)]
         B = chosen.shape[0]
@@ -306,7 +306,7 @@ def bench_seed_runs():
     return runs, wc, dims, p, np.array(dig, dtype=np.float64)
 
 
-def bench_seed_oracle(runs, wc, dims, p, progress=print):
+def bench_seed_oracle(runs, wc, dims, p, progress=print, mx8=False):
     """The bf16 and fp32 oracles (forward + loss) of each run, with the HIP path's dropout masks replayed:
     {"r16": [3, 2B], "r32": [3, 2B], "loss16": [3], "loss32": [3], "call": [3], "M": [3]} (six 30-layer CPU
     passes, ~1-2 min each: progress() after each)."""
@@ -318,7 +318,7 @@ def bench_seed_oracle(runs, wc, dims, p, progress=print):
         masks = _LazyMasks(M, kin, 42, call, p)
         tl = _unpad(text)
         for dt, tag in ((torch.bfloat16, "16"), (torch.float32, "32")):
-            o = O.simpo_step(tl, ch, rj, wc, odims, dtype=dt, backward=False, dropout_masks=masks)
+            o = O.simpo_step(tl, ch, rj, wc, odims, dtype=dt, backward=False, dropout_masks=masks, mx8=mx8)
             out["r" + tag].append(torch.cat([o.chosen_logps, o.rejected_logps]).float().numpy())
             out["loss" + tag].append(float(o.loss))
             progress(f"bench config seed {s}: {'bf16' if tag == '16' else 'fp32'} oracle done")
@@ -387,6 +387,63 @@ def test_bench_config_three_seeds_vs_oracle(capsys):
     record_parity("bench_config_three_seeds_pooled", logp_hip_vs_fp32=d_hip, logp_oracle_bf16_vs_fp32=d_ora,
                   ratio=d_hip / d_ora)
     assert d_hip <= LOGP_NOISE_RATIO * d_ora, (d_hip, d_ora)
+
+
+BENCH_MX8_FIXTURE = "bench_mx8_r32_seed_oracle.npz"
+
+
+def _bench_mx8_30_layers(capsys):
+    """Config 5 at depth: the MXFP8 bench workload (``bench.py --linear-dtype mx8 --lora-r 32``: bench.simpo_setup
+    with MXFP8 decoder Linears, LoRA r = 32, dropout 0.05, 4 ragged pairs, all 30 layers), batch 0's forward +
+    SimPO loss, and the oracle's fp8 mode (oracle/mx8_ref.py quantizers) in bf16 and fp32 with the masks replayed:
+    the committed fixture tests/golden/bench_mx8_r32_seed_oracle.npz (tools/make_bench_seeds_fixture.py --mx8,
+    digest-pinned as the bf16 3-seed test's; recomputed live when the digest differs)."""
+    runs, wc, dims, p, dig = bench_seed_runs(n_seeds=1, lora_r=32, linear_dtype="mx8")
+    ref = None
+    if FX.exists(BENCH_MX8_FIXTURE):
+        z = FX.load(BENCH_MX8_FIXTURE)
+        if z["digest"].shape == dig.shape and np.allclose(z["digest"], dig, rtol=1e-12, atol=0):
+            ref = {k: z[k] for k in ("r16", "r32", "loss16", "loss32", "call", "M")}
+    if ref is None:
+        def progress(msg):
+            with capsys.disabled():
+                print(msg, flush=True)
+        progress("bench mx8 config: fixture digest differs or fixture absent, running the fp8 oracles")
+        ref = bench_seed_oracle(runs, wc, dims, p, progress, mx8=True)
+    text, ch, rj, logps, loss, call, M = runs[0]
+    assert int(ref["call"][0]) == call and int(ref["M"][0]) == M, (call, M)
+    r16, r32 = torch.from_numpy(ref["r16"][0]).float(), torch.from_numpy(ref["r32"][0]).float()
+    e16, e32, d_ora = rel(logps, r16), rel(logps, r32), rel(r16, r32)
+    record_parity("bench_mx8_r32_30_layers", logp_vs_mx8_bf16_oracle=e16, logp_vs_mx8_fp32_oracle=e32,
+                  mx8_oracle_bf16_vs_fp32=d_ora, ratio=e32 / d_ora, loss=loss, loss_mx8_bf16_oracle=float(ref["loss16"][0]),
+                  loss_mx8_fp32_oracle=float(ref["loss32"][0]), hip=logps.tolist(), oracle_bf16=r16.tolist(),
+                  oracle_fp32=r32.tolist())
+    print(f"\nbench mx8 r32 30 layers: logp rel err vs the fp8 oracle bf16 {e16:.2e} fp32 {e32:.2e} (oracle bf16 vs "
+          f"fp32 {d_ora:.2e}); loss {loss:.6f} vs {float(ref['loss16'][0]):.6f} / {float(ref['loss32'][0]):.6f}",
+          flush=True)
+    return logps, loss, ch.shape[0], r16, r32, e32, d_ora
+
+
+def test_bench_mx8_r32_30_layers_gross_errors(capsys):
+    """Config 5 at 30 layers (see _bench_mx8_30_layers): every log-prob within 1e-2 relative of both fp8 oracles
+    and the loss kernel within 1e-5 of the formula (the gross-error part of the criterion fixed before the run)."""
+    logps, loss, B, r16, r32, _, _ = _bench_mx8_30_layers(capsys)
+    assert abs(float(O.simpo_loss(logps[:B], logps[B:])[0].mean()) - loss) < 1e-5
+    assert (logps.float() - r16).abs().div(r16.abs()).max() < 1e-2
+    assert (logps.float() - r32).abs().div(r32.abs()).max() < 1e-2
+
+
+@pytest.mark.xfail(strict=True, reason="measured round 6 (DESIGN section 8): the HIP fp8 log-probs sit 2.06e-3 "
+                                       "from the fp32 fp8 oracle against the bf16 fp8 oracle's 1.43e-3 (1.44x > "
+                                       "1.25x); they sit 1.0e-3 from the bf16 fp8 oracle")
+def test_bench_mx8_r32_30_layers_noise_criterion(capsys):
+    """The bf16 gate's noise criterion applied to config 5, fixed before the run: the HIP log-probs no further from
+    the fp32 fp8 oracle than 1.25x the bf16 fp8 oracle's own distance from it.  It FAILS (1.44x) and is kept as
+    a strict xfail, not loosened: in the fp8 arithmetic the fp32 oracle quantizes unrounded activations, so its
+    fp8 codes differ from those of both bf16 paths (HIP and the bf16 oracle quantize bf16 activations alike), and
+    the fp32 oracle is not the common target it is in bf16."""
+    _, _, _, _, _, e32, d_ora = _bench_mx8_30_layers(capsys)
+    assert e32 <= LOGP_NOISE_RATIO * d_ora, (e32, d_ora)
 
 
 def test_step_7b_shapes_8_pairs_two_layers():
