@@ -5,7 +5,6 @@ in ``_lib``; there is no eager-PyTorch fallback on this path.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -360,14 +359,13 @@ def lora_da(x: torch.Tensor, s: torch.Tensor, out: torch.Tensor, *, s_cols: int,
     return out
 
 
-_DA_WGS_PER_CU = float(os.environ.get("OSPO_DA_WGS_PER_CU", "2"))  # A/B knob (tools/); the product default is 2
-
-
 def lora_da_splits(K: int, N: int, device=None) -> int:
-    """K-tile ranges per 128-column stripe of lora_da: ~2 workgroups per CU, >= 4 K-tiles each."""
+    """K-tile ranges per 128-column stripe of lora_da: ~2 workgroups per CU, >= 4 K-tiles each.  (Round 6, on
+    the side stream in the step: 1, 2 or 4 workgroups per CU within 0.1 % of each other over 4 alternating rounds,
+    profiles/r06/da_wgs_per_cu_ab.txt.)"""
     cus = torch.cuda.get_device_properties(device).multi_processor_count if torch.cuda.is_available() else 256
     stripes = max(1, N // 128)
-    return int(max(1, min(K // 64 // 4, round(_DA_WGS_PER_CU * cus / stripes))))
+    return int(max(1, min(K // 64 // 4, round(2 * cus / stripes))))
 
 
 def f32_to_bf16(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
