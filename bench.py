@@ -69,6 +69,7 @@ def simpo_setup(layers=30, lora_r=16, pairs=4, text_len=24, img_tokens=576, lora
                       da_stream=not (round2_lora or "da_tiles" in lora_variant), keep_bits=not round2_lora,
                       fuse_swiglu_u=not (round2_lora or "swiglu_unfused" in lora_variant),
                       fuse_swiglu_gdb=not (round2_lora or "swiglu_gdb_unfused" in lora_variant),
+                      fuse_gdb="gdb_unfused" not in lora_variant,
                       gdb_groups=("gu",) if "gdb_gu_only" in lora_variant else ("qkv", "o", "gu", "down"),
                       side_main=tuple(g for g in ("qkv", "o", "gu", "down") if f"main_{g}" in lora_variant))
     # each rank draws its own pairs (the DistributedSampler shard of the global batch)

@@ -36,8 +36,10 @@ const char* ospo_strerror(int status);
 /* ABI revision; bumped whenever a signature, a workspace layout or the dropout masks a seed produces change.
  * 2 (round 6): ospo_lora_gdb's partials sit behind a zero-at-allocation counter head (OSPO_WS_LORA_GDB), the
  * round-5 dropout hash (new masks for every seed), ospo_ws_counter_bytes and ospo_gemm_clock_probe_bf16.
+ * 3 (round 6): ospo_lora_gdb_r / ospo_swiglu_lora_gdb_r (LoRA rank 16 or 32; the rank-16 entry points are
+ * their r = 16 forms).
  * Bindings check it when they load the library (ospo_amd/_lib.py). */
-#define OSPO_ABI_VERSION 2
+#define OSPO_ABI_VERSION 3
 int ospo_abi_version(void);
 
 /* Box probe (measurement aid, no reference counterpart): C = A . B^T with the product's bf16 256 x 256 K loop,
@@ -383,6 +385,12 @@ size_t ospo_lora_gdb_ws_bytes(int M, int nmods, int Nmod);
 int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M, int M_out,
                   int nmods, int Nmod, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
                   size_t ws_bytes, hipStream_t stream);
+/* The same for LoRA rank r = 16 or 32 (round 6; configs/peft/lora.yaml ships r = 32): a module's r columns are
+ * r / 16 halves of 16 over the same dy columns -- Bt [nmods*r, Nmod], u [M, >= r*nmods], g columns r*j + c,
+ * dB [nmods*Nmod, r] -- and the workspace is ospo_lora_gdb_ws_bytes(M, nmods * r / 16, Nmod). */
+int ospo_lora_gdb_r(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M, int M_out,
+                    int nmods, int Nmod, int r, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
+                    size_t ws_bytes, hipStream_t stream);
 
 /* The SwiGLU backward fused with the gate|up group's g / dB (LoRA rank 16; the backward of
  * down_proj(act_fn(gate) * up) and of gate|up's peft adapters, ospo/wrapper/train.py:352):
@@ -393,6 +401,10 @@ int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* 
 int ospo_swiglu_lora_gdb(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu, const void* Bt,
                          int ldb, const void* u, int ldu, int M, int M_out, int F, float scale, void* out, int ldo,
                          int out_cols, float* dB, void* ws, size_t ws_bytes, hipStream_t stream);
+/* rank r = 16 or 32 (round 6): Bt [2r, F], u [M, >= 2r], out / ws / dB as ospo_lora_gdb_r with nmods = 2. */
+int ospo_swiglu_lora_gdb_r(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu, const void* Bt,
+                           int ldb, const void* u, int ldu, int M, int M_out, int F, int r, float scale, void* out,
+                           int ldo, int out_cols, float* dB, void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* ------------------------------------------------------------ MXFP8 variant ---
  * BASELINE config 5 / SURVEY §8f rank 1: the frozen Linears of the SimPO step

@@ -18,7 +18,7 @@ P, I, L, F, Z, U = c_void_p, c_int, c_long, c_float, c_size_t, c_uint
 
 # include/ospo_hip.h OSPO_ABI_VERSION: a library built from other sources (another workspace layout, other
 # dropout masks) is refused at load instead of silently mis-driven
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # name -> argtypes (restype is c_int = ospo_status unless listed in RESTYPES)
 SIGNATURES = {
@@ -70,8 +70,10 @@ SIGNATURES = {
     "ospo_simpo_bwd": [P, I, F, F, F, I, P, P, P],
     "ospo_lora_pack": [P, P, I, I, I, I, I, P, P, P, P, I, L, P],
     "ospo_lora_gdb": [P, I, P, I, P, I, I, I, I, I, F, P, I, I, P, P, Z, P],
+    "ospo_lora_gdb_r": [P, I, P, I, P, I, I, I, I, I, I, F, P, I, I, P, P, Z, P],
     "ospo_lora_gdb_ws_bytes": [I, I, I],
     "ospo_swiglu_lora_gdb": [P, I, P, I, P, I, P, I, P, I, I, I, I, F, P, I, I, P, P, Z, P],
+    "ospo_swiglu_lora_gdb_r": [P, I, P, I, P, I, P, I, P, I, I, I, I, I, F, P, I, I, P, P, Z, P],
     "ospo_lora_skinny": [P, I, P, I, I, I, I, I, I, I, I, F, P, I, I, P, Z, U, F, P, I, P, P],
     "ospo_lora_skinny_ws_bytes": [I, I, I],
     "ospo_decode_gemv_ws_bytes": [I, I, I],

@@ -664,7 +664,8 @@ template <int RSB, int NS = 4, int YA = 0, bool INL = false>  // YA: cache-polic
 __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ dy, int ldy, const bf16* __restrict__ Bt,
                                                        int ldb, const bf16* __restrict__ u, int ldu, int M, int Nmod,
                                                        int nch, float* __restrict__ ws, int Mw,
-                                                       float* __restrict__ dB, const GdbInl inl = GdbInl{}) {
+                                                       float* __restrict__ dB, const GdbInl inl = GdbInl{},
+                                                       int hpm = 1) {
   // NS-stage ring of 8-KiB dy sub-tiles, NS - 1 in flight (a 6-stage ring measured 10-30 % slower)
   constexpr int STAGE = 8192;
   constexpr int BT_OFF = NS * STAGE, BT_BYTES = 16 * 4 * 128;  // up to nch = 4
@@ -676,9 +677,12 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
   const int l16 = lane & 15, g = lane >> 4, r8 = lane >> 3, c8 = lane & 7;
   const int rb0 = blockIdx.x * ROWS;
   const int nsplit = Nmod / (64 * nch);
+  // mod: a 16-column half of a module (LoRA r = 16 hpm): module mod / hpm of dy, rows 16 mod of Bt, columns
+  // 16 mod of u and g, columns 16 (mod % hpm) of the module's [Nmod][r] dB block
   const int mod = blockIdx.y / nsplit, sp = blockIdx.y % nsplit;
-  const int kc0 = sp * 64 * nch;             // first column of the workgroup within its module
-  const long col0 = (long)mod * Nmod + kc0;  // ... within dy
+  const int kc0 = sp * 64 * nch;                     // first column of the workgroup within its module
+  const long col0 = (long)(mod / hpm) * Nmod + kc0;  // ... within dy
+  const int rdb = 16 * hpm, cdb = 16 * (mod % hpm);  // dB row stride (r) and this half's first column
   const int btrow = nch * 128;               // bytes per Bt image row
 
   // Bt image [16 j][nch*64 k]: 16-B chunk q of row j at physical chunk q ^ j (source-side swizzle)
@@ -773,7 +777,7 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
       if (rb == RSB - 1 && !(INL && cc == nch - 1)) {  // the chunk's dB over the workgroup's rows
         const long n0 = col0 + cc * 64 + 16 * wave + 4 * g;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[i]);
+        for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * rdb + cdb + l16, accb[i]);
         accb = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
@@ -799,7 +803,7 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
     {  // the last chunk's dB atomics after the partial stores: the wait below leaves them in flight
       const long n0 = col0 + (nch - 1) * 64 + 16 * wave + 4 * g;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[i]);
+      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * rdb + cdb + l16, accb[i]);
     }
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this lane's partial stores acknowledged
     __syncthreads();
@@ -867,7 +871,9 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
 // to the f32 atomics' order) to ospo_swiglu_bwd + ospo_lora_gdb.
 // LAUX / SAUX: cache-policy bits of the input loads / dgu stores.  DBG (measurement only): 1 no MFMA phase,
 // 2 no dgu stores.
-template <int RSB, int PF, int NCH, int DBG = 0, int LAUX = 2, int SAUX = 16>
+// HPM (round 6): 16-column halves per module (LoRA r = 16 HPM): 2 HPM Bt / u images and accumulator sets, the
+// dB block of a module [F][16 HPM]
+template <int RSB, int PF, int NCH, int DBG = 0, int LAUX = 2, int SAUX = 16, int HPM = 1>
 __global__ __launch_bounds__(256) void swiglu_gdb_kernel(const bf16* __restrict__ dh, int lddh,
                                                          const bf16* __restrict__ gu, int ldg, bf16* __restrict__ dgu,
                                                          int lddg, const bf16* __restrict__ Bt, int ldb,
@@ -876,10 +882,11 @@ __global__ __launch_bounds__(256) void swiglu_gdb_kernel(const bf16* __restrict_
   static_assert(NCH % PF == 0, "the prefetch slot must be a compile-time index");
   constexpr int nch = NCH;
   constexpr int TILE = 8192;  // a 64 x 64 bf16 image; [dgate | dup] at 0 and TILE
-  constexpr int BT_OFF = 2 * TILE, BT_BYTES = 16 * 4 * 128;  // per module, up to nch = 4
+  constexpr int NV = 2 * HPM;  // 16-column halves of the two modules
+  constexpr int BT_OFF = 2 * TILE, BT_BYTES = 16 * 4 * 128;  // per half, up to nch = 4
   constexpr int ROWS = 64 * RSB;
-  constexpr int U_OFF = BT_OFF + 2 * BT_BYTES;  // per module ROWS * 32 B
-  __shared__ __attribute__((aligned(16))) char smem[U_OFF + 2 * ROWS * 32];
+  constexpr int U_OFF = BT_OFF + NV * BT_BYTES;  // per half ROWS * 32 B
+  __shared__ __attribute__((aligned(16))) char smem[U_OFF + NV * ROWS * 32];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l16 = lane & 15, g = lane >> 4;
@@ -893,9 +900,9 @@ __global__ __launch_bounds__(256) void swiglu_gdb_kernel(const bf16* __restrict_
   // the compiler's vmcnt tracking of the register prefetch below stays exact.  All loads first, then the writes.
   {
     const int off = lane * 16, rpp = 1024 / btrow;
-    u32x4 bv[2][2], uv[ROWS / 32 / 2];
+    u32x4 bv[NV][2], uv[NV * ROWS / 32 / 4];
 #pragma unroll
-    for (int mod = 0; mod < 2; ++mod)
+    for (int mod = 0; mod < NV; ++mod)
 #pragma unroll
       for (int k = 0; k < 2; ++k) {  // pieces p = wave + 4k < 2 nch (nch = 2: k = 0 only)
         const int p = min(wave + 4 * k, 2 * nch - 1);
@@ -903,19 +910,19 @@ __global__ __launch_bounds__(256) void swiglu_gdb_kernel(const bf16* __restrict_
         bv[mod][k] = *reinterpret_cast<const u32x4*>(Bt + (long)(mod * 16 + j) * ldb + kc0 + (pc ^ j) * 8);
       }
 #pragma unroll
-    for (int k = 0; k < ROWS / 32 / 2; ++k) {  // pieces p = wave + 4k of the two modules' u images
+    for (int k = 0; k < NV * ROWS / 32 / 4; ++k) {  // pieces p = wave + 4k of the halves' u images
       const int p = wave + 4 * k, mod = p / (ROWS / 32), pp = p % (ROWS / 32);
       const int row = min(rb0 + pp * 32 + (lane >> 1), M - 1);
       uv[k] = *reinterpret_cast<const u32x4*>(u + (long)row * ldu + mod * 16 + (lane & 1) * 8);
     }
 #pragma unroll
-    for (int mod = 0; mod < 2; ++mod)
+    for (int mod = 0; mod < NV; ++mod)
 #pragma unroll
       for (int k = 0; k < 2; ++k)
         if (wave + 4 * k < 2 * nch)
           *reinterpret_cast<u32x4*>(smem + BT_OFF + mod * BT_BYTES + (wave + 4 * k) * 1024 + off) = bv[mod][k];
 #pragma unroll
-    for (int k = 0; k < ROWS / 32 / 2; ++k) {
+    for (int k = 0; k < NV * ROWS / 32 / 4; ++k) {
       const int p = wave + 4 * k, mod = p / (ROWS / 32), pp = p % (ROWS / 32);
       *reinterpret_cast<u32x4*>(smem + U_OFF + mod * ROWS * 32 + pp * 1024 + off) = uv[k];
     }
@@ -948,13 +955,17 @@ __global__ __launch_bounds__(256) void swiglu_gdb_kernel(const bf16* __restrict_
 #pragma unroll
   for (int s = 0; s < PF - 1; ++s) load(s, in[s]);
 
-  f32x4 accb[2][NCH];
+  f32x4 accb[NV][NCH];
 #pragma unroll
-  for (int cc = 0; cc < NCH; ++cc) accb[0][cc] = accb[1][cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int mod = 0; mod < NV; ++mod)
+#pragma unroll
+    for (int cc = 0; cc < NCH; ++cc) accb[mod][cc] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int li = l16, q4 = li >> 2, p4 = li & 3;
   const int grow = 16 * wave + l16;
   for (int rb = 0; rb < RSB; ++rb) {
-    f32x4 accg[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 accg[NV];
+#pragma unroll
+    for (int mod = 0; mod < NV; ++mod) accg[mod] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int cc = 0; cc < NCH; ++cc) {
       const int t = rb * NCH + cc;
@@ -985,8 +996,8 @@ __global__ __launch_bounds__(256) void swiglu_gdb_kernel(const bf16* __restrict_
       __builtin_amdgcn_s_barrier();  // both images complete
       asm volatile("" ::: "memory");
 #pragma unroll
-      for (int mod = 0; mod < 2; ++mod) {
-        const char* st = smem + mod * TILE;
+      for (int mod = 0; mod < NV; ++mod) {
+        const char* st = smem + (mod / HPM) * TILE;  // dgate (halves 0 .. HPM - 1) or dup
         const char* bts = smem + BT_OFF + mod * BT_BYTES;
         const char* us = smem + U_OFF + mod * ROWS * 32;
 #pragma unroll
@@ -1013,18 +1024,18 @@ __global__ __launch_bounds__(256) void swiglu_gdb_kernel(const bf16* __restrict_
         }
       }
     }
-    const int m = rb0 + rb * 64 + grow;  // g partials of this row sub-block: ws [mod][sp][Mw][16]
+    const int m = rb0 + rb * 64 + grow;  // g partials of this row sub-block: ws [half][sp][Mw][16]
 #pragma unroll
-    for (int mod = 0; mod < 2; ++mod)
+    for (int mod = 0; mod < NV; ++mod)
       if (m < Mw) *reinterpret_cast<f32x4*>(ws + (((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[mod];
   }
 #pragma unroll
-  for (int mod = 0; mod < 2; ++mod)
+  for (int mod = 0; mod < NV; ++mod)
 #pragma unroll
     for (int cc = 0; cc < NCH; ++cc) {  // each chunk's dB over the workgroup's rows
-      const long n0 = (long)mod * F + kc0 + cc * 64 + 16 * wave + 4 * g;
+      const long n0 = (long)(mod / HPM) * F + kc0 + cc * 64 + 16 * wave + 4 * g;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[mod][cc][i]);
+      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * (16 * HPM) + 16 * (mod % HPM) + l16, accb[mod][cc][i]);
     }
 }
 
@@ -1618,22 +1629,24 @@ static long gdb_inl_capacity() {
 }
 #endif
 
-extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M, int M_out,
-                             int nmods, int Nmod, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
-                             size_t ws_bytes, hipStream_t stream) {
+extern "C" int ospo_lora_gdb_r(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M,
+                               int M_out, int nmods, int Nmod, int r, float scale, void* out, int ldo, int out_cols,
+                               float* dB, void* ws, size_t ws_bytes, hipStream_t stream) {
   if (!dy || !Bt || !u || !out || !dB || !ws) return OSPO_ERR_ARG;
+  if (r != 16 && r != 32) return OSPO_ERR_UNSUPPORTED;
+  const int hpm = r / 16, vm = nmods * hpm;  // 16-column halves: the kernel's "modules"
   if (M <= 0 || M_out < M || nmods < 1 || nmods > 4 || Nmod <= 0 || Nmod % 128) return OSPO_ERR_SHAPE;
-  if (ldy < nmods * Nmod || ldb < Nmod || ldu < 16 * nmods || ldo < out_cols || out_cols < 16 * nmods ||
+  if (ldy < nmods * Nmod || ldb < Nmod || ldu < 16 * vm || ldo < out_cols || out_cols < 16 * vm ||
       out_cols % 4 || ldy % 8 || ldb % 8 || ldu % 8 || ldo % 4)
     return OSPO_ERR_SHAPE;
-  if (ws_bytes < ospo_lora_gdb_ws_bytes(M, nmods, Nmod)) return OSPO_ERR_SHAPE;
+  if (ws_bytes < ospo_lora_gdb_ws_bytes(M, vm, Nmod)) return OSPO_ERR_SHAPE;
   if (!aligned16(dy) || !aligned16(Bt) || !aligned16(u) || !aligned16(ws) || ((uintptr_t)dB & 3) ||
       ((uintptr_t)out & 7))
     return OSPO_ERR_ALIGN;
-  const int nch = gdb_nch(M, nmods, Nmod);
+  const int nch = gdb_nch(M, vm, Nmod);
   const int nsplit = Nmod / (64 * nch);
   const int Mw = (M + 63) / 64 * 64;
-  const dim3 grid((M + 511) / 512, nmods * nsplit);
+  const dim3 grid((M + 511) / 512, vm * nsplit);
   float* part = (float*)((char*)ws + GDB_CNT_BYTES);
   // A/B (ablation build, OSPO_GDB_INL=1): the partials summed inside the launch where the whole grid fits on the
   // device at once -- bit-identical, and no faster in the step (36.44 / 36.37 against 36.47 / 36.37 pairs/s,
@@ -1646,7 +1659,7 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   if (inl) {
     const GdbInl gi{(unsigned*)ws, M_out, scale, (bf16*)out, ldo, out_cols};
     hipLaunchKernelGGL((lora_gdb_kernel<8, 4, 0, true>), grid, dim3(256), 0, stream, (const bf16*)dy, ldy,
-                       (const bf16*)Bt, ldb, (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, gi);
+                       (const bf16*)Bt, ldb, (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, gi, hpm);
     OSPO_CHECK_LAUNCH();
     return OSPO_OK;
   }
@@ -1660,40 +1673,53 @@ extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, c
   const long n = (long)M_out * (out_cols / 4);
   if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
   hipLaunchKernelGGL(kfn, grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
-                     (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, GdbInl{});
+                     (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, GdbInl{}, hpm);
   OSPO_CHECK_LAUNCH();
   hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part,
-                     nmods, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
+                     vm, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
 }
 
-extern "C" int ospo_swiglu_lora_gdb(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu,
-                                    const void* Bt, int ldb, const void* u, int ldu, int M, int M_out, int F,
-                                    float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
-                                    size_t ws_bytes, hipStream_t stream) {
+extern "C" int ospo_lora_gdb(const void* dy, int ldy, const void* Bt, int ldb, const void* u, int ldu, int M, int M_out,
+                             int nmods, int Nmod, float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
+                             size_t ws_bytes, hipStream_t stream) {
+  return ospo_lora_gdb_r(dy, ldy, Bt, ldb, u, ldu, M, M_out, nmods, Nmod, 16, scale, out, ldo, out_cols, dB, ws,
+                         ws_bytes, stream);
+}
+
+extern "C" int ospo_swiglu_lora_gdb_r(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu,
+                                      const void* Bt, int ldb, const void* u, int ldu, int M, int M_out, int F, int r,
+                                      float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
+                                      size_t ws_bytes, hipStream_t stream) {
   if (!dh || !gu || !dgu || !Bt || !u || !out || !dB || !ws) return OSPO_ERR_ARG;
+  if (r != 16 && r != 32) return OSPO_ERR_UNSUPPORTED;
+  const int hpm = r / 16, vm = 2 * hpm;
   if (M <= 0 || M_out < M || F <= 0 || F % 128) return OSPO_ERR_SHAPE;
-  if (ld_dh < F || ld_gu < 2 * F || ld_dgu < 2 * F || ldb < F || ldu < 32 || ldo < out_cols || out_cols < 32 ||
-      out_cols % 4 || ld_dh % 8 || ld_gu % 8 || ld_dgu % 8 || ldb % 8 || ldu % 8 || ldo % 4)
+  if (ld_dh < F || ld_gu < 2 * F || ld_dgu < 2 * F || ldb < F || ldu < 16 * vm || ldo < out_cols ||
+      out_cols < 16 * vm || out_cols % 4 || ld_dh % 8 || ld_gu % 8 || ld_dgu % 8 || ldb % 8 || ldu % 8 || ldo % 4)
     return OSPO_ERR_SHAPE;
-  if (ws_bytes < ospo_lora_gdb_ws_bytes(M, 2, F)) return OSPO_ERR_SHAPE;
+  if (ws_bytes < ospo_lora_gdb_ws_bytes(M, vm, F)) return OSPO_ERR_SHAPE;
   if (!aligned16(dh) || !aligned16(gu) || !aligned16(dgu) || !aligned16(Bt) || !aligned16(u) || !aligned16(ws) ||
       ((uintptr_t)dB & 3) || ((uintptr_t)out & 7))
     return OSPO_ERR_ALIGN;
   const long Mr = (long)(M + 511) / 512 * 512;  // rows the grid addresses (clamped by the ranges, not the offsets)
   if (Mr * ld_dgu * 2 >= (1L << 31) || Mr * ld_gu * 2 >= (1L << 31) || Mr * ld_dh * 2 >= (1L << 31))
     return OSPO_ERR_UNSUPPORTED;  // the buffer ranges / offsets (32-bit)
-  const int nch = gdb_nch(M, 2, F);  // as ospo_lora_gdb on dgu: the same partials
+  const int nch = gdb_nch(M, vm, F);  // as ospo_lora_gdb_r on dgu: the same partials
   const int nsplit = F / (64 * nch);
   const int Mw = (M + 63) / 64 * 64;
   // one sub-tile of prefetch, non-temporal input loads (gu, dh are dead after this pass) and sc1 dgu stores:
   // 103.6 us at the step shape against 125.0 with default policies and 150 for the two launches
   // (profiles/r04/swiglu_gdb_variants.log)
   auto kfn = nch == 4 ? swiglu_gdb_kernel<8, 2, 4> : swiglu_gdb_kernel<8, 2, 2>;
-  const int rows = 512;
+  int rows = 512;
+  if (hpm == 2) {  // r = 32: four halves' Bt / u images; 256-row workgroups keep two per CU (80 KiB of LDS)
+    kfn = nch == 4 ? swiglu_gdb_kernel<4, 2, 4, 0, 2, 16, 2> : swiglu_gdb_kernel<4, 2, 2, 0, 2, 16, 2>;
+    rows = 256;
+  }
 #ifdef OSPO_ABLATION
-  if (const char* e = getenv("OSPO_SWGDB")) {  // A/B: prefetch depth, cache policies, phases removed
+  if (const char* e = getenv("OSPO_SWGDB"); e && hpm == 1) {  // A/B: prefetch depth, cache policies, phases removed
     const int v = atoi(e);
     if (nch == 4) {
       if (v == 1) kfn = swiglu_gdb_kernel<8, 2, 4, 0, 0, 0>;
@@ -1714,10 +1740,18 @@ extern "C" int ospo_swiglu_lora_gdb(const void* dh, int ld_dh, const void* gu, i
                      (const bf16*)dh, ld_dh, (const bf16*)gu, ld_gu, (bf16*)dgu, ld_dgu, (const bf16*)Bt, ldb,
                      (const bf16*)u, ldu, M, F, part, Mw, dB);
   OSPO_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part, 2,
+  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part, vm,
                      nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
+}
+
+extern "C" int ospo_swiglu_lora_gdb(const void* dh, int ld_dh, const void* gu, int ld_gu, void* dgu, int ld_dgu,
+                                    const void* Bt, int ldb, const void* u, int ldu, int M, int M_out, int F,
+                                    float scale, void* out, int ldo, int out_cols, float* dB, void* ws,
+                                    size_t ws_bytes, hipStream_t stream) {
+  return ospo_swiglu_lora_gdb_r(dh, ld_dh, gu, ld_gu, dgu, ld_dgu, Bt, ldb, u, ldu, M, M_out, F, 16, scale, out, ldo,
+                                out_cols, dB, ws, ws_bytes, stream);
 }
 
 // dA of one adapter group (lora_da_kernel): C [s_cols][N] fp32 += S^T . dropout(X) over K = nt * 64 rows.

@@ -157,9 +157,10 @@ class SimPOEngine:
                     torch.zeros(max(L, 1), g.nmods * r, g.Nmod, dtype=BF16, device=dev))
             for gname, g in self.layout.groups.items()}
         self.packed = [{gname: tuple(t[i] for t in ts) for gname, ts in self._packed_all.items()} for i in range(L)]
-        # fuse_gdb (LoRA r = 16): g = s dy.B and dB += dy^T u of a group in one stream over dy on the main stream
-        # (ospo_lora_gdb); the side stream then runs only dA.  Off: g on the main stream, dB with dA on the side.
-        self.fuse_gdb = bool(fuse_gdb) and dims.lora_r == 16
+        # fuse_gdb (LoRA r = 16, or 32 since round 6): g = s dy.B and dB += dy^T u of a group in one stream over dy
+        # on the main stream (ospo_lora_gdb_r); the side stream then runs only dA.  Off: g on the main stream, dB with
+        # dA on the side.
+        self.fuse_gdb = bool(fuse_gdb) and dims.lora_r in (16, 32)
         # fuse_swiglu_gdb (with fuse_gdb, bf16): the SwiGLU backward and the gate|up group's g / dB in one stream
         # over (dh, gu) -- dgu written once, never read back by a separate g / dB pass (ospo_swiglu_lora_gdb)
         self.fuse_swiglu_gdb = bool(fuse_swiglu_gdb) and self.fuse_gdb
@@ -262,11 +263,11 @@ class SimPOEngine:
         self.ds_ws = ops.flash_attn_bwd_ws(S, Tm, H, dev)
         self.dz = z(R, Dg)
         self.dhsel = z(R, D)
-        # fp32 g partials of the fused g / dB stream (ospo_lora_gdb, r = 16), sized once for the capacity
+        # fp32 g partials of the fused g / dB stream (ospo_lora_gdb_r), sized once for the capacity
         # (the size grows with the rows); every group's call fits
         self._gdb_ws = None
         if self.fuse_gdb:
-            nb = max((int(ops.query_gdb_ws(Mc, g.nmods, g.Nmod)) for g in self.layout.groups.values()
+            nb = max((ops.query_gdb_ws(Mc, g.nmods, g.Nmod, dims.lora_r) for g in self.layout.groups.values()
                       if g.Nmod % 128 == 0 and g.nmods <= 4), default=0)
             if nb > 0:
                 self._gdb_ws = torch.zeros((nb + 15) // 16 * 4, dtype=F32, device=dev)  # (counters: zero)
@@ -377,27 +378,28 @@ class SimPOEngine:
         """(g_s, dB done): with fuse_gdb, g_s = bf16(scale * dy . Bcat) and dB += dy^T . u in one stream over dy
         (ospo_lora_gdb); else _lora_g and the side stream computes dB."""
         r = self.layout.r
-        if not (self.fuse_gdb and g.name in self.gdb_groups and self._gdb_ws is not None and r == 16
-                and g.Nmod % 128 == 0 and g.nmods <= 4):
+        if not (self.fuse_gdb and g.name in self.gdb_groups and self._gdb_ws is not None and r in (16, 32)
+                and g.Nmod % 128 == 0 and g.nmods <= 4 and g.nmods * r <= g.Rp):
             return self._lora_g(dy, g, Bcat, BT, M, par), False
         out = self.gsc2[g.name][par]
         b_off = gbase + g.b_off
         dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
-        ops.lora_gdb(dy, BT, u, out, dB, M, self.Mk, g.nmods, g.Nmod, self.scale, ws=self._gdb_ws)
+        ops.lora_gdb(dy, BT, u, out, dB, M, self.Mk, g.nmods, g.Nmod, self.scale, ws=self._gdb_ws, r=r)
         return out, True
 
     def _swiglu_g_db(self, g, M, par, a, dgu, gbase, BT):
         """dgu = swiglu_bwd(dh, gu) with the gate|up group's g_s and dB in one stream (ospo_swiglu_lora_gdb);
         None when the shapes do not fit it (the caller then runs swiglu_bwd and _lora_g_db)."""
         r = self.layout.r
-        if not (self.fuse_swiglu_gdb and self._gdb_ws is not None and r == 16 and g.nmods == 2
+        if not (self.fuse_swiglu_gdb and self._gdb_ws is not None and r in (16, 32) and g.nmods == 2
                 and g.Nmod % 128 == 0 and self.dh is not None and self._mxo(2 * g.Nmod) is None
                 and dgu.shape[0] * dgu.stride(0) * 2 < 2 ** 31):
             return None
         out = self.gsc2[g.name][par]
         b_off = gbase + g.b_off
         dB = self.grads[b_off: b_off + g.nmods * g.Nmod * r].view(g.nmods * g.Nmod, r)
-        ops.swiglu_lora_gdb(self.dh, a["gu"], dgu, BT, a["u_gu"], out, dB, M, self.Mk, self.scale, ws=self._gdb_ws)
+        ops.swiglu_lora_gdb(self.dh, a["gu"], dgu, BT, a["u_gu"], out, dB, M, self.Mk, self.scale, ws=self._gdb_ws,
+                            r=r)
         return out
 
     def _lora_g(self, dy, g, Bcat, BT, M, par=0):

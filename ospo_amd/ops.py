@@ -627,39 +627,40 @@ def swiglu_fwd_lora_down(gu, h, bt, out, M, M_out, F, n_tiles, scale=1.0, b_rows
          ws.numel() * ws.element_size(), int(seed) & 0xFFFFFFFF, float(p), _p(keep_bits), _s())
 
 
-def query_gdb_ws(M, nmods, Nmod) -> int:
-    return int(query("ospo_lora_gdb_ws_bytes", M, nmods, Nmod))
+def query_gdb_ws(M, nmods, Nmod, r=16) -> int:
+    """Bytes of ospo_lora_gdb_r's workspace (a module's r columns are r / 16 halves of 16)."""
+    return int(query("ospo_lora_gdb_ws_bytes", M, nmods * (r // 16), Nmod))
 
 
-def lora_gdb_ws(M, nmods, Nmod, device="cuda") -> torch.Tensor:
-    """Workspace for ospo_lora_gdb: its row-block counters (zero at allocation, left zero) and the fp32 partials
+def lora_gdb_ws(M, nmods, Nmod, device="cuda", r=16) -> torch.Tensor:
+    """Workspace for ospo_lora_gdb_r: its row-block counters (zero at allocation, left zero) and the fp32 partials
     of g."""
-    n = int(query("ospo_lora_gdb_ws_bytes", M, nmods, Nmod))
+    n = query_gdb_ws(M, nmods, Nmod, r)
     return torch.zeros((n + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
-def lora_gdb(dy, bt, u, out, dB, M, M_out, nmods, Nmod, scale, ws=None):
-    """One stream over dy (LoRA r = 16): out[:M_out] (bf16) = scale * dy . B (block diagonal, as
-    lora_skinny's g; rows M.. and columns 16*nmods.. zero) and dB [nmods*Nmod, 16] (fp32) += dy^T . u."""
+def lora_gdb(dy, bt, u, out, dB, M, M_out, nmods, Nmod, scale, ws=None, r=16):
+    """One stream over dy (LoRA r = 16 or 32): out[:M_out] (bf16) = scale * dy . B (block diagonal, as
+    lora_skinny's g; rows M.. and columns r*nmods.. zero) and dB [nmods*Nmod, r] (fp32) += dy^T . u."""
     _chk(dB, torch.float32, "dB")
     if ws is None:
-        ws = lora_gdb_ws(M, nmods, Nmod, dy.device)
-    call("ospo_lora_gdb", _p(dy), _ld(dy), _p(bt), _ld(bt), _p(u), _ld(u), M, M_out, nmods, Nmod, float(scale),
-         _p(out), _ld(out), out.shape[1], _p(dB), _p(ws), ws.numel() * ws.element_size(), _s())
+        ws = lora_gdb_ws(M, nmods, Nmod, dy.device, r)
+    call("ospo_lora_gdb_r", _p(dy), _ld(dy), _p(bt), _ld(bt), _p(u), _ld(u), M, M_out, nmods, Nmod, int(r),
+         float(scale), _p(out), _ld(out), out.shape[1], _p(dB), _p(ws), ws.numel() * ws.element_size(), _s())
 
 
-def swiglu_lora_gdb(dh, gu, dgu, bt, u, out, dB, M, M_out, scale, ws=None):
-    """dgu[:M] = swiglu_bwd(dh, gu) and lora_gdb(dgu, nmods=2, Nmod=F) in one stream over (dh, gu)
-    (ospo_swiglu_lora_gdb; same bits as swiglu_bwd + lora_gdb)."""
+def swiglu_lora_gdb(dh, gu, dgu, bt, u, out, dB, M, M_out, scale, ws=None, r=16):
+    """dgu[:M] = swiglu_bwd(dh, gu) and lora_gdb(dgu, nmods=2, Nmod=F, r) in one stream over (dh, gu)
+    (ospo_swiglu_lora_gdb_r; same bits as swiglu_bwd + lora_gdb)."""
     _chk(dB, torch.float32, "dB")
     F = dh.shape[1]
     if gu.shape[1] < 2 * F or dgu.shape[1] < 2 * F:
         raise ValueError(f"swiglu_lora_gdb: gu/dgu need 2F = {2 * F} columns")
     if ws is None:
-        ws = lora_gdb_ws(M, 2, F, dh.device)
-    call("ospo_swiglu_lora_gdb", _p(dh), _ld(dh), _p(gu), _ld(gu), _p(dgu), _ld(dgu), _p(bt), _ld(bt), _p(u), _ld(u),
-         M, M_out, F, float(scale), _p(out), _ld(out), out.shape[1], _p(dB), _p(ws), ws.numel() * ws.element_size(),
-         _s())
+        ws = lora_gdb_ws(M, 2, F, dh.device, r)
+    call("ospo_swiglu_lora_gdb_r", _p(dh), _ld(dh), _p(gu), _ld(gu), _p(dgu), _ld(dgu), _p(bt), _ld(bt), _p(u),
+         _ld(u), M, M_out, F, int(r), float(scale), _p(out), _ld(out), out.shape[1], _p(dB), _p(ws),
+         ws.numel() * ws.element_size(), _s())
 
 
 # -------------------------------------------------------------- optimizer

@@ -42,7 +42,7 @@ def test_library_exports_every_header_symbol(lib):
 
 def test_abi_version_and_strerror(lib):
     from ospo_amd import _lib
-    assert lib.ospo_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.ospo_abi_version() == _lib.ABI_VERSION == 3
     assert lib.ospo_strerror(1) == b"shape / leading-dimension violation"
 
 
@@ -78,7 +78,7 @@ def test_abi_version_mismatch_is_refused(monkeypatch):
     monkeypatch.setattr(_lib, "ABI_VERSION", 999)
     with pytest.raises(_lib.OspoError, match="ABI version"):
         _lib.lib()
-    monkeypatch.setattr(_lib, "ABI_VERSION", 2)
+    monkeypatch.setattr(_lib, "ABI_VERSION", 3)
     monkeypatch.setattr(_lib, "_lib", None)
     _lib.lib()
 

@@ -704,7 +704,18 @@ def test_gemm_dropout_keep_bits_equal_rehash(M, N, K, K2, split):
 def test_lora_gdb_exact_integers(M, M_out, nm, Nmod):
     """The fused g = s dy.B / dB += dy^T u stream: exact on small integers against the two products
     it replaces (block diagonal over the modules; rows >= M of u and dy ignored, g rows M.. zeroed)."""
-    r = 16
+    _lora_gdb_exact(M, M_out, nm, Nmod, 16)
+
+
+@pytest.mark.parametrize("M,M_out,nm,Nmod", [(4800, 4864, 3, 4096), (4800, 4864, 1, 4096), (640, 704, 1, 11008),
+                                            (1000, 1100, 2, 1024)])
+def test_lora_gdb_rank32_exact_integers(M, M_out, nm, Nmod):
+    """Round 6, LoRA r = 32 (ospo_lora_gdb_r: a module's 32 columns are two halves of 16 over the same dy
+    columns, dB [nmods*Nmod, 32]): exact on small integers as the r = 16 form."""
+    _lora_gdb_exact(M, M_out, nm, Nmod, 32)
+
+
+def _lora_gdb_exact(M, M_out, nm, Nmod, r):
     dy = ints(M_out, nm * Nmod, lo=-2, hi=3)
     BT = ints(nm * r, Nmod, lo=-2, hi=3)
     Rp = 64 if nm * r <= 64 else 128
@@ -712,7 +723,7 @@ def test_lora_gdb_exact_integers(M, M_out, nm, Nmod):
     u[M:] = 99.0  # rows past M must not contribute
     out = torch.full((M_out, Rp), 7.0, device=DEV, dtype=torch.bfloat16)
     dB = torch.ones(nm * Nmod, r, device=DEV, dtype=torch.float32)  # accumulates onto what is there
-    ops().lora_gdb(dy, BT, u, out, dB, M, M_out, nm, Nmod, 1.0)
+    ops().lora_gdb(dy, BT, u, out, dB, M, M_out, nm, Nmod, 1.0, r=r)
     dyd, Bd, ud = dy[:M].double(), BT.double(), u[:M].double()
     g_ref = torch.cat([dyd[:, j * Nmod:(j + 1) * Nmod] @ Bd[j * r:(j + 1) * r].T for j in range(nm)], 1)
     assert torch.equal(out[:M, : nm * r].float(), bf(g_ref.float()).float())
@@ -754,25 +765,35 @@ def test_lora_gdb_in_launch_sum(M, M_out, nm, Nmod):
 def test_swiglu_lora_gdb_equals_two_launches(M, M_out, F):
     """ospo_swiglu_lora_gdb == ospo_swiglu_bwd then ospo_lora_gdb (nmods 2, Nmod F): dgu and g bit-equal (rows
     >= M of dgu untouched), dB equal up to the f32 atomics' order and against fp64."""
-    r = 16
+    _swiglu_lora_gdb_vs_two(M, M_out, F, 16)
+
+
+@pytest.mark.parametrize("M,M_out,F", [(4800, 4864, 11008), (700, 768, 1024), (100, 128, 512)])
+def test_swiglu_lora_gdb_rank32_equals_two_launches(M, M_out, F):
+    """Round 6, LoRA r = 32 (ospo_swiglu_lora_gdb_r, 256-row workgroups with four halves' images): as the
+    r = 16 form against ospo_swiglu_bwd + ospo_lora_gdb_r."""
+    _swiglu_lora_gdb_vs_two(M, M_out, F, 32)
+
+
+def _swiglu_lora_gdb_vs_two(M, M_out, F, r):
     dh, gu = rnd(M_out, F), rnd(M_out, 2 * F, s=3.0)
     BT, u = rnd(2 * r, F), rnd(M_out, 64)
     dgu_ref = torch.full((M_out, 2 * F), 5.0, device=DEV, dtype=torch.bfloat16)
     out_ref = torch.full((M_out, 64), 7.0, device=DEV, dtype=torch.bfloat16)
     dB_ref = torch.zeros(2 * F, r, device=DEV)
     ops().swiglu_bwd(dh[:M], gu[:M], dgu_ref[:M])
-    ops().lora_gdb(dgu_ref, BT, u, out_ref, dB_ref, M, M_out, 2, F, 0.75)
+    ops().lora_gdb(dgu_ref, BT, u, out_ref, dB_ref, M, M_out, 2, F, 0.75, r=r)
     dgu = torch.full((M_out, 2 * F), 5.0, device=DEV, dtype=torch.bfloat16)
     out = torch.full((M_out, 64), 7.0, device=DEV, dtype=torch.bfloat16)
     dB = torch.zeros(2 * F, r, device=DEV)
-    ops().swiglu_lora_gdb(dh, gu, dgu, BT, u, out, dB, M, M_out, 0.75)
+    ops().swiglu_lora_gdb(dh, gu, dgu, BT, u, out, dB, M, M_out, 0.75, r=r)
     assert torch.equal(dgu, dgu_ref)
     assert torch.equal(out, out_ref)
     assert relerr(dB, dB_ref) < 1e-6
     # dB against fp64 dgu^T u over the kernel's own dgu (silu keeps dgu off the integers)
     u_i = ints(M_out, 64, lo=-2, hi=3)
     dB2 = torch.zeros(2 * F, r, device=DEV)
-    ops().swiglu_lora_gdb(dh, gu, dgu, BT, u_i, out, dB2, M, M_out, 1.0)
+    ops().swiglu_lora_gdb(dh, gu, dgu, BT, u_i, out, dB2, M, M_out, 1.0, r=r)
     ref2 = torch.cat([dgu[:M, j * F:(j + 1) * F].double().T @ u_i[:M, j * r:(j + 1) * r].double() for j in range(2)])
     assert relerr(dB2.double(), ref2) < 1e-6
 
