@@ -643,6 +643,10 @@ __device__ __forceinline__ void tr4_wait(i16x4& a, i16x4& b, i16x4& c, i16x4& d)
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
   __builtin_amdgcn_sched_barrier(0);
 }
+__device__ __forceinline__ void tr6_wait(i16x4& a, i16x4& b, i16x4& c, i16x4& d, i16x4& e, i16x4& f) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // In-launch sum of the g partials (INL, round 5, ablation A/B: bit-identical, no faster in the step than
 // gdb_reduce_kernel's launch, ~7.7 us each, 90 per step):
@@ -660,49 +664,55 @@ struct GdbInl {
 constexpr int GDB_CNT_BYTES = OSPO_WS_LORA_GDB_CNT_BYTES;
 constexpr unsigned GDB_SPIN_LIMIT = 1u << 24;
 
-template <int RSB, int NS = 4, int YA = 0, bool INL = false>  // YA: cache-policy bits of the dy loads
+// HPM (round 6): 16-column halves per module (LoRA r = 16 HPM): one workgroup reads its dy tile once for all
+// of them -- HPM Bt / u images and accumulator sets; the partials of half h of module mod are those of the
+// "module" mod HPM + h (gdb_reduce_kernel sums nmods HPM of them), the dB block of a module is [Nmod][16 HPM]
+template <int RSB, int NS = 4, int YA = 0, bool INL = false, int HPM = 1>  // YA: cache-policy bits of the dy loads
 __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ dy, int ldy, const bf16* __restrict__ Bt,
                                                        int ldb, const bf16* __restrict__ u, int ldu, int M, int Nmod,
                                                        int nch, float* __restrict__ ws, int Mw,
-                                                       float* __restrict__ dB, const GdbInl inl = GdbInl{},
-                                                       int hpm = 1) {
+                                                       float* __restrict__ dB, const GdbInl inl = GdbInl{}) {
+  static_assert(!(INL && HPM != 1), "the in-launch sum is r = 16 only");
   // NS-stage ring of 8-KiB dy sub-tiles, NS - 1 in flight (a 6-stage ring measured 10-30 % slower)
   constexpr int STAGE = 8192;
-  constexpr int BT_OFF = NS * STAGE, BT_BYTES = 16 * 4 * 128;  // up to nch = 4
-  constexpr int U_OFF = BT_OFF + BT_BYTES;
+  constexpr int BT_OFF = NS * STAGE, BT_BYTES = 16 * 4 * 128;  // up to nch = 4, per half
   constexpr int ROWS = 64 * RSB;
-  __shared__ __attribute__((aligned(16))) char smem[U_OFF + ROWS * 32];
+  constexpr int U_OFF = BT_OFF + HPM * BT_BYTES, U_BYTES = ROWS * 32;  // per half
+  __shared__ __attribute__((aligned(16))) char smem[U_OFF + HPM * U_BYTES];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, g = lane >> 4, r8 = lane >> 3, c8 = lane & 7;
   const int rb0 = blockIdx.x * ROWS;
   const int nsplit = Nmod / (64 * nch);
-  // mod: a 16-column half of a module (LoRA r = 16 hpm): module mod / hpm of dy, rows 16 mod of Bt, columns
-  // 16 mod of u and g, columns 16 (mod % hpm) of the module's [Nmod][r] dB block
+  // mod: the module (dy columns mod Nmod ..); half h of it: rows 16 (mod HPM + h) of Bt, columns 16 (mod HPM + h)
+  // of u and g, columns 16 h of the module's [Nmod][16 HPM] dB block
   const int mod = blockIdx.y / nsplit, sp = blockIdx.y % nsplit;
-  const int kc0 = sp * 64 * nch;                     // first column of the workgroup within its module
-  const long col0 = (long)(mod / hpm) * Nmod + kc0;  // ... within dy
-  const int rdb = 16 * hpm, cdb = 16 * (mod % hpm);  // dB row stride (r) and this half's first column
+  const int kc0 = sp * 64 * nch;              // first column of the workgroup within its module
+  const long col0 = (long)mod * Nmod + kc0;   // ... within dy
   const int btrow = nch * 128;               // bytes per Bt image row
 
-  // Bt image [16 j][nch*64 k]: 16-B chunk q of row j at physical chunk q ^ j (source-side swizzle)
+  // Bt images [16 j][nch*64 k]: 16-B chunk q of row j at physical chunk q ^ j (source-side swizzle)
   {
     const int rpp = 1024 / btrow;  // rows per 1-KiB piece (2 or 4)
-    for (int p = wave; p < 2 * nch; p += 4) {
-      const int off = lane * 16;
-      const int j = p * rpp + off / btrow, pc = (off % btrow) >> 4;
-      const int q = pc ^ j;
-      __builtin_amdgcn_global_load_lds(Bt + (long)(mod * 16 + j) * ldb + kc0 + q * 8,
-                                       (LDS_AS void*)(smem + BT_OFF + p * 1024), 16, 0, 0);
-    }
-  }
-  // u image [ROWS][16] (32 B per row), rows clamped (masked at the fragment)
 #pragma unroll
-  for (int p = wave; p < ROWS / 32; p += 4) {
-    const int row = min(rb0 + p * 32 + (lane >> 1), M - 1);
-    __builtin_amdgcn_global_load_lds(u + (long)row * ldu + mod * 16 + (lane & 1) * 8,
-                                     (LDS_AS void*)(smem + U_OFF + p * 1024), 16, 0, 0);
+    for (int h = 0; h < HPM; ++h)
+      for (int p = wave; p < 2 * nch; p += 4) {
+        const int off = lane * 16;
+        const int j = p * rpp + off / btrow, pc = (off % btrow) >> 4;
+        const int q = pc ^ j;
+        __builtin_amdgcn_global_load_lds(Bt + (long)((mod * HPM + h) * 16 + j) * ldb + kc0 + q * 8,
+                                         (LDS_AS void*)(smem + BT_OFF + h * BT_BYTES + p * 1024), 16, 0, 0);
+      }
   }
+  // u images [ROWS][16] (32 B per row), rows clamped (masked at the fragment)
+#pragma unroll
+  for (int h = 0; h < HPM; ++h)
+#pragma unroll
+    for (int p = wave; p < ROWS / 32; p += 4) {
+      const int row = min(rb0 + p * 32 + (lane >> 1), M - 1);
+      __builtin_amdgcn_global_load_lds(u + (long)row * ldu + (mod * HPM + h) * 16 + (lane & 1) * 8,
+                                       (LDS_AS void*)(smem + U_OFF + h * U_BYTES + p * 1024), 16, 0, 0);
+    }
   auto stage = [&](int t) {  // sub-tile t = (chunk t / RSB, row sub-block t % RSB): 2 pieces per wave
     char* st = smem + (t % NS) * STAGE;
     const int cc = t / RSB, rb = t % RSB;
@@ -721,10 +731,14 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
   // g: every wave computes its 16-row group (rows 16 wave .. +15) of every 64-row sub-block, 2 MFMAs per
   // sub-tile (the sub-block's 64 rows used to go to one wave, 8 MFMAs while the other three waited at
   // the next barrier); same per-row accumulation order (chunks, then k steps), bit-identical partials
-  f32x4 accg[RSB];
+  f32x4 accg[HPM][RSB];
+  f32x4 accb[HPM];
 #pragma unroll
-  for (int a = 0; a < RSB; ++a) accg[a] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int h = 0; h < HPM; ++h) {
+#pragma unroll
+    for (int a = 0; a < RSB; ++a) accg[h][a] = f32x4{0.f, 0.f, 0.f, 0.f};
+    accb[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const int li = l16, q4 = li >> 2, p4 = li & 3;
   const int grow = 16 * wave + l16;  // this lane's row of the g product inside a sub-tile
   for (int cc = 0; cc < nch; ++cc) {
@@ -748,9 +762,13 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int qk = cc * 8 + 4 * s2 + g;  // Bt chunk (8 bf16) of this lane's k group
-        const bf16x8 bt = *reinterpret_cast<const bf16x8*>(smem + BT_OFF + l16 * btrow + ((qk ^ l16) << 4));
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + grow * 128 + (((4 * s2 + g) ^ (grow & 7)) << 4));
-        accg[rb] = MFMA(bt, a, accg[rb]);  // D[j = 4g..][m = l16]
+#pragma unroll
+        for (int h = 0; h < HPM; ++h) {
+          const bf16x8 bt =
+              *reinterpret_cast<const bf16x8*>(smem + BT_OFF + h * BT_BYTES + l16 * btrow + ((qk ^ l16) << 4));
+          accg[h][rb] = MFMA(bt, a, accg[h][rb]);  // D[j = 4g..][m = l16]
+        }
       }
       // dB: columns 16 wave .. +15 of the chunk, the sub-block's 64 rows as K
 #pragma unroll
@@ -758,37 +776,53 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
         const int r1 = 32 * s + 8 * g + q4, r2 = r1 + 4;
         const int x = 2 * wave + (p4 >> 1), h = (p4 & 1) << 3;
         const int ur = rb * 64 + 32 * s + 8 * g;  // u image row of element 0
-        i16x4 lo, hi, ulo, uhi;
+        i16x4 lo, hi, ulo[HPM], uhi[HPM];
         tr4_issue(st + r1 * 128 + ((x ^ (r1 & 7)) << 4) + h, lo);
         tr4_issue(st + r2 * 128 + ((x ^ (r2 & 7)) << 4) + h, hi);
-        tr4_issue(smem + U_OFF + (ur + q4) * 32 + p4 * 8, ulo);
-        tr4_issue(smem + U_OFF + (ur + 4 + q4) * 32 + p4 * 8, uhi);
-        tr4_wait(lo, hi, ulo, uhi);
-        const int mrow = rb0 + ur;  // global row of element 0
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ulo[e] = (mrow + e < M) ? ulo[e] : (short)0;
-          uhi[e] = (mrow + 4 + e < M) ? uhi[e] : (short)0;
+        for (int hh = 0; hh < HPM; ++hh) {
+          tr4_issue(smem + U_OFF + hh * U_BYTES + (ur + q4) * 32 + p4 * 8, ulo[hh]);
+          tr4_issue(smem + U_OFF + hh * U_BYTES + (ur + 4 + q4) * 32 + p4 * 8, uhi[hh]);
         }
+        if constexpr (HPM == 1)
+          tr4_wait(lo, hi, ulo[0], uhi[0]);
+        else
+          tr6_wait(lo, hi, ulo[0], uhi[0], ulo[1], uhi[1]);
+        const int mrow = rb0 + ur;  // global row of element 0
         const i16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const i16x8 bv = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
-        accb = MFMA(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), accb);  // D[n = 4g+i][j = l16]
+#pragma unroll
+        for (int hh = 0; hh < HPM; ++hh) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ulo[hh][e] = (mrow + e < M) ? ulo[hh][e] : (short)0;
+            uhi[hh][e] = (mrow + 4 + e < M) ? uhi[hh][e] : (short)0;
+          }
+          const i16x8 bv = {ulo[hh][0], ulo[hh][1], ulo[hh][2], ulo[hh][3],
+                            uhi[hh][0], uhi[hh][1], uhi[hh][2], uhi[hh][3]};
+          accb[hh] = MFMA(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), accb[hh]);  // D[n][j]
+        }
       }
       if (rb == RSB - 1 && !(INL && cc == nch - 1)) {  // the chunk's dB over the workgroup's rows
         const long n0 = col0 + cc * 64 + 16 * wave + 4 * g;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * rdb + cdb + l16, accb[i]);
-        accb = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int hh = 0; hh < HPM; ++hh) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * (16 * HPM) + 16 * hh + l16, accb[hh][i]);
+          accb[hh] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
       }
     }
   }
   if constexpr (!INL) {
-    // g partials of this column block: ws [mod][sp][Mw][16]
+    // g partials of this column block: ws [mod HPM + h][sp][Mw][16]
 #pragma unroll
-    for (int rb = 0; rb < RSB; ++rb) {
-      const int m = rb0 + rb * 64 + grow;
-      if (m < Mw) *reinterpret_cast<f32x4*>(ws + (((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[rb];
-    }
+    for (int hh = 0; hh < HPM; ++hh)
+#pragma unroll
+      for (int rb = 0; rb < RSB; ++rb) {
+        const int m = rb0 + rb * 64 + grow;
+        if (m < Mw)
+          *reinterpret_cast<f32x4*>(ws + ((((long)mod * HPM + hh) * nsplit + sp) * Mw + m) * 16 + 4 * g) = accg[hh][rb];
+      }
   } else {
     const int nmods = gridDim.y / nsplit;
     const __amdgpu_buffer_rsrc_t rsW =
@@ -797,13 +831,13 @@ __global__ __launch_bounds__(256) void lora_gdb_kernel(const bf16* __restrict__ 
     for (int rb = 0; rb < RSB; ++rb) {
       const int m = rb0 + rb * 64 + grow;
       if (m < Mw)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, accg[rb]), rsW,
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, accg[0][rb]), rsW,
                                                (uint32_t)(((((long)mod * nsplit + sp) * Mw + m) * 16 + 4 * g) * 4), 0, 16);
     }
     {  // the last chunk's dB atomics after the partial stores: the wait below leaves them in flight
       const long n0 = col0 + (nch - 1) * 64 + 16 * wave + 4 * g;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * rdb + cdb + l16, accb[i]);
+      for (int i = 0; i < 4; ++i) atomicAdd(dB + (n0 + i) * 16 + l16, accb[0][i]);
     }
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this lane's partial stores acknowledged
     __syncthreads();
@@ -1643,37 +1677,47 @@ extern "C" int ospo_lora_gdb_r(const void* dy, int ldy, const void* Bt, int ldb,
   if (!aligned16(dy) || !aligned16(Bt) || !aligned16(u) || !aligned16(ws) || ((uintptr_t)dB & 3) ||
       ((uintptr_t)out & 7))
     return OSPO_ERR_ALIGN;
-  const int nch = gdb_nch(M, vm, Nmod);
+  // one workgroup covers all hpm halves of its module's column block (dy read once); at r = 32 on 256 rows
+  // (RSB 4: the two halves' g accumulators of 512 rows left one wave per SIMD)
+  const int nch = gdb_nch(M, nmods, Nmod);
   const int nsplit = Nmod / (64 * nch);
   const int Mw = (M + 63) / 64 * 64;
-  const dim3 grid((M + 511) / 512, vm * nsplit);
+  int wrows = hpm == 2 ? 256 : 512;
+#ifdef OSPO_ABLATION
+  const bool rsb4 = hpm == 1 && getenv("OSPO_GDB_RSB4");  // A/B: 256-row workgroups at r = 16
+  const bool ns6r32 = hpm == 2 && getenv("OSPO_GDB_NS6");  // A/B: a 6-stage ring at r = 32
+  if (rsb4) wrows = 256;
+#endif
+  const dim3 grid((M + wrows - 1) / wrows, nmods * nsplit);
   float* part = (float*)((char*)ws + GDB_CNT_BYTES);
   // A/B (ablation build, OSPO_GDB_INL=1): the partials summed inside the launch where the whole grid fits on the
   // device at once -- bit-identical, and no faster in the step (36.44 / 36.37 against 36.47 / 36.37 pairs/s,
   // profiles/r05/gdb_inlaunch_ab.txt): the product keeps the reduce launch
   bool inl = false;
 #ifdef OSPO_ABLATION
-  if (getenv("OSPO_GDB_INL"))
+  if (getenv("OSPO_GDB_INL") && hpm == 1)
     inl = grid.x <= 1024 && (long)grid.x * grid.y <= gdb_inl_capacity() && (long)M_out * out_cols < (1L << 31);
 #endif
   if (inl) {
     const GdbInl gi{(unsigned*)ws, M_out, scale, (bf16*)out, ldo, out_cols};
     hipLaunchKernelGGL((lora_gdb_kernel<8, 4, 0, true>), grid, dim3(256), 0, stream, (const bf16*)dy, ldy,
-                       (const bf16*)Bt, ldb, (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, gi, hpm);
+                       (const bf16*)Bt, ldb, (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, gi);
     OSPO_CHECK_LAUNCH();
     return OSPO_OK;
   }
-  auto kfn = lora_gdb_kernel<8, 4>;
+  auto kfn = hpm == 2 ? lora_gdb_kernel<4, 4, 0, false, 2> : lora_gdb_kernel<8, 4>;
 #ifdef OSPO_ABLATION
-  if (getenv("OSPO_GDB_NS6")) kfn = lora_gdb_kernel<8, 6>;  // A/B: a 6-stage ring
-  if (getenv("OSPO_GDB_NS2")) kfn = lora_gdb_kernel<8, 2>;  // A/B: 2- and 3-stage rings (more residency)
-  if (getenv("OSPO_GDB_NS3")) kfn = lora_gdb_kernel<8, 3>;
-  if (getenv("OSPO_NT_GDB")) kfn = lora_gdb_kernel<8, 4, 2>;  // A/B: non-temporal dy loads
+  if (hpm == 1 && getenv("OSPO_GDB_NS6")) kfn = lora_gdb_kernel<8, 6>;  // A/B: a 6-stage ring
+  if (hpm == 1 && getenv("OSPO_GDB_NS2")) kfn = lora_gdb_kernel<8, 2>;  // A/B: 2- and 3-stage rings (more residency)
+  if (hpm == 1 && getenv("OSPO_GDB_NS3")) kfn = lora_gdb_kernel<8, 3>;
+  if (hpm == 1 && getenv("OSPO_NT_GDB")) kfn = lora_gdb_kernel<8, 4, 2>;  // A/B: non-temporal dy loads
+  if (rsb4) kfn = getenv("OSPO_GDB_NS6") ? lora_gdb_kernel<4, 6> : lora_gdb_kernel<4, 4>;
+  if (ns6r32) kfn = lora_gdb_kernel<4, 6, 0, false, 2>;
 #endif
   const long n = (long)M_out * (out_cols / 4);
   if (n >= (1L << 31)) return OSPO_ERR_SHAPE;  // the reduce's 32-bit index
   hipLaunchKernelGGL(kfn, grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
-                     (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, GdbInl{}, hpm);
+                     (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, GdbInl{});
   OSPO_CHECK_LAUNCH();
   hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part,
                      vm, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
@@ -1706,7 +1750,7 @@ extern "C" int ospo_swiglu_lora_gdb_r(const void* dh, int ld_dh, const void* gu,
   const long Mr = (long)(M + 511) / 512 * 512;  // rows the grid addresses (clamped by the ranges, not the offsets)
   if (Mr * ld_dgu * 2 >= (1L << 31) || Mr * ld_gu * 2 >= (1L << 31) || Mr * ld_dh * 2 >= (1L << 31))
     return OSPO_ERR_UNSUPPORTED;  // the buffer ranges / offsets (32-bit)
-  const int nch = gdb_nch(M, vm, F);  // as ospo_lora_gdb_r on dgu: the same partials
+  const int nch = gdb_nch(M, 2, F);  // as ospo_lora_gdb_r on dgu: the same partials
   const int nsplit = F / (64 * nch);
   const int Mw = (M + 63) / 64 * 64;
   // one sub-tile of prefetch, non-temporal input loads (gu, dh are dead after this pass) and sc1 dgu stores:

@@ -25,19 +25,33 @@ def timeit(fn, it=20):
     return e0.elapsed_time(e1) / it * 1e3
 
 
-def main():
+def run(r):
     out = {}
     for name, nm, Nmod in GROUPS:
         dy = torch.randn(M, nm * Nmod, device="cuda").bfloat16()
-        bt = (torch.randn(nm * 16, Nmod, device="cuda") * 0.02).bfloat16()
-        Rp = 64 if nm * 16 <= 64 else 128
+        bt = (torch.randn(nm * r, Nmod, device="cuda") * 0.02).bfloat16()
+        Rp = 64 if nm * r <= 64 else 128
         u = torch.randn(M, Rp, device="cuda").bfloat16()
         g = torch.empty(M, Rp, device="cuda", dtype=torch.bfloat16)
-        dB = torch.zeros(nm * Nmod, 16, device="cuda")
-        ws = ops.lora_gdb_ws(M, nm, Nmod, "cuda")
-        us = timeit(lambda: ops.lora_gdb(dy, bt, u, g, dB, M, M, nm, Nmod, 2.0, ws))
+        dB = torch.zeros(nm * Nmod, r, device="cuda")
+        ws = ops.lora_gdb_ws(M, nm, Nmod, "cuda", r=r)
+        us = timeit(lambda: ops.lora_gdb(dy, bt, u, g, dB, M, M, nm, Nmod, 2.0, ws, r=r))
         out[name] = {"us": round(us, 1), "dy_TBps": round(dy.numel() * 2 / us / 1e6, 2)}
-    print(json.dumps(out))
+        del dy, u, g, dB, ws
+    return out
+
+
+def main():
+    # argv: r (16 / 32), then the ablation variants to interleave (comma-separated env names, "" = default)
+    r = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    variants = sys.argv[2].split(",") if len(sys.argv) > 2 else [""]
+    for rep in range(2):
+        for v in variants:
+            for k in ("OSPO_GDB_NS6", "OSPO_GDB_NS2", "OSPO_GDB_NS3", "OSPO_GDB_RSB4", "OSPO_NT_GDB"):
+                os.environ.pop(k, None)
+            for k in filter(None, v.split("+")):
+                os.environ[k] = "1"
+            print(json.dumps({"r": r, "variant": v or "default", "rep": rep, **run(r)}), flush=True)
 
 
 if __name__ == "__main__":
