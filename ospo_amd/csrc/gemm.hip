@@ -2011,7 +2011,7 @@ SplitPlan plan_split(int M, int N, int ntot, int K2, bool mx, bool drop, int cus
   return pl;
 }
 
-constexpr size_t W4_CNT_BYTES = OSPO_WS_GEMM_TAIL_CNT_BYTES;  // the w4 tail's arrival counters at the END of the split-K workspace
+[[maybe_unused]] constexpr size_t W4_CNT_BYTES = OSPO_WS_GEMM_TAIL_CNT_BYTES;  // the w4 tail's arrival counters at the END of the split-K workspace
 #include "gemm_w4.h"
 
 // The 4-wave hand-scheduled kernel (gemm_w4.h) when the shape fits it: bf16, <= 2 LoRA extension tiles,
@@ -2600,7 +2600,7 @@ int launch_v3(const GemmArgs& a, hipStream_t s) {
 uint32_t* g_dbg_buf = nullptr;  // variant 29: s_memtime stamps, 16 words per wave
 int g_gemm_variant = 0;  // 0 = SP schedule + split-K tail (default); 17 = the 8-phase schedule; others: A/B, see dispatch
 #else
-constexpr int g_gemm_variant = 0;  // the product library runs the default schedule only
+[[maybe_unused]] constexpr int g_gemm_variant = 0;  // the product library runs the default schedule only
 #endif
 
 // the bf16 256 x 256 schedule every entry point runs (the ablation build can switch it for A/B)

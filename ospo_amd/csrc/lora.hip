@@ -1136,7 +1136,6 @@ __global__ __launch_bounds__(256) void lora_da_kernel(const bf16* __restrict__ X
                                                       int nt, float* __restrict__ C, int ldc, uint32_t dseed,
                                                       uint32_t dthresh, float dscale, int drop_ld,
                                                       const uint8_t* __restrict__ kbits, int k_bytes) {
-  constexpr bool DROP = DM > 0;
   constexpr int STG = DA_STG + (DM == 2 ? 1024 : 0);
   constexpr int PW = DA_PW + (DM == 2 ? 1 : 0);
   __shared__ __attribute__((aligned(16))) char smem[DA_NS * STG];
@@ -1439,7 +1438,7 @@ static int launch_skinny3(const bf16* a, int lda, const bf16* b, int ldb, int b_
   // and wave: the LDS-DMA issue, a barrier, the dropout hash's quarter-rate multiplies), so residency beats
   // depth: per call 19.3 / 17.5 / 93.7 us at 2 stages against 20.3 / 18.7 / 97.1 at 4 and 29.0 / 25.1 / 121.4
   // at 8 (u_qkv / u_o / SwiGLU + u_d, profiles/r03/skinny_ring_depth.jsonl).  Ablation: OSPO_SK3_NS.
-  int ns = 2;
+  [[maybe_unused]] int ns = 2;
 #ifdef OSPO_ABLATION
   static const int ns_env = [] {
     const char* e = getenv("OSPO_SK3_NS");
