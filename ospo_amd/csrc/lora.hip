@@ -1627,8 +1627,8 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
 }
 
 // ---------------------------------------------------------------------------------- lora_gdb
-static int gdb_nch(int M, int nmods, int Nmod) {
-  const int rbk = (M + 511) / 512;
+static int gdb_nch(int M, int nmods, int Nmod, int rows = 512) {  // rows: the workgroup's row block
+  const int rbk = (M + rows - 1) / rows;
   int min_wgs = 256;
 #ifdef OSPO_ABLATION
   if (const char* e = getenv("OSPO_GDB_MINWG")) min_wgs = atoi(e);  // A/B: grid size below which nch = 2
@@ -1676,17 +1676,21 @@ extern "C" int ospo_lora_gdb_r(const void* dy, int ldy, const void* Bt, int ldb,
   if (!aligned16(dy) || !aligned16(Bt) || !aligned16(u) || !aligned16(ws) || ((uintptr_t)dB & 3) ||
       ((uintptr_t)out & 7))
     return OSPO_ERR_ALIGN;
-  // one workgroup covers all hpm halves of its module's column block (dy read once); at r = 32 on 256 rows
-  // (RSB 4: the two halves' g accumulators of 512 rows left one wave per SIMD)
-  const int nch = gdb_nch(M, nmods, Nmod);
-  const int nsplit = Nmod / (64 * nch);
-  const int Mw = (M + 63) / 64 * 64;
-  int wrows = hpm == 2 ? 256 : 512;
+  // one workgroup covers all hpm halves of its module's column block (dy read once).  Row blocks of 256 at
+  // r = 32 (RSB 4: the two halves' g accumulators of 512 rows left one wave per SIMD) and for one-module groups
+  // (o, down: 304 workgroups of 256 columns instead of 320 of 128, half the g partials; 18.5-18.9 against
+  // 20.6-21.4 us per call at r = 16, 26-28 against 29-30 at r = 32, profiles/r06/gdb_variant_sweep_*b.log);
+  // 512 for the multi-module groups at r = 16 (q|k|v 32.5 against 37.0 us at 256)
+  int wrows = (hpm == 2 || nmods == 1) ? 256 : 512;
 #ifdef OSPO_ABLATION
   const bool rsb4 = hpm == 1 && getenv("OSPO_GDB_RSB4");  // A/B: 256-row workgroups at r = 16
   const bool ns6r32 = hpm == 2 && getenv("OSPO_GDB_NS6");  // A/B: a 6-stage ring at r = 32
   if (rsb4) wrows = 256;
+  if (hpm == 1 && getenv("OSPO_GDB_RSB8")) wrows = 512;  // A/B: the round-5 512-row blocks for every group
 #endif
+  const int nch = gdb_nch(M, nmods, Nmod, wrows);
+  const int nsplit = Nmod / (64 * nch);
+  const int Mw = (M + 63) / 64 * 64;
   const dim3 grid((M + wrows - 1) / wrows, nmods * nsplit);
   float* part = (float*)((char*)ws + GDB_CNT_BYTES);
   // A/B (ablation build, OSPO_GDB_INL=1): the partials summed inside the launch where the whole grid fits on the
@@ -1694,7 +1698,7 @@ extern "C" int ospo_lora_gdb_r(const void* dy, int ldy, const void* Bt, int ldb,
   // profiles/r05/gdb_inlaunch_ab.txt): the product keeps the reduce launch
   bool inl = false;
 #ifdef OSPO_ABLATION
-  if (getenv("OSPO_GDB_INL") && hpm == 1)
+  if (getenv("OSPO_GDB_INL") && wrows == 512)
     inl = grid.x <= 1024 && (long)grid.x * grid.y <= gdb_inl_capacity() && (long)M_out * out_cols < (1L << 31);
 #endif
   if (inl) {
@@ -1704,12 +1708,13 @@ extern "C" int ospo_lora_gdb_r(const void* dy, int ldy, const void* Bt, int ldb,
     OSPO_CHECK_LAUNCH();
     return OSPO_OK;
   }
-  auto kfn = hpm == 2 ? lora_gdb_kernel<4, 4, 0, false, 2> : lora_gdb_kernel<8, 4>;
+  auto kfn = hpm == 2 ? lora_gdb_kernel<4, 4, 0, false, 2> : wrows == 256 ? lora_gdb_kernel<4, 4> : lora_gdb_kernel<8, 4>;
 #ifdef OSPO_ABLATION
-  if (hpm == 1 && getenv("OSPO_GDB_NS6")) kfn = lora_gdb_kernel<8, 6>;  // A/B: a 6-stage ring
-  if (hpm == 1 && getenv("OSPO_GDB_NS2")) kfn = lora_gdb_kernel<8, 2>;  // A/B: 2- and 3-stage rings (more residency)
-  if (hpm == 1 && getenv("OSPO_GDB_NS3")) kfn = lora_gdb_kernel<8, 3>;
-  if (hpm == 1 && getenv("OSPO_NT_GDB")) kfn = lora_gdb_kernel<8, 4, 2>;  // A/B: non-temporal dy loads
+  const bool r8 = hpm == 1 && wrows == 512;
+  if (r8 && getenv("OSPO_GDB_NS6")) kfn = lora_gdb_kernel<8, 6>;  // A/B: a 6-stage ring
+  if (r8 && getenv("OSPO_GDB_NS2")) kfn = lora_gdb_kernel<8, 2>;  // A/B: 2- and 3-stage rings (more residency)
+  if (r8 && getenv("OSPO_GDB_NS3")) kfn = lora_gdb_kernel<8, 3>;
+  if (r8 && getenv("OSPO_NT_GDB")) kfn = lora_gdb_kernel<8, 4, 2>;  // A/B: non-temporal dy loads
   if (rsb4) kfn = getenv("OSPO_GDB_NS6") ? lora_gdb_kernel<4, 6> : lora_gdb_kernel<4, 4>;
   if (ns6r32) kfn = lora_gdb_kernel<4, 6, 0, false, 2>;
 #endif
@@ -1749,7 +1754,7 @@ extern "C" int ospo_swiglu_lora_gdb_r(const void* dh, int ld_dh, const void* gu,
   const long Mr = (long)(M + 511) / 512 * 512;  // rows the grid addresses (clamped by the ranges, not the offsets)
   if (Mr * ld_dgu * 2 >= (1L << 31) || Mr * ld_gu * 2 >= (1L << 31) || Mr * ld_dh * 2 >= (1L << 31))
     return OSPO_ERR_UNSUPPORTED;  // the buffer ranges / offsets (32-bit)
-  const int nch = gdb_nch(M, 2, F);  // as ospo_lora_gdb_r on dgu: the same partials
+  const int nch = gdb_nch(M, 2, F, hpm == 2 ? 256 : 512);  // as ospo_lora_gdb_r on dgu: the same partials
   const int nsplit = F / (64 * nch);
   const int Mw = (M + 63) / 64 * 64;
   // one sub-tile of prefetch, non-temporal input loads (gu, dh are dead after this pass) and sc1 dgu stores:
