@@ -1259,6 +1259,10 @@ __global__ __launch_bounds__(256) void lora_da_kernel(const bf16* __restrict__ X
 }
 
 // out[m][16 mod + c] = bf16(scale * sum_sp ws[mod][sp][m][c]) (m < M; 0 for M <= m < M_out), pad columns 0
+// PB partial loads in flight per thread (the same left-to-right sum for any PB, bit-identical).  16 instead of 8
+// measured no faster (kernel + reduce per group within 0.5 us either way, profiles/r06/gdb_reduce_pb_ab.log):
+// the product keeps 8, the ablation build's OSPO_GDB_RED16 runs 16
+template <int PB = 8>
 __global__ void gdb_reduce_kernel(const float* __restrict__ ws, int nmods, int nsplit, int Mw, int M, int M_out,
                                   float scale, bf16* __restrict__ out, int ldo, int out_cols) {
   const unsigned cq = (unsigned)out_cols / 4;  // 32-bit index math: M_out * cq < 2^31 (host check)
@@ -1268,15 +1272,15 @@ __global__ void gdb_reduce_kernel(const float* __restrict__ ws, int nmods, int n
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   const int mod = c / 16;
   if (m < M && mod < nmods) {
-    for (int s0 = 0; s0 < nsplit; s0 += 8) {
-      f32x4 p[8];
+    for (int s0 = 0; s0 < nsplit; s0 += PB) {
+      f32x4 p[PB];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < PB; ++k)
         if (s0 + k < nsplit)  // (non-temporal: each partial is read once)
           p[k] = __builtin_nontemporal_load(
               reinterpret_cast<const f32x4*>(ws + (((long)mod * nsplit + s0 + k) * Mw + m) * 16 + (c & 15)));
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < PB; ++k)
         if (s0 + k < nsplit) v += p[k];
     }
   }
@@ -1627,6 +1631,14 @@ extern "C" int ospo_lora_skinny(const void* A, int lda, const void* Bt, int ldb,
 }
 
 // ---------------------------------------------------------------------------------- lora_gdb
+using GdbReduceFn = void (*)(const float*, int, int, int, int, int, float, bf16*, int, int);
+static GdbReduceFn gdb_reduce_fn() {
+#ifdef OSPO_ABLATION
+  if (getenv("OSPO_GDB_RED16")) return gdb_reduce_kernel<16>;  // A/B: 16 partial loads in flight
+#endif
+  return gdb_reduce_kernel<8>;
+}
+
 static int gdb_nch(int M, int nmods, int Nmod, int rows = 512) {  // rows: the workgroup's row block
   const int rbk = (M + rows - 1) / rows;
   int min_wgs = 256;
@@ -1723,7 +1735,7 @@ extern "C" int ospo_lora_gdb_r(const void* dy, int ldy, const void* Bt, int ldb,
   hipLaunchKernelGGL(kfn, grid, dim3(256), 0, stream, (const bf16*)dy, ldy, (const bf16*)Bt, ldb,
                      (const bf16*)u, ldu, M, Nmod, nch, part, Mw, dB, GdbInl{});
   OSPO_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part,
+  hipLaunchKernelGGL(gdb_reduce_fn(), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part,
                      vm, nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;
@@ -1788,7 +1800,7 @@ extern "C" int ospo_swiglu_lora_gdb_r(const void* dh, int ld_dh, const void* gu,
                      (const bf16*)dh, ld_dh, (const bf16*)gu, ld_gu, (bf16*)dgu, ld_dgu, (const bf16*)Bt, ldb,
                      (const bf16*)u, ldu, M, F, part, Mw, dB);
   OSPO_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gdb_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part, vm,
+  hipLaunchKernelGGL(gdb_reduce_fn(), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const float*)part, vm,
                      nsplit, Mw, M, M_out, scale, (bf16*)out, ldo, out_cols);
   OSPO_CHECK_LAUNCH();
   return OSPO_OK;

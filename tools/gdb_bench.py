@@ -47,7 +47,7 @@ def main():
     variants = sys.argv[2].split(",") if len(sys.argv) > 2 else [""]
     for rep in range(2):
         for v in variants:
-            for k in ("OSPO_GDB_NS6", "OSPO_GDB_NS2", "OSPO_GDB_NS3", "OSPO_GDB_RSB4", "OSPO_NT_GDB", "OSPO_GDB_MINWG", "OSPO_GDB_RSB8"):
+            for k in ("OSPO_GDB_NS6", "OSPO_GDB_NS2", "OSPO_GDB_NS3", "OSPO_GDB_RSB4", "OSPO_NT_GDB", "OSPO_GDB_MINWG", "OSPO_GDB_RSB8", "OSPO_GDB_RED8", "OSPO_GDB_RED16"):
                 os.environ.pop(k, None)
             for k in filter(None, v.split("+")):
                 os.environ[k] = "1"
